@@ -1,0 +1,188 @@
+#!/usr/bin/env python
+"""bench.py -- fp64 GMRES iterations/s on MI355X (BASELINE.json metric).
+
+Workload (N=1): config C2 of BASELINE.json -- 1000x1000 5-point Laplacian CSR
+(n = 1,000,000, nnz = 4,996,000), ILU(0) left preconditioner, GMRES(30),
+tol 1e-8, b = A*1, x0 = 0.  One step = one full solve (device-resident b, x;
+the ILU factorization and H2D copies are setup, outside the timed region).
+
+value = inner (Arnoldi) iterations of all ranks / max-over-ranks wall time.
+roofline: the dominant kernel family, timed live inside the timed region with
+hipEvent pairs on the solver's stream (gg_profile_*), algorithmic bytes from
+SURVEY.md 8(d).  cpu_baseline: the fp64 oracle restatement (oracle/, serial C)
+on a bounded sample of the same workload, rank 0 only.
+
+Multi-GPU (torchrun, one rank per GPU): every rank solves its own C2 system
+(replicas, "scaling": "weak"); the arrow-partitioned sharded solve is DESIGN.md
+"Multi-GPU".
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "gpu-gmres_amd"))
+
+import numpy as np
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "fp64 GMRES iterations/sec + SpMV HBM GB/s, 1M-row CSR @1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--grid", type=int, default=1000, help="grid side (1000 = C2, 100 = C1)")
+    p.add_argument("--restart", type=int, default=30)
+    p.add_argument("--tol", type=float, default=1e-8)
+    p.add_argument("--max-iter", type=int, default=20000)
+    p.add_argument("--cpu-iters", type=int, default=120,
+                   help="oracle iterations timed for cpu_baseline (0 = skip)")
+    p.add_argument("--no-profile", action="store_true", help="do not bracket kernels with events")
+    return p.parse_args()
+
+
+def mgs_bytes(n, m, inner_list):
+    """Algorithmic MGS bytes for the inner iterations actually run:
+    iteration with cycle index i moves 40 n (i+1) (dot + AXPY per k) + 24 n (norm+scale)."""
+    tot = 0.0
+    iters = 0
+    for inner in inner_list:
+        full, rem = divmod(inner, m)
+        for i in list(range(m)) * full + list(range(rem)):
+            tot += 40.0 * n * (i + 1) + 24.0 * n
+            iters += 1
+    return tot, iters
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import ggmres
+    from ggmres import matrices as M
+
+    A = M.laplacian_5pt(a.grid)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    s = ggmres.Solver(local)
+    t_setup = time.perf_counter()
+    s.set_matrix(A)
+    s.set_precond_ilu0()
+    t_setup = time.perf_counter() - t_setup
+    db = torch.from_numpy(b).cuda()
+    dx = torch.zeros(n, dtype=torch.float64, device="cuda")
+
+    def step():
+        dx.zero_()
+        torch.cuda.synchronize()
+        return s.solve_device(db.data_ptr(), dx.data_ptr(), restart=a.restart,
+                              max_iter=a.max_iter, tol=a.tol)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    s.profile(not a.no_profile)
+    barrier()
+    t0 = time.perf_counter()
+    res = [step() for _ in range(a.steps)]
+    barrier()
+    el = time.perf_counter() - t0
+
+    inner = sum(r["inner"] for r in res)
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    it = torch.tensor([float(inner)], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(it, op=dist.ReduceOp.SUM)
+    el_max, inner_all = float(t.item()), float(it.item())
+    value = inner_all / el_max
+
+    # ---- per-kernel-family timing from the timed region -----------------------
+    fam = {}
+    spmv_bytes = s.bytes_spmv()
+    pre_bytes = s.bytes_precond()
+    mgs_tot, mgs_it = mgs_bytes(n, a.restart, [r["inner"] for r in res])
+    for name, kind, per in (("spmv", ggmres.PROF_SPMV, spmv_bytes),
+                            ("ilu0_apply", ggmres.PROF_PRECOND, pre_bytes),
+                            ("mgs_givens", ggmres.PROF_MGS, None)):
+        cnt, ms = s.profile_get(kind)
+        if cnt == 0:
+            continue
+        avg_us = ms * 1e3 / cnt
+        byt = per if per is not None else mgs_tot / max(mgs_it, 1)
+        fam[name] = {"launches": cnt, "avg_us": round(avg_us, 3),
+                     "alg_bytes_per_launch": byt,
+                     "achieved_gbs": round(byt / (avg_us * 1e-6) / 1e9, 1),
+                     "share_of_step": round(ms / (el * 1e3), 4)}
+    dom = max(fam, key=lambda k: fam[k]["share_of_step"]) if fam else None
+    roof = None
+    if dom:
+        f = fam[dom]
+        roof = {"kernel": dom, "bound": "hbm", "achieved": f["achieved_gbs"],
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"]}
+    # isolated SpMV (4 rotating copies of A, x, y: > 256 MiB, not Infinity-Cache served)
+    spmv_iso_ms = s.time_spmv(reps=100, nrot=4)
+    spmv_iso = {"avg_us": round(spmv_iso_ms * 1e3, 3),
+                "achieved_gbs": round(spmv_bytes / (spmv_iso_ms * 1e-3) / 1e9, 1),
+                "frac": round(spmv_bytes / (spmv_iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    # ---- CPU baseline (rank 0, N=1): the oracle restatement -----------------------
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_iters > 0:
+        import oracle as O
+        L, U = O.ilu0(A)
+        t1 = time.perf_counter()
+        o = O.gmres_left(A, L, U, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
+        ct = time.perf_counter() - t1
+        cpu = {"value": round(o["inner"] / ct, 3), "unit": "iterations/s", "cores": 1,
+               "kind": "port",
+               "sample": f"oracle/ fp64 serial C restatement of GMRES_leftILU0 on the same C2 "
+                         f"system, first {o['inner']} inner iterations ({ct:.1f} s)"}
+
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el_max * 1e3 / a.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU(0) left, "
+                               f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step",
+                   "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
+                   "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
+                   "wavefront_sptrsv": s.uses_wavefront,
+                   "parallelism": "single" if world == 1 else f"replicas{world}",
+                   "setup_s": round(t_setup, 3)},
+        "roofline": roof,
+        "kernels": fam,
+        "spmv_isolated": spmv_iso,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    s.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

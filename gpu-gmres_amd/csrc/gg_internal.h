@@ -1,0 +1,150 @@
+// gg_internal.h -- internal types of the MI355X GMRES solver (host + device).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "ggmres.h"
+
+namespace gg {
+
+// ------------------------------------------------------------------ errors
+void set_error(const std::string &msg);
+struct Error {
+    int code;
+    std::string msg;
+};
+#define GG_HIP(call)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            throw ::gg::Error{GG_EHIP, std::string(#call) + ": " + hipGetErrorString(e_) + \
+                                           " @" + __FILE__ + ":" + std::to_string(__LINE__)}; \
+    } while (0)
+#define GG_REQUIRE(cond, code, msg)                                                    \
+    do {                                                                               \
+        if (!(cond)) throw ::gg::Error{code, msg};                                     \
+    } while (0)
+
+// ---------------------------------------------------------------- host CSR
+struct Csr {
+    int n = 0;
+    std::vector<int> rp, ci;
+    std::vector<double> v;
+    int nnz() const { return rp.empty() ? 0 : rp[n]; }
+};
+
+// A triangular solve in "canonical" form: for each row r (in its solve order)
+//   x[r] = (b[r] - sum_k off_v[k] * x[off_c[k]]) / d[r]
+// with the off-diagonal terms listed in exactly the reference's summation
+// order.  A unit or skipped diagonal is d = 1 (division by 1 is exact).
+struct CanonTri {
+    bool lower = true;
+    Csr off;                 // off-diagonal entries, reference order
+    std::vector<double> d;   // divisors
+};
+
+// host-side factorization (host/factor.cpp)
+void ilu0_left(const Csr &A, Csr &L, Csr &U);                 // leftILU semantics
+int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U);        // lofC + ilukC, 0 or GG_EZEROPIVOT
+
+// canonical forms (host/analysis.cpp)
+CanonTri canon_lower_unit(const Csr &L);        // LUSolve_ignoreZero forward (diag never applied)
+CanonTri canon_upper_ignorezero(const Csr &U);  // LUSolve_ignoreZero backward
+CanonTri canon_lower_lastdiag(const Csr &L);    // MyILUPP HostPrecond_left (divide by last)
+CanonTri canon_upper_firstdiag(const Csr &U);   // MyILUPP HostPrecond_right (divide by first)
+
+// level sets for a canonical triangle: rows grouped by dependency depth
+struct Levels {
+    std::vector<int> ptr;    // nlev+1
+    std::vector<int> rows;   // n
+};
+Levels level_sets(const CanonTri &T);
+
+// 2D structured-grid wavefront layout (SURVEY.md 7 hard parts)
+//   natural row r = j*nx + i  ->  layout slot ((j/64)*T + i + j%64)*64 + j%64,
+//   T = nx + 63 rounded up to a multiple of 16 (the kernel's batch)
+struct Wave2D {
+    bool ok = false;
+    int nx = 0, ny = 0, nbands = 0, T = 0;
+    long long P = 0;         // padded layout length
+    long long slot(int r) const {
+        int j = r / nx, i = r % nx;
+        return ((long long)(j >> 6) * T + i + (j & 63)) * 64 + (j & 63);
+    }
+};
+// detect: L off-diagonals only at offsets {nx (first), 1 (second)} and U only at
+// {nx (first), 1 (second)}, no wrap-around entries.  Returns ok=false otherwise.
+Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U);
+
+// SpMV row blocks: each block <= 256 rows and <= kSpmvCap nnz (CSR-stream)
+constexpr int kSpmvCap = 2048;
+std::vector<int> spmv_blocks(const Csr &A, std::vector<int> &long_rows);
+
+// ----------------------------------------------------------- device buffers
+template <class T>
+struct DBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf &) = delete;
+    DBuf &operator=(const DBuf &) = delete;
+    ~DBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        release();
+        if (count == 0) count = 1;
+        hipError_t e = hipMalloc(&p, count * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            throw Error{GG_ENOMEM, "hipMalloc(" + std::to_string(count * sizeof(T)) + " B) failed"};
+        }
+        n = count;
+    }
+    void upload(const T *h, size_t count, hipStream_t st) {
+        alloc(count);
+        if (count) GG_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, st));
+    }
+    void upload(const std::vector<T> &h, hipStream_t st) { upload(h.data(), h.size(), st); }
+};
+
+struct DevCsr {
+    int n = 0, nnz = 0;
+    DBuf<int> rp, ci;
+    DBuf<double> v;
+    // CSR-stream partition
+    int nblk = 0;
+    DBuf<int> blk;           // nblk+1 row boundaries
+    int nlong = 0;
+    DBuf<int> long_rows;     // rows too long for one block (vector-per-row path)
+    void upload(const Csr &A, hipStream_t st);
+};
+
+// device triangular solve
+struct DevTri {
+    enum Kind { NONE, LEVEL, WAVE2D } kind = NONE;
+    bool lower = true;
+    int n = 0;
+    // LEVEL
+    DevCsr off;
+    DBuf<double> d;
+    std::vector<int> lev_ptr;    // host
+    DBuf<int> lev_rows;
+    // WAVE2D (layout arrays, length P)
+    Wave2D wl;
+    DBuf<double> c1, c2, dw;     // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor
+    bool unit = false;           // dw == 1 everywhere: skip the division load
+    DBuf<unsigned long long> bnd;  // nbands * nx boundary granules (sentinel = not ready)
+    double bytes = 0;            // algorithmic bytes per solve
+};
+
+struct DevState;   // device-side GMRES control block (kernels.h)
+
+}  // namespace gg

@@ -1,0 +1,178 @@
+// analysis.cpp -- setup-time analysis for the device triangular solves / SpMV.
+//
+//  * canonical solve forms: the off-diagonal terms of each row in exactly the
+//    summation order the reference uses, plus the divisor, so the device
+//    kernels reproduce the reference arithmetic order:
+//      LUSolve_ignoreZero           src/SpMV_compute.cpp:92-136
+//      MyILUPP::HostPrecond_left    src/preconditioner.cu:1094-1114
+//      MyILUPP::HostPrecond_right   src/preconditioner.cu:1117-1137
+//  * level sets (replaces cusparse*csrsv_analysis, src/preconditioner.cu:1313-1316)
+//  * 2D structured-grid detection for the wavefront solve
+//  * CSR-stream row blocks for SpMV
+#include <algorithm>
+#include <cmath>
+
+#include "../gg_internal.h"
+
+namespace gg {
+
+namespace {
+inline bool near_zero(double a) { return std::fabs(a) < 1e-9; }
+void push(Csr &C, int c, double v) { C.ci.push_back(c); C.v.push_back(v); }
+CanonTri start(const Csr &T, bool lower)
+{
+    CanonTri C;
+    C.lower = lower;
+    C.off.n = T.n;
+    C.off.rp.assign(T.n + 1, 0);
+    C.off.ci.reserve(T.nnz());
+    C.off.v.reserve(T.nnz());
+    C.d.assign(T.n, 1.0);
+    return C;
+}
+}  // namespace
+
+CanonTri canon_lower_unit(const Csr &L)
+{
+    CanonTri C = start(L, true);
+    for (int r = 0; r < L.n; r++) {
+        for (int k = L.rp[r]; k < L.rp[r + 1]; k++) {
+            if (L.ci[k] >= r) break;          // forward loop stops at the diagonal
+            push(C.off, L.ci[k], L.v[k]);
+        }
+        C.off.rp[r + 1] = (int)C.off.ci.size();
+    }
+    return C;
+}
+
+CanonTri canon_upper_ignorezero(const Csr &U)
+{
+    CanonTri C = start(U, false);
+    for (int r = 0; r < U.n; r++) {
+        int lb = U.rp[r], j = U.rp[r + 1] - 1;
+        for (; j >= lb; j--) {                // backward loop from the row end
+            if (U.ci[j] <= r) break;
+            push(C.off, U.ci[j], U.v[j]);
+        }
+        if (j >= lb && U.ci[j] == r && !near_zero(U.v[j])) C.d[r] = U.v[j];
+        C.off.rp[r + 1] = (int)C.off.ci.size();
+    }
+    return C;
+}
+
+CanonTri canon_lower_lastdiag(const Csr &L)
+{
+    CanonTri C = start(L, true);
+    for (int r = 0; r < L.n; r++) {
+        int lb = L.rp[r], ub = L.rp[r + 1];
+        GG_REQUIRE(ub > lb, GG_EINVAL, "split L: empty row " + std::to_string(r));
+        for (int k = lb; k < ub - 1; k++) push(C.off, L.ci[k], L.v[k]);
+        C.d[r] = L.v[ub - 1];
+        C.off.rp[r + 1] = (int)C.off.ci.size();
+    }
+    return C;
+}
+
+CanonTri canon_upper_firstdiag(const Csr &U)
+{
+    CanonTri C = start(U, false);
+    for (int r = 0; r < U.n; r++) {
+        int lb = U.rp[r], ub = U.rp[r + 1];
+        GG_REQUIRE(ub > lb, GG_EINVAL, "split U: empty row " + std::to_string(r));
+        for (int k = lb + 1; k < ub; k++) push(C.off, U.ci[k], U.v[k]);
+        C.d[r] = U.v[lb];
+        C.off.rp[r + 1] = (int)C.off.ci.size();
+    }
+    return C;
+}
+
+Levels level_sets(const CanonTri &T)
+{
+    const int n = T.off.n;
+    std::vector<int> lev(n, 0);
+    int maxlev = 0;
+    auto row = [&](int r) {
+        int l = 0;
+        for (int k = T.off.rp[r]; k < T.off.rp[r + 1]; k++) {
+            int c = T.off.ci[k];
+            GG_REQUIRE(T.lower ? c < r : c > r, GG_EINVAL,
+                       std::string(T.lower ? "lower" : "upper") + " factor has an entry on the wrong side of the diagonal at row " +
+                           std::to_string(r));
+            l = std::max(l, lev[c] + 1);
+        }
+        lev[r] = l;
+        maxlev = std::max(maxlev, l);
+    };
+    if (T.lower) for (int r = 0; r < n; r++) row(r);
+    else for (int r = n - 1; r >= 0; r--) row(r);
+    Levels L;
+    L.ptr.assign(maxlev + 2, 0);
+    for (int r = 0; r < n; r++) L.ptr[lev[r] + 1]++;
+    for (int l = 0; l <= maxlev; l++) L.ptr[l + 1] += L.ptr[l];
+    L.rows.resize(n);
+    std::vector<int> pos(L.ptr.begin(), L.ptr.end() - 1);
+    for (int r = 0; r < n; r++) L.rows[pos[lev[r]]++] = r;
+    if (n == 0) L.ptr.assign(1, 0);
+    return L;
+}
+
+Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
+{
+    Wave2D w;
+    const int n = L.off.n;
+    if (n < 128 || U.off.n != n) return w;
+    int nx = 0;
+    for (int r = 0; r < n; r++)
+        for (int k = L.off.rp[r]; k < L.off.rp[r + 1]; k++) nx = std::max(nx, r - L.off.ci[k]);
+    if (nx < 2 || n % nx != 0 || n / nx < 2) return w;
+    // L rows: [r-nx][r-1] in this order (either may be absent), no wrap of r-1
+    for (int r = 0; r < n; r++) {
+        int lb = L.off.rp[r], ub = L.off.rp[r + 1], k = lb;
+        if (k < ub && L.off.ci[k] == r - nx) k++;
+        if (k < ub && L.off.ci[k] == r - 1 && (r % nx) != 0) k++;
+        if (k != ub) return w;
+    }
+    // U rows: [r+nx][r+1] in this order (LUSolve_ignoreZero walks from the row end)
+    for (int r = 0; r < n; r++) {
+        int lb = U.off.rp[r], ub = U.off.rp[r + 1], k = lb;
+        if (k < ub && U.off.ci[k] == r + nx) k++;
+        if (k < ub && U.off.ci[k] == r + 1 && (r % nx) != nx - 1) k++;
+        if (k != ub) return w;
+    }
+    w.ok = true;
+    w.nx = nx;
+    w.ny = n / nx;
+    w.nbands = (w.ny + 63) / 64;
+    w.T = (nx + 63 + 15) / 16 * 16;   // whole 16-step batches (kWaveBatch)
+    w.P = (long long)w.nbands * w.T * 64;
+    return w;
+}
+
+std::vector<int> spmv_blocks(const Csr &A, std::vector<int> &long_rows)
+{
+    std::vector<int> b;
+    b.push_back(0);
+    long_rows.clear();
+    int r = 0;
+    const int n = A.n;
+    while (r < n) {
+        int len = A.rp[r + 1] - A.rp[r];
+        if (len > kSpmvCap) {           // a row alone, handled by the long-row path
+            long_rows.push_back(r);
+            r++;
+            b.push_back(r);
+            continue;
+        }
+        int start = r, nnz = 0;
+        while (r < n && r - start < 256) {
+            int l = A.rp[r + 1] - A.rp[r];
+            if (l > kSpmvCap || nnz + l > kSpmvCap) break;
+            nnz += l;
+            r++;
+        }
+        b.push_back(r);
+    }
+    return b;
+}
+
+}  // namespace gg

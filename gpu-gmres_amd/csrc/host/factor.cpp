@@ -1,0 +1,220 @@
+// factor.cpp -- host-side ILU(0) / ILU(k) setup for the MI355X solver.
+//
+// Setup phase only (factored once, reused for every solve / time step,
+// SURVEY.md 2.2).  Arithmetic follows the reference entry-for-entry in fp64:
+//   ilu0_left   leftILU                 src/leftILU.cu:27-336 (column kernel of
+//                                       cpuSequentialTriSolve :769-825, level
+//                                       order generateLevel :339-368, split
+//                                       splitLU_csr :481-541)
+//   iluk_itsol  lofC + ilukC            src/iluk.cpp:56-334
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+
+#include "../gg_internal.h"
+
+namespace gg {
+
+namespace {
+
+inline bool near_zero(double a) { return std::fabs(a) < 1e-9; }  // Equal(a,0), src/defs.h:45-47
+
+// transpose a square CSR (row order inside each output row ascending)
+void transpose(int n, const std::vector<int> &rp, const std::vector<int> &ci,
+               const std::vector<double> &v, std::vector<int> &tp, std::vector<int> &ti,
+               std::vector<double> &tv)
+{
+    const int nnz = rp[n];
+    tp.assign(n + 1, 0);
+    ti.resize(nnz);
+    tv.resize(nnz);
+    for (int k = 0; k < nnz; k++) tp[ci[k] + 1]++;
+    for (int c = 0; c < n; c++) tp[c + 1] += tp[c];
+    std::vector<int> pos(tp.begin(), tp.end() - 1);
+    for (int r = 0; r < n; r++)
+        for (int k = rp[r]; k < rp[r + 1]; k++) {
+            int p = pos[ci[k]]++;
+            ti[p] = r;
+            tv[p] = v[k];
+        }
+}
+
+}  // namespace
+
+void ilu0_left(const Csr &A, Csr &L, Csr &U)
+{
+    const int n = A.n;
+    // dependency levels on the original values (generateLevel)
+    std::vector<int> level(n, 0);
+    for (int r = 0; r < n; r++)
+        for (int k = A.rp[r]; k < A.rp[r + 1]; k++) {
+            int c = A.ci[k];
+            if (c > r && !near_zero(A.v[k]) && level[c] < level[r] + 1) level[c] = level[r] + 1;
+        }
+    std::vector<int> order(n);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return level[a] < level[b]; });
+
+    // CSC image of A (rows ascending per column)
+    std::vector<int> cp, ri;
+    std::vector<double> cv;
+    transpose(n, A.rp, A.ci, A.v, cp, ri, cv);
+
+    // left-looking column elimination, merge-based L lookup
+    for (int tgt : order) {
+        const int lb = cp[tgt], ub = cp[tgt + 1];
+        double u_diag = 0.0;
+        for (int k = lb; k < ub - 1; k++) {
+            const int cr = ri[k];
+            if (cr > tgt) break;
+            if (cr == tgt) { u_diag = cv[k]; break; }
+            // column cr: entries with row > cr are its (final) L part
+            int q = cp[cr];
+            const int qe = cp[cr + 1];
+            const double ukt = cv[k];
+            for (int p = k + 1; p < ub; p++) {
+                const int r2 = ri[p];
+                while (q < qe && ri[q] < r2) q++;
+                if (q == qe) break;
+                if (ri[q] == r2) cv[p] -= cv[q] * ukt;
+            }
+        }
+        for (int k = lb; k < ub; k++) {
+            if (ri[k] <= tgt) continue;
+            cv[k] = near_zero(u_diag) ? 0.0 : cv[k] / u_diag;
+        }
+    }
+
+    // back to CSR, split with the 1e-9 drop, unit diagonal appended LAST in L
+    std::vector<int> rp2, ci2;
+    std::vector<double> v2;
+    transpose(n, cp, ri, cv, rp2, ci2, v2);
+    L.n = U.n = n;
+    L.rp.assign(n + 1, 0);
+    U.rp.assign(n + 1, 0);
+    L.ci.clear(); L.v.clear(); U.ci.clear(); U.v.clear();
+    L.ci.reserve(rp2[n] / 2 + n); L.v.reserve(rp2[n] / 2 + n);
+    U.ci.reserve(rp2[n] / 2 + n); U.v.reserve(rp2[n] / 2 + n);
+    for (int r = 0; r < n; r++) {
+        for (int k = rp2[r]; k < rp2[r + 1]; k++) {
+            if (near_zero(v2[k])) continue;
+            if (ci2[k] < r) { L.ci.push_back(ci2[k]); L.v.push_back(v2[k]); }
+            else { U.ci.push_back(ci2[k]); U.v.push_back(v2[k]); }
+        }
+        L.ci.push_back(r);
+        L.v.push_back(1.0);
+        L.rp[r + 1] = (int)L.ci.size();
+        U.rp[r + 1] = (int)U.ci.size();
+    }
+}
+
+int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U)
+{
+    const int n = A.n;
+    // ---- symbolic (lofC): per row, L part in leftmost-pivot order, U part in
+    //      insertion order, with levels of fill
+    std::vector<std::vector<int>> Lja(n), Uja(n), ulvl(n);
+    std::vector<int> jbuf(n + 1), levls(n + 1), iw(n, -1);
+    for (int i = 0; i < n; i++) {
+        int incl = 0, incu = i;
+        for (int k = A.rp[i]; k < A.rp[i + 1]; k++) {
+            int col = A.ci[k];
+            if (col < i) { jbuf[incl] = col; levls[incl] = 0; iw[col] = incl++; }
+            else if (col > i) { jbuf[incu] = col; levls[incu] = 0; iw[col] = incu++; }
+        }
+        int jpiv = -1;
+        while (++jpiv < incl) {
+            int k = jbuf[jpiv], kmin = k, jmin = jpiv;
+            for (int j = jpiv + 1; j < incl; j++)
+                if (jbuf[j] < kmin) { kmin = jbuf[j]; jmin = j; }
+            if (jmin != jpiv) {
+                jbuf[jpiv] = kmin; jbuf[jmin] = k;
+                iw[kmin] = jpiv; iw[k] = jmin;
+                std::swap(levls[jpiv], levls[jmin]);
+                k = kmin;
+            }
+            const std::vector<int> &uk = Uja[k];
+            const std::vector<int> &lk = ulvl[k];
+            for (size_t j = 0; j < uk.size(); j++) {
+                int col = uk[j];
+                int it = lk[j] + levls[jpiv] + 1;
+                if (it > lof) continue;
+                int ip = iw[col];
+                if (ip == -1) {
+                    if (col < i) { jbuf[incl] = col; levls[incl] = it; iw[col] = incl++; }
+                    else if (col > i) { jbuf[incu] = col; levls[incu] = it; iw[col] = incu++; }
+                } else if (it < levls[ip]) {
+                    levls[ip] = it;
+                }
+            }
+        }
+        for (int j = 0; j < incl; j++) iw[jbuf[j]] = -1;
+        for (int j = i; j < incu; j++) iw[jbuf[j]] = -1;
+        Lja[i].assign(jbuf.begin(), jbuf.begin() + incl);
+        Uja[i].assign(jbuf.begin() + i, jbuf.begin() + incu);
+        ulvl[i].assign(levls.begin() + i, levls.begin() + incu);
+    }
+    for (auto &u : ulvl) std::vector<int>().swap(u);
+
+    // ---- numeric (ilukC): D kept inverted, multipliers scaled by D[jrow]
+    std::vector<std::vector<double>> Lma(n), Uma(n);
+    std::vector<double> D(n), Draw(n);
+    std::vector<int> &jw = iw;
+    for (int i = 0; i < n; i++) {
+        Lma[i].assign(Lja[i].size(), 0.0);
+        Uma[i].assign(Uja[i].size(), 0.0);
+        for (size_t j = 0; j < Lja[i].size(); j++) jw[Lja[i][j]] = (int)j;
+        jw[i] = i;
+        D[i] = 0.0;
+        for (size_t j = 0; j < Uja[i].size(); j++) jw[Uja[i][j]] = (int)j;
+        for (int k = A.rp[i]; k < A.rp[i + 1]; k++) {
+            int col = A.ci[k], jpos = jw[col];
+            if (col < i) Lma[i][jpos] = A.v[k];
+            else if (col == i) D[i] = A.v[k];
+            else Uma[i][jpos] = A.v[k];
+        }
+        for (size_t j = 0; j < Lja[i].size(); j++) {
+            int jrow = Lja[i][j];
+            Lma[i][j] *= D[jrow];
+            const double lij = Lma[i][j];
+            for (size_t k = 0; k < Uja[jrow].size(); k++) {
+                int col = Uja[jrow][k], jpos = jw[col];
+                if (jpos == -1) continue;
+                if (col < i) Lma[i][jpos] -= lij * Uma[jrow][k];
+                else if (col == i) D[i] -= lij * Uma[jrow][k];
+                else Uma[i][jpos] -= lij * Uma[jrow][k];
+            }
+        }
+        for (int c : Lja[i]) jw[c] = -1;
+        jw[i] = -1;
+        for (int c : Uja[i]) jw[c] = -1;
+        if (D[i] == 0.0) return GG_EZEROPIVOT;
+        Draw[i] = D[i];
+        D[i] = 1.0 / D[i];
+    }
+
+    // ---- emit: L strict ascending + unit diag last; U diag (un-inverted)
+    //      first + strict upper ascending
+    L.n = U.n = n;
+    L.rp.assign(n + 1, 0);
+    U.rp.assign(n + 1, 0);
+    L.ci.clear(); L.v.clear(); U.ci.clear(); U.v.clear();
+    std::vector<int> idx;
+    for (int i = 0; i < n; i++) {
+        for (size_t j = 0; j < Lja[i].size(); j++) { L.ci.push_back(Lja[i][j]); L.v.push_back(Lma[i][j]); }
+        L.ci.push_back(i);
+        L.v.push_back(1.0);
+        L.rp[i + 1] = (int)L.ci.size();
+        U.ci.push_back(i);
+        U.v.push_back(Draw[i]);
+        idx.resize(Uja[i].size());
+        std::iota(idx.begin(), idx.end(), 0);
+        std::sort(idx.begin(), idx.end(), [&](int a, int b) { return Uja[i][a] < Uja[i][b]; });
+        for (int t : idx) { U.ci.push_back(Uja[i][t]); U.v.push_back(Uma[i][t]); }
+        U.rp[i + 1] = (int)U.ci.size();
+    }
+    return 0;
+}
+
+}  // namespace gg

@@ -1,0 +1,75 @@
+// kernels.h -- launchers for the hand-written gfx950 kernels of the GMRES path.
+#pragma once
+
+#include "gg_internal.h"
+
+namespace gg {
+
+// Device-side GMRES control block (one per solver, lives in HBM).  Kernels of
+// a restart cycle read it to skip work once converged, so a whole cycle can be
+// enqueued (or replayed as a hipGraph) with a single host sync per cycle.
+struct DevState {
+    double normb, beta, resid, tol;
+    int done;       // bit flags: 1 inner-converged, 2 restart-converged, 4 converged at start
+    int conv_i;     // inner index of convergence
+    int j;          // reference iteration counter at the start of the cycle
+    int max_iter;
+    int nit;        // inner iterations allowed in this cycle = min(m, max_iter - j + 1)
+    int hist_len;   // history entries recorded before this cycle
+    int m;
+    int upd_k;      // column count - 1 used by the last Update
+    int err;        // device-side error (1 = wavefront wait timed out)
+    int pad;
+};
+constexpr int DONE_INNER = 1, DONE_RESTART = 2, DONE_INIT = 4;
+
+// A kernel is skipped when (*done & mask) != 0, or (nit && i >= *nit).
+struct Gate {
+    const int *done = nullptr;
+    int mask = 0;
+    const int *nit = nullptr;
+    int i = 0;
+};
+
+constexpr int kBlock = 256;
+constexpr unsigned long long kSentinel = 0x7FF4DEAD0000BEEFull;  // sNaN payload: "not ready"
+
+int reduce_grid(long long units);  // blocks for the vector kernels (units = Ppad/2)
+
+// ---- vector ops (lengths are Ppad, a multiple of 512) --------------------
+void launch_fill_u64(unsigned long long *p, long long n, unsigned long long v, hipStream_t st);
+void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st);  // out[i] = idx[i]<0 ? 0 : in[idx[i]]
+void launch_copy(const double *in, double *out, long long n, hipStream_t st);
+void launch_dot(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, hipStream_t st);
+
+// ---- split (PG) elementwise maps -------------------------------------------
+void launch_mul(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in*s
+void launch_div(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in/s
+void launch_gather_divsrc(Gate g, const double *in, const double *s, const int *perm, double *out, int n, hipStream_t st);  // out[i] = in[p]/s[p]
+void launch_gather_divdst(Gate g, const double *in, const double *s, const int *perm, double *out, int n, hipStream_t st);  // out[i] = in[p]/s[i]
+void launch_scatter_mul(Gate g, const double *in, const double *s, const int *perm, double *out, int n, hipStream_t st);    // out[p] = in[i]*s[i]
+
+// ---- SpMV ------------------------------------------------------------------
+// y = A x  (resid=false)  or  y = b - A x  (resid=true)
+void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, double *y, bool resid,
+                 hipStream_t st);
+
+// ---- triangular solves ---------------------------------------------------------
+void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st);
+
+// ---- GMRES scalar / MGS kernels ----------------------------------------------
+void launch_set_normb(const double *part, int G, DevState *ds, hipStream_t st);
+void launch_init_beta(const double *part, int G, DevState *ds, double *hist, hipStream_t st);
+void launch_init_cycle(DevState *ds, const double *r, double *v0, double *s, int G, long long Ppad,
+                       hipStream_t st);
+void launch_mgs_step(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
+                     const double *part_in, double *part_out, double *H, int G, long long Ppad,
+                     hipStream_t st);
+void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *part, int G,
+                             const double *w, double *vnext, double *H, double *cs, double *sn,
+                             double *s, double *hist, long long Ppad, hipStream_t st);
+void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
+                   const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st);
+void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st);
+
+}  // namespace gg

@@ -1,0 +1,902 @@
+// solver.hip -- device-resident restarted GMRES(m) for MI355X and its C ABI.
+//
+// Engines:
+//   left  : GMRES_GPU_leftILU0 / GMRES_leftILU0   src/gmres.cu:1438-1696, :566-717
+//   split : GMRESilu_GPU / GMRESilu               src/gmres.cu:2254-2446, :2069-2252
+// Differences from the reference, all deliberate:
+//   * fp64 everywhere; H, Givens, s on the device; one host sync per restart
+//     cycle instead of (i+2) blocking scalar reads per inner iteration;
+//   * Update uses the last filled column when max_iter cuts a cycle short;
+//   * lucky breakdown (H[i+1,i] == 0) does not divide by zero.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <numeric>
+
+#include "kernels.h"
+
+namespace gg {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+void DevCsr::upload(const Csr &A, hipStream_t st)
+{
+    n = A.n;
+    nnz = A.nnz();
+    rp.upload(A.rp, st);
+    ci.upload(A.ci, st);
+    v.upload(A.v, st);
+    std::vector<int> lr;
+    std::vector<int> b = spmv_blocks(A, lr);
+    nblk = (int)b.size() - 1;
+    blk.upload(b, st);
+    nlong = (int)lr.size();
+    long_rows.upload(lr, st);
+}
+
+namespace {
+
+long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
+
+// Build a device triangular solve from a canonical triangle.  WAVE2D when a
+// grid layout is active, else LEVEL (one launch per dependency level).
+void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector<long long> *nat2lay,
+               long long Ppad, hipStream_t st)
+{
+    T.lower = C.lower;
+    T.n = C.off.n;
+    const int n = C.off.n;
+    if (wl && wl->ok) {
+        T.kind = DevTri::WAVE2D;
+        T.wl = *wl;
+        std::vector<double> c1(Ppad, 0.0), c2(Ppad, 0.0), dv(Ppad, 1.0);
+        bool unit = true;
+        const int nx = wl->nx;
+        for (int r = 0; r < n; r++) {
+            const long long p = (*nat2lay)[r];
+            for (int k = C.off.rp[r]; k < C.off.rp[r + 1]; k++) {
+                const int off = std::abs(C.off.ci[k] - r);
+                (off == nx ? c1 : c2)[p] = C.off.v[k];
+            }
+            dv[p] = C.d[r];
+            if (C.d[r] != 1.0) unit = false;
+        }
+        T.unit = unit;
+        T.c1.upload(c1, st);
+        T.c2.upload(c2, st);
+        if (!unit) T.dw.upload(dv, st);
+        const long long stride = round_up(nx, 16);
+        T.bnd.alloc((size_t)wl->nbands * stride);
+        launch_fill_u64(T.bnd.p, (long long)wl->nbands * stride, kSentinel, st);
+        // algorithmic bytes: b, two coefficients, (divisor), x  per grid point
+        T.bytes = (double)n * (8.0 * (unit ? 4 : 5));
+    } else {
+        T.kind = DevTri::LEVEL;
+        T.off.upload(C.off, st);
+        T.d.upload(C.d, st);
+        Levels lv = level_sets(C);
+        T.lev_ptr = lv.ptr;
+        T.lev_rows.upload(lv.rows, st);
+        T.bytes = 12.0 * C.off.nnz() + 4.0 * (n + 1) + 24.0 * n;
+    }
+}
+
+}  // namespace
+
+}  // namespace gg
+
+using namespace gg;
+
+struct gg_solver {
+    int device = 0;
+    hipStream_t st = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+    Csr A;
+    bool have_A = false;
+    int pkind = -1;       // -1: not set
+
+    // vector space (natural or wavefront layout)
+    bool wave = false;
+    Wave2D wl;
+    long long P = 0, Ppad = 0;
+    std::vector<long long> nat2lay_h;
+    DBuf<long long> lay2nat, nat2lay;
+    int G = 1;
+
+    DevCsr dA;
+    DevTri L, U;
+    // split (PG) extras, natural layout
+    DBuf<double> middle, lscale, rscale;
+    DBuf<int> prow, pcol;
+    DevCsr dUfull;
+
+    // workspace
+    int m_alloc = -1;
+    DBuf<double> V, w, ww, r, rr, bb, t1, t2, z, xv, bv, y;
+    DBuf<double> partA, partB, H, s, cs, sn, ysm;
+    DBuf<double> hist;
+    long long hist_cap = 0;
+    DBuf<DevState> ds;
+    DBuf<int> err;
+    DBuf<double> nat_in, nat_out;   // staging for host-vector entry points
+    std::vector<double> last_hist;
+
+    // in-solve kernel timing (gg_profile_*)
+    bool prof_on = false;
+    std::vector<hipEvent_t> prof_pool;
+    size_t prof_used = 0;
+    struct Mark { int kind, i, e0, e1; };
+    std::vector<Mark> marks;
+    double prof_ms[GG_PROF_NKINDS] = {0, 0, 0};
+    long long prof_cnt[GG_PROF_NKINDS] = {0, 0, 0};
+};
+
+namespace {
+
+int fail(const Error &e)
+{
+    set_error(e.msg);
+    return e.code;
+}
+
+#define GG_API_BEGIN try {
+#define GG_API_END                                                   \
+    }                                                                \
+    catch (const gg::Error &e) { return fail(e); }                   \
+    catch (const std::bad_alloc &) { return fail({GG_ENOMEM, "host allocation failed"}); } \
+    catch (const std::exception &e) { return fail({GG_EINVAL, e.what()}); }
+
+void check_csr(int n, const int *rp, const int *ci, const double *v, const char *what)
+{
+    GG_REQUIRE(n >= 0, GG_EINVAL, std::string(what) + ": negative n");
+    GG_REQUIRE(rp && (n == 0 || (ci && v) || rp[n] == 0), GG_EINVAL, std::string(what) + ": null array");
+    GG_REQUIRE(rp[0] == 0, GG_EINVAL, std::string(what) + ": row_ptr[0] != 0");
+    for (int r = 0; r < n; r++) {
+        GG_REQUIRE(rp[r + 1] >= rp[r], GG_EINVAL, std::string(what) + ": row_ptr not monotone");
+        for (int k = rp[r]; k < rp[r + 1]; k++)
+            GG_REQUIRE(ci[k] >= 0 && ci[k] < n, GG_EINVAL,
+                       std::string(what) + ": column index out of range at row " + std::to_string(r));
+    }
+}
+
+Csr make_csr(int n, const int *rp, const int *ci, const double *v)
+{
+    Csr C;
+    C.n = n;
+    C.rp.assign(rp, rp + n + 1);
+    C.ci.assign(ci, ci + rp[n]);
+    C.v.assign(v, v + rp[n]);
+    return C;
+}
+
+void set_device(gg_solver *s) { GG_HIP(hipSetDevice(s->device)); }
+
+// choose the vector space and upload A in it
+void setup_space(gg_solver *s, const Wave2D *wl)
+{
+    const int n = s->A.n;
+    s->wave = wl && wl->ok;
+    if (s->wave) {
+        s->wl = *wl;
+        s->P = wl->P;
+    } else {
+        s->wl = Wave2D{};
+        s->P = n;
+    }
+    s->Ppad = round_up(std::max<long long>(s->P, 1), 512);
+    s->nat2lay_h.resize(n);
+    std::vector<long long> l2n(s->Ppad, -1);
+    for (int r = 0; r < n; r++) {
+        long long p = s->wave ? wl->slot(r) : r;
+        s->nat2lay_h[r] = p;
+        l2n[p] = r;
+    }
+    s->lay2nat.upload(l2n, s->st);
+    s->nat2lay.upload(s->nat2lay_h, s->st);
+    s->G = reduce_grid(s->Ppad / 2);
+    // A in layout space: row p = A row nat(p), columns remapped, entry order kept
+    if (!s->wave) {
+        Csr Ap = s->A;
+        Ap.n = (int)s->P;
+        s->dA.upload(Ap, s->st);
+    } else {
+        Csr Ap;
+        Ap.n = (int)s->P;
+        Ap.rp.assign(s->P + 1, 0);
+        for (long long p = 0; p < s->P; p++) {
+            long long r = l2n[p];
+            Ap.rp[p + 1] = Ap.rp[p] + (r >= 0 ? s->A.rp[r + 1] - s->A.rp[r] : 0);
+        }
+        Ap.ci.resize(s->A.nnz());
+        Ap.v.resize(s->A.nnz());
+        for (long long p = 0; p < s->P; p++) {
+            long long r = l2n[p];
+            if (r < 0) continue;
+            int o = Ap.rp[p];
+            for (int k = s->A.rp[r]; k < s->A.rp[r + 1]; k++, o++) {
+                Ap.ci[o] = (int)s->nat2lay_h[s->A.ci[k]];
+                Ap.v[o] = s->A.v[k];
+            }
+        }
+        s->dA.upload(Ap, s->st);
+    }
+    s->m_alloc = -1;   // workspace follows the space
+}
+
+void ensure_workspace(gg_solver *s, int m)
+{
+    if (s->m_alloc == m) return;
+    const long long P = s->Ppad;
+    s->V.alloc((size_t)(m + 1) * P);
+    GG_HIP(hipMemsetAsync(s->V.p, 0, (size_t)(m + 1) * P * sizeof(double), s->st));
+    for (DBuf<double> *b : {&s->w, &s->ww, &s->r, &s->rr, &s->bb, &s->t1, &s->t2, &s->z, &s->xv,
+                            &s->bv, &s->y}) {
+        b->alloc(P);
+        GG_HIP(hipMemsetAsync(b->p, 0, P * sizeof(double), s->st));
+    }
+    s->partA.alloc(1024);
+    s->partB.alloc(1024);
+    s->H.alloc((size_t)(m + 1) * m);
+    GG_HIP(hipMemsetAsync(s->H.p, 0, (size_t)(m + 1) * m * sizeof(double), s->st));
+    s->s.alloc(m + 1);
+    s->cs.alloc(m + 1);
+    s->sn.alloc(m + 1);
+    s->ysm.alloc(m + 1);
+    if (!s->ds.p) s->ds.alloc(1);
+    if (!s->err.p) s->err.alloc(1);
+    s->m_alloc = m;
+}
+
+// ---- preconditioner operators (enqueue only; graph-capturable) ----------
+void apply_minv(gg_solver *s, Gate g, const double *in, double *out)
+{
+    if (s->pkind == GG_PRECOND_NONE) {
+        Gate g2 = g;
+        (void)g2;
+        launch_copy(in, out, s->Ppad, s->st);   // copy is not gated: harmless
+        return;
+    }
+    launch_trsv(g, s->L, in, s->t1.p, s->err.p, s->st);
+    launch_trsv(g, s->U, s->t1.p, out, s->err.p, s->st);
+}
+// split: Ml(v) = L^-1 P_r D_l^-1 v   (DevPrecond_left, src/preconditioner.cu:1592-1626)
+void apply_left(gg_solver *s, Gate g, const double *in, double *out)
+{
+    const int n = s->A.n;
+    launch_gather_divsrc(g, in, s->lscale.p, s->prow.p, s->t1.p, n, s->st);
+    launch_trsv(g, s->L, s->t1.p, out, s->err.p, s->st);
+}
+// split: Mr(v) = D_r^-1 P_c U^-1 M v   (DevPrecond_right, :1629-1657)
+void apply_right(gg_solver *s, Gate g, const double *in, double *out)
+{
+    const int n = s->A.n;
+    launch_mul(g, in, s->middle.p, s->t1.p, n, s->st);
+    launch_trsv(g, s->U, s->t1.p, s->t2.p, s->err.p, s->st);
+    launch_gather_divdst(g, s->t2.p, s->rscale.p, s->pcol.p, out, n, s->st);
+}
+// split: Mr^-1(x) = M^-1 U P_c^-1 D_r x   (DevPrecond_starting_value, :1561-1589)
+void apply_start(gg_solver *s, Gate g, const double *in, double *out)
+{
+    const int n = s->A.n;
+    launch_scatter_mul(g, in, s->rscale.p, s->pcol.p, s->t1.p, n, s->st);
+    launch_spmv(g, s->dUfull, s->t1.p, nullptr, s->t2.p, false, s->st);
+    launch_div(g, s->t2.p, s->middle.p, out, n, s->st);
+}
+void apply_rhs(gg_solver *s, Gate g, const double *in, double *out)
+{
+    if (s->pkind == GG_PRECOND_SPLIT) apply_left(s, g, in, out);
+    else apply_minv(s, g, in, out);
+}
+
+// ---- in-solve profiling ---------------------------------------------------------
+int prof_event(gg_solver *s)
+{
+    if (s->prof_used == s->prof_pool.size()) {
+        hipEvent_t e;
+        GG_HIP(hipEventCreate(&e));
+        s->prof_pool.push_back(e);
+    }
+    GG_HIP(hipEventRecord(s->prof_pool[s->prof_used], s->st));
+    return (int)s->prof_used++;
+}
+void prof_begin(gg_solver *s, int kind, int i)
+{
+    if (!s->prof_on) return;
+    s->marks.push_back({kind, i, prof_event(s), -1});
+}
+void prof_end(gg_solver *s)
+{
+    if (!s->prof_on) return;
+    s->marks.back().e1 = prof_event(s);
+}
+// after a cycle has completed: account marks of iterations that really ran
+void prof_collect(gg_solver *s, int executed)
+{
+    if (!s->prof_on) return;
+    for (const auto &mk : s->marks) {
+        if (mk.i >= executed || mk.e1 < 0) continue;
+        float ms = 0.f;
+        GG_HIP(hipEventElapsedTime(&ms, s->prof_pool[mk.e0], s->prof_pool[mk.e1]));
+        s->prof_ms[mk.kind] += ms;
+        s->prof_cnt[mk.kind]++;
+    }
+    s->marks.clear();
+    s->prof_used = 0;
+}
+
+// ---- GMRES phases ------------------------------------------------------------
+void enqueue_init(gg_solver *s)
+{
+    Gate none;
+    DevState *ds = s->ds.p;
+    const bool split = s->pkind == GG_PRECOND_SPLIT;
+    apply_rhs(s, none, s->bv.p, s->bb.p);                                     // bb = M b
+    launch_dot(none, s->bb.p, s->bb.p, s->partA.p, s->G, s->Ppad, s->st);
+    launch_set_normb(s->partA.p, s->G, ds, s->st);
+    if (split) apply_start(s, none, s->xv.p, s->y.p);                          // y = Mr^-1 x0
+    launch_spmv(none, s->dA, s->xv.p, s->bv.p, s->rr.p, true, s->st);         // rr = b - A x
+    apply_rhs(s, none, s->rr.p, s->r.p);                                      // r = M rr
+    launch_dot(none, s->r.p, s->r.p, s->partA.p, s->G, s->Ppad, s->st);
+    launch_init_beta(s->partA.p, s->G, ds, s->hist.p, s->st);
+}
+
+void enqueue_cycle(gg_solver *s, int m)
+{
+    DevState *ds = s->ds.p;
+    const long long P = s->Ppad;
+    const bool split = s->pkind == GG_PRECOND_SPLIT;
+    launch_init_cycle(ds, s->r.p, s->V.p, s->s.p, s->G, P, s->st);
+    for (int i = 0; i < m; i++) {
+        Gate gi;
+        gi.done = &ds->done;
+        gi.mask = ~0;
+        gi.nit = &ds->nit;
+        gi.i = i;
+        double *vi = s->V.p + (long long)i * P;
+        if (!split) {
+            prof_begin(s, GG_PROF_SPMV, i);
+            launch_spmv(gi, s->dA, vi, nullptr, s->ww.p, false, s->st);        // ww = A v_i
+            prof_end(s);
+            prof_begin(s, GG_PROF_PRECOND, i);
+            apply_minv(s, gi, s->ww.p, s->w.p);                                // w = M^-1 ww
+            prof_end(s);
+        } else {
+            apply_right(s, gi, vi, s->z.p);                                    // z = Mr v_i
+            prof_begin(s, GG_PROF_SPMV, i);
+            launch_spmv(gi, s->dA, s->z.p, nullptr, s->ww.p, false, s->st);    // ww = A z
+            prof_end(s);
+            prof_begin(s, GG_PROF_PRECOND, i);
+            apply_left(s, gi, s->ww.p, s->w.p);                                // w = Ml ww
+            prof_end(s);
+        }
+        prof_begin(s, GG_PROF_MGS, i);
+        double *pin = s->partA.p, *pout = s->partB.p;
+        launch_dot(gi, s->w.p, s->V.p, pin, s->G, P, s->st);                   // <w, v_0>
+        for (int k = 0; k <= i; k++) {
+            const double *vk = s->V.p + (long long)k * P;
+            const double *vn = (k < i) ? s->V.p + (long long)(k + 1) * P : s->w.p;
+            launch_mgs_step(gi, i, k, m, s->w.p, vk, vn, pin, pout, s->H.p, s->G, P, s->st);
+            std::swap(pin, pout);
+        }
+        launch_arnoldi_finalize(gi, i, m, ds, pin, s->G, s->w.p, s->V.p + (long long)(i + 1) * P,
+                                s->H.p, s->cs.p, s->sn.p, s->s.p, s->hist.p, P, s->st);
+        prof_end(s);
+    }
+    Gate gu;
+    gu.done = &ds->done;
+    gu.mask = DONE_RESTART | DONE_INIT;
+    launch_update(gu, m, ds, s->H.p, s->s.p, s->ysm.p, s->V.p, P, split ? s->y.p : s->xv.p, s->G, P,
+                  s->st);
+    if (split) apply_right(s, gu, s->y.p, s->xv.p);                            // x = Mr y
+    Gate gr;
+    gr.done = &ds->done;
+    gr.mask = ~0;
+    launch_spmv(gr, s->dA, s->xv.p, s->bv.p, s->rr.p, true, s->st);           // rr = b - A x
+    apply_rhs(s, gr, s->rr.p, s->r.p);
+    launch_dot(gr, s->r.p, s->r.p, s->partA.p, s->G, P, s->st);
+    launch_end_cycle(s->partA.p, s->G, ds, s->hist.p, s->st);
+}
+
+DevState read_state(gg_solver *s)
+{
+    DevState h;
+    GG_HIP(hipMemcpyAsync(&h, s->ds.p, sizeof(DevState), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
+    return h;
+}
+
+int solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
+                 gg_result *res)
+{
+    GG_REQUIRE(s->have_A, GG_ESTATE, "gg_solve: no matrix (call gg_set_matrix)");
+    GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "gg_solve: no preconditioner (call gg_set_precond_*)");
+    GG_REQUIRE(opt, GG_EINVAL, "gg_solve: null options");
+    const int m = opt->restart;
+    GG_REQUIRE(m >= 1 && m <= 512, GG_EINVAL, "gg_solve: restart must be in [1, 512]");
+    GG_REQUIRE(opt->max_iter >= 0, GG_EINVAL, "gg_solve: negative max_iter");
+    const int n = s->A.n;
+    set_device(s);
+    ensure_workspace(s, m);
+    const long long need = (long long)opt->max_iter + opt->max_iter / m + 4;
+    if (need > s->hist_cap) {
+        s->hist.alloc(need);
+        s->hist_cap = need;
+    }
+    // inputs into the solver's vector space
+    launch_gather(d_b, s->lay2nat.p, s->bv.p, s->Ppad, s->st);
+    launch_gather(d_x, s->lay2nat.p, s->xv.p, s->Ppad, s->st);
+    if (s->pkind == GG_PRECOND_SPLIT)
+        GG_HIP(hipMemsetAsync(s->y.p, 0, s->Ppad * sizeof(double), s->st));
+    for (DevTri *T : {&s->L, &s->U})
+        if (T->kind == DevTri::WAVE2D)
+            launch_fill_u64(T->bnd.p, (long long)T->wl.nbands * round_up(T->wl.nx, 16), kSentinel,
+                            s->st);
+    DevState h{};
+    h.tol = opt->tol;
+    h.max_iter = opt->max_iter;
+    h.m = m;
+    h.j = 1;
+    GG_HIP(hipMemcpyAsync(s->ds.p, &h, sizeof(DevState), hipMemcpyHostToDevice, s->st));
+    GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
+
+    GG_HIP(hipEventRecord(s->ev0, s->st));
+    enqueue_init(s);
+    h = read_state(s);
+    int ret = 1, iters = 0, inner = 0, restarts = 0;
+    long long hist_len = 1;
+    double relres = h.resid;
+    if (h.done & DONE_INIT) {
+        ret = 0;
+        iters = 0;
+    } else {
+        while (true) {
+            if (h.j > opt->max_iter) {   // while (j <= *max_iter) exhausted
+                ret = 1;
+                relres = h.resid;
+                iters = opt->max_iter;   // the reference leaves *max_iter untouched
+                hist_len = h.hist_len;
+                break;
+            }
+            restarts++;
+            enqueue_cycle(s, m);
+            DevState prev = h;
+            h = read_state(s);
+            int err = 0;
+            GG_HIP(hipMemcpy(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost));
+            GG_REQUIRE(err == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+            prof_collect(s, (h.done & DONE_INNER) ? h.conv_i + 1 : h.nit);
+            if (h.done & DONE_INNER) {
+                ret = 0;
+                iters = prev.j + h.conv_i;
+                inner += h.conv_i + 1;
+                relres = h.resid;
+                hist_len = h.hist_len + h.conv_i + 1;
+                break;
+            }
+            inner += h.nit;
+            if (h.done & DONE_RESTART) {
+                ret = 0;
+                iters = h.j;
+                relres = h.resid;
+                hist_len = h.hist_len;
+                break;
+            }
+            hist_len = h.hist_len;
+            relres = h.resid;
+        }
+    }
+    GG_HIP(hipEventRecord(s->ev1, s->st));
+    launch_gather(s->xv.p, s->nat2lay.p, d_x, n, s->st);
+    GG_HIP(hipStreamSynchronize(s->st));
+    float ms = 0.f;
+    GG_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_hist.resize(hist_len);
+    if (hist_len)
+        GG_HIP(hipMemcpy(s->last_hist.data(), s->hist.p, hist_len * sizeof(double),
+                         hipMemcpyDeviceToHost));
+    if (res) {
+        res->status = ret;
+        res->iters = iters;
+        res->inner_iters = inner;
+        res->restarts = restarts;
+        res->relres = relres;
+        res->solve_ms = ms;
+    }
+    return ret;
+}
+
+void stage_in(gg_solver *s, const double *h, DBuf<double> &d)
+{
+    const int n = s->A.n;
+    if (d.n < (size_t)std::max(n, 1)) d.alloc(std::max(n, 1));
+    if (n) GG_HIP(hipMemcpyAsync(d.p, h, n * sizeof(double), hipMemcpyHostToDevice, s->st));
+}
+void stage_out(gg_solver *s, const DBuf<double> &d, double *h)
+{
+    const int n = s->A.n;
+    if (n) GG_HIP(hipMemcpyAsync(h, d.p, n * sizeof(double), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
+}
+
+}  // namespace
+
+// ======================================================================= C ABI
+extern "C" {
+
+int gg_abi_version(void) { return GG_ABI_VERSION; }
+
+const char *gg_strerror(int status)
+{
+    switch (status) {
+    case GG_OK: return "converged";
+    case GG_NOT_CONVERGED: return "not converged";
+    case GG_EINVAL: return "invalid argument";
+    case GG_EHIP: return "HIP runtime error";
+    case GG_EZEROPIVOT: return "zero pivot in factorization";
+    case GG_ENOMEM: return "out of memory";
+    case GG_ESTATE: return "invalid call order";
+    case GG_ETIMEOUT: return "device wait timed out";
+    case GG_ECOMM: return "communication error";
+    default: return "unknown status";
+    }
+}
+
+const char *gg_last_error(void) { return g_last_error.c_str(); }
+
+int gg_device_count(int *count)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(count, GG_EINVAL, "null count");
+    int c = 0;
+    GG_HIP(hipGetDeviceCount(&c));
+    *count = c;
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_create(int device, gg_solver **out)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(out, GG_EINVAL, "null out");
+    std::unique_ptr<gg_solver> s(new gg_solver());
+    s->device = device;
+    set_device(s.get());
+    GG_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+    GG_HIP(hipEventCreate(&s->ev0));
+    GG_HIP(hipEventCreate(&s->ev1));
+    *out = s.release();
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_destroy(gg_solver *s)
+{
+    if (!s) return GG_OK;
+    (void)hipSetDevice(s->device);
+    if (s->st) (void)hipStreamSynchronize(s->st);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    for (hipEvent_t e : s->prof_pool) (void)hipEventDestroy(e);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    hipStream_t st = s->st;
+    delete s;
+    if (st) (void)hipStreamDestroy(st);
+    return GG_OK;
+}
+
+int gg_set_matrix(gg_solver *s, int n, const int *row_ptr, const int *col_idx, const double *val)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s, GG_EINVAL, "null solver");
+    check_csr(n, row_ptr, col_idx, val, "A");
+    set_device(s);
+    s->A = make_csr(n, row_ptr, col_idx, val);
+    s->have_A = true;
+    s->pkind = -1;
+    s->L.kind = s->U.kind = DevTri::NONE;
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_set_precond_none(gg_solver *s)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "set_precond before set_matrix");
+    set_device(s);
+    setup_space(s, nullptr);
+    s->L.kind = s->U.kind = DevTri::NONE;
+    s->pkind = GG_PRECOND_NONE;
+    GG_HIP(hipStreamSynchronize(s->st));
+    return GG_OK;
+    GG_API_END
+}
+
+static void setup_left(gg_solver *s, const Csr &Lf, const Csr &Uf, int kind)
+{
+    CanonTri cl = canon_lower_unit(Lf);
+    CanonTri cu = canon_upper_ignorezero(Uf);
+    Wave2D wl;
+    const char *env = std::getenv("GG_NO_WAVEFRONT");
+    if (!(env && env[0] == '1')) wl = detect_wave2d(cl, cu);
+    if (wl.ok && wl.nbands > 512) wl.ok = false;   // every band must be co-resident
+    setup_space(s, &wl);
+    build_tri(s->L, cl, &wl, &s->nat2lay_h, s->Ppad, s->st);
+    build_tri(s->U, cu, &wl, &s->nat2lay_h, s->Ppad, s->st);
+    s->pkind = kind;
+    GG_HIP(hipStreamSynchronize(s->st));
+}
+
+int gg_set_precond_ilu0(gg_solver *s)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "set_precond before set_matrix");
+    set_device(s);
+    Csr Lf, Uf;
+    ilu0_left(s->A, Lf, Uf);
+    setup_left(s, Lf, Uf, GG_PRECOND_ILU0);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_set_precond_iluk(gg_solver *s, int level)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "set_precond before set_matrix");
+    GG_REQUIRE(level >= 0, GG_EINVAL, "ILU(k): negative level");
+    set_device(s);
+    Csr Lf, Uf;
+    int rc = iluk_itsol(s->A, level, Lf, Uf);
+    GG_REQUIRE(rc == 0, GG_EZEROPIVOT, "ILU(k): zero pivot (src/iluk.cpp:175-185)");
+    setup_left(s, Lf, Uf, GG_PRECOND_ILUK);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_set_precond_lu(gg_solver *s, const int *l_rp, const int *l_ci, const double *l_v,
+                      const int *u_rp, const int *u_ci, const double *u_v)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "set_precond before set_matrix");
+    const int n = s->A.n;
+    check_csr(n, l_rp, l_ci, l_v, "L");
+    check_csr(n, u_rp, u_ci, u_v, "U");
+    set_device(s);
+    setup_left(s, make_csr(n, l_rp, l_ci, l_v), make_csr(n, u_rp, u_ci, u_v), GG_PRECOND_LU);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const double *l_v,
+                         const int *u_rp, const int *u_ci, const double *u_v, const double *middle,
+                         const int *perm_row, const int *perm_col, const double *lscale,
+                         const double *rscale)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "set_precond before set_matrix");
+    const int n = s->A.n;
+    check_csr(n, l_rp, l_ci, l_v, "L");
+    check_csr(n, u_rp, u_ci, u_v, "U");
+    GG_REQUIRE(middle && perm_row && perm_col && lscale && rscale, GG_EINVAL, "split: null vector");
+    for (int i = 0; i < n; i++)
+        GG_REQUIRE(perm_row[i] >= 0 && perm_row[i] < n && perm_col[i] >= 0 && perm_col[i] < n,
+                   GG_EINVAL, "split: permutation index out of range");
+    set_device(s);
+    Csr Lf = make_csr(n, l_rp, l_ci, l_v), Uf = make_csr(n, u_rp, u_ci, u_v);
+    CanonTri cl = canon_lower_lastdiag(Lf);
+    CanonTri cu = canon_upper_firstdiag(Uf);
+    setup_space(s, nullptr);
+    build_tri(s->L, cl, nullptr, &s->nat2lay_h, s->Ppad, s->st);
+    build_tri(s->U, cu, nullptr, &s->nat2lay_h, s->Ppad, s->st);
+    s->middle.upload(middle, n, s->st);
+    s->lscale.upload(lscale, n, s->st);
+    s->rscale.upload(rscale, n, s->st);
+    s->prow.upload(perm_row, n, s->st);
+    s->pcol.upload(perm_col, n, s->st);
+    s->dUfull.upload(Uf, s->st);
+    s->pkind = GG_PRECOND_SPLIT;
+    GG_HIP(hipStreamSynchronize(s->st));
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_precond_kind(gg_solver *s) { return s ? s->pkind : GG_EINVAL; }
+int gg_uses_wavefront(gg_solver *s) { return (s && s->wave) ? 1 : 0; }
+
+int gg_solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
+                    gg_result *res)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s, GG_EINVAL, "null solver");
+    return solve_device(s, d_b, d_x, opt, res);
+    GG_API_END
+}
+
+int gg_solve(gg_solver *s, const double *b, double *x, const gg_options *opt, gg_result *res)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && b && x, GG_EINVAL, "null argument");
+    GG_REQUIRE(s->have_A, GG_ESTATE, "gg_solve: no matrix");
+    set_device(s);
+    stage_in(s, b, s->nat_in);
+    stage_in(s, x, s->nat_out);
+    int rc = solve_device(s, s->nat_in.p, s->nat_out.p, opt, res);
+    stage_out(s, s->nat_out, x);
+    return rc;
+    GG_API_END
+}
+
+int gg_get_history(gg_solver *s, double *out, int cap)
+{
+    if (!s) return GG_EINVAL;
+    int len = (int)s->last_hist.size();
+    if (out && cap > 0) std::memcpy(out, s->last_hist.data(), sizeof(double) * std::min(len, cap));
+    return len;
+}
+
+int gg_spmv(gg_solver *s, const double *x, double *y)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && x && y, GG_EINVAL, "null argument");
+    GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "gg_spmv: call gg_set_precond_* first (fixes the layout)");
+    set_device(s);
+    ensure_workspace(s, std::max(s->m_alloc, 1));
+    stage_in(s, x, s->nat_in);
+    launch_gather(s->nat_in.p, s->lay2nat.p, s->xv.p, s->Ppad, s->st);
+    launch_spmv(Gate{}, s->dA, s->xv.p, nullptr, s->ww.p, false, s->st);
+    if (s->nat_out.n < (size_t)std::max(s->A.n, 1)) s->nat_out.alloc(std::max(s->A.n, 1));
+    launch_gather(s->ww.p, s->nat2lay.p, s->nat_out.p, s->A.n, s->st);
+    stage_out(s, s->nat_out, y);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_precond_apply(gg_solver *s, int op, const double *in, double *out)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && in && out, GG_EINVAL, "null argument");
+    GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner");
+    const bool split = s->pkind == GG_PRECOND_SPLIT;
+    GG_REQUIRE(split ? (op >= GG_APPLY_LEFT && op <= GG_APPLY_START) : op == GG_APPLY_MINV, GG_EINVAL,
+               "operator not defined for this preconditioner");
+    set_device(s);
+    ensure_workspace(s, std::max(s->m_alloc, 1));
+    for (DevTri *T : {&s->L, &s->U})
+        if (T->kind == DevTri::WAVE2D)
+            launch_fill_u64(T->bnd.p, (long long)T->wl.nbands * round_up(T->wl.nx, 16), kSentinel,
+                            s->st);
+    GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
+    stage_in(s, in, s->nat_in);
+    launch_gather(s->nat_in.p, s->lay2nat.p, s->xv.p, s->Ppad, s->st);
+    Gate none;
+    switch (op) {
+    case GG_APPLY_MINV: apply_minv(s, none, s->xv.p, s->ww.p); break;
+    case GG_APPLY_LEFT: apply_left(s, none, s->xv.p, s->ww.p); break;
+    case GG_APPLY_RIGHT: apply_right(s, none, s->xv.p, s->ww.p); break;
+    case GG_APPLY_START: apply_start(s, none, s->xv.p, s->ww.p); break;
+    }
+    if (s->nat_out.n < (size_t)std::max(s->A.n, 1)) s->nat_out.alloc(std::max(s->A.n, 1));
+    launch_gather(s->ww.p, s->nat2lay.p, s->nat_out.p, s->A.n, s->st);
+    stage_out(s, s->nat_out, out);
+    int err = 0;
+    GG_HIP(hipMemcpy(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost));
+    GG_REQUIRE(err == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_time_spmv(gg_solver *s, int reps, int nrot, double *avg_ms)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && avg_ms && reps > 0 && nrot > 0, GG_EINVAL, "bad argument");
+    GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner / layout");
+    set_device(s);
+    // nrot independent copies of (A, x, y) so repeats are not served on-die
+    std::vector<std::unique_ptr<DevCsr>> As;
+    std::vector<std::unique_ptr<DBuf<double>>> xs, ys;
+    for (int k = 0; k < nrot; k++) {
+        auto A = std::make_unique<DevCsr>();
+        DevCsr &src = s->dA;
+        A->n = src.n; A->nnz = src.nnz; A->nblk = src.nblk; A->nlong = src.nlong;
+        A->rp.alloc(src.rp.n); A->ci.alloc(src.ci.n); A->v.alloc(src.v.n); A->blk.alloc(src.blk.n);
+        GG_HIP(hipMemcpyAsync(A->rp.p, src.rp.p, src.rp.n * 4, hipMemcpyDeviceToDevice, s->st));
+        GG_HIP(hipMemcpyAsync(A->ci.p, src.ci.p, src.ci.n * 4, hipMemcpyDeviceToDevice, s->st));
+        GG_HIP(hipMemcpyAsync(A->v.p, src.v.p, src.v.n * 8, hipMemcpyDeviceToDevice, s->st));
+        GG_HIP(hipMemcpyAsync(A->blk.p, src.blk.p, src.blk.n * 4, hipMemcpyDeviceToDevice, s->st));
+        As.push_back(std::move(A));
+        auto x = std::make_unique<DBuf<double>>();
+        auto y = std::make_unique<DBuf<double>>();
+        x->alloc(s->Ppad);
+        y->alloc(s->Ppad);
+        std::vector<double> h(s->Ppad, 1.0);
+        GG_HIP(hipMemcpyAsync(x->p, h.data(), s->Ppad * 8, hipMemcpyHostToDevice, s->st));
+        GG_HIP(hipStreamSynchronize(s->st));
+        xs.push_back(std::move(x));
+        ys.push_back(std::move(y));
+    }
+    for (int k = 0; k < nrot; k++)   // warm-up
+        launch_spmv(Gate{}, *As[k], xs[k]->p, nullptr, ys[k]->p, false, s->st);
+    GG_HIP(hipEventRecord(s->ev0, s->st));
+    for (int r = 0; r < reps; r++) {
+        int k = r % nrot;
+        launch_spmv(Gate{}, *As[k], xs[k]->p, nullptr, ys[k]->p, false, s->st);
+    }
+    GG_HIP(hipEventRecord(s->ev1, s->st));
+    GG_HIP(hipEventSynchronize(s->ev1));
+    float ms = 0.f;
+    GG_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    *avg_ms = ms / reps;
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_time_precond(gg_solver *s, int reps, double *avg_ms)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && avg_ms && reps > 0, GG_EINVAL, "bad argument");
+    GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner");
+    set_device(s);
+    ensure_workspace(s, std::max(s->m_alloc, 1));
+    GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
+    Gate none;
+    auto once = [&]() {
+        if (s->pkind == GG_PRECOND_SPLIT) apply_left(s, none, s->bv.p, s->ww.p);
+        else apply_minv(s, none, s->bv.p, s->ww.p);
+    };
+    once();
+    GG_HIP(hipEventRecord(s->ev0, s->st));
+    for (int r = 0; r < reps; r++) once();
+    GG_HIP(hipEventRecord(s->ev1, s->st));
+    GG_HIP(hipEventSynchronize(s->ev1));
+    float ms = 0.f;
+    GG_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    *avg_ms = ms / reps;
+    int err = 0;
+    GG_HIP(hipMemcpy(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost));
+    GG_REQUIRE(err == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_profile_enable(gg_solver *s, int on)
+{
+    if (!s) return GG_EINVAL;
+    s->prof_on = on != 0;
+    return GG_OK;
+}
+
+int gg_profile_reset(gg_solver *s)
+{
+    if (!s) return GG_EINVAL;
+    for (int k = 0; k < GG_PROF_NKINDS; k++) {
+        s->prof_ms[k] = 0;
+        s->prof_cnt[k] = 0;
+    }
+    return GG_OK;
+}
+
+int gg_profile_get(gg_solver *s, int kind, int *launches, double *total_ms)
+{
+    if (!s || kind < 0 || kind >= GG_PROF_NKINDS) return GG_EINVAL;
+    if (launches) *launches = (int)s->prof_cnt[kind];
+    if (total_ms) *total_ms = s->prof_ms[kind];
+    return GG_OK;
+}
+
+double gg_bytes_spmv(gg_solver *s)
+{
+    if (!s || !s->have_A) return 0.0;
+    const double n = s->A.n, nnz = s->A.nnz();
+    return 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;   // SURVEY.md 8(d) B_spmv
+}
+
+double gg_bytes_precond(gg_solver *s)
+{
+    if (!s || s->pkind < 0) return 0.0;
+    return s->L.bytes + s->U.bytes;
+}
+
+}  // extern "C"

@@ -1,0 +1,233 @@
+"""ggmres -- Python binding of libggmres.so (the MI355X GMRES solver C ABI).
+
+Thin ctypes layer over include/ggmres.h: every call goes through the C ABI
+into the hand-written HIP kernels.  There is no CPU fallback: if the built
+library is missing, importing the solver raises.  The CPU restatement used to
+check results lives in oracle/ and is test infrastructure only.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libggmres.so")
+
+GG_OK, GG_NOT_CONVERGED = 0, 1
+PRECOND_NONE, PRECOND_ILU0, PRECOND_ILUK, PRECOND_LU, PRECOND_SPLIT = range(5)
+APPLY_MINV, APPLY_LEFT, APPLY_RIGHT, APPLY_START = range(4)
+FLAG_NO_GRAPH, FLAG_NO_WAVEFRONT = 0x1, 0x2
+
+# every symbol include/ggmres.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "gg_abi_version", "gg_strerror", "gg_last_error", "gg_device_count", "gg_create",
+    "gg_destroy", "gg_set_matrix", "gg_set_precond_none", "gg_set_precond_ilu0",
+    "gg_set_precond_iluk", "gg_set_precond_lu", "gg_set_precond_split", "gg_precond_kind",
+    "gg_uses_wavefront", "gg_solve", "gg_solve_device", "gg_get_history", "gg_spmv",
+    "gg_precond_apply", "gg_time_spmv", "gg_time_precond", "gg_bytes_spmv",
+    "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
+]
+PROF_SPMV, PROF_PRECOND, PROF_MGS = range(3)
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("restart", ctypes.c_int), ("max_iter", ctypes.c_int),
+                ("tol", ctypes.c_double), ("flags", ctypes.c_int)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int), ("iters", ctypes.c_int),
+                ("inner_iters", ctypes.c_int), ("restarts", ctypes.c_int),
+                ("relres", ctypes.c_double), ("solve_ms", ctypes.c_double)]
+
+
+class GGError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"ggmres error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_D = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_VP = ctypes.c_void_p
+
+
+def lib():
+    """Load libggmres.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` "
+                              "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.gg_strerror.restype = ctypes.c_char_p
+        L.gg_last_error.restype = ctypes.c_char_p
+        L.gg_create.argtypes = [ctypes.c_int, ctypes.POINTER(_VP)]
+        L.gg_destroy.argtypes = [_VP]
+        L.gg_set_matrix.argtypes = [_VP, ctypes.c_int, _I, _I, _D]
+        for f in ("gg_set_precond_none", "gg_set_precond_ilu0", "gg_precond_kind",
+                  "gg_uses_wavefront"):
+            getattr(L, f).argtypes = [_VP]
+        L.gg_set_precond_iluk.argtypes = [_VP, ctypes.c_int]
+        L.gg_set_precond_lu.argtypes = [_VP, _I, _I, _D, _I, _I, _D]
+        L.gg_set_precond_split.argtypes = [_VP, _I, _I, _D, _I, _I, _D, _D, _I, _I, _D, _D]
+        L.gg_solve.argtypes = [_VP, _D, _D, ctypes.POINTER(Options), ctypes.POINTER(Result)]
+        L.gg_solve_device.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options),
+                                      ctypes.POINTER(Result)]
+        L.gg_get_history.argtypes = [_VP, ctypes.c_void_p, ctypes.c_int]
+        L.gg_spmv.argtypes = [_VP, _D, _D]
+        L.gg_precond_apply.argtypes = [_VP, ctypes.c_int, _D, _D]
+        L.gg_time_spmv.argtypes = [_VP, ctypes.c_int, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_double)]
+        L.gg_time_precond.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        L.gg_bytes_spmv.argtypes = [_VP]
+        L.gg_bytes_spmv.restype = ctypes.c_double
+        L.gg_bytes_precond.argtypes = [_VP]
+        L.gg_bytes_precond.restype = ctypes.c_double
+        L.gg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.gg_profile_enable.argtypes = [_VP, ctypes.c_int]
+        L.gg_profile_reset.argtypes = [_VP]
+        L.gg_profile_get.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                     ctypes.POINTER(ctypes.c_double)]
+        _lib = L
+    return _lib
+
+
+def _check(rc, allow_nc=False):
+    if rc < 0 or (rc == GG_NOT_CONVERGED and not allow_nc):
+        raise GGError(rc, lib().gg_last_error().decode())
+    return rc
+
+
+def _csr_arrays(M):
+    """scipy matrix / oracle CSR tuple -> (n, rp, ci, v) contiguous."""
+    if hasattr(M, "tocsr"):
+        M = M.tocsr()
+        return (M.shape[0], np.ascontiguousarray(M.indptr, np.int32),
+                np.ascontiguousarray(M.indices, np.int32), np.ascontiguousarray(M.data, np.float64))
+    n, rp, ci, v = M
+    return (n, np.ascontiguousarray(rp, np.int32), np.ascontiguousarray(ci, np.int32),
+            np.ascontiguousarray(v, np.float64))
+
+
+class Solver:
+    """One solver on one GPU (handle of the C ABI)."""
+
+    def __init__(self, device=0):
+        h = _VP()
+        _check(lib().gg_create(int(device), ctypes.byref(h)))
+        self.h = h
+        self.n = 0
+
+    def close(self):
+        if self.h:
+            lib().gg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- setup -----------------------------------------------------------
+    def set_matrix(self, A):
+        n, rp, ci, v = _csr_arrays(A)
+        self.n = n
+        _check(lib().gg_set_matrix(self.h, n, rp, ci, v))
+
+    def set_precond_none(self):
+        _check(lib().gg_set_precond_none(self.h))
+
+    def set_precond_ilu0(self):
+        _check(lib().gg_set_precond_ilu0(self.h))
+
+    def set_precond_iluk(self, level):
+        _check(lib().gg_set_precond_iluk(self.h, int(level)))
+
+    def set_precond_lu(self, L, U):
+        _, lrp, lci, lv = _csr_arrays(L)
+        _, urp, uci, uv = _csr_arrays(U)
+        _check(lib().gg_set_precond_lu(self.h, lrp, lci, lv, urp, uci, uv))
+
+    def set_precond_split(self, L, U, middle, perm_row, perm_col, lscale, rscale):
+        _, lrp, lci, lv = _csr_arrays(L)
+        _, urp, uci, uv = _csr_arrays(U)
+        f = lambda a: np.ascontiguousarray(a, np.float64)
+        i = lambda a: np.ascontiguousarray(a, np.int32)
+        _check(lib().gg_set_precond_split(self.h, lrp, lci, lv, urp, uci, uv, f(middle),
+                                          i(perm_row), i(perm_col), f(lscale), f(rscale)))
+
+    @property
+    def uses_wavefront(self):
+        return bool(lib().gg_uses_wavefront(self.h))
+
+    # ---- solve -------------------------------------------------------------
+    def solve(self, b, x0=None, restart=30, max_iter=3000, tol=1e-10, flags=0):
+        b = np.ascontiguousarray(b, np.float64)
+        x = np.zeros(self.n) if x0 is None else np.array(x0, np.float64, copy=True)
+        o = Options(int(restart), int(max_iter), float(tol), int(flags))
+        r = Result()
+        rc = _check(lib().gg_solve(self.h, b, x, ctypes.byref(o), ctypes.byref(r)), allow_nc=True)
+        return dict(ret=rc, x=x, iters=r.iters, inner=r.inner_iters, restarts=r.restarts,
+                    relres=r.relres, solve_ms=r.solve_ms, hist=self.history())
+
+    def solve_device(self, b_ptr, x_ptr, restart=30, max_iter=3000, tol=1e-10, flags=0):
+        """b_ptr / x_ptr: device addresses (e.g. torch tensor .data_ptr()), natural order."""
+        o = Options(int(restart), int(max_iter), float(tol), int(flags))
+        r = Result()
+        rc = _check(lib().gg_solve_device(self.h, _VP(b_ptr), _VP(x_ptr), ctypes.byref(o),
+                                          ctypes.byref(r)), allow_nc=True)
+        return dict(ret=rc, iters=r.iters, inner=r.inner_iters, restarts=r.restarts,
+                    relres=r.relres, solve_ms=r.solve_ms)
+
+    def history(self):
+        n = lib().gg_get_history(self.h, None, 0)
+        out = np.zeros(max(n, 1))
+        lib().gg_get_history(self.h, out.ctypes.data_as(ctypes.c_void_p), n)
+        return out[:n]
+
+    # ---- single operators ----------------------------------------------------
+    def spmv(self, x):
+        y = np.zeros(self.n)
+        _check(lib().gg_spmv(self.h, np.ascontiguousarray(x, np.float64), y))
+        return y
+
+    def precond_apply(self, op, v):
+        out = np.zeros(self.n)
+        _check(lib().gg_precond_apply(self.h, int(op), np.ascontiguousarray(v, np.float64), out))
+        return out
+
+    def time_spmv(self, reps=50, nrot=4):
+        ms = ctypes.c_double()
+        _check(lib().gg_time_spmv(self.h, int(reps), int(nrot), ctypes.byref(ms)))
+        return ms.value
+
+    def time_precond(self, reps=20):
+        ms = ctypes.c_double()
+        _check(lib().gg_time_precond(self.h, int(reps), ctypes.byref(ms)))
+        return ms.value
+
+    def profile(self, on=True):
+        _check(lib().gg_profile_enable(self.h, int(bool(on))))
+        _check(lib().gg_profile_reset(self.h))
+
+    def profile_get(self, kind):
+        """(launches, total_ms) of one kernel family over the profiled solves."""
+        n, ms = ctypes.c_int(), ctypes.c_double()
+        _check(lib().gg_profile_get(self.h, int(kind), ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+    def bytes_spmv(self):
+        return lib().gg_bytes_spmv(self.h)
+
+    def bytes_precond(self):
+        return lib().gg_bytes_precond(self.h)
+
+
+def device_count():
+    c = ctypes.c_int()
+    _check(lib().gg_device_count(ctypes.byref(c)))
+    return c.value

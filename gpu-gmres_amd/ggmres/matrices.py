@@ -1,0 +1,136 @@
+"""Synthetic and fixture matrices for the GMRES path.
+
+Configs:
+  C1  100x100 5-pt Dirichlet Laplacian (diag 4, off -1), natural order, n=10,000
+  C2  1000x1000 5-pt, n=1,000,000, nnz=4,996,000
+  C4  7-pt 3D thermal grid, kx=ky=1, kz=10, diag = sum|off| + 1e-3
+  C5  A = G + C/h with C = c*I
+
+All matrices are scipy.sparse CSR, float64 values, int32 indices sorted per row.
+"""
+import numpy as np
+import scipy.sparse as sp
+
+
+def _finish(A):
+    A = sp.csr_matrix(A)
+    A.sum_duplicates()
+    A.sort_indices()
+    A.indptr = A.indptr.astype(np.int32)
+    A.indices = A.indices.astype(np.int32)
+    A.data = A.data.astype(np.float64)
+    return A
+
+
+def laplacian_5pt(nx, ny=None, diag=4.0, off=-1.0):
+    """2D 5-point stencil, natural row-major order (row r = j*nx + i)."""
+    ny = nx if ny is None else ny
+    n = nx * ny
+    r = np.arange(n, dtype=np.int64)
+    i = r % nx
+    j = r // nx
+    rows = [r]
+    cols = [r]
+    vals = [np.full(n, diag)]
+    for di, dj in ((-1, 0), (1, 0), (0, -1), (0, 1)):
+        ok = (i + di >= 0) & (i + di < nx) & (j + dj >= 0) & (j + dj < ny)
+        rows.append(r[ok])
+        cols.append(r[ok] + di + dj * nx)
+        vals.append(np.full(int(ok.sum()), off))
+    A = sp.coo_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                      shape=(n, n))
+    return _finish(A)
+
+
+def grid_7pt(nx, ny=None, nz=None, kx=1.0, ky=1.0, kz=10.0, shift=1e-3, upwind=0.0,
+             const_diag=None):
+    """3D 7-point thermal grid (C4).  Off-diagonals -k per direction (x gets an
+    optional +-upwind asymmetry); diagonal = sum|off| + shift (convective
+    boundary), or const_diag everywhere (Dirichlet Laplacian, e.g. 7)."""
+    ny = nx if ny is None else ny
+    nz = nx if nz is None else nz
+    n = nx * ny * nz
+    r = np.arange(n, dtype=np.int64)
+    i = r % nx
+    j = (r // nx) % ny
+    k = r // (nx * ny)
+    rows, cols, vals = [], [], []
+    dsum = np.zeros(n)
+    for (di, dj, dk, w) in ((-1, 0, 0, kx * (1 + upwind)), (1, 0, 0, kx * (1 - upwind)),
+                            (0, -1, 0, ky), (0, 1, 0, ky), (0, 0, -1, kz), (0, 0, 1, kz)):
+        ok = ((i + di >= 0) & (i + di < nx) & (j + dj >= 0) & (j + dj < ny)
+              & (k + dk >= 0) & (k + dk < nz))
+        rows.append(r[ok])
+        cols.append(r[ok] + di + dj * nx + dk * nx * ny)
+        vals.append(np.full(int(ok.sum()), -w))
+        dsum[ok] += w
+    rows.append(r)
+    cols.append(r)
+    vals.append(dsum + shift if const_diag is None else np.full(n, float(const_diag)))
+    A = sp.coo_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                      shape=(n, n))
+    return _finish(A)
+
+
+def transient(G, c=1e-3, h=1e-2):
+    """A = G + C/h with C = c*I (C5, backward Euler)."""
+    n = G.shape[0]
+    return _finish(G + sp.identity(n, format="csr") * (c / h))
+
+
+def read_mtx(path):
+    import scipy.io
+    return _finish(scipy.io.mmread(path))
+
+
+def _fortran_width(fmt):
+    """'(10I8)' -> (10, 8); '(5E16.8)' -> (5, 16); '(4D20.12)' -> (4, 20)."""
+    import re
+    m = re.search(r"(\d+)\s*[IEDFGiedfg]\s*(\d+)", fmt.replace("1P", "").replace("1p", ""))
+    return int(m.group(1)), int(m.group(2))
+
+
+def read_rua(path):
+    """Harwell-Boeing real unsymmetric assembled matrix (e.g. sherman1.rua).
+    Columns are stored compressed (CSC); right-hand-side blocks are ignored."""
+    with open(path) as f:
+        lines = f.read().split("\n")
+    counts = lines[1]
+    ptrcrd, indcrd, valcrd = int(counts[14:28]), int(counts[28:42]), int(counts[42:56])
+    mxtype = lines[2][:3].upper()
+    if mxtype != "RUA":
+        raise ValueError(f"{path}: only RUA supported, got {mxtype}")
+    nrow, ncol, nnz = int(lines[2][14:28]), int(lines[2][28:42]), int(lines[2][42:56])
+    fmts = lines[3]
+    pw = _fortran_width(fmts[0:16])[1]
+    iw = _fortran_width(fmts[16:32])[1]
+    vw = _fortran_width(fmts[32:52])[1]
+    rhscrd = counts[56:70].strip()
+    start = 4 + (1 if rhscrd and int(rhscrd) > 0 else 0)
+
+    def fields(block, w):
+        out = []
+        for ln in block:
+            ln = ln.rstrip()
+            out.extend(ln[k:k + w] for k in range(0, len(ln), w))
+        return [t for t in out if t.strip()]
+
+    ptr = np.array([int(t) for t in fields(lines[start:start + ptrcrd], pw)], np.int64) - 1
+    start += ptrcrd
+    ind = np.array([int(t) for t in fields(lines[start:start + indcrd], iw)], np.int64) - 1
+    start += indcrd
+    val = np.array([float(t.replace("D", "E").replace("d", "e"))
+                    for t in fields(lines[start:start + valcrd], vw)])
+    assert len(ptr) == ncol + 1 and len(ind) == nnz and len(val) == nnz
+    A = sp.csc_matrix((val, ind, ptr), shape=(nrow, ncol))
+    return _finish(A.tocsr())
+
+
+def rhs_ones(A):
+    """b = A * 1 (the x_exact = 1 idiom, src/mna_solve_gmres.cpp:302-303)."""
+    return A @ np.ones(A.shape[0])
+
+
+def rhs_uniform(n, seed=20261015):
+    """b ~ U[0,1) from PCG64(seed)."""
+    return np.random.Generator(np.random.PCG64(seed)).random(n)

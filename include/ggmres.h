@@ -1,0 +1,163 @@
+/*
+ * ggmres.h -- C ABI of the MI355X-native preconditioned GMRES solver.
+ *
+ * This is the drop-in boundary for the reference's hot path.
+ * Every entry point below replaces one reference interface; the citation is
+ * the reference file:line it stands in for (sheldonucr/GPU-GMRES):
+ *
+ *   gg_set_matrix          MySpMatrix / gpuMallocCpyCSRmySpM  src/SpMV.h:57-84, src/SpMV_alloc.cu:121-165
+ *   gg_set_precond_ilu0    MyILU0::Initilize / leftILU        src/preconditioner.h:119-144, src/leftILU.cu:27-336
+ *   gg_set_precond_iluk    MyILUK::Initilize (ilukC, lofC)     src/preconditioner.cu:1659-1753, src/iluk.cpp:56-334
+ *   gg_set_precond_lu      GMRES_GPU_leftILU0 L/U arguments     src/gmres.h:206-213 (src/gmres.cu:1438-1444)
+ *   gg_set_precond_split   MyILUPPfloat::Initilize              src/preconditioner.cu:1205-1334
+ *                          gmresInterfacePGfloat::setPrecondPG  src/gmres_interface_pg.cu:30-60
+ *   gg_solve / gg_solve_device
+ *                          GMRES_GPU_leftILU0 (left engine)     src/gmres.cu:1438-1696
+ *                          GMRESilu_GPU (split engine)          src/gmres.cu:2254-2446
+ *                          gmresInterfacePGfloat::GMRES_dev_PG  src/gmres_interface_pg.cu:110-139
+ *   (no CPU twin is shipped: the reference's CPU engines GMRES_leftILU0 /
+ *    GMRESilu are restated only in oracle/, which is test code)
+ *   gg_spmv                cusparseScsrmv / SpMV kernel          src/gmres.cu:2351-2353, src/SpMV_kernel.cu:166-251
+ *   gg_precond_apply       Preconditioner::DevPrecond_{left,right,rhs,starting_value}
+ *                                                               src/preconditioner.cu:1419-1657, src/gmres.cu:1398-1428
+ *
+ * Conventions: CSR, 0-based int32 indices, fp64 values.  Host arrays passed
+ * to gg_set_* are copied (the solver never keeps a host pointer).  Vectors
+ * passed to gg_solve are host arrays in the caller's (natural) row order;
+ * gg_solve_device takes device (HBM) pointers in natural order.
+ *
+ * Return codes: GG_OK (0) converged / success, GG_NOT_CONVERGED (1) -- the
+ * reference's 0/1 convention (src/gmres.h:14-16) -- and negative errors.
+ * Thread safety: one solver per host thread; solvers are independent.
+ */
+#ifndef GGMRES_H_
+#define GGMRES_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GG_ABI_VERSION 1
+
+enum gg_status {
+    GG_OK = 0,
+    GG_NOT_CONVERGED = 1,
+    GG_EINVAL = -1,        /* bad argument / shape                         */
+    GG_EHIP = -2,          /* HIP runtime error                            */
+    GG_EZEROPIVOT = -3,    /* ILU(k) zero pivot (src/iluk.cpp:175-185)     */
+    GG_ENOMEM = -4,        /* device allocation failed                     */
+    GG_ESTATE = -5,        /* call order (e.g. solve before set_matrix)    */
+    GG_ETIMEOUT = -6,      /* a device-side wait exceeded its spin bound   */
+    GG_ECOMM = -7          /* RCCL / multi-GPU error                       */
+};
+
+enum gg_precond_kind {
+    GG_PRECOND_NONE = 0,
+    GG_PRECOND_ILU0 = 1,   /* left, factored from A                        */
+    GG_PRECOND_ILUK = 2,   /* left, factored from A                        */
+    GG_PRECOND_LU = 3,     /* left, caller-supplied L,U                    */
+    GG_PRECOND_SPLIT = 4   /* ILU++/PG split: Ml = L^-1 P_r D_l^-1, Mr = D_r^-1 P_c U^-1 M */
+};
+
+/* which operator gg_precond_apply applies */
+enum gg_precond_op {
+    GG_APPLY_MINV = 0,     /* left engines: (LU)^-1           (LUSolve_gpu)                    */
+    GG_APPLY_LEFT = 1,     /* split: Ml   (DevPrecond_left / _rhs)                             */
+    GG_APPLY_RIGHT = 2,    /* split: Mr   (DevPrecond_right)                                   */
+    GG_APPLY_START = 3     /* split: Mr^-1 (DevPrecond_starting_value)                         */
+};
+
+/* solver flags */
+#define GG_FLAG_NO_GRAPH      0x1   /* launch eagerly instead of replaying a hipGraph per cycle */
+#define GG_FLAG_NO_WAVEFRONT  0x2   /* force the generic level-scheduled triangular solve      */
+
+typedef struct gg_solver gg_solver;
+
+typedef struct gg_options {
+    int restart;       /* m  (reference default 32, src/defs.h:11)                 */
+    int max_iter;      /* reference semantics: in = limit                          */
+    double tol;        /* relative residual target on ||M r|| / ||M b||            */
+    int flags;         /* GG_FLAG_*                                               */
+} gg_options;
+
+typedef struct gg_result {
+    int status;        /* GG_OK / GG_NOT_CONVERGED / error                        */
+    int iters;         /* the reference's *max_iter output (src/gmres.cu:2174)    */
+    int inner_iters;   /* Arnoldi iterations actually performed                   */
+    int restarts;      /* restart cycles started                                  */
+    double relres;     /* the reference's *tol output                             */
+    double solve_ms;   /* device time of the solve phase (hipEvents)              */
+} gg_result;
+
+int gg_abi_version(void);
+const char *gg_strerror(int status);
+const char *gg_last_error(void);            /* detail of the last error on this thread */
+int gg_device_count(int *count);
+
+int gg_create(int device, gg_solver **out);
+int gg_destroy(gg_solver *s);
+
+int gg_set_matrix(gg_solver *s, int n, const int *row_ptr, const int *col_idx,
+                  const double *val);
+
+int gg_set_precond_none(gg_solver *s);
+int gg_set_precond_ilu0(gg_solver *s);
+int gg_set_precond_iluk(gg_solver *s, int level);
+/* L: unit lower (strict entries + unit diagonal LAST in each row; the diagonal is
+ *    not applied, LUSolve_ignoreZero semantics); U: upper, diagonal first. */
+int gg_set_precond_lu(gg_solver *s,
+                      const int *l_row_ptr, const int *l_col_idx, const double *l_val,
+                      const int *u_row_ptr, const int *u_col_idx, const double *u_val);
+/* ILU++/PG split preconditioner (MyILUPPfloat).  L: non-unit lower, diagonal LAST;
+ * U: non-unit upper, diagonal FIRST; perm_row / perm_col as extracted at
+ * src/mna_solve_gpu_gmres.cpp:396-474. */
+int gg_set_precond_split(gg_solver *s,
+                         const int *l_row_ptr, const int *l_col_idx, const double *l_val,
+                         const int *u_row_ptr, const int *u_col_idx, const double *u_val,
+                         const double *middle, const int *perm_row, const int *perm_col,
+                         const double *lscale, const double *rscale);
+int gg_precond_kind(gg_solver *s);
+/* 1 if the structured-grid wavefront triangular solve is active, else 0 */
+int gg_uses_wavefront(gg_solver *s);
+
+int gg_solve(gg_solver *s, const double *b, double *x, const gg_options *opt,
+             gg_result *res);
+int gg_solve_device(gg_solver *s, const double *d_b, double *d_x,
+                    const gg_options *opt, gg_result *res);
+/* residual history of the last solve: [beta0/normb, |s[i+1]|/normb per inner
+ * iteration, beta/normb after each restart ...] in event order.  Returns the
+ * number of entries (may exceed cap; only cap are written). */
+int gg_get_history(gg_solver *s, double *out, int cap);
+
+/* single operators (host vectors, natural order) for parity tests */
+int gg_spmv(gg_solver *s, const double *x, double *y);
+int gg_precond_apply(gg_solver *s, int op, const double *in, double *out);
+
+/* device-timed kernel measurements on the solver's stream (hipEvents).
+ * gg_time_spmv: y = A x over nrot rotating copies of (x, y) so the Infinity
+ * Cache cannot serve repeats when nrot * footprint > 256 MiB; avg_ms per launch. */
+int gg_time_spmv(gg_solver *s, int reps, int nrot, double *avg_ms);
+/* average device time of one preconditioner application (L then U solve) */
+int gg_time_precond(gg_solver *s, int reps, double *avg_ms);
+
+/* In-solve kernel timing: when enabled, every inner iteration brackets each
+ * kernel family below with a hipEvent pair on the solver's stream; totals
+ * accumulate over gg_solve* calls until gg_profile_reset. */
+enum gg_prof_kind {
+    GG_PROF_SPMV = 0,      /* ww = A v_i                                  */
+    GG_PROF_PRECOND = 1,   /* w = M^-1 ww (both triangular solves)        */
+    GG_PROF_MGS = 2,       /* <w,v_0>, i+1 fused MGS steps, norm + Givens */
+    GG_PROF_NKINDS = 3
+};
+int gg_profile_enable(gg_solver *s, int on);
+int gg_profile_reset(gg_solver *s);
+int gg_profile_get(gg_solver *s, int kind, int *launches, double *total_ms);
+
+/* bytes the solver moves per unit of work (algorithmic) */
+double gg_bytes_spmv(gg_solver *s);
+double gg_bytes_precond(gg_solver *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,211 @@
+"""ctypes binding of the fp64 oracle (oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Importable from tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg -- never from the product package.
+"""
+import ctypes
+import os
+import subprocess
+from collections import namedtuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+CSR = namedtuple("CSR", "n rp ci v")
+
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_PI = ctypes.POINTER(ctypes.c_int)
+_PD = ctypes.POINTER(ctypes.c_double)
+
+
+class SplitT(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int),
+        ("l_rp", _PI), ("l_ci", _PI), ("l_v", _PD),
+        ("u_rp", _PI), ("u_ci", _PI), ("u_v", _PD),
+        ("middle", _PD), ("lscale", _PD), ("rscale", _PD),
+        ("perm_row", _PI), ("perm_col", _PI),
+    ]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(
+                os.path.join(_HERE, "oracle.c")):
+            build()
+        L = ctypes.CDLL(_LIB)
+        L.orc_spmv.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p]
+        L.orc_residual.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
+        for f in (L.orc_ilu0,):
+            f.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p,
+                          _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
+                          _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD)]
+            f.restype = ctypes.c_int
+        L.orc_iluk.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p,
+                               _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
+                               _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD)]
+        L.orc_iluk.restype = ctypes.c_int
+        L.orc_free.argtypes = [ctypes.c_void_p]
+        L.orc_lusolve.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _i32p, _i32p, _f64p,
+                                  _f64p, _f64p]
+        for f in (L.orc_split_left, L.orc_split_right, L.orc_split_start):
+            f.argtypes = [ctypes.POINTER(SplitT), _f64p, _f64p]
+        L.orc_gen_rot.argtypes = [ctypes.c_double, ctypes.c_double, _PD, _PD]
+        L.orc_apply_rot.argtypes = [_PD, _PD, ctypes.c_double, ctypes.c_double]
+        common = [_f64p, _f64p, ctypes.c_int, _PI, _PD, _f64p, ctypes.c_int, _PI, _PI]
+        L.orc_gmres_left.argtypes = ([ctypes.c_int, _i32p, _i32p, _f64p,
+                                      _i32p, _i32p, _f64p, _i32p, _i32p, _f64p] + common)
+        L.orc_gmres_left.restype = ctypes.c_int
+        L.orc_gmres_split.argtypes = ([ctypes.c_int, _i32p, _i32p, _f64p,
+                                       ctypes.POINTER(SplitT)] + common)
+        L.orc_gmres_split.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def csr(A):
+    """scipy.sparse matrix (or CSR tuple) -> oracle CSR with sorted int32 indices."""
+    if isinstance(A, CSR):
+        return A
+    A = A.tocsr()
+    A.sort_indices()
+    return CSR(A.shape[0], np.ascontiguousarray(A.indptr, dtype=np.int32),
+               np.ascontiguousarray(A.indices, dtype=np.int32),
+               np.ascontiguousarray(A.data, dtype=np.float64))
+
+
+def spmv(A, x):
+    A = csr(A)
+    y = np.zeros(A.n)
+    lib().orc_spmv(A.n, A.rp, A.ci, A.v, np.ascontiguousarray(x, np.float64), y)
+    return y
+
+
+def residual(A, x, b):
+    A = csr(A)
+    r = np.zeros(A.n)
+    lib().orc_residual(A.n, A.rp, A.ci, A.v, np.ascontiguousarray(x, np.float64),
+                       np.ascontiguousarray(b, np.float64), r)
+    return r
+
+
+def _take(n, rp, ci_p, v_p):
+    nnz = int(rp[n])
+    ci = np.ctypeslib.as_array(ci_p, shape=(max(nnz, 1),))[:nnz].copy()
+    v = np.ctypeslib.as_array(v_p, shape=(max(nnz, 1),))[:nnz].copy()
+    lib().orc_free(ctypes.cast(ci_p, ctypes.c_void_p))
+    lib().orc_free(ctypes.cast(v_p, ctypes.c_void_p))
+    return CSR(n, rp, ci.astype(np.int32), v)
+
+
+def ilu0(A):
+    """leftILU restated (src/leftILU.cu:27-336) -> (L, U)."""
+    A = csr(A)
+    n = A.n
+    l_rp = np.zeros(n + 1, np.int32)
+    u_rp = np.zeros(n + 1, np.int32)
+    lci, lv, uci, uv = _PI(), _PD(), _PI(), _PD()
+    rc = lib().orc_ilu0(n, A.rp, A.ci, A.v, l_rp, ctypes.byref(lci), ctypes.byref(lv),
+                        u_rp, ctypes.byref(uci), ctypes.byref(uv))
+    assert rc == 0
+    return _take(n, l_rp, lci, lv), _take(n, u_rp, uci, uv)
+
+
+def iluk(A, k):
+    """ITSOL lofC+ilukC restated (src/iluk.cpp:56-334) -> (L, U); raises on zero pivot."""
+    A = csr(A)
+    n = A.n
+    l_rp = np.zeros(n + 1, np.int32)
+    u_rp = np.zeros(n + 1, np.int32)
+    lci, lv, uci, uv = _PI(), _PD(), _PI(), _PD()
+    rc = lib().orc_iluk(int(k), n, A.rp, A.ci, A.v, l_rp, ctypes.byref(lci), ctypes.byref(lv),
+                        u_rp, ctypes.byref(uci), ctypes.byref(uv))
+    if rc != 0:
+        raise ZeroDivisionError("ILU(k): zero pivot (iluk.cpp:175-185)")
+    return _take(n, l_rp, lci, lv), _take(n, u_rp, uci, uv)
+
+
+def lusolve(L, U, y):
+    x = np.zeros(L.n)
+    lib().orc_lusolve(L.n, L.rp, L.ci, L.v, U.rp, U.ci, U.v,
+                      np.ascontiguousarray(y, np.float64), x)
+    return x
+
+
+class Split:
+    """ILU++-style split preconditioner arrays (PG boundary)."""
+
+    def __init__(self, L, U, middle, perm_row, perm_col, lscale, rscale):
+        self.L, self.U = L, U
+        self.middle = np.ascontiguousarray(middle, np.float64)
+        self.lscale = np.ascontiguousarray(lscale, np.float64)
+        self.rscale = np.ascontiguousarray(rscale, np.float64)
+        self.perm_row = np.ascontiguousarray(perm_row, np.int32)
+        self.perm_col = np.ascontiguousarray(perm_col, np.int32)
+        c = lambda a, t: a.ctypes.data_as(t)
+        self.s = SplitT(L.n, c(L.rp, _PI), c(L.ci, _PI), c(L.v, _PD),
+                        c(U.rp, _PI), c(U.ci, _PI), c(U.v, _PD),
+                        c(self.middle, _PD), c(self.lscale, _PD), c(self.rscale, _PD),
+                        c(self.perm_row, _PI), c(self.perm_col, _PI))
+
+    def _apply(self, f, v):
+        out = np.zeros(self.L.n)
+        f(ctypes.byref(self.s), np.ascontiguousarray(v, np.float64), out)
+        return out
+
+    def left(self, v):
+        return self._apply(lib().orc_split_left, v)
+
+    def right(self, v):
+        return self._apply(lib().orc_split_right, v)
+
+    def start(self, v):
+        return self._apply(lib().orc_split_start, v)
+
+
+def gen_rot(dx, dy):
+    cs, sn = ctypes.c_double(), ctypes.c_double()
+    lib().orc_gen_rot(dx, dy, ctypes.byref(cs), ctypes.byref(sn))
+    return cs.value, sn.value
+
+
+def _gmres_out(ret, x, mi, tl, hist, hl, inner):
+    return dict(ret=ret, x=x, iters=mi.value, relres=tl.value,
+                hist=hist[:hl.value].copy(), inner=inner.value)
+
+
+def gmres_left(A, L, U, b, x0=None, m=30, max_iter=3000, tol=1e-10, hist_cap=None):
+    """GMRES_leftILU0 restated (src/gmres.cu:566-717)."""
+    A = csr(A)
+    x = np.zeros(A.n) if x0 is None else np.array(x0, np.float64, copy=True)
+    cap = hist_cap or (max_iter + max_iter // max(m, 1) + 8)
+    hist = np.zeros(cap)
+    mi, tl, hl, inner = ctypes.c_int(max_iter), ctypes.c_double(tol), ctypes.c_int(), ctypes.c_int()
+    ret = lib().orc_gmres_left(A.n, A.rp, A.ci, A.v, L.rp, L.ci, L.v, U.rp, U.ci, U.v,
+                               np.ascontiguousarray(b, np.float64), x, int(m),
+                               ctypes.byref(mi), ctypes.byref(tl), hist, cap,
+                               ctypes.byref(hl), ctypes.byref(inner))
+    return _gmres_out(ret, x, mi, tl, hist, hl, inner)
+
+
+def gmres_split(A, P, b, x0=None, m=32, max_iter=10000, tol=1e-7, hist_cap=None):
+    """GMRESilu restated (src/gmres.cu:2069-2252) with a Split preconditioner."""
+    A = csr(A)
+    x = np.zeros(A.n) if x0 is None else np.array(x0, np.float64, copy=True)
+    cap = hist_cap or (max_iter + max_iter // max(m, 1) + 8)
+    hist = np.zeros(cap)
+    mi, tl, hl, inner = ctypes.c_int(max_iter), ctypes.c_double(tol), ctypes.c_int(), ctypes.c_int()
+    ret = lib().orc_gmres_split(A.n, A.rp, A.ci, A.v, ctypes.byref(P.s),
+                                np.ascontiguousarray(b, np.float64), x, int(m),
+                                ctypes.byref(mi), ctypes.byref(tl), hist, cap,
+                                ctypes.byref(hl), ctypes.byref(inner))
+    return _gmres_out(ret, x, mi, tl, hist, hl, inner)

@@ -1,0 +1,605 @@
+/*
+ * oracle.c -- fp64 CPU restatement of the reference GPU-GMRES hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Compiled with -ffp-contract=off
+ * so every a*b+c is two roundings, as in the reference's scalar loops.
+ * Reference citations are file:line in sheldonucr/GPU-GMRES.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* Equal(a, 0) with eps = 1e-9 (src/defs.h:45-47), evaluated with fabs. */
+static int is_zero(double a) { return fabs(a) < 1e-9; }
+
+void orc_free(void *p) { free(p); }
+
+/* ------------------------------------------------------------------ SpMV */
+void orc_spmv(int n, const int *rp, const int *ci, const double *v,
+              const double *x, double *y)
+{
+    /* computeSpMV (src/SpMV_compute.cpp:19-36): serial per-row sum in CSR order */
+    for (int i = 0; i < n; i++) {
+        double t = 0.0;
+        for (int j = rp[i]; j < rp[i + 1]; j++) t += v[j] * x[ci[j]];
+        y[i] = t;
+    }
+}
+
+void orc_residual(int n, const int *rp, const int *ci, const double *v,
+                  const double *x, const double *b, double *r)
+{
+    /* sgemv(v, A, alpha=-1, x, beta=1, y=b) (src/gmres.cu:77-88) */
+    double *t = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    orc_spmv(n, rp, ci, v, x, t);
+    for (int i = 0; i < n; i++) r[i] = -1.0 * t[i] + 1.0 * b[i];
+    free(t);
+}
+
+/* ---------------------------------------------------------------- ILU(0) */
+/* CSR -> CSC with rows ascending inside each column (csr2csc, src/leftILU.cu:371-417) */
+static void csr_to_csc(int n, const int *rp, const int *ci, const double *v,
+                       int *cp, int *ri, double *cv)
+{
+    int nnz = rp[n];
+    int *cnt = (int *)calloc((size_t)n + 1, sizeof(int));
+    for (int j = 0; j < nnz; j++) cnt[ci[j] + 1]++;
+    cp[0] = 0;
+    for (int c = 0; c < n; c++) cp[c + 1] = cp[c] + cnt[c + 1];
+    int *pos = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    for (int c = 0; c < n; c++) pos[c] = cp[c];
+    for (int r = 0; r < n; r++)
+        for (int j = rp[r]; j < rp[r + 1]; j++) {
+            int c = ci[j];
+            ri[pos[c]] = r;
+            cv[pos[c]] = v[j];
+            pos[c]++;
+        }
+    free(pos);
+    free(cnt);
+}
+
+/* liSearchLowerBound (src/leftILU.cu:831-840) */
+static int lower_bound_lin(int target, int lpos, int upos, const int *a)
+{
+    for (int i = lpos; i < upos; i++)
+        if (a[i] >= target) return i;
+    return upos;
+}
+
+/* cpuSequentialTriSolve body for one column (src/leftILU.cu:774-821) */
+static void ilu0_column(int tgt, const int *cp, const int *ri, double *cv)
+{
+    int lb = cp[tgt], ub = cp[tgt + 1];
+    double u_diag = 0.0;
+    for (int k = lb; k < ub - 1; k++) {
+        int cur_row = ri[k];
+        if (cur_row > tgt) break;
+        if (cur_row == tgt) { u_diag = cv[k]; break; }
+        int left_lb = cp[cur_row], left_ub = cp[cur_row + 1];
+        for (int p = k + 1; p < ub; p++) {
+            int r2 = ri[p];
+            int q = lower_bound_lin(r2, left_lb, left_ub, ri);
+            if (q < left_ub && ri[q] == r2) cv[p] -= cv[q] * cv[k];
+        }
+    }
+    for (int k = lb; k < ub; k++) {
+        if (ri[k] <= tgt) continue;
+        if (!is_zero(u_diag)) cv[k] /= u_diag;
+        else cv[k] = 0.0;
+    }
+}
+
+/* splitLU_csr (src/leftILU.cu:481-541): drop |v|<1e-9, L gets a unit diag LAST */
+static void split_lu(int n, const int *rp, const int *ci, const double *v,
+                     int *l_rp, int **l_ci, double **l_v,
+                     int *u_rp, int **u_ci, double **u_v)
+{
+    l_rp[0] = 0; u_rp[0] = 0;
+    for (int r = 0; r < n; r++) {
+        int nl = 0, nu = 0;
+        for (int j = rp[r]; j < rp[r + 1]; j++) {
+            if (is_zero(v[j])) continue;
+            if (ci[j] < r) nl++; else nu++;
+        }
+        l_rp[r + 1] = l_rp[r] + nl + 1;
+        u_rp[r + 1] = u_rp[r] + nu;
+    }
+    *l_ci = (int *)malloc((size_t)(l_rp[n] > 0 ? l_rp[n] : 1) * sizeof(int));
+    *l_v = (double *)malloc((size_t)(l_rp[n] > 0 ? l_rp[n] : 1) * sizeof(double));
+    *u_ci = (int *)malloc((size_t)(u_rp[n] > 0 ? u_rp[n] : 1) * sizeof(int));
+    *u_v = (double *)malloc((size_t)(u_rp[n] > 0 ? u_rp[n] : 1) * sizeof(double));
+    for (int r = 0; r < n; r++) {
+        int pl = l_rp[r], pu = u_rp[r];
+        for (int j = rp[r]; j < rp[r + 1]; j++) {
+            if (is_zero(v[j])) continue;
+            if (ci[j] < r) { (*l_ci)[pl] = ci[j]; (*l_v)[pl] = v[j]; pl++; }
+            else { (*u_ci)[pu] = ci[j]; (*u_v)[pu] = v[j]; pu++; }
+        }
+        (*l_ci)[pl] = r; (*l_v)[pl] = 1.0;
+    }
+}
+
+int orc_ilu0(int n, const int *rp, const int *ci, const double *v,
+             int *l_rp, int **l_ci, double **l_v,
+             int *u_rp, int **u_ci, double **u_v)
+{
+    int nnz = rp[n];
+    size_t cap = (size_t)(nnz > 0 ? nnz : 1);
+    /* generateLevel (src/leftILU.cu:339-368) on the original values */
+    int *level = (int *)calloc((size_t)n + 1, sizeof(int));
+    int maxlev = 0;
+    for (int r = 0; r < n; r++)
+        for (int j = rp[r]; j < rp[r + 1]; j++)
+            if (!is_zero(v[j]) && ci[j] > r) {
+                int c = ci[j];
+                if (level[c] < level[r] + 1) level[c] = level[r] + 1;
+            }
+    for (int r = 0; r < n; r++) if (level[r] > maxlev) maxlev = level[r];
+    /* egraph: columns bucketed by level, ascending index inside a level (:41-49) */
+    int *lcnt = (int *)calloc((size_t)maxlev + 2, sizeof(int));
+    for (int r = 0; r < n; r++) lcnt[level[r] + 1]++;
+    for (int l = 0; l <= maxlev; l++) lcnt[l + 1] += lcnt[l];
+    int *order = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    for (int r = 0; r < n; r++) order[lcnt[level[r]]++] = r;
+
+    int *cp = (int *)malloc(((size_t)n + 1) * sizeof(int));
+    int *ri = (int *)malloc(cap * sizeof(int));
+    double *cv = (double *)malloc(cap * sizeof(double));
+    csr_to_csc(n, rp, ci, v, cp, ri, cv);
+    /* the reference runs its GPU kernel sparseTriSolve_V2 on levels >= 32 nodes;
+     * that kernel races, so every column follows
+     * the CPU kernel here, in the same level order */
+    for (int k = 0; k < n; k++) ilu0_column(order[k], cp, ri, cv);
+
+    /* csr2csc(csc) back to CSR (src/leftILU.cu:297), then split (:298) */
+    int *crp = (int *)malloc(((size_t)n + 1) * sizeof(int));
+    int *cci = (int *)malloc(cap * sizeof(int));
+    double *cvv = (double *)malloc(cap * sizeof(double));
+    csr_to_csc(n, cp, ri, cv, crp, cci, cvv); /* transpose of CSC == CSR */
+    split_lu(n, crp, cci, cvv, l_rp, l_ci, l_v, u_rp, u_ci, u_v);
+
+    free(crp); free(cci); free(cvv);
+    free(cp); free(ri); free(cv);
+    free(order); free(lcnt); free(level);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- ILU(k) */
+static int cmp_int_pair(const void *a, const void *b)
+{
+    int x = *(const int *)a, y = *(const int *)b;
+    return (x > y) - (x < y);
+}
+
+int orc_iluk(int lofM, int n, const int *rp, const int *ci, const double *v,
+             int *l_rp, int **l_ci, double **l_v,
+             int *u_rp, int **u_ci, double **u_v)
+{
+    /* symbolic: lofC (src/iluk.cpp:192-334) */
+    int **Lja = (int **)calloc((size_t)n + 1, sizeof(int *));
+    int **Uja = (int **)calloc((size_t)n + 1, sizeof(int *));
+    int **ulvl = (int **)calloc((size_t)n + 1, sizeof(int *));
+    int *Lnz = (int *)calloc((size_t)n + 1, sizeof(int));
+    int *Unz = (int *)calloc((size_t)n + 1, sizeof(int));
+    int *levls = (int *)malloc(((size_t)n + 1) * sizeof(int));
+    int *jbuf = (int *)malloc(((size_t)n + 1) * sizeof(int));
+    int *iw = (int *)malloc(((size_t)n + 1) * sizeof(int));
+    for (int j = 0; j < n; j++) iw[j] = -1;
+    for (int i = 0; i < n; i++) {
+        int incl = 0, incu = i;
+        for (int j = rp[i]; j < rp[i + 1]; j++) {
+            int col = ci[j];
+            if (col < i) { jbuf[incl] = col; levls[incl] = 0; iw[col] = incl++; }
+            else if (col > i) { jbuf[incu] = col; levls[incu] = 0; iw[col] = incu++; }
+        }
+        int jpiv = -1;
+        while (++jpiv < incl) {
+            int k = jbuf[jpiv], kmin = k, jmin = jpiv;
+            for (int j = jpiv + 1; j < incl; j++)
+                if (jbuf[j] < kmin) { kmin = jbuf[j]; jmin = j; }
+            if (jmin != jpiv) {  /* select leftmost pivot (:263-281) */
+                jbuf[jpiv] = kmin; jbuf[jmin] = k;
+                iw[kmin] = jpiv; iw[k] = jmin;
+                int t = levls[jpiv]; levls[jpiv] = levls[jmin]; levls[jmin] = t;
+                k = kmin;
+            }
+            for (int j = 0; j < Unz[k]; j++) {
+                int col = Uja[k][j];
+                int it = ulvl[k][j] + levls[jpiv] + 1;
+                if (it > lofM) continue;
+                int ip = iw[col];
+                if (ip == -1) {
+                    if (col < i) { jbuf[incl] = col; levls[incl] = it; iw[col] = incl++; }
+                    else if (col > i) { jbuf[incu] = col; levls[incu] = it; iw[col] = incu++; }
+                } else if (it < levls[ip]) {
+                    levls[ip] = it;
+                }
+            }
+        }
+        for (int j = 0; j < incl; j++) iw[jbuf[j]] = -1;
+        for (int j = i; j < incu; j++) iw[jbuf[j]] = -1;
+        Lnz[i] = incl;
+        Lja[i] = (int *)malloc((size_t)(incl > 0 ? incl : 1) * sizeof(int));
+        memcpy(Lja[i], jbuf, sizeof(int) * (size_t)incl);
+        int ku = incu - i;
+        Unz[i] = ku;
+        Uja[i] = (int *)malloc((size_t)(ku > 0 ? ku : 1) * sizeof(int));
+        ulvl[i] = (int *)malloc((size_t)(ku > 0 ? ku : 1) * sizeof(int));
+        memcpy(Uja[i], jbuf + i, sizeof(int) * (size_t)ku);
+        memcpy(ulvl[i], levls + i, sizeof(int) * (size_t)ku);
+    }
+    /* numeric: ilukC (src/iluk.cpp:56-190), diagonal kept inverted in D */
+    double **Lma = (double **)calloc((size_t)n + 1, sizeof(double *));
+    double **Uma = (double **)calloc((size_t)n + 1, sizeof(double *));
+    double *D = (double *)malloc(((size_t)n + 1) * sizeof(double));
+    double *Draw = (double *)malloc(((size_t)n + 1) * sizeof(double));
+    int *jw = iw;
+    int ierr = 0;
+    for (int j = 0; j < n; j++) jw[j] = -1;
+    for (int i = 0; i < n && !ierr; i++) {
+        Lma[i] = (double *)malloc((size_t)(Lnz[i] > 0 ? Lnz[i] : 1) * sizeof(double));
+        Uma[i] = (double *)malloc((size_t)(Unz[i] > 0 ? Unz[i] : 1) * sizeof(double));
+        for (int j = 0; j < Lnz[i]; j++) { jw[Lja[i][j]] = j; Lma[i][j] = 0.0; }
+        jw[i] = i;
+        D[i] = 0.0;
+        for (int j = 0; j < Unz[i]; j++) { jw[Uja[i][j]] = j; Uma[i][j] = 0.0; }
+        for (int j = rp[i]; j < rp[i + 1]; j++) {
+            int col = ci[j], jpos = jw[col];
+            if (col < i) Lma[i][jpos] = v[j];
+            else if (col == i) D[i] = v[j];
+            else Uma[i][jpos] = v[j];
+        }
+        for (int j = 0; j < Lnz[i]; j++) {
+            int jrow = Lja[i][j];
+            Lma[i][j] *= D[jrow];
+            for (int k = 0; k < Unz[jrow]; k++) {
+                int col = Uja[jrow][k], jpos = jw[col];
+                if (jpos == -1) continue;
+                if (col < i) Lma[i][jpos] -= Lma[i][j] * Uma[jrow][k];
+                else if (col == i) D[i] -= Lma[i][j] * Uma[jrow][k];
+                else Uma[i][jpos] -= Lma[i][j] * Uma[jrow][k];
+            }
+        }
+        for (int j = 0; j < Lnz[i]; j++) jw[Lja[i][j]] = -1;
+        jw[i] = -1;
+        for (int j = 0; j < Unz[i]; j++) jw[Uja[i][j]] = -1;
+        if (D[i] == 0.0) { ierr = -2; break; }
+        Draw[i] = D[i];
+        D[i] = 1.0 / D[i];
+    }
+    if (!ierr) {
+        /* emit: L strict (ascending, as lofC leaves it) + unit diag last;
+         * U: diag (un-inverted) first, strict upper sorted ascending */
+        l_rp[0] = 0; u_rp[0] = 0;
+        for (int i = 0; i < n; i++) {
+            l_rp[i + 1] = l_rp[i] + Lnz[i] + 1;
+            u_rp[i + 1] = u_rp[i] + Unz[i] + 1;
+        }
+        *l_ci = (int *)malloc((size_t)l_rp[n] * sizeof(int) + 4);
+        *l_v = (double *)malloc((size_t)l_rp[n] * sizeof(double) + 8);
+        *u_ci = (int *)malloc((size_t)u_rp[n] * sizeof(int) + 4);
+        *u_v = (double *)malloc((size_t)u_rp[n] * sizeof(double) + 8);
+        int *pairs = (int *)malloc(((size_t)n + 1) * 2 * sizeof(int));
+        for (int i = 0; i < n; i++) {
+            int p = l_rp[i];
+            for (int j = 0; j < Lnz[i]; j++) { (*l_ci)[p] = Lja[i][j]; (*l_v)[p] = Lma[i][j]; p++; }
+            (*l_ci)[p] = i; (*l_v)[p] = 1.0;
+            p = u_rp[i];
+            (*u_ci)[p] = i; (*u_v)[p] = Draw[i]; p++;
+            for (int j = 0; j < Unz[i]; j++) { pairs[2 * j] = Uja[i][j]; pairs[2 * j + 1] = j; }
+            qsort(pairs, (size_t)Unz[i], 2 * sizeof(int), cmp_int_pair);
+            for (int j = 0; j < Unz[i]; j++) {
+                (*u_ci)[p] = pairs[2 * j]; (*u_v)[p] = Uma[i][pairs[2 * j + 1]]; p++;
+            }
+        }
+        free(pairs);
+    }
+    for (int i = 0; i < n; i++) {
+        free(Lja[i]); free(Uja[i]); free(ulvl[i]); free(Lma[i]); free(Uma[i]);
+    }
+    free(Lja); free(Uja); free(ulvl); free(Lma); free(Uma);
+    free(Lnz); free(Unz); free(levls); free(jbuf); free(iw); free(D); free(Draw);
+    return ierr;
+}
+
+/* ------------------------------------------------------- triangular solve */
+void orc_lusolve(int n, const int *l_rp, const int *l_ci, const double *l_v,
+                 const int *u_rp, const int *u_ci, const double *u_v,
+                 const double *y, double *x)
+{
+    /* LUSolve_ignoreZero (src/SpMV_compute.cpp:92-136).  The L diagonal is
+     * never applied (the reference divides the scratch x, :112), i.e. unit L. */
+    double *w = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    memcpy(w, y, (size_t)n * sizeof(double));
+    for (int i = 0; i < n; i++) {
+        for (int j = l_rp[i]; j < l_rp[i + 1]; j++) {
+            if (l_ci[j] >= i) break;
+            w[i] -= l_v[j] * w[l_ci[j]];
+        }
+    }
+    memcpy(x, w, (size_t)n * sizeof(double));
+    for (int i = n - 1; i >= 0; i--) {
+        int lb = u_rp[i], j = u_rp[i + 1] - 1;
+        for (; j >= lb; j--) {
+            if (u_ci[j] <= i) break;
+            x[i] -= u_v[j] * x[u_ci[j]];
+        }
+        if (j >= lb && u_ci[j] == i && !is_zero(u_v[j])) x[i] /= u_v[j];
+    }
+    free(w);
+}
+
+/* ---------------------------------------------- split (PG) preconditioner */
+void orc_split_left(const orc_split_t *p, const double *in, double *out)
+{
+    /* MyILUPP::HostPrecond_left (src/preconditioner.cu:1094-1114) */
+    int n = p->n;
+    double *t = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    for (int i = 0; i < n; i++) t[i] = in[i] / p->lscale[i];
+    for (int i = 0; i < n; i++) out[i] = t[p->perm_row[i]];
+    for (int i = 0; i < n; i++) {
+        int lb = p->l_rp[i], ub = p->l_rp[i + 1];
+        for (int j = lb; j < ub - 1; j++) out[i] -= p->l_v[j] * out[p->l_ci[j]];
+        out[i] /= p->l_v[ub - 1];
+    }
+    free(t);
+}
+
+void orc_split_right(const orc_split_t *p, const double *in, double *out)
+{
+    /* MyILUPP::HostPrecond_right (src/preconditioner.cu:1117-1137) */
+    int n = p->n;
+    double *t = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    for (int i = 0; i < n; i++) t[i] = in[i] * p->middle[i];
+    for (int i = n - 1; i >= 0; i--) {
+        int lb = p->u_rp[i], ub = p->u_rp[i + 1];
+        for (int j = lb + 1; j < ub; j++) t[i] -= p->u_v[j] * t[p->u_ci[j]];
+        t[i] /= p->u_v[lb];
+    }
+    for (int i = 0; i < n; i++) out[i] = t[p->perm_col[i]] / p->rscale[i];
+    free(t);
+}
+
+void orc_split_start(const orc_split_t *p, const double *in, double *out)
+{
+    /* MyILUPP::HostPrecond_starting_value (src/preconditioner.cu:1074-1091) */
+    int n = p->n;
+    double *t = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    double *z = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    for (int i = 0; i < n; i++) t[i] = in[i] * p->rscale[i];
+    for (int i = 0; i < n; i++) z[p->perm_col[i]] = t[i];
+    for (int i = 0; i < n; i++) {
+        double s = 0.0;
+        for (int j = p->u_rp[i]; j < p->u_rp[i + 1]; j++) s += p->u_v[j] * z[p->u_ci[j]];
+        t[i] = s;
+    }
+    for (int i = 0; i < n; i++) out[i] = t[i] / p->middle[i];
+    free(z);
+    free(t);
+}
+
+/* ---------------------------------------------------------------- Givens */
+void orc_apply_rot(double *dx, double *dy, double cs, double sn)
+{
+    /* ApplyPlaneRotation (src/gmres.cu:192-197) */
+    double temp = cs * (*dx) + sn * (*dy);
+    *dy = -sn * (*dx) + cs * (*dy);
+    *dx = temp;
+}
+
+void orc_gen_rot(double dx, double dy, double *cs, double *sn)
+{
+    /* GeneratePlaneRotation (src/gmres.cu:200-216): 1/sqrt(1+t^2), not hypot */
+    if (dy == 0.0) { *cs = 1.0; *sn = 0.0; }
+    else if (fabs(dy) > fabs(dx)) {
+        double temp = dx / dy;
+        *sn = 1.0 / sqrt(1.0 + temp * temp);
+        *cs = temp * (*sn);
+    } else {
+        double temp = dy / dx;
+        *cs = 1.0 / sqrt(1.0 + temp * temp);
+        *sn = temp * (*cs);
+    }
+}
+
+/* ------------------------------------------------------------ BLAS-1 (serial) */
+static double dot(const double *x, const double *y, int n)
+{
+    double t = 0.0;                 /* dot (src/gmres.cu:68-74) */
+    for (int i = 0; i < n; i++) t += x[i] * y[i];
+    return t;
+}
+static double norm2(const double *v, int n)
+{
+    double t = 0.0;                 /* norm2 (src/gmres.cu:60-66) */
+    for (int i = 0; i < n; i++) t += v[i] * v[i];
+    return sqrt(t);
+}
+
+/* Update (src/gmres.cu:93-116): y = H(0:k,0:k)^-1 s; x += V y */
+static void update(double *x, int k, const double *H, int m, const double *s,
+                   const double *V, int n)
+{
+    double *y = (double *)malloc((size_t)(k + 1) * sizeof(double));
+    for (int i = 0; i <= k; i++) y[i] = s[i];
+    for (int i = k; i >= 0; i--) {
+        y[i] /= H[i + i * (m + 1)];
+        for (int j = i - 1; j >= 0; j--) y[j] -= H[j + i * (m + 1)] * y[i];
+    }
+    for (int j = 0; j <= k; j++)
+        for (int i = 0; i < n; i++) x[i] += V[(size_t)j * n + i] * y[j];
+    free(y);
+}
+
+typedef struct {
+    double *h; int cap; int len;
+} hist_t;
+static void hist_push(hist_t *h, double v)
+{
+    if (h->h && h->len < h->cap) h->h[h->len] = v;
+    h->len++;
+}
+
+/* Operator abstraction so GMRES_leftILU0 and GMRESilu share one restated loop.
+ * kind 0 = left ILU (M^-1 = (LU)^-1), kind 1 = split PG. */
+typedef struct {
+    int kind;
+    int n;
+    const int *rp, *ci; const double *v;
+    const int *l_rp, *l_ci; const double *l_v;
+    const int *u_rp, *u_ci; const double *u_v;
+    const orc_split_t *sp;
+} op_t;
+
+static int gmres_core(const op_t *op, const double *b, double *x, int m,
+                      int *max_iter, double *tol, double *hist, int hist_cap,
+                      int *hist_len, int *inner_iters)
+{
+    int n = op->n;
+    size_t nn = (size_t)(n > 0 ? n : 1);
+    double resid;
+    int i, j = 1, k;
+    int done_iters = 0;
+    double *s = (double *)calloc((size_t)m + 1, sizeof(double));
+    double *cs = (double *)calloc((size_t)m + 1, sizeof(double));
+    double *sn = (double *)calloc((size_t)m + 1, sizeof(double));
+    double *w = (double *)malloc(nn * sizeof(double));
+    double *ww = (double *)malloc(nn * sizeof(double));
+    double *r = (double *)malloc(nn * sizeof(double));
+    double *rr = (double *)malloc(nn * sizeof(double));
+    double *bb = (double *)malloc(nn * sizeof(double));
+    double *H = (double *)calloc((size_t)(m + 1) * (size_t)m, sizeof(double));
+    double *V = (double *)malloc((size_t)(m + 1) * nn * sizeof(double));
+    double *y = (double *)calloc(nn, sizeof(double));   /* split: Mr^-1 x */
+    double *acc = x;                                     /* left: update x directly */
+    hist_t hs = {hist, hist_cap, 0};
+    int ret = 1;
+
+    /* normb = ||M b||  (left: :593-594 ; split: HostPrecond_rhs :2096-2098) */
+    if (op->kind == 0)
+        orc_lusolve(n, op->l_rp, op->l_ci, op->l_v, op->u_rp, op->u_ci, op->u_v, b, bb);
+    else
+        orc_split_left(op->sp, b, bb);
+    double normb = norm2(bb, n);
+    if (normb == 0.0) normb = 1.0;
+
+    if (op->kind == 1) {
+        orc_split_start(op->sp, x, y);   /* :2102 */
+        acc = y;
+    }
+    orc_residual(n, op->rp, op->ci, op->v, x, b, rr);
+    if (op->kind == 0)
+        orc_lusolve(n, op->l_rp, op->l_ci, op->l_v, op->u_rp, op->u_ci, op->u_v, rr, r);
+    else
+        orc_split_left(op->sp, rr, r);
+    double beta = norm2(r, n);
+    resid = beta / normb;
+    hist_push(&hs, resid);
+    if (resid <= *tol) {                 /* note "<=" (:608 / :2112) */
+        *tol = resid;
+        *max_iter = 0;
+        ret = 0;
+        goto out;
+    }
+
+    while (j <= *max_iter) {
+        double inv = 1.0 / beta;
+        for (int t = 0; t < n; t++) V[t] = inv * r[t];
+        for (int t = 0; t <= m; t++) s[t] = 0.0;
+        s[0] = beta;
+        for (i = 0; i < m && j <= *max_iter; i++, j++) {
+            double *vi = V + (size_t)i * nn;
+            if (op->kind == 0) {
+                orc_spmv(n, op->rp, op->ci, op->v, vi, ww);              /* :635 */
+                orc_lusolve(n, op->l_rp, op->l_ci, op->l_v, op->u_rp, op->u_ci,
+                            op->u_v, ww, w);                           /* :636 */
+            } else {
+                orc_split_right(op->sp, vi, w);                        /* :2143 */
+                orc_spmv(n, op->rp, op->ci, op->v, w, ww);             /* :2144 */
+                orc_split_left(op->sp, ww, w);                         /* :2145 */
+            }
+            for (k = 0; k <= i; k++) {                                 /* MGS :638-641 */
+                const double *vk = V + (size_t)k * nn;
+                double h = dot(w, vk, n);
+                H[k + i * (m + 1)] = h;
+                double a = -h;
+                for (int t = 0; t < n; t++) w[t] = a * vk[t] + w[t];
+            }
+            double hn = norm2(w, n);
+            H[(i + 1) + i * (m + 1)] = hn;
+            /* v_{i+1} = w * (1/H(i+1,i)) (:645); lucky breakdown guarded */
+            double *vn = V + (size_t)(i + 1) * nn;
+            if (hn != 0.0) {
+                double hinv = 1.0 / hn;
+                for (int t = 0; t < n; t++) vn[t] = hinv * w[t];
+            } else {
+                for (int t = 0; t < n; t++) vn[t] = 0.0;
+            }
+            for (k = 0; k < i; k++)
+                orc_apply_rot(&H[k + i * (m + 1)], &H[(k + 1) + i * (m + 1)], cs[k], sn[k]);
+            orc_gen_rot(H[i + i * (m + 1)], H[(i + 1) + i * (m + 1)], &cs[i], &sn[i]);
+            orc_apply_rot(&H[i + i * (m + 1)], &H[(i + 1) + i * (m + 1)], cs[i], sn[i]);
+            orc_apply_rot(&s[i], &s[i + 1], cs[i], sn[i]);
+            done_iters++;
+            resid = fabs(s[i + 1]) / normb;
+            hist_push(&hs, resid);
+            if (resid < *tol) {                                        /* "<" :654 */
+                update(acc, i, H, m, s, V, n);
+                if (op->kind == 1) orc_split_right(op->sp, y, x);     /* :2176 */
+                *tol = resid;
+                *max_iter = j;
+                ret = 0;
+                goto out;
+            }
+        }
+        /* Update(m-1) in the reference even when j>max_iter cut the cycle
+         * short (src/gmres.cu:677,2196); the restatement uses the last filled
+         * column i-1 (deliberate fix, as ILU++ does). */
+        update(acc, i - 1, H, m, s, V, n);
+        if (op->kind == 1) orc_split_right(op->sp, y, x);
+        orc_residual(n, op->rp, op->ci, op->v, x, b, rr);
+        if (op->kind == 0)
+            orc_lusolve(n, op->l_rp, op->l_ci, op->l_v, op->u_rp, op->u_ci, op->u_v, rr, r);
+        else
+            orc_split_left(op->sp, rr, r);
+        beta = norm2(r, n);
+        resid = beta / normb;
+        hist_push(&hs, resid);
+        if (resid < *tol) {
+            *tol = resid;
+            *max_iter = j;
+            ret = 0;
+            goto out;
+        }
+    }
+    *tol = resid;
+    ret = 1;
+out:
+    if (hist_len) *hist_len = hs.len < hist_cap ? hs.len : hist_cap;
+    if (inner_iters) *inner_iters = done_iters;
+    free(s); free(cs); free(sn); free(w); free(ww); free(r); free(rr); free(bb);
+    free(H); free(V); free(y);
+    return ret;
+}
+
+int orc_gmres_left(int n, const int *rp, const int *ci, const double *v,
+                   const int *l_rp, const int *l_ci, const double *l_v,
+                   const int *u_rp, const int *u_ci, const double *u_v,
+                   const double *b, double *x, int m, int *max_iter, double *tol,
+                   double *hist, int hist_cap, int *hist_len, int *inner_iters)
+{
+    op_t op = {0, n, rp, ci, v, l_rp, l_ci, l_v, u_rp, u_ci, u_v, NULL};
+    return gmres_core(&op, b, x, m, max_iter, tol, hist, hist_cap, hist_len, inner_iters);
+}
+
+int orc_gmres_split(int n, const int *rp, const int *ci, const double *v,
+                    const orc_split_t *p,
+                    const double *b, double *x, int m, int *max_iter, double *tol,
+                    double *hist, int hist_cap, int *hist_len, int *inner_iters)
+{
+    op_t op = {1, n, rp, ci, v, NULL, NULL, NULL, NULL, NULL, NULL, p};
+    return gmres_core(&op, b, x, m, max_iter, tol, hist, hist_cap, hist_len, inner_iters);
+}

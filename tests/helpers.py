@@ -1,0 +1,56 @@
+"""Shared test helpers: synthetic split (ILU++/PG) preconditioners, comparisons."""
+import numpy as np
+import scipy.sparse as sp
+
+import oracle as O
+
+
+def csr_sp(T):
+    """oracle CSR tuple -> scipy csr"""
+    return sp.csr_matrix((T.v, T.ci, T.rp), shape=(T.n, T.n))
+
+
+def make_split(A, seed=7):
+    """Synthetic PG split preconditioner for A.
+
+    With pcol = prow^-1, B = P_r D_l^-1 A D_r^-1 P_c is a symmetric permutation
+    of a scaled A; B ~= Lt Ut (oracle ILU(0)); L = Lt D1 (non-unit, diag last),
+    U = M D1^-1 Ut (diag first) so that Ml A Mr = L^-1 B U^-1 M ~= I."""
+    A = sp.csr_matrix(A)
+    n = A.shape[0]
+    rng = np.random.default_rng(seed)
+    prow = rng.permutation(n).astype(np.int32)
+    pcol = np.argsort(prow).astype(np.int32)
+    lscale = rng.uniform(0.5, 2.0, n)
+    rscale = rng.uniform(0.5, 2.0, n)
+    middle = rng.uniform(0.5, 2.0, n)
+    d1 = rng.uniform(0.5, 2.0, n)
+    Pr = sp.csr_matrix((np.ones(n), (np.arange(n), prow)), shape=(n, n))
+    Pc = sp.csr_matrix((np.ones(n), (np.arange(n), pcol)), shape=(n, n))
+    B = (Pr @ sp.diags(1.0 / lscale) @ A @ sp.diags(1.0 / rscale) @ Pc).tocsr()
+    B.sort_indices()
+    Lt, Ut = O.ilu0(B)
+    Ls = csr_sp(Lt) @ sp.diags(d1)
+    Us = sp.diags(middle / d1) @ csr_sp(Ut)
+    L = O.csr(Ls)
+    U = O.csr(Us)
+    return O.Split(L, U, middle, prow, pcol, lscale, rscale)
+
+
+def rel_err(a, b):
+    a = np.asarray(a, float)
+    b = np.asarray(b, float)
+    d = np.linalg.norm(a - b)
+    s = np.linalg.norm(b)
+    return d / s if s else d
+
+
+def hist_close(h_test, h_ref, rtol):
+    """Residual histories equal in length and within rtol elementwise (relative)."""
+    h_test = np.asarray(h_test)
+    h_ref = np.asarray(h_ref)
+    if h_test.shape != h_ref.shape:
+        return False, f"length {h_test.shape} vs {h_ref.shape}"
+    denom = np.maximum(np.abs(h_ref), 1e-300)
+    dev = np.max(np.abs(h_test - h_ref) / denom) if h_ref.size else 0.0
+    return dev <= rtol, f"max rel dev {dev:.3e}"

@@ -1,0 +1,173 @@
+"""The C-ABI library: builds, loads, exports every declared symbol; host-side
+setup code (factorization, grid detection) matches the oracle.  CPU only --
+no GPU compute is called here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import PKG, REPO, fixture_path
+from ggmres import matrices as M
+
+HEADERS = ["ggmres.h", "ggmres_host.h"]
+
+
+def declared(header):
+    txt = open(os.path.join(REPO, "include", header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gg_\w+)\s*\(", txt)))
+
+
+def exported():
+    out = subprocess.check_output(["nm", "-D", "--defined-only", os.path.join(PKG, "lib", "libggmres.so")],
+                                  text=True)
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+def test_library_exports_every_declared_symbol(ggmres_lib):
+    syms = exported()
+    for h in HEADERS:
+        names = declared(h)
+        assert names, h
+        missing = [s for s in names if s not in syms]
+        assert not missing, f"{h}: not exported: {missing}"
+    import ggmres
+    assert set(ggmres.EXPORTS) == set(declared("ggmres.h"))
+    for name in ggmres.EXPORTS:
+        getattr(ggmres_lib, name)   # resolvable through ctypes
+
+
+def test_reference_boundary_classes_exported(ggmres_lib):
+    out = subprocess.check_output(
+        f"nm -D --defined-only {os.path.join(PKG, 'lib', 'libggmres.so')} | c++filt", shell=True, text=True)
+    for sig in ["gmresInterfacePGfloat::setPrecondPG(MySpMatrix*, MySpMatrixDouble*, MySpMatrixDouble*, "
+                "MySpMatrix*, MySpMatrix*, MySpMatrix*, MySpMatrix*, MySpMatrix*)",
+                "gmresInterfacePGfloat::GMRES_dev_PG()", "gmresInterfacePGfloat::GMRES_host_PG()",
+                "gmresInterfacePGfloat::~gmresInterfacePGfloat()",
+                "gmresInterfacePG::setPrecondPG(MySpMatrix*, MySpMatrixDouble*, MySpMatrixDouble*, "
+                "MySpMatrix*, MySpMatrix*, MySpMatrix*, MySpMatrixDouble*, MySpMatrixDouble*)",
+                "gmresInterfacePG::GMRES_host_PG()", "gmresInterfacePG::~gmresInterfacePG()"]:
+        assert sig in out, sig
+
+
+def test_headers_compile_as_c_and_cpp(tmp_path):
+    c = tmp_path / "t.c"
+    c.write_text('#include "ggmres.h"\n#include "ggmres_host.h"\nint main(void){gg_options o; (void)o; return 0;}\n')
+    subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only",
+                           f"-I{REPO}/include", str(c)])
+    cc = tmp_path / "t.cpp"
+    cc.write_text('#include "gmres_interface_pg.h"\n#include <cstddef>\n'
+                  'static_assert(sizeof(gmresInterfacePGfloat) == 120, "layout");\n'
+                  'static_assert(offsetof(gmresInterfacePGfloat, rhs_h) == 80, "layout");\n'
+                  'int main(){return 0;}\n')
+    subprocess.check_call(["g++", "-std=c++11", "-Wall", "-fsyntax-only",
+                           f"-I{REPO}/include/compat", f"-I{REPO}/include", str(cc)])
+
+
+def test_status_strings_and_version(ggmres_lib):
+    ggmres_lib.gg_strerror.restype = ctypes.c_char_p
+    assert ggmres_lib.gg_abi_version() == 1
+    assert ggmres_lib.gg_strerror(0) == b"converged"
+    assert ggmres_lib.gg_strerror(1) == b"not converged"
+    assert ggmres_lib.gg_strerror(-3) == b"zero pivot in factorization"
+
+
+# ------------------------------------------------------ host setup vs oracle
+PI = ctypes.POINTER(ctypes.c_int)
+PD = ctypes.POINTER(ctypes.c_double)
+
+
+def host_factor(lib, A, level=None):
+    A = O.csr(A)
+    n = A.n
+    lrp = np.zeros(n + 1, np.int32)
+    urp = np.zeros(n + 1, np.int32)
+    lci, lv, uci, uv = PI(), PD(), PI(), PD()
+    args = [ctypes.c_int(n), A.rp.ctypes.data_as(PI), A.ci.ctypes.data_as(PI), A.v.ctypes.data_as(PD),
+            lrp.ctypes.data_as(PI), ctypes.byref(lci), ctypes.byref(lv),
+            urp.ctypes.data_as(PI), ctypes.byref(uci), ctypes.byref(uv)]
+    rc = lib.gg_host_ilu0(*args) if level is None else lib.gg_host_iluk(ctypes.c_int(level), *args)
+    if rc != 0:
+        return rc, None, None
+
+    def take(rp, ci, v):
+        nnz = int(rp[n])
+        out = O.CSR(n, rp, np.ctypeslib.as_array(ci, (max(nnz, 1),))[:nnz].copy(),
+                    np.ctypeslib.as_array(v, (max(nnz, 1),))[:nnz].copy())
+        lib.gg_host_free(ctypes.cast(ci, ctypes.c_void_p))
+        lib.gg_host_free(ctypes.cast(v, ctypes.c_void_p))
+        return out
+    return 0, take(lrp, lci, lv), take(urp, uci, uv)
+
+
+CASES = ["5pt_10x10.mtx", "7pt_10x10x10.mtx", "9pt_10x10.mtx", "3pt_100.mtx", "sherman1.rua"]
+
+
+def load(name):
+    return M.read_rua(fixture_path(name)) if name.endswith(".rua") else M.read_mtx(fixture_path(name))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_host_ilu0_bitexact_vs_oracle(ggmres_lib, name):
+    A = load(name)
+    rc, L, U = host_factor(ggmres_lib, A)
+    assert rc == 0
+    Lo, Uo = O.ilu0(A)
+    for a, b in ((L, Lo), (U, Uo)):
+        assert np.array_equal(a.rp, b.rp) and np.array_equal(a.ci, b.ci)
+        assert np.array_equal(a.v, b.v)   # bit-exact
+
+
+def test_host_ilu0_c1_bitexact(ggmres_lib):
+    A = M.laplacian_5pt(100)
+    rc, L, U = host_factor(ggmres_lib, A)
+    Lo, Uo = O.ilu0(A)
+    assert rc == 0 and np.array_equal(L.v, Lo.v) and np.array_equal(U.v, Uo.v)
+
+
+@pytest.mark.parametrize("name,k", [("5pt_10x10.mtx", 1), ("7pt_10x10x10.mtx", 1), ("9pt_10x10.mtx", 2),
+                                    ("sherman1.rua", 1)])
+def test_host_iluk_bitexact_vs_oracle(ggmres_lib, name, k):
+    A = load(name)
+    rc, L, U = host_factor(ggmres_lib, A, level=k)
+    try:
+        Lo, Uo = O.iluk(A, k)
+    except ZeroDivisionError:
+        assert rc == -3
+        return
+    assert rc == 0
+    for a, b in ((L, Lo), (U, Uo)):
+        assert np.array_equal(a.rp, b.rp) and np.array_equal(a.ci, b.ci)
+        assert np.array_equal(a.v, b.v)
+
+
+def test_host_iluk_zero_pivot(ggmres_lib):
+    import scipy.sparse as sp
+    A = sp.csr_matrix(np.array([[0.0, 1.0], [1.0, 1.0]]))
+    rc, _, _ = host_factor(ggmres_lib, A, level=1)
+    assert rc == -3
+
+
+def wave(lib, L, U):
+    nx, ny = ctypes.c_int(), ctypes.c_int()
+    ok = lib.gg_host_wave2d(ctypes.c_int(L.n), L.rp.ctypes.data_as(PI), L.ci.ctypes.data_as(PI),
+                            L.v.ctypes.data_as(PD), U.rp.ctypes.data_as(PI), U.ci.ctypes.data_as(PI),
+                            U.v.ctypes.data_as(PD), ctypes.byref(nx), ctypes.byref(ny))
+    return ok, nx.value, ny.value
+
+
+def test_wavefront_detection(ggmres_lib):
+    for nx, ny in ((100, 100), (37, 64), (200, 3)):
+        A = M.laplacian_5pt(nx, ny)
+        L, U = O.ilu0(A)
+        assert wave(ggmres_lib, L, U) == (1, nx, ny)
+    # 3D 7-pt, 9-pt and ILU(1) factors do not have the 2D 5-pt structure
+    for A in (M.grid_7pt(8), load("9pt_10x10.mtx")):
+        L, U = O.ilu0(A)
+        assert wave(ggmres_lib, L, U)[0] == 0
+    L, U = O.iluk(M.laplacian_5pt(30), 1)
+    assert wave(ggmres_lib, L, U)[0] == 0

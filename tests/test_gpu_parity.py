@@ -1,0 +1,225 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the fp64 oracle.
+
+Bars (DESIGN.md "Parity"):
+  * SpMV, triangular solves, split preconditioner maps: bit-exact (same
+    per-row operation order, contraction off);
+  * GMRES residual history and solution: within 1e-10 relative per entry
+    (north_star), identical iteration counts and return codes.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import ggmres
+import oracle as O
+from conftest import fixture_path
+from ggmres import matrices as M
+from helpers import hist_close, make_split, rel_err
+
+pytestmark = pytest.mark.gpu
+HIST_RTOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def solver():
+    s = ggmres.Solver(0)
+    yield s
+    s.close()
+
+
+def load(name):
+    return M.read_rua(fixture_path(name)) if name.endswith(".rua") else M.read_mtx(fixture_path(name))
+
+
+MATS = {
+    "c1_5pt_100x100": lambda: M.laplacian_5pt(100),
+    "5pt_37x64": lambda: M.laplacian_5pt(37, 64),
+    "5pt_10x10": lambda: load("5pt_10x10.mtx"),
+    "7pt_10x10x10": lambda: load("7pt_10x10x10.mtx"),
+    "9pt_10x10": lambda: load("9pt_10x10.mtx"),
+    "3pt_100": lambda: load("3pt_100.mtx"),
+    "sherman1": lambda: load("sherman1.rua"),
+    "thermal_7pt_12": lambda: M.grid_7pt(12),
+}
+WAVE = {"c1_5pt_100x100", "5pt_37x64"}
+
+
+@pytest.mark.parametrize("name", sorted(MATS))
+def test_spmv_bitexact(solver, name):
+    A = MATS[name]()
+    x = np.random.default_rng(1).standard_normal(A.shape[0])
+    solver.set_matrix(A)
+    solver.set_precond_none()
+    assert np.array_equal(solver.spmv(x), O.spmv(A, x))
+    solver.set_precond_ilu0()   # wavefront layout where it applies
+    assert solver.uses_wavefront == (name in WAVE)
+    assert np.array_equal(solver.spmv(x), O.spmv(A, x))
+
+
+@pytest.mark.parametrize("name", sorted(MATS))
+@pytest.mark.parametrize("force_level", [False, True])
+def test_ilu0_apply_bitexact(solver, name, force_level, monkeypatch):
+    if force_level:
+        monkeypatch.setenv("GG_NO_WAVEFRONT", "1")
+    A = MATS[name]()
+    L, U = O.ilu0(A)
+    y = np.random.default_rng(2).standard_normal(A.shape[0])
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert solver.uses_wavefront == (name in WAVE and not force_level)
+    z = solver.precond_apply(ggmres.APPLY_MINV, y)
+    assert np.array_equal(z, O.lusolve(L, U, y))
+
+
+def test_lu_precond_user_factors(solver):
+    A = M.laplacian_5pt(50, 70)
+    L, U = O.iluk(A, 1)   # ILU(1) factors: not grid-structured -> level path
+    solver.set_matrix(A)
+    solver.set_precond_lu(L, U)
+    assert not solver.uses_wavefront
+    y = np.random.default_rng(4).random(A.shape[0])
+    assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
+
+
+def test_split_maps_bitexact(solver):
+    A = M.laplacian_5pt(30)
+    P = make_split(A, seed=5)
+    solver.set_matrix(A)
+    solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    v = np.random.default_rng(6).standard_normal(A.shape[0])
+    assert np.array_equal(solver.precond_apply(ggmres.APPLY_LEFT, v), P.left(v))
+    assert np.array_equal(solver.precond_apply(ggmres.APPLY_RIGHT, v), P.right(v))
+    assert np.array_equal(solver.precond_apply(ggmres.APPLY_START, v), P.start(v))
+
+
+def check_gmres(g, o):
+    assert g["ret"] == o["ret"]
+    assert g["iters"] == o["iters"]
+    assert g["inner"] == o["inner"]
+    ok, msg = hist_close(g["hist"], o["hist"], HIST_RTOL)
+    assert ok, msg
+    assert abs(g["relres"] - o["relres"]) <= HIST_RTOL * max(o["relres"], 1e-300)
+    assert rel_err(g["x"], o["x"]) <= 1e-10
+
+
+@pytest.mark.parametrize("m", [30, 32])
+@pytest.mark.parametrize("rhs", ["ones", "uniform"])
+def test_gmres_left_c1_parity(solver, m, rhs):
+    A = M.laplacian_5pt(100)
+    b = M.rhs_ones(A) if rhs == "ones" else M.rhs_uniform(A.shape[0])
+    L, U = O.ilu0(A)
+    o = O.gmres_left(A, L, U, b, m=m, max_iter=3000, tol=1e-10)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert solver.uses_wavefront
+    g = solver.solve(b, restart=m, max_iter=3000, tol=1e-10)
+    check_gmres(g, o)
+
+
+def test_gmres_left_fixed_iterations(solver):
+    # fixed-length run (tol unreachable): exhaustion semantics + full history
+    A = M.laplacian_5pt(100)
+    b = M.rhs_uniform(A.shape[0])
+    L, U = O.ilu0(A)
+    o = O.gmres_left(A, L, U, b, m=30, max_iter=100, tol=1e-300)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    g = solver.solve(b, restart=30, max_iter=100, tol=1e-300)
+    assert o["ret"] == 1 and o["iters"] == 100
+    check_gmres(g, o)
+
+
+@pytest.mark.parametrize("name", ["7pt_10x10x10", "sherman1", "thermal_7pt_12", "5pt_37x64"])
+def test_gmres_left_other_matrices(solver, name):
+    A = MATS[name]()
+    b = M.rhs_uniform(A.shape[0])
+    L, U = O.ilu0(A)
+    o = O.gmres_left(A, L, U, b, m=30, max_iter=2000, tol=1e-10)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    g = solver.solve(b, restart=30, max_iter=2000, tol=1e-10)
+    check_gmres(g, o)
+
+
+def test_gmres_iluk_parity(solver):
+    A = M.grid_7pt(10, 10, 8)
+    b = M.rhs_uniform(A.shape[0])
+    L, U = O.iluk(A, 1)
+    o = O.gmres_left(A, L, U, b, m=20, max_iter=1000, tol=1e-10)
+    solver.set_matrix(A)
+    solver.set_precond_iluk(1)
+    g = solver.solve(b, restart=20, max_iter=1000, tol=1e-10)
+    check_gmres(g, o)
+
+
+def test_gmres_split_parity(solver):
+    A = M.laplacian_5pt(40)
+    P = make_split(A, seed=9)
+    b = M.rhs_uniform(A.shape[0])
+    x0 = np.random.default_rng(3).random(A.shape[0]) * 0.1
+    o = O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11)
+    solver.set_matrix(A)
+    solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    g = solver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
+    check_gmres(g, o)
+
+
+def test_edge_cases(solver):
+    A = M.laplacian_5pt(100)
+    L, U = O.ilu0(A)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    n = A.shape[0]
+    # converged at the initial check ("<=", iters = 0)
+    x0 = np.ones(n)
+    g = solver.solve(A @ x0, x0=x0, restart=10, max_iter=50, tol=1e-10)
+    o = O.gmres_left(A, L, U, A @ x0, x0=x0, m=10, max_iter=50, tol=1e-10)
+    check_gmres(g, o)
+    # zero right-hand side (normb -> 1)
+    g = solver.solve(np.zeros(n), restart=10, max_iter=50, tol=1e-10)
+    assert g["ret"] == 0 and g["iters"] == 0 and np.all(g["x"] == 0)
+    # max_iter = 0: not converged, history = [beta0/normb]
+    b = M.rhs_uniform(n)
+    g = solver.solve(b, restart=10, max_iter=0, tol=1e-10)
+    o = O.gmres_left(A, L, U, b, m=10, max_iter=0, tol=1e-10)
+    check_gmres(g, o)
+    # restart m = 1 and a cycle cut short by max_iter (Update of the last filled column)
+    for m, mi in ((1, 17), (7, 25)):
+        g = solver.solve(b, restart=m, max_iter=mi, tol=1e-300)
+        o = O.gmres_left(A, L, U, b, m=m, max_iter=mi, tol=1e-300)
+        check_gmres(g, o)
+
+
+def test_repeated_solves_identical(solver):
+    A = M.laplacian_5pt(100)
+    b = M.rhs_uniform(A.shape[0])
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    g1 = solver.solve(b, restart=30, max_iter=500, tol=1e-10)
+    g2 = solver.solve(b, restart=30, max_iter=500, tol=1e-10)
+    assert np.array_equal(g1["x"], g2["x"]) and np.array_equal(g1["hist"], g2["hist"])
+
+
+@pytest.mark.slow
+def test_c2_full_size_properties(solver):
+    """C2 (1M rows): first cycle vs the oracle, then size-independent properties."""
+    A = M.laplacian_5pt(1000)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    L, U = O.ilu0(A)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert solver.uses_wavefront
+    # one full restart cycle against the oracle
+    o = O.gmres_left(A, L, U, b, m=30, max_iter=30, tol=1e-300)
+    g = solver.solve(b, restart=30, max_iter=30, tol=1e-300)
+    check_gmres(g, o)
+    # full solve to 1e-8: convergence, true preconditioned residual, monotone cycles
+    g = solver.solve(b, restart=30, max_iter=3000, tol=1e-8)
+    assert g["ret"] == 0 and g["relres"] < 1e-8
+    normb = np.linalg.norm(O.lusolve(L, U, b))
+    true = np.linalg.norm(O.lusolve(L, U, b - A @ g["x"])) / normb
+    assert true < 1e-7
+    h = g["hist"]
+    assert np.all(np.isfinite(h)) and h[0] == pytest.approx(1.0, rel=1e-12)
