@@ -59,6 +59,8 @@ def lib():
                                   _f64p, _f64p]
         for f in (L.orc_split_left, L.orc_split_right, L.orc_split_start):
             f.argtypes = [ctypes.POINTER(SplitT), _f64p, _f64p]
+        L.orc_set_dot_order.argtypes = [ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
+                                        ctypes.c_void_p]
         L.orc_gen_rot.argtypes = [ctypes.c_double, ctypes.c_double, _PD, _PD]
         L.orc_apply_rot.argtypes = [_PD, _PD, ctypes.c_double, ctypes.c_double]
         common = [_f64p, _f64p, ctypes.c_int, _PI, _PD, _f64p, ctypes.c_int, _PI, _PI]
@@ -170,6 +172,21 @@ class Split:
 
     def start(self, v):
         return self._apply(lib().orc_split_start, v)
+
+
+_dot_keep = None
+
+
+def set_dot_order(lay2nat=None, G=1):
+    """None: serial dots (reference CPU engine).  Otherwise restate the device
+    reduction tree over the slot->natural map lay2nat (int64, -1 = padding)."""
+    global _dot_keep
+    if lay2nat is None:
+        _dot_keep = None
+        lib().orc_set_dot_order(0, 0, 1, None)
+    else:
+        _dot_keep = np.ascontiguousarray(lay2nat, np.int64)
+        lib().orc_set_dot_order(1, len(_dot_keep), int(G), _dot_keep.ctypes.data)
 
 
 def gen_rot(dx, dy):

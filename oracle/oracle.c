@@ -405,15 +405,77 @@ void orc_gen_rot(double dx, double dy, double *cs, double *sn)
     }
 }
 
-/* ------------------------------------------------------------ BLAS-1 (serial) */
+/* ------------------------------------------------------------ BLAS-1 */
+/* Summation order of dot products / norms.  The reference's CPU engine sums
+ * serially (src/gmres.cu:60-74); its GPU engine calls cublasSdot/Snrm2, a
+ * parallel tree of unspecified order.  Mode "blocked" restates one concrete
+ * tree -- the device kernels' (DESIGN.md "Reduction order") -- so a solve can
+ * be compared bit-for-bit: vectors laid out by lay2nat over ppad slots
+ * (-1 = padding zero), G blocks of 256 threads, each thread summing its
+ * grid-stride double2 units, 64-lane xor butterflies, (w0+w1)+(w2+w3). */
+static int g_blocked = 0;
+static long long g_ppad = 0;
+static int g_G = 1;
+static const long long *g_lay2nat = NULL;
+
+void orc_set_dot_order(int blocked, long long ppad, int G, const long long *lay2nat)
+{
+    g_blocked = blocked;
+    g_ppad = ppad;
+    g_G = G > 0 ? G : 1;
+    g_lay2nat = lay2nat;
+}
+
+static double block_sum256(double *v)
+{
+    double t[256];
+    for (int w = 0; w < 4; w++)
+        for (int o = 32; o > 0; o >>= 1) {
+            for (int l = 0; l < 64; l++) t[w * 64 + l] = v[w * 64 + l] + v[w * 64 + (l ^ o)];
+            for (int l = 0; l < 64; l++) v[w * 64 + l] = t[w * 64 + l];
+        }
+    return (v[0] + v[64]) + (v[128] + v[192]);
+}
+
+static double dot_blocked(const double *x, const double *y)
+{
+    const long long units = g_ppad / 2;
+    double *part = (double *)malloc((size_t)g_G * sizeof(double));
+    double v[256];
+    for (int blk = 0; blk < g_G; blk++) {
+        for (int t = 0; t < 256; t++) {
+            double acc = 0.0;
+            for (long long u = (long long)blk * 256 + t; u < units; u += (long long)g_G * 256) {
+                long long p0 = g_lay2nat[2 * u], p1 = g_lay2nat[2 * u + 1];
+                double a0 = p0 >= 0 ? x[p0] : 0.0, b0 = p0 >= 0 ? y[p0] : 0.0;
+                double a1 = p1 >= 0 ? x[p1] : 0.0, b1 = p1 >= 0 ? y[p1] : 0.0;
+                acc += a0 * b0;
+                acc += a1 * b1;
+            }
+            v[t] = acc;
+        }
+        part[blk] = block_sum256(v);
+    }
+    for (int t = 0; t < 256; t++) {
+        double acc = 0.0;
+        for (int k = t; k < g_G; k += 256) acc += part[k];
+        v[t] = acc;
+    }
+    double r = block_sum256(v);
+    free(part);
+    return r;
+}
+
 static double dot(const double *x, const double *y, int n)
 {
+    if (g_blocked) return dot_blocked(x, y);
     double t = 0.0;                 /* dot (src/gmres.cu:68-74) */
     for (int i = 0; i < n; i++) t += x[i] * y[i];
     return t;
 }
 static double norm2(const double *v, int n)
 {
+    if (g_blocked) return sqrt(dot_blocked(v, v));
     double t = 0.0;                 /* norm2 (src/gmres.cu:60-66) */
     for (int i = 0; i < n; i++) t += v[i] * v[i];
     return sqrt(t);

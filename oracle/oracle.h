@@ -67,6 +67,11 @@ void orc_split_left(const orc_split_t *p, const double *in, double *out);
 void orc_split_right(const orc_split_t *p, const double *in, double *out);
 void orc_split_start(const orc_split_t *p, const double *in, double *out);
 
+/* Dot-product summation order used by the GMRES restatements: blocked = 0
+ * is the reference CPU engine's serial loop (default); blocked = 1 restates
+ * the device kernels' reduction tree over a laid-out vector (see oracle.c). */
+void orc_set_dot_order(int blocked, long long ppad, int G, const long long *lay2nat);
+
 /* Givens (src/gmres.cu:192-216) */
 void orc_apply_rot(double *dx, double *dy, double cs, double sn);
 void orc_gen_rot(double dx, double dy, double *cs, double *sn);
