@@ -65,15 +65,16 @@ struct Levels {
 Levels level_sets(const CanonTri &T);
 
 // 2D structured-grid wavefront layout (SURVEY.md 7 hard parts)
-//   natural row r = j*nx + i  ->  layout slot ((j/64)*T + i + j%64)*64 + j%64,
-//   T = nx + 63 rounded up to a multiple of 16 (the kernel's batch)
+//   natural row r = j*nx + i, band = j/64, lane l = j%64, step t = i + l:
+//   slot = ((band*(T/2) + t/2)*64 + l)*2 + t%2     (a lane's step pair adjacent)
+//   T = nx + 63 rounded up to a multiple of 32 (two 16-step kernel batches)
 struct Wave2D {
     bool ok = false;
     int nx = 0, ny = 0, nbands = 0, T = 0;
     long long P = 0;         // padded layout length
     long long slot(int r) const {
-        int j = r / nx, i = r % nx;
-        return ((long long)(j >> 6) * T + i + (j & 63)) * 64 + (j & 63);
+        int j = r / nx, i = r % nx, l = j & 63, t = i + l;
+        return (((long long)(j >> 6) * (T / 2) + t / 2) * 64 + l) * 2 + (t & 1);
     }
 };
 // detect: L off-diagonals only at offsets {nx (first), 1 (second)} and U only at

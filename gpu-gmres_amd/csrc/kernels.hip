@@ -221,88 +221,189 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
 }
 
 // 2D structured-grid wavefront solve.  Layout (gg_internal.h Wave2D): band =
-// 64 grid lines = one wave, lane l = line 64*band+l, step t = column i + l.
-// Each step a lane needs its own previous value (same line, column i-+1) and
-// the neighbour line's value from the previous step, moved in-register with
-// DPP wave_shr/wave_shl.  The band boundary (lane 0 / lane 63) is exchanged
-// between bands (workgroups on different CUs) through 8-byte granules whose
-// payload is the flag (sentinel = not ready): relaxed agent-scope (sc1) store
-// by the producer lane, relaxed agent-scope polling loads by the consumer,
-// which resets the slot for the next launch.
-constexpr int kWaveBatch = 16;
+// 64 grid lines, lane l = line 64*band+l, step t = column i + l; a lane's two
+// consecutive steps are adjacent in memory (16 B per array per step pair, 1 KiB
+// per wave instruction).
+//
+// One workgroup per band, four waves, one per SIMD:
+//  * wave 0 (compute) runs the recurrence: each step a lane needs its own
+//    previous value (same line, column i-+1) and the neighbour line's value
+//    from the previous step, moved in-register with DPP wave_shr/wave_shl.  It
+//    reads right-hand side and coefficients from LDS only, so its vector-memory
+//    queue holds nothing but fire-and-forget stores;
+//  * waves 2-3 (loaders) stream b / coefficients HBM -> LDS with LDS-DMA
+//    (global_load_lds_dwordx4) into a kWaveR-slot ring, kWaveR-1 batches ahead,
+//    each retiring a batch with its own counted vmcnt before the barrier;
+//  * wave 1 (boundary) polls the neighbouring band's edge-lane values one batch
+//    ahead and hands them over through LDS.
+// The four waves meet at one raw s_barrier per 16-step batch (no fence, no
+// drain).  Band-to-band hand-off (workgroups on different CUs): 8-byte granules
+// whose payload is the flag (sentinel = not ready): the producing compute wave
+// stores one 16-lane batch per 16 steps with relaxed agent-scope (sc1) stores;
+// the boundary wave polls with relaxed agent-scope loads and re-arms each slot
+// (sc1 sentinel store) for the next launch.  Every spin is bounded.
+constexpr int kWaveBatch = 16;             // steps per batch
+constexpr int kWavePB = kWaveBatch / 2;    // step pairs per batch
+constexpr int kWaveR = 4;                  // LDS ring slots (batches)
 constexpr int kSpinLimit = 1 << 20;
 
-template <bool FWD, bool UNIT>
-__global__ __launch_bounds__(64) void k_trsv_wave2d(Gate g, int nx, int T, int nbands,
-                                                    const double *__restrict__ b,
-                                                    const double *__restrict__ c1,
-                                                    const double *__restrict__ c2,
-                                                    const double *__restrict__ dv,
-                                                    double *__restrict__ x,
-                                                    unsigned long long *bnd, int *err)
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+// s_waitcnt immediate: wait until <= n vector-memory ops are outstanding (gfx9)
+__host__ __device__ constexpr int vm_wait(int n)
 {
+    return (n & 15) | (7 << 4) | (0xF << 8) | (((n >> 4) & 3) << 14);
+}
+
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// loader wave: NA arrays starting at a0, batch j -> ring slot j % kWaveR
+template <bool FWD, int A, int NA>
+__device__ __forceinline__ void wave_loader(const double2 *const *src, int a0, double2 *lds, int np,
+                                            int nbatch)
+{
+    constexpr int SLOT = A * kWavePB * 64;      // double2 per ring slot
+    constexpr int NPER = NA * kWavePB;          // DMA instructions per batch
+    auto issue = [&](int j) {
+        double2 *slot = lds + (j % kWaveR) * SLOT;
+#pragma unroll
+        for (int ai = 0; ai < NA; ai++)
+#pragma unroll
+            for (int kk = 0; kk < kWavePB; kk++) {
+                const int p = j * kWavePB + kk;
+                const long long q = (long long)(FWD ? p : np - 1 - p) * 64;
+                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src[a0 + ai] + q),
+                                                 (lds_void_t *)(slot + (a0 + ai) * kWavePB * 64 + kk * 64),
+                                                 16, 0, 0);
+            }
+    };
+    for (int j = 0; j < kWaveR - 1 && j < nbatch; j++) issue(j);
+    for (int j = 0; j < nbatch; j++) {
+        // batch j has landed when at most the batches issued after it are in flight
+        const int after = (j + kWaveR - 1 < nbatch ? j + kWaveR - 1 : nbatch) - j - 1;
+        if (after >= 2) __builtin_amdgcn_s_waitcnt(vm_wait(2 * NPER));
+        else if (after == 1) __builtin_amdgcn_s_waitcnt(vm_wait(NPER));
+        else __builtin_amdgcn_s_waitcnt(vm_wait(0));
+        raw_barrier();                          // batch j visible; slot (j-1) % R free
+        if (j + kWaveR - 1 < nbatch) issue(j + kWaveR - 1);
+    }
+}
+
+template <bool FWD, bool UNIT>
+__global__ __launch_bounds__(256) void k_trsv_wave2d(Gate g, int nx, int T, int nbands,
+                                                     const double *__restrict__ b,
+                                                     const double *__restrict__ c1,
+                                                     const double *__restrict__ c2,
+                                                     const double *__restrict__ dv,
+                                                     double *__restrict__ x,
+                                                     unsigned long long *bnd, int *err)
+{
+    static_assert(kWaveR == 4, "loader waits are written for a 4-slot ring");
     if (gated(g)) return;
+    constexpr int A = UNIT ? 3 : 4;             // streamed arrays: b, c1, c2 (, d)
+    constexpr int SLOT = A * kWavePB * 64;      // double2 per ring slot
+    // one LDS object: data ring, then the 2 x 16 boundary values
+    __shared__ double2 lds[kWaveR * SLOT + kWaveBatch];
+    double *bring = reinterpret_cast<double *>(lds + kWaveR * SLOT);
     const int band = FWD ? blockIdx.x : (nbands - 1 - blockIdx.x);
-    const int lane = threadIdx.x;
-    const long long base = (long long)band * T * 64 + lane;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int np = T / 2;                       // step pairs per band
+    const int nbatch = T / kWaveBatch;          // T is a multiple of kWaveBatch
     const bool has_src = FWD ? (band > 0) : (band < nbands - 1);
     const bool is_prod = FWD ? (band < nbands - 1) : (band > 0);
-    const int edge = FWD ? 0 : 63;          // lane that consumes the boundary
-    unsigned long long *src = bnd + (long long)(FWD ? band - 1 : band + 1) * nx;
-    unsigned long long *dst = bnd + (long long)band * nx;
+    const long long boff = (long long)band * np * 64 + lane;    // double2 units
 
-    double xp = 0.0;                        // this lane's previous step value
-    const int nbatch = T / kWaveBatch;      // T is a multiple of kWaveBatch
-    bool dead = false;                      // gave up waiting once: never wait again
-    for (int bi = 0; bi < nbatch; bi++) {
-        // ---- boundary batch: lane k holds the value the edge lane needs at
-        //      batch step k (FWD: column t; BWD: column t-63)
-        double bv = 0.0;
-        if (has_src && !dead) {
-            const int tk = FWD ? bi * kWaveBatch + lane : (T - 1) - (bi * kWaveBatch + lane);
-            const int col = FWD ? tk : tk - 63;
-            const bool need = lane < kWaveBatch && col >= 0 && col < nx &&
-                              (FWD ? tk < T : tk >= 0);
-            unsigned long long bits = kSentinel;
-            int spins = 0;
-            while (true) {
-                if (need) bits = ld_agent(src + col);
-                const bool ok = !need || bits != kSentinel;
-                if (__all(ok)) break;
-                if (++spins > kSpinLimit) {
-                    if (lane == 0) atomicOr(err, 1);
-                    dead = true;
-                    break;
+    if (wave >= 2) {
+        // ------------------------------------------------ loader waves
+        const double2 *src[4] = {reinterpret_cast<const double2 *>(b) + boff,
+                                 reinterpret_cast<const double2 *>(c1) + boff,
+                                 reinterpret_cast<const double2 *>(c2) + boff,
+                                 UNIT ? nullptr : reinterpret_cast<const double2 *>(dv) + boff};
+        if (wave == 2) wave_loader<FWD, A, 2>(src, 0, lds, np, nbatch);
+        else wave_loader<FWD, A, A - 2>(src, 2, lds, np, nbatch);
+        return;
+    }
+    if (wave == 1) {
+        // ------------------------------------------------ boundary wave
+        // before barrier j it has placed batch j's values in bring[j & 1];
+        // between barriers j and j+1 it fetches batch j+1
+        unsigned long long *src = bnd + (long long)(FWD ? band - 1 : band + 1) * nx;
+        bool dead = false;
+        for (int bi = 0; bi < nbatch; bi++) {
+            if (has_src) {
+                // column the compute wave's edge lane needs at step `lane` of batch bi
+                const int t = FWD ? bi * kWaveBatch + lane : (T - 1) - (bi * kWaveBatch + lane);
+                const int c = FWD ? t : t - 63;
+                const int col = (lane < kWaveBatch && c >= 0 && c < nx) ? c : -1;
+                unsigned long long v = (col >= 0 && !dead) ? ld_agent(src + col) : 0ull;
+                int spins = 0;
+                while (!dead && !__all(col < 0 || v != kSentinel)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (col >= 0 && v == kSentinel) v = ld_agent(src + col);
+                    if (++spins > kSpinLimit) {
+                        dead = true;
+                        if (lane == 0) atomicOr(err, 1);
+                    }
                 }
-                __builtin_amdgcn_s_sleep(1);
+                if (col >= 0) st_agent(src + col, kSentinel);   // re-arm for the next launch
+                if (lane < kWaveBatch)
+                    bring[(bi & 1) * kWaveBatch + lane] =
+                        (col >= 0) ? __longlong_as_double((long long)v) : 0.0;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
-            if (need) {
-                bv = __longlong_as_double((long long)bits);
-                src[col] = kSentinel;   // re-arm for the next launch
-            }
+            raw_barrier();
         }
+        return;
+    }
+
+    // ---------------------------------------------------- compute wave
+    double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
+    constexpr int edge = FWD ? 0 : 63;      // lane that consumes the boundary
+    constexpr int plane = FWD ? 63 : 0;     // lane whose values the next band needs
+    unsigned long long *dst = bnd + (long long)band * nx;
+    double xp = 0.0;                        // this lane's previous step value
+    double bacc = 0.0;                      // producer-lane values of this batch (lane k = step k)
+    for (int bi = 0; bi < nbatch; bi++) {
+        raw_barrier();                      // batch bi's data and boundary values are in LDS
+        const double2 *sl = lds + (bi % kWaveR) * SLOT + lane;
+        const double bv = (has_src && lane < kWaveBatch) ? bring[(bi & 1) * kWaveBatch + lane] : 0.0;
 #pragma unroll
-        for (int tt = 0; tt < kWaveBatch; tt++) {
-            const int t = FWD ? bi * kWaveBatch + tt : (T - 1) - (bi * kWaveBatch + tt);
-            const long long idx = base + (long long)t * 64;
-            const double bb = b[idx], a1 = c1[idx], a2 = c2[idx];
-            double xs = FWD ? dpp_shr1(xp) : dpp_shl1(xp);
-            const double bval = readlane_d(bv, tt);
-            if (lane == edge) xs = has_src ? bval : 0.0;
-            double acc = bb - a1 * xs;      // line neighbour first (|offset| = nx)
-            acc = acc - a2 * xp;            // then the in-line neighbour (|offset| = 1)
-            if (!UNIT) acc = acc / dv[idx];
-            xp = acc;
-            x[idx] = acc;
-            if (is_prod) {
-                if (FWD) {
-                    if (lane == 63 && t - 63 >= 0 && t - 63 < nx)
-                        st_agent(dst + (t - 63), (unsigned long long)__double_as_longlong(acc));
-                } else {
-                    if (lane == 0 && t < nx)
-                        st_agent(dst + t, (unsigned long long)__double_as_longlong(acc));
-                }
+        for (int kk = 0; kk < kWavePB; kk++) {
+            const int p = bi * kWavePB + kk;
+            const double2 cb = sl[0 * kWavePB * 64 + kk * 64];
+            const double2 a1 = sl[1 * kWavePB * 64 + kk * 64];
+            const double2 a2 = sl[2 * kWavePB * 64 + kk * 64];
+            double2 dd = make_double2(1.0, 1.0);
+            if (!UNIT) dd = sl[3 * kWavePB * 64 + kk * 64];
+            double xo0 = 0.0, xo1 = 0.0;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int tt = 2 * kk + h;                       // step within the batch
+                const bool sx = FWD ? (h == 0) : (h == 1);       // even step <-> .x
+                const double bb = sx ? cb.x : cb.y, e1 = sx ? a1.x : a1.y, e2 = sx ? a2.x : a2.y;
+                double xs = FWD ? dpp_shr1(xp) : dpp_shl1(xp);
+                const double bval = readlane_d(bv, tt);
+                if (lane == edge) xs = has_src ? bval : 0.0;
+                double acc = bb - e1 * xs;      // line neighbour first (|offset| = nx)
+                acc = acc - e2 * xp;            // then the in-line neighbour (|offset| = 1)
+                if (!UNIT) acc = acc / (sx ? dd.x : dd.y);
+                xp = acc;
+                if (sx) xo0 = acc; else xo1 = acc;
+                const double pv = readlane_d(acc, plane);
+                if (lane == tt) bacc = pv;
             }
+            X2[(long long)(FWD ? p : np - 1 - p) * 64] = make_double2(xo0, xo1);
+        }
+        // ---- publish this batch's producer-lane values (lanes 0..15), issued by
+        //      every lane (lanes with nothing to publish write a dummy slot)
+        {
+            const int t = FWD ? bi * kWaveBatch + lane : (T - 1) - (bi * kWaveBatch + lane);
+            const int c = FWD ? t - 63 : t;
+            const bool real = is_prod && lane < kWaveBatch && c >= 0 && c < nx;
+            st_agent(real ? dst + c : bnd + (long long)nbands * nx + lane,
+                     (unsigned long long)__double_as_longlong(bacc));
         }
     }
 }
@@ -578,7 +679,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         }
     } else if (T.kind == DevTri::WAVE2D) {
         const Wave2D &w = T.wl;
-        dim3 grid(w.nbands), blk(64);
+        dim3 grid(w.nbands), blk(256);
         if (T.lower) {
             if (T.unit)
                 k_trsv_wave2d<true, true><<<grid, blk, 0, st>>>(g, w.nx, w.T, w.nbands, b, T.c1.p,

@@ -70,7 +70,7 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         T.c2.upload(c2, st);
         if (!unit) T.dw.upload(dv, st);
         const long long stride = round_up(nx, 16);
-        T.bnd.alloc((size_t)wl->nbands * stride);
+        T.bnd.alloc((size_t)wl->nbands * stride + 64);   // + 64 dummy slots (kernels.hip)
         launch_fill_u64(T.bnd.p, (long long)wl->nbands * stride, kSentinel, st);
         // algorithmic bytes: b, two coefficients, (divisor), x  per grid point
         T.bytes = (double)n * (8.0 * (unit ? 4 : 5));

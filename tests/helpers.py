@@ -59,20 +59,23 @@ def hist_close(h_test, h_ref, rtol):
 # ---- the device vector space (DESIGN.md "Wavefront layout", "Reduction order")
 def device_layout(n, nx=None):
     """(lay2nat, G) of the solver's vector space: natural order, or -- for a 2D
-    grid of line length nx on the wavefront path -- band b = 64 lines, slot
-    ((j//64)*T + i + j%64)*64 + j%64 with T = roundup(nx+63, 16); padded to a
-    multiple of 512 slots; G = min(1024, ceil(Ppad/2 / 1024)) reduction blocks."""
+    grid of line length nx on the wavefront path -- band = j//64, lane l = j%64,
+    step t = i + l, slot ((band*T/2 + t//2)*64 + l)*2 + t%2 with
+    T = roundup(nx+63, 32); padded to a multiple of 512 slots;
+    G = min(1024, ceil(Ppad/2 / 1024)) reduction blocks."""
     if nx is None:
         P = n
         slots = np.arange(n, dtype=np.int64)
     else:
         ny = n // nx
-        T = (nx + 63 + 15) // 16 * 16
+        T = (nx + 63 + 31) // 32 * 32
         nb = (ny + 63) // 64
         P = nb * T * 64
         r = np.arange(n, dtype=np.int64)
         j, i = r // nx, r % nx
-        slots = ((j // 64) * T + i + j % 64) * 64 + j % 64
+        lane = j % 64
+        t = i + lane
+        slots = (((j // 64) * (T // 2) + t // 2) * 64 + lane) * 2 + t % 2
     ppad = max((max(P, 1) + 511) // 512 * 512, 512)
     lay2nat = np.full(ppad, -1, np.int64)
     lay2nat[slots] = np.arange(n, dtype=np.int64)
