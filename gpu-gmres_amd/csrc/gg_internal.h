@@ -67,7 +67,7 @@ Levels level_sets(const CanonTri &T);
 // 2D structured-grid wavefront layout (SURVEY.md 7 hard parts)
 //   natural row r = j*nx + i, band = j/64, lane l = j%64, step t = i + l:
 //   slot = ((band*(T/2) + t/2)*64 + l)*2 + t%2     (a lane's step pair adjacent)
-//   T = nx + 63 rounded up to a multiple of 32 (two 16-step kernel batches)
+//   T = nx + 63 rounded up to a multiple of 64 (four 16-step kernel batches)
 struct Wave2D {
     bool ok = false;
     int nx = 0, ny = 0, nbands = 0, T = 0;
@@ -128,6 +128,9 @@ struct DevCsr {
     void upload(const Csr &A, hipStream_t st);
 };
 
+// wavefront division modes: unit diagonal, IEEE division, reciprocal + FMA corrections
+enum WaveDiv { WD_UNIT = 0, WD_HW = 1, WD_RCP = 2 };
+
 // device triangular solve
 struct DevTri {
     enum Kind { NONE, LEVEL, WAVE2D } kind = NONE;
@@ -140,9 +143,11 @@ struct DevTri {
     DBuf<int> lev_rows;
     // WAVE2D (layout arrays, length P)
     Wave2D wl;
-    DBuf<double> c1, c2, dw;     // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor
-    bool unit = false;           // dw == 1 everywhere: skip the division load
-    DBuf<unsigned long long> bnd;  // nbands * nx boundary granules (sentinel = not ready)
+    DBuf<double> c1, c2, dw, rw; // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor, rw: RN(1/dw)
+    int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
+    bool rcp_ok = false;         // every divisor admits WD_RCP
+    DBuf<unsigned long long> bnd;  // nbands * T hand-off granules (sentinel = not ready) + 128 dummies
+    long long *trace = nullptr;  // diagnostics: per band, nbatch+1 timestamps (gg_trace_precond)
     double bytes = 0;            // algorithmic bytes per solve
 };
 

@@ -143,7 +143,7 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
     w.nx = nx;
     w.ny = n / nx;
     w.nbands = (w.ny + 63) / 64;
-    w.T = (nx + 63 + 31) / 32 * 32;   // whole 16-step batches, even batch count (ring turns)
+    w.T = (nx + 63 + 63) / 64 * 64;   // whole 16-step batches, batch count a multiple of 4
     w.P = (long long)w.nbands * w.T * 64;
     return w;
 }

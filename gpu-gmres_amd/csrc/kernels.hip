@@ -64,28 +64,7 @@ __device__ __forceinline__ void st2(double *p, long long u, double2 v)
     reinterpret_cast<double2 *>(p)[u] = v;
 }
 
-// ---- DPP lane shifts (gfx9 wave_shr:1 / wave_shl:1) -----------------------------
-__device__ __forceinline__ double dpp_shr1(double v)
-{
-    int lo = __double2loint(v), hi = __double2hiint(v);
-    lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xf, 0xf, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double dpp_shl1(double v)
-{
-    int lo = __double2loint(v), hi = __double2hiint(v);
-    lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xf, 0xf, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double readlane_d(double v, int l)
-{
-    int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-
+// ---- relaxed agent-scope loads/stores for the band hand-off --------------------
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -225,27 +204,56 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
 // consecutive steps are adjacent in memory (16 B per array per step pair, 1 KiB
 // per wave instruction).
 //
-// One workgroup per band, four waves, one per SIMD:
-//  * wave 0 (compute) runs the recurrence: each step a lane needs its own
+// One workgroup per band, 3 + A waves (A = streamed arrays: b, c1, c2 and, for
+// a non-unit triangle, the divisor d and its reciprocal):
+//  * wave 0 (compute) runs the recurrence.  Each step a lane needs its own
 //    previous value (same line, column i-+1) and the neighbour line's value
-//    from the previous step, moved in-register with DPP wave_shr/wave_shl.  It
-//    reads right-hand side and coefficients from LDS only, so its vector-memory
-//    queue holds nothing but fire-and-forget stores;
-//  * waves 2-3 (loaders) stream b / coefficients HBM -> LDS with LDS-DMA
-//    (global_load_lds_dwordx4) into a kWaveR-slot ring, kWaveR-1 batches ahead,
-//    each retiring a batch with its own counted vmcnt before the barrier;
-//  * wave 1 (boundary) polls the neighbouring band's edge-lane values one batch
-//    ahead and hands them over through LDS.
-// The four waves meet at one raw s_barrier per 16-step batch (no fence, no
-// drain).  Band-to-band hand-off (workgroups on different CUs): 8-byte granules
-// whose payload is the flag (sentinel = not ready): the producing compute wave
-// stores one 16-lane batch per 16 steps with relaxed agent-scope (sc1) stores;
-// the boundary wave polls with relaxed agent-scope loads and re-arms each slot
-// (sc1 sentinel store) for the next launch.  Every spin is bounded.
-constexpr int kWaveBatch = 16;             // steps per batch
+//    from the previous step, moved in-register with DPP wave_shr/wave_shl; the
+//    edge lane keeps the DPP "old" operand, which holds the neighbouring band's
+//    value.  Its operands come from LDS one batch ahead (a register ring of
+//    step pairs refilled right after use), so the recurrence never waits on
+//    memory; its results go to LDS staging (a global store costs the issuing
+//    wave ~50 cycles, an LDS write a few);
+//  * wave 2 (writer) stores the compute wave's x from LDS staging to HBM and
+//    publishes the band's edge values, one batch behind;
+//  * waves 3.. (loaders, one array each) stream HBM -> LDS with LDS-DMA
+//    (global_load_lds_dwordx4) into an R-slot ring, each retiring batches with
+//    its own counted vmcnt before the barrier (batches j and j+1 by barrier j);
+//  * wave 1 (boundary) polls the neighbouring band's edge values and hands
+//    them over through LDS.
+// All waves meet at one raw s_barrier per batch (no fence, no drain).
+// Band-to-band hand-off (workgroups on different CUs): one 8-byte granule per
+// step, bnd[band*T + t], whose payload is the flag (sentinel = not ready).  The
+// producing band's writer wave stores the edge values of a batch with one
+// relaxed agent-scope (sc1) store; the consumer polls with relaxed agent-scope loads
+// and re-arms each granule it read (sc1 sentinel store) for the next launch.
+// Every spin is bounded.
+//
+// Division (non-unit triangles).  x = RN(acc / d) is needed bit-exactly.  The
+// IEEE division sequence (div_scale/rcp/fma/div_fmas/div_fixup) is ~70 cycles
+// of dependent latency per step; WD_RCP instead uses the host-computed
+// reciprocal y = RN(1/d) and two FMA corrections (Markstein):
+//   q0 = RN(acc*y); q1 = RN(q0 + RN(acc - d*q0)*y); q2 = RN(q1 + (acc - d*q1)*y)
+// q1 is within one ulp of acc/d, so acc - d*q1 is exact and q2 = RN(acc/d)
+// (Markstein's theorem; y within half an ulp of 1/d).  The remainders are
+// formed as -(d*q - acc) so signed zeros come out as in acc/d.  The theorem
+// needs every intermediate in the normal range: the host admits WD_RCP only for
+// 2^-100 <= |d| <= 2^100, and each step flags |acc| outside [2^-900, 2^900]
+// (err bit 2), on which the caller repeats the work with WD_HW.
+constexpr int kWaveBatch = 8;              // steps per batch
 constexpr int kWavePB = kWaveBatch / 2;    // step pairs per batch
-constexpr int kWaveR = 4;                  // LDS ring slots (batches)
 constexpr int kSpinLimit = 1 << 20;
+
+template <int DIV>
+struct WaveCfg {
+    static constexpr int A = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;   // streamed arrays
+    static constexpr int SLOT = A * kWavePB * 64;                        // double2 per ring slot
+    static constexpr int R = (144 * 1024) / (SLOT * 16);                 // ring slots: 12 / 9 / 7
+    static constexpr int THREADS = (3 + A) * 64;                        // compute, boundary, writer, loaders
+    static constexpr int LDS2 = R * SLOT + 64 + 2 * kWavePB * 64;        // ring, boundary, x staging
+    static_assert(R >= 4 && (R - 3) * kWavePB <= 63, "ring depth vs vmcnt range");
+    static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
+};
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
@@ -255,156 +263,275 @@ __host__ __device__ constexpr int vm_wait(int n)
 {
     return (n & 15) | (7 << 4) | (0xF << 8) | (((n >> 4) & 3) << 14);
 }
-
-__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
-// loader wave: NA arrays starting at a0, batch j -> ring slot j % kWaveR
-template <bool FWD, int A, int NA>
-__device__ __forceinline__ void wave_loader(const double2 *const *src, int a0, double2 *lds, int np,
-                                            int nbatch)
+// wait until at most max(min(after, K), 0) batches of NPER instructions are in flight
+template <int K, int NPER>
+__device__ __forceinline__ void vm_wait_batches(int after)
 {
-    constexpr int SLOT = A * kWavePB * 64;      // double2 per ring slot
-    constexpr int NPER = NA * kWavePB;          // DMA instructions per batch
-    auto issue = [&](int j) {
-        double2 *slot = lds + (j % kWaveR) * SLOT;
-#pragma unroll
-        for (int ai = 0; ai < NA; ai++)
-#pragma unroll
-            for (int kk = 0; kk < kWavePB; kk++) {
-                const int p = j * kWavePB + kk;
-                const long long q = (long long)(FWD ? p : np - 1 - p) * 64;
-                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src[a0 + ai] + q),
-                                                 (lds_void_t *)(slot + (a0 + ai) * kWavePB * 64 + kk * 64),
-                                                 16, 0, 0);
-            }
-    };
-    for (int j = 0; j < kWaveR - 1 && j < nbatch; j++) issue(j);
-    for (int j = 0; j < nbatch; j++) {
-        // batch j has landed when at most the batches issued after it are in flight
-        const int after = (j + kWaveR - 1 < nbatch ? j + kWaveR - 1 : nbatch) - j - 1;
-        if (after >= 2) __builtin_amdgcn_s_waitcnt(vm_wait(2 * NPER));
-        else if (after == 1) __builtin_amdgcn_s_waitcnt(vm_wait(NPER));
-        else __builtin_amdgcn_s_waitcnt(vm_wait(0));
-        raw_barrier();                          // batch j visible; slot (j-1) % R free
-        if (j + kWaveR - 1 < nbatch) issue(j + kWaveR - 1);
+    if constexpr (K == 0) {
+        __builtin_amdgcn_s_waitcnt(vm_wait(0));
+    } else {
+        static_assert(K * NPER <= 63, "vmcnt is 6 bits");
+        if (after >= K) __builtin_amdgcn_s_waitcnt(vm_wait(K * NPER));
+        else vm_wait_batches<K - 1, NPER>(after);
     }
 }
 
-template <bool FWD, bool UNIT>
-__global__ __launch_bounds__(256) void k_trsv_wave2d(Gate g, int nx, int T, int nbands,
-                                                     const double *__restrict__ b,
-                                                     const double *__restrict__ c1,
-                                                     const double *__restrict__ c2,
-                                                     const double *__restrict__ dv,
-                                                     double *__restrict__ x,
-                                                     unsigned long long *bnd, int *err)
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// 64-bit DPP lane shift whose out-of-range lane keeps `old`
+template <int CTRL>
+__device__ __forceinline__ double dpp_shift_old(double v, double old)
 {
-    static_assert(kWaveR == 4, "loader waits are written for a 4-slot ring");
+    int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, 0xf, 0xf, false);
+    int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+// loader wave: one array; batch j -> ring slot j % R; batches j, j+1 landed by barrier j
+template <bool FWD, int R, int SLOT>
+__device__ __forceinline__ void wave_loader(const double2 *src, double2 *lds, int np, int nbatch)
+{
+    auto issue = [&](int j) {
+        double2 *slot = lds + (j % R) * SLOT;
+#pragma unroll
+        for (int kk = 0; kk < kWavePB; kk++) {
+            const int p = j * kWavePB + kk;
+            const long long q = (long long)(FWD ? p : np - 1 - p) * 64;
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + q), (lds_void_t *)(slot + kk * 64), 16, 0, 0);
+        }
+    };
+    for (int j = 0; j < R - 1 && j < nbatch; j++) issue(j);
+    for (int j = 0; j < nbatch; j++) {
+        // batches after j+1 may stay in flight
+        const int issued = j + R - 1 < nbatch ? j + R - 1 : nbatch;
+        vm_wait_batches<R - 3, kWavePB>(issued - (j + 2));
+        raw_barrier();                          // slot (j-1) % R is free from here on
+        if (j + R - 1 < nbatch) issue(j + R - 1);
+    }
+}
+
+template <bool FWD, int DIV, bool TRACE>
+__global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
+    Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
+    const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
+    double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace)
+{
+    using C = WaveCfg<DIV>;
+    constexpr int PB = kWavePB * 64;            // double2 per array per slot
     if (gated(g)) return;
-    constexpr int A = UNIT ? 3 : 4;             // streamed arrays: b, c1, c2 (, d)
-    constexpr int SLOT = A * kWavePB * 64;      // double2 per ring slot
-    // one LDS object: data ring, then the 2 x 16 boundary values
-    __shared__ double2 lds[kWaveR * SLOT + kWaveBatch];
-    double *bring = reinterpret_cast<double *>(lds + kWaveR * SLOT);
+    // one LDS object: data ring [R][A][kWavePB][64] double2, 2 x 64 boundary values
+    // (lanes 0..kWaveBatch-1 of each half are used), x staging [2][kWavePB][64]
+    __shared__ double2 lds[C::LDS2];
+    double *bring = reinterpret_cast<double *>(lds + C::R * C::SLOT);
+    double2 *xbuf = lds + C::R * C::SLOT + 64;
     const int band = FWD ? blockIdx.x : (nbands - 1 - blockIdx.x);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int np = T / 2;                       // step pairs per band
-    const int nbatch = T / kWaveBatch;          // T is a multiple of kWaveBatch
+    const int nbatch = T / kWaveBatch;          // T is a multiple of 8 * kWaveBatch
     const bool has_src = FWD ? (band > 0) : (band < nbands - 1);
     const bool is_prod = FWD ? (band < nbands - 1) : (band > 0);
     const long long boff = (long long)band * np * 64 + lane;    // double2 units
 
-    if (wave >= 2) {
+    constexpr int plane = FWD ? 63 : 0;     // lane whose values the next band needs
+    unsigned long long *pub = bnd + (long long)band * T;
+    if (wave >= 3) {
         // ------------------------------------------------ loader waves
-        const double2 *src[4] = {reinterpret_cast<const double2 *>(b) + boff,
-                                 reinterpret_cast<const double2 *>(c1) + boff,
-                                 reinterpret_cast<const double2 *>(c2) + boff,
-                                 UNIT ? nullptr : reinterpret_cast<const double2 *>(dv) + boff};
-        if (wave == 2) wave_loader<FWD, A, 2>(src, 0, lds, np, nbatch);
-        else wave_loader<FWD, A, A - 2>(src, 2, lds, np, nbatch);
+        const double *arr = wave == 3 ? b : wave == 4 ? c1 : wave == 5 ? c2 : wave == 6 ? dv : rv;
+        wave_loader<FWD, C::R, C::SLOT>(reinterpret_cast<const double2 *>(arr) + boff,
+                                        lds + (wave - 3) * PB, np, nbatch);
+        raw_barrier();                      // final barrier (the writer drains the last batch)
+        return;
+    }
+    if (wave == 2) {
+        // ------------------------------------------------ writer wave
+        // After barrier bi+1 the compute wave's x of batch bi sits in xbuf[bi & 1]:
+        // store it to HBM and publish the edge lane's values of the batch as
+        // hand-off granules (lanes 0..kWaveBatch-1, one coalesced sc1 store).
+        double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
+        for (int bi = 0; bi <= nbatch; bi++) {
+            raw_barrier();
+            if (bi == 0) continue;
+            const int pb = bi - 1;
+            const double2 *xb = xbuf + (pb & 1) * PB;
+            double2 v[kWavePB];
+#pragma unroll
+            for (int kk = 0; kk < kWavePB; kk++) v[kk] = xb[kk * 64 + lane];
+            const int tt = lane & (kWaveBatch - 1);
+            const double e = reinterpret_cast<const double *>(xb + (tt >> 1) * 64 + plane)
+                [FWD ? (tt & 1) : 1 - (tt & 1)];
+#pragma unroll
+            for (int kk = 0; kk < kWavePB; kk++) {
+                const int p = pb * kWavePB + kk;
+                X2[(long long)(FWD ? p : np - 1 - p) * 64] = v[kk];
+            }
+            if (is_prod && lane < kWaveBatch) {
+                const int t = FWD ? pb * kWaveBatch + tt : (T - 1) - (pb * kWaveBatch + tt);
+                st_agent(pub + t, (unsigned long long)__double_as_longlong(e));
+            }
+        }
         return;
     }
     if (wave == 1) {
         // ------------------------------------------------ boundary wave
-        // before barrier j it has placed batch j's values in bring[j & 1];
-        // between barriers j and j+1 it fetches batch j+1
-        unsigned long long *src = bnd + (long long)(FWD ? band - 1 : band + 1) * nx;
+        // Before barrier bi it places batch bi's values in bring[bi & 1].  Step
+        // t of this band's edge lane needs the source band's step t -+ 63.  Polls
+        // are pipelined kPoll batches deep (one register per ring position): the
+        // load for batch bi+kPoll is issued right after batch bi is handed over,
+        // so in steady state a batch's granules have arrived when it is checked.
+        // Every memory op is issued by all lanes (lanes with nothing to do use
+        // the dummy granules after the bands: 64 zeros to read, 64 to write),
+        // which keeps the vmcnt arithmetic exact.
+        constexpr int kPoll = 4;
+        unsigned long long *src = bnd + (long long)(FWD ? band - 1 : band + 1) * T;
+        unsigned long long *dummy_ld = bnd + (long long)nbands * T + lane;
+        unsigned long long *dummy_st = dummy_ld + 64;
+        auto gaddr = [&](int bj) {
+            const int t = FWD ? bj * kWaveBatch + lane : (T - 1) - (bj * kWaveBatch + lane);
+            const int gi = FWD ? t + 63 : t - 63;
+            const bool need = has_src && lane < kWaveBatch && bj < nbatch && gi >= 0 && gi < T;
+            return need ? src + gi : (unsigned long long *)nullptr;
+        };
+        // the prologue mirrors the steady-state issue order (re-arm store, poll)
+        // so the same vmcnt holds in every iteration
+        unsigned long long v[kPoll];
+#pragma unroll
+        for (int u = 0; u < kPoll; u++) {
+            if (u > 0) st_agent(dummy_st, kSentinel);
+            unsigned long long *ga = gaddr(u);
+            v[u] = ld_agent(ga ? ga : dummy_ld);
+        }
         bool dead = false;
-        for (int bi = 0; bi < nbatch; bi++) {
-            if (has_src) {
-                // column the compute wave's edge lane needs at step `lane` of batch bi
-                const int t = FWD ? bi * kWaveBatch + lane : (T - 1) - (bi * kWaveBatch + lane);
-                const int c = FWD ? t : t - 63;
-                const int col = (lane < kWaveBatch && c >= 0 && c < nx) ? c : -1;
-                unsigned long long v = (col >= 0 && !dead) ? ld_agent(src + col) : 0ull;
+        for (int bi0 = 0; bi0 < nbatch; bi0 += kPoll) {     // nbatch is a multiple of kPoll
+#pragma unroll
+            for (int u = 0; u < kPoll; u++) {
+                const int bi = bi0 + u;
+                unsigned long long *ga = gaddr(bi);
+                // oldest poll done: after it come kPoll-1 loads and kPoll-1 re-arm stores
+                __builtin_amdgcn_s_waitcnt(vm_wait(2 * (kPoll - 1)));
                 int spins = 0;
-                while (!dead && !__all(col < 0 || v != kSentinel)) {
+                while (!dead && !__all(v[u] != kSentinel)) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (col >= 0 && v == kSentinel) v = ld_agent(src + col);
+                    v[u] = ld_agent(ga ? ga : dummy_ld);
                     if (++spins > kSpinLimit) {
                         dead = true;
                         if (lane == 0) atomicOr(err, 1);
                     }
+                    __builtin_amdgcn_s_waitcnt(vm_wait(0));
                 }
-                if (col >= 0) st_agent(src + col, kSentinel);   // re-arm for the next launch
-                if (lane < kWaveBatch)
-                    bring[(bi & 1) * kWaveBatch + lane] =
-                        (col >= 0) ? __longlong_as_double((long long)v) : 0.0;
+                bring[(bi & 1) * 64 + lane] = __longlong_as_double((long long)v[u]);
+                st_agent(ga ? ga : dummy_st, kSentinel);       // re-arm for the next launch
+                unsigned long long *gn = gaddr(bi + kPoll);
+                v[u] = ld_agent(gn ? gn : dummy_ld);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                raw_barrier();
             }
-            raw_barrier();
         }
+        raw_barrier();                      // final barrier (the writer drains the last batch)
         return;
     }
 
     // ---------------------------------------------------- compute wave
-    double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
-    constexpr int edge = FWD ? 0 : 63;      // lane that consumes the boundary
-    constexpr int plane = FWD ? 63 : 0;     // lane whose values the next band needs
-    unsigned long long *dst = bnd + (long long)band * nx;
+    constexpr int ctrl = FWD ? 0x138 : 0x130;   // wave_shr:1 / wave_shl:1
+    long long *tr = TRACE ? trace + (long long)band * (nbatch + 5) : nullptr;
+    long long ph[4] = {0, 0, 0, 0};     // TRACE: barrier wait, top->step0, step0->last, last->end
+    long long t_top = 0;
     double xp = 0.0;                        // this lane's previous step value
-    double bacc = 0.0;                      // producer-lane values of this batch (lane k = step k)
+    bool bad = false;                       // WD_RCP range guard
+    // Register ring: operands of pair kk of the current batch, refilled from the
+    // next batch right after use.  The last pair is fetched after the batch's
+    // boundary values instead (LDS returns in order, and the boundary values
+    // are needed first).
+    double2 rg[kWavePB][C::A];
+    raw_barrier();                          // barrier 0: batches 0 and 1 are in LDS
+#pragma unroll
+    for (int kk = 0; kk < kWavePB - 1; kk++)
+#pragma unroll
+        for (int a = 0; a < C::A; a++) rg[kk][a] = lds[a * PB + kk * 64 + lane];
     for (int bi = 0; bi < nbatch; bi++) {
-        raw_barrier();                      // batch bi's data and boundary values are in LDS
-        const double2 *sl = lds + (bi % kWaveR) * SLOT + lane;
-        const double bv = (has_src && lane < kWaveBatch) ? bring[(bi & 1) * kWaveBatch + lane] : 0.0;
+        if (bi > 0) {
+            // x staging writes of batch bi-1 complete before the barrier (writer)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (TRACE) {
+                const long long ta = (long long)__builtin_amdgcn_s_memtime();
+                ph[3] += ta - t_top;
+                raw_barrier();
+                ph[0] += (long long)__builtin_amdgcn_s_memtime() - ta;
+            } else {
+                raw_barrier();              // batch bi's boundary values, batch bi+1's data
+            }
+        }
+        if constexpr (TRACE) {
+            if (lane == 0) tr[bi] = (long long)__builtin_amdgcn_s_memrealtime();
+        }
+        const double2 *br = reinterpret_cast<const double2 *>(bring + (bi & 1) * 64);
+        double2 bv[kWavePB];
+#pragma unroll
+        for (int kk = 0; kk < kWavePB; kk++) bv[kk] = br[kk];    // broadcast reads
+        if constexpr (TRACE) t_top = (long long)__builtin_amdgcn_s_memtime();
+        const double2 *sc = lds + (bi % C::R) * C::SLOT + lane;
+#pragma unroll
+        for (int a = 0; a < C::A; a++) rg[kWavePB - 1][a] = sc[a * PB + (kWavePB - 1) * 64];
+        __builtin_amdgcn_sched_barrier(0);          // boundary values first, then the last pair
+        const double2 *sn = lds + ((bi + 1) % C::R) * C::SLOT + lane;
+        double xv[kWaveBatch];
 #pragma unroll
         for (int kk = 0; kk < kWavePB; kk++) {
-            const int p = bi * kWavePB + kk;
-            const double2 cb = sl[0 * kWavePB * 64 + kk * 64];
-            const double2 a1 = sl[1 * kWavePB * 64 + kk * 64];
-            const double2 a2 = sl[2 * kWavePB * 64 + kk * 64];
-            double2 dd = make_double2(1.0, 1.0);
-            if (!UNIT) dd = sl[3 * kWavePB * 64 + kk * 64];
-            double xo0 = 0.0, xo1 = 0.0;
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                const int tt = 2 * kk + h;                       // step within the batch
-                const bool sx = FWD ? (h == 0) : (h == 1);       // even step <-> .x
-                const double bb = sx ? cb.x : cb.y, e1 = sx ? a1.x : a1.y, e2 = sx ? a2.x : a2.y;
-                double xs = FWD ? dpp_shr1(xp) : dpp_shl1(xp);
-                const double bval = readlane_d(bv, tt);
-                if (lane == edge) xs = has_src ? bval : 0.0;
+                const int tt = 2 * kk + h;
+                const bool sx = FWD ? (h == 0) : (h == 1);     // even step <-> .x
+                const double bb = sx ? rg[kk][0].x : rg[kk][0].y;
+                const double e1 = sx ? rg[kk][1].x : rg[kk][1].y;
+                const double e2 = sx ? rg[kk][2].x : rg[kk][2].y;
+                const double old = h ? bv[kk].y : bv[kk].x;
+                const double xs = dpp_shift_old<ctrl>(xp, old);
                 double acc = bb - e1 * xs;      // line neighbour first (|offset| = nx)
                 acc = acc - e2 * xp;            // then the in-line neighbour (|offset| = 1)
-                if (!UNIT) acc = acc / (sx ? dd.x : dd.y);
+                if constexpr (DIV == WD_HW) {
+                    acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
+                } else if constexpr (DIV == WD_RCP) {
+                    const double d = sx ? rg[kk][3].x : rg[kk][3].y;
+                    const double y = sx ? rg[kk][4].x : rg[kk][4].y;
+                    bad |= (unsigned)(__builtin_amdgcn_frexp_exp(acc) + 900) > 1800u;
+                    const double q0 = acc * y;
+                    const double q1 = __builtin_fma(-__builtin_fma(q0, d, -acc), y, q0);
+                    acc = __builtin_fma(-__builtin_fma(q1, d, -acc), y, q1);
+                }
                 xp = acc;
-                if (sx) xo0 = acc; else xo1 = acc;
-                const double pv = readlane_d(acc, plane);
-                if (lane == tt) bacc = pv;
+                xv[tt] = acc;
+                if constexpr (TRACE) {      // phase stamps at the first and last step
+                    if (tt == 0 || tt == kWaveBatch - 1) {
+                        const int f = __builtin_amdgcn_readfirstlane(__double2hiint(acc));
+                        asm volatile("; use %0" ::"s"(f));
+                        const long long now = (long long)__builtin_amdgcn_s_memtime();
+                        ph[tt == 0 ? 1 : 2] += now - t_top;
+                        t_top = now;
+                    }
+                }
             }
-            X2[(long long)(FWD ? p : np - 1 - p) * 64] = make_double2(xo0, xo1);
+            // the pair's results go to LDS staging (the writer wave stores them
+            // and publishes the edge values), then pair kk is refilled from the
+            // next batch (landed by barrier bi); the scheduling fence keeps it
+            // all inside this pair, in the recurrence's latency bubbles
+            xbuf[(bi & 1) * PB + kk * 64 + lane] =
+                FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
+            if (kk < kWavePB - 1) {
+#pragma unroll
+                for (int a = 0; a < C::A; a++) rg[kk][a] = sn[a * PB + kk * 64];
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        // ---- publish this batch's producer-lane values (lanes 0..15), issued by
-        //      every lane (lanes with nothing to publish write a dummy slot)
-        {
-            const int t = FWD ? bi * kWaveBatch + lane : (T - 1) - (bi * kWaveBatch + lane);
-            const int c = FWD ? t - 63 : t;
-            const bool real = is_prod && lane < kWaveBatch && c >= 0 && c < nx;
-            st_agent(real ? dst + c : bnd + (long long)nbands * nx + lane,
-                     (unsigned long long)__double_as_longlong(bacc));
-        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();                          // final barrier: the writer drains the last batch
+    if constexpr (DIV == WD_RCP) {
+        if (__any(bad) && lane == 0) atomicOr(err, 2);
+    }
+    if (TRACE && lane == 0) {
+        tr[nbatch] = (long long)__builtin_amdgcn_s_memrealtime();
+#pragma unroll
+        for (int k = 0; k < 4; k++) tr[nbatch + 1 + k] = ph[k];
     }
 }
 
@@ -679,22 +806,28 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         }
     } else if (T.kind == DevTri::WAVE2D) {
         const Wave2D &w = T.wl;
-        dim3 grid(w.nbands), blk(256);
+        dim3 grid(w.nbands);
+        const double *dv = T.div == WD_UNIT ? nullptr : T.dw.p;
+        const double *rv = T.div == WD_RCP ? T.rw.p : nullptr;
+#define GG_WAVE_LAUNCH(FWD, DIV)                                                             \
+    do {                                                                                     \
+        if (T.trace)                                                                         \
+            k_trsv_wave2d<FWD, DIV, true><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(           \
+                g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, T.trace);      \
+        else                                                                                 \
+            k_trsv_wave2d<FWD, DIV, false><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(          \
+                g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr);      \
+    } while (0)
         if (T.lower) {
-            if (T.unit)
-                k_trsv_wave2d<true, true><<<grid, blk, 0, st>>>(g, w.nx, w.T, w.nbands, b, T.c1.p,
-                                                                T.c2.p, nullptr, x, T.bnd.p, err);
-            else
-                k_trsv_wave2d<true, false><<<grid, blk, 0, st>>>(g, w.nx, w.T, w.nbands, b, T.c1.p,
-                                                                 T.c2.p, T.dw.p, x, T.bnd.p, err);
+            if (T.div == WD_UNIT) GG_WAVE_LAUNCH(true, WD_UNIT);
+            else if (T.div == WD_HW) GG_WAVE_LAUNCH(true, WD_HW);
+            else GG_WAVE_LAUNCH(true, WD_RCP);
         } else {
-            if (T.unit)
-                k_trsv_wave2d<false, true><<<grid, blk, 0, st>>>(g, w.nx, w.T, w.nbands, b, T.c1.p,
-                                                                 T.c2.p, nullptr, x, T.bnd.p, err);
-            else
-                k_trsv_wave2d<false, false><<<grid, blk, 0, st>>>(g, w.nx, w.T, w.nbands, b, T.c1.p,
-                                                                  T.c2.p, T.dw.p, x, T.bnd.p, err);
+            if (T.div == WD_UNIT) GG_WAVE_LAUNCH(false, WD_UNIT);
+            else if (T.div == WD_HW) GG_WAVE_LAUNCH(false, WD_HW);
+            else GG_WAVE_LAUNCH(false, WD_RCP);
         }
+#undef GG_WAVE_LAUNCH
     }
 }
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -53,8 +54,8 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
     if (wl && wl->ok) {
         T.kind = DevTri::WAVE2D;
         T.wl = *wl;
-        std::vector<double> c1(Ppad, 0.0), c2(Ppad, 0.0), dv(Ppad, 1.0);
-        bool unit = true;
+        std::vector<double> c1(Ppad, 0.0), c2(Ppad, 0.0), dv(Ppad, 1.0), rv(Ppad, 1.0);
+        bool unit = true, rcp_ok = true;
         const int nx = wl->nx;
         for (int r = 0; r < n; r++) {
             const long long p = (*nat2lay)[r];
@@ -62,18 +63,33 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
                 const int off = std::abs(C.off.ci[k] - r);
                 (off == nx ? c1 : c2)[p] = C.off.v[k];
             }
-            dv[p] = C.d[r];
-            if (C.d[r] != 1.0) unit = false;
+            const double d = C.d[r];
+            dv[p] = d;
+            rv[p] = 1.0 / d;
+            if (d != 1.0) unit = false;
+            // WD_RCP keeps every intermediate normal for 2^-100 <= |d| <= 2^100
+            if (!(std::fabs(d) >= 0x1p-100 && std::fabs(d) <= 0x1p100)) rcp_ok = false;
         }
-        T.unit = unit;
         T.c1.upload(c1, st);
         T.c2.upload(c2, st);
-        if (!unit) T.dw.upload(dv, st);
-        const long long stride = round_up(nx, 16);
-        T.bnd.alloc((size_t)wl->nbands * stride + 64);   // + 64 dummy slots (kernels.hip)
-        launch_fill_u64(T.bnd.p, (long long)wl->nbands * stride, kSentinel, st);
-        // algorithmic bytes: b, two coefficients, (divisor), x  per grid point
-        T.bytes = (double)n * (8.0 * (unit ? 4 : 5));
+        T.rcp_ok = false;
+        if (unit) {
+            T.div = WD_UNIT;
+        } else {
+            T.dw.upload(dv, st);
+            const char *hw = std::getenv("GG_WAVE_HWDIV");
+            T.rcp_ok = rcp_ok && !(hw && hw[0] == '1');
+            if (T.rcp_ok) T.rw.upload(rv, st);
+            T.div = T.rcp_ok ? WD_RCP : WD_HW;
+        }
+        // one hand-off granule per band and step, then 64 zero granules (dummy
+        // reads) and 64 write-only ones (dummy re-arms); kernels.hip k_trsv_wave2d
+        const long long ngran = (long long)wl->nbands * wl->T;
+        T.bnd.alloc((size_t)ngran + 128);
+        launch_fill_u64(T.bnd.p, ngran, kSentinel, st);
+        launch_fill_u64(T.bnd.p + ngran, 128, 0ull, st);
+        // algorithmic bytes: b, two coefficients, (divisor (, reciprocal)), x per grid point
+        T.bytes = (double)n * (8.0 * (unit ? 4 : T.rcp_ok ? 6 : 5));
     } else {
         T.kind = DevTri::LEVEL;
         T.off.upload(C.off, st);
@@ -410,7 +426,24 @@ DevState read_state(gg_solver *s)
     return h;
 }
 
-int solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
+// Device error word: bit 0 = wavefront boundary wait timed out, bit 1 = a
+// WD_RCP step saw a numerator outside its safe range (repeat with WD_HW).
+struct RcpFallback {};
+void check_err(gg_solver *s)
+{
+    int err = 0;
+    GG_HIP(hipMemcpy(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost));
+    GG_REQUIRE((err & 1) == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+    if (err & 2) throw RcpFallback{};
+}
+// switch every WD_RCP triangle to IEEE division for the rest of the solver's life
+void demote_rcp(gg_solver *s)
+{
+    for (DevTri *T : {&s->L, &s->U})
+        if (T->kind == DevTri::WAVE2D && T->div == WD_RCP) T->div = WD_HW;
+}
+
+int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
                  gg_result *res)
 {
     GG_REQUIRE(s->have_A, GG_ESTATE, "gg_solve: no matrix (call gg_set_matrix)");
@@ -434,8 +467,7 @@ int solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options 
         GG_HIP(hipMemsetAsync(s->y.p, 0, s->Ppad * sizeof(double), s->st));
     for (DevTri *T : {&s->L, &s->U})
         if (T->kind == DevTri::WAVE2D)
-            launch_fill_u64(T->bnd.p, (long long)T->wl.nbands * round_up(T->wl.nx, 16), kSentinel,
-                            s->st);
+            launch_fill_u64(T->bnd.p, (long long)T->wl.nbands * T->wl.T, kSentinel, s->st);
     DevState h{};
     h.tol = opt->tol;
     h.max_iter = opt->max_iter;
@@ -466,9 +498,7 @@ int solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options 
             enqueue_cycle(s, m);
             DevState prev = h;
             h = read_state(s);
-            int err = 0;
-            GG_HIP(hipMemcpy(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost));
-            GG_REQUIRE(err == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+            check_err(s);
             prof_collect(s, (h.done & DONE_INNER) ? h.conv_i + 1 : h.nit);
             if (h.done & DONE_INNER) {
                 ret = 0;
@@ -491,6 +521,7 @@ int solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options 
         }
     }
     GG_HIP(hipEventRecord(s->ev1, s->st));
+    check_err(s);
     launch_gather(s->xv.p, s->nat2lay.p, d_x, n, s->st);
     GG_HIP(hipStreamSynchronize(s->st));
     float ms = 0.f;
@@ -508,6 +539,17 @@ int solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options 
         res->solve_ms = ms;
     }
     return ret;
+}
+
+int solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
+                 gg_result *res)
+{
+    try {
+        return solve_device_once(s, d_b, d_x, opt, res);
+    } catch (RcpFallback &) {
+        demote_rcp(s);      // d_x is written only at the very end, so simply start over
+        return solve_device_once(s, d_b, d_x, opt, res);
+    }
 }
 
 void stage_in(gg_solver *s, const double *h, DBuf<double> &d)
@@ -766,24 +808,29 @@ int gg_precond_apply(gg_solver *s, int op, const double *in, double *out)
     ensure_workspace(s, std::max(s->m_alloc, 1));
     for (DevTri *T : {&s->L, &s->U})
         if (T->kind == DevTri::WAVE2D)
-            launch_fill_u64(T->bnd.p, (long long)T->wl.nbands * round_up(T->wl.nx, 16), kSentinel,
-                            s->st);
-    GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
+            launch_fill_u64(T->bnd.p, (long long)T->wl.nbands * T->wl.T, kSentinel, s->st);
     stage_in(s, in, s->nat_in);
     launch_gather(s->nat_in.p, s->lay2nat.p, s->xv.p, s->Ppad, s->st);
-    Gate none;
-    switch (op) {
-    case GG_APPLY_MINV: apply_minv(s, none, s->xv.p, s->ww.p); break;
-    case GG_APPLY_LEFT: apply_left(s, none, s->xv.p, s->ww.p); break;
-    case GG_APPLY_RIGHT: apply_right(s, none, s->xv.p, s->ww.p); break;
-    case GG_APPLY_START: apply_start(s, none, s->xv.p, s->ww.p); break;
+    auto run = [&]() {
+        GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
+        Gate none;
+        switch (op) {
+        case GG_APPLY_MINV: apply_minv(s, none, s->xv.p, s->ww.p); break;
+        case GG_APPLY_LEFT: apply_left(s, none, s->xv.p, s->ww.p); break;
+        case GG_APPLY_RIGHT: apply_right(s, none, s->xv.p, s->ww.p); break;
+        case GG_APPLY_START: apply_start(s, none, s->xv.p, s->ww.p); break;
+        }
+        check_err(s);
+    };
+    try {
+        run();
+    } catch (RcpFallback &) {
+        demote_rcp(s);
+        run();
     }
     if (s->nat_out.n < (size_t)std::max(s->A.n, 1)) s->nat_out.alloc(std::max(s->A.n, 1));
     launch_gather(s->ww.p, s->nat2lay.p, s->nat_out.p, s->A.n, s->st);
     stage_out(s, s->nat_out, out);
-    int err = 0;
-    GG_HIP(hipMemcpy(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost));
-    GG_REQUIRE(err == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
     return GG_OK;
     GG_API_END
 }
@@ -856,7 +903,35 @@ int gg_time_precond(gg_solver *s, int reps, double *avg_ms)
     *avg_ms = ms / reps;
     int err = 0;
     GG_HIP(hipMemcpy(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost));
-    GG_REQUIRE(err == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+    GG_REQUIRE((err & 1) == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int *nbands,
+                     int *nbatch)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && out && nbands && nbatch && (which == 0 || which == 1), GG_EINVAL, "bad argument");
+    GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner");
+    DevTri &T = which == 0 ? s->L : s->U;
+    GG_REQUIRE(T.kind == DevTri::WAVE2D, GG_ESTATE, "wavefront path not active");
+    set_device(s);
+    ensure_workspace(s, std::max(s->m_alloc, 1));
+    const int nb = T.wl.nbands, nbt = T.wl.T / 8;   // kernels.hip kWaveBatch
+    const long long need = (long long)nb * (nbt + 5);
+    GG_REQUIRE(cap >= need, GG_EINVAL, "trace buffer too small");
+    DBuf<long long> buf;
+    buf.alloc((size_t)need);
+    GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
+    T.trace = buf.p;
+    Gate none;
+    launch_trsv(none, T, s->bv.p, s->t1.p, s->err.p, s->st);
+    T.trace = nullptr;
+    GG_HIP(hipMemcpyAsync(out, buf.p, need * sizeof(long long), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
+    *nbands = nb;
+    *nbatch = nbt;
     return GG_OK;
     GG_API_END
 }

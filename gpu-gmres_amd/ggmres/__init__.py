@@ -27,6 +27,7 @@ EXPORTS = [
     "gg_uses_wavefront", "gg_solve", "gg_solve_device", "gg_get_history", "gg_spmv",
     "gg_precond_apply", "gg_time_spmv", "gg_time_precond", "gg_bytes_spmv",
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
+    "gg_trace_precond",
 ]
 PROF_SPMV, PROF_PRECOND, PROF_MGS = range(3)
 
@@ -82,6 +83,9 @@ def lib():
         L.gg_time_spmv.argtypes = [_VP, ctypes.c_int, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_double)]
         L.gg_time_precond.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        L.gg_trace_precond.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong),
+                                       ctypes.c_longlong, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_int)]
         L.gg_bytes_spmv.argtypes = [_VP]
         L.gg_bytes_spmv.restype = ctypes.c_double
         L.gg_bytes_precond.argtypes = [_VP]
@@ -204,6 +208,19 @@ class Solver:
         ms = ctypes.c_double()
         _check(lib().gg_time_spmv(self.h, int(reps), int(nrot), ctypes.byref(ms)))
         return ms.value
+
+    def trace_precond(self, which=0, cap=1 << 20):
+        """Per-band batch-start timestamps (100 MHz clock) of one wavefront
+        triangular solve: array [nbands, nbatch+5]: batch starts, end, then
+        core-cycle totals of four batch phases (barrier wait, top -> first
+        result, first -> last result, last result -> next barrier)."""
+        import numpy as np
+        buf = (ctypes.c_longlong * cap)()
+        nb, nbt = ctypes.c_int(), ctypes.c_int()
+        _check(lib().gg_trace_precond(self.h, int(which), buf, cap, ctypes.byref(nb),
+                                      ctypes.byref(nbt)))
+        a = np.ctypeslib.as_array(buf)[: nb.value * (nbt.value + 5)].copy()
+        return a.reshape(nb.value, nbt.value + 5)
 
     def time_precond(self, reps=20):
         ms = ctypes.c_double()

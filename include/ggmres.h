@@ -157,6 +157,15 @@ int gg_profile_get(gg_solver *s, int kind, int *launches, double *total_ms);
 double gg_bytes_spmv(gg_solver *s);
 double gg_bytes_precond(gg_solver *s);
 
+/* Diagnostics: run one wavefront triangular solve (which: 0 = L / Ml, 1 = U / Mr)
+ * on the current right-hand side and return, per band, the device real-time
+ * clock (100 MHz) at the start of each 8-step batch plus one end stamp, then
+ * core-cycle totals of four phases of the compute wave's batches (barrier wait,
+ * batch top to first result, first to last result, last result to the next
+ * barrier): out[band * (nbatch + 5) + k].  GG_ESTATE unless the wavefront path is active. */
+int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int *nbands,
+                     int *nbatch);
+
 #ifdef __cplusplus
 }
 #endif

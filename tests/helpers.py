@@ -61,14 +61,14 @@ def device_layout(n, nx=None):
     """(lay2nat, G) of the solver's vector space: natural order, or -- for a 2D
     grid of line length nx on the wavefront path -- band = j//64, lane l = j%64,
     step t = i + l, slot ((band*T/2 + t//2)*64 + l)*2 + t%2 with
-    T = roundup(nx+63, 32); padded to a multiple of 512 slots;
+    T = roundup(nx+63, 64); padded to a multiple of 512 slots;
     G = min(1024, ceil(Ppad/2 / 1024)) reduction blocks."""
     if nx is None:
         P = n
         slots = np.arange(n, dtype=np.int64)
     else:
         ny = n // nx
-        T = (nx + 63 + 31) // 32 * 32
+        T = (nx + 63 + 63) // 64 * 64
         nb = (ny + 63) // 64
         P = nb * T * 64
         r = np.arange(n, dtype=np.int64)
