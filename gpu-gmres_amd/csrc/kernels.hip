@@ -238,17 +238,23 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
 // (Markstein's theorem; y within half an ulp of 1/d).  The remainders are
 // formed as -(d*q - acc) so signed zeros come out as in acc/d.  The theorem
 // needs every intermediate in the normal range: the host admits WD_RCP only for
-// 2^-100 <= |d| <= 2^100, and each step flags |acc| outside [2^-900, 2^900]
+// 2^-100 <= |d| <= 2^100, and the writer wave flags results outside rcp_safe
 // (err bit 2), on which the caller repeats the work with WD_HW.
 constexpr int kWaveBatch = 8;              // steps per batch
 constexpr int kWavePB = kWaveBatch / 2;    // step pairs per batch
 constexpr int kSpinLimit = 1 << 20;
+// Ring depth: batches j and j+1 are in LDS at barrier j and kWaveRing-3 more are
+// in flight (enough to cover the HBM latency at this stream rate).
+#ifndef GG_WAVE_RING
+#define GG_WAVE_RING 5
+#endif
+constexpr int kWaveRing = GG_WAVE_RING;
 
 template <int DIV>
 struct WaveCfg {
     static constexpr int A = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;   // streamed arrays
     static constexpr int SLOT = A * kWavePB * 64;                        // double2 per ring slot
-    static constexpr int R = (144 * 1024) / (SLOT * 16);                 // ring slots: 12 / 9 / 7
+    static constexpr int R = kWaveRing;                                  // ring slots
     static constexpr int THREADS = (3 + A) * 64;                        // compute, boundary, writer, loaders
     static constexpr int LDS2 = R * SLOT + 64 + 2 * kWavePB * 64;        // ring, boundary, x staging
     static_assert(R >= 4 && (R - 3) * kWavePB <= 63, "ring depth vs vmcnt range");
@@ -285,6 +291,17 @@ __device__ __forceinline__ double dpp_shift_old(double v, double old)
     int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, 0xf, 0xf, false);
     int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, 0xf, 0xf, false);
     return __hiloint2double(hi, lo);
+}
+
+// WD_RCP's range condition, checked on the results x (by the writer wave, off
+// the recurrence): with 2^-100 <= |d| <= 2^100, |x| in [2^-800, 2^800] keeps
+// |acc| = |x d| inside [2^-900, 2^900], where every intermediate of the two
+// corrections is normal.  x == 0 comes from acc == 0, or from a quotient below
+// 2^-1074 that both roundings flush alike except within one subnormal ulp.
+__device__ __forceinline__ bool rcp_safe(double v)
+{
+    const double a = __builtin_fabs(v);
+    return v == 0.0 || (a >= 0x1p-800 && a <= 0x1p800);
 }
 
 // loader wave: one array; batch j -> ring slot j % R; batches j, j+1 landed by barrier j
@@ -349,26 +366,35 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
         // store it to HBM and publish the edge lane's values of the batch as
         // hand-off granules (lanes 0..kWaveBatch-1, one coalesced sc1 store).
         double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
+        [[maybe_unused]] bool bad = false;  // WD_RCP range guard (see rcp_safe)
         for (int bi = 0; bi <= nbatch; bi++) {
             raw_barrier();
             if (bi == 0) continue;
             const int pb = bi - 1;
             const double2 *xb = xbuf + (pb & 1) * PB;
-            double2 v[kWavePB];
-#pragma unroll
-            for (int kk = 0; kk < kWavePB; kk++) v[kk] = xb[kk * 64 + lane];
+            // the hand-off granules first: they are on the critical path, x is not
             const int tt = lane & (kWaveBatch - 1);
             const double e = reinterpret_cast<const double *>(xb + (tt >> 1) * 64 + plane)
                 [FWD ? (tt & 1) : 1 - (tt & 1)];
-#pragma unroll
-            for (int kk = 0; kk < kWavePB; kk++) {
-                const int p = pb * kWavePB + kk;
-                X2[(long long)(FWD ? p : np - 1 - p) * 64] = v[kk];
-            }
             if (is_prod && lane < kWaveBatch) {
                 const int t = FWD ? pb * kWaveBatch + tt : (T - 1) - (pb * kWaveBatch + tt);
                 st_agent(pub + t, (unsigned long long)__double_as_longlong(e));
             }
+            double2 v[kWavePB];
+#pragma unroll
+            for (int kk = 0; kk < kWavePB; kk++) v[kk] = xb[kk * 64 + lane];
+#pragma unroll
+            for (int kk = 0; kk < kWavePB; kk++) {
+                const int p = pb * kWavePB + kk;
+                X2[(long long)(FWD ? p : np - 1 - p) * 64] = v[kk];
+                if constexpr (DIV == WD_RCP) bad |= !rcp_safe(v[kk].x) || !rcp_safe(v[kk].y);
+            }
+            if (TRACE && lane == 0)
+                trace[(long long)band * (3 * nbatch + 8) + nbatch + 8 + pb] =
+                    (long long)__builtin_amdgcn_s_memrealtime();
+        }
+        if constexpr (DIV == WD_RCP) {
+            if (__any(bad) && lane == 0) atomicOr(err, 2);
         }
         return;
     }
@@ -402,6 +428,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
             v[u] = ld_agent(ga ? ga : dummy_ld);
         }
         bool dead = false;
+        long long bw_spins = 0, bw_cyc = 0;     // TRACE: poll retries, cycles in retry loops
         for (int bi0 = 0; bi0 < nbatch; bi0 += kPoll) {     // nbatch is a multiple of kPoll
 #pragma unroll
             for (int u = 0; u < kPoll; u++) {
@@ -410,6 +437,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 // oldest poll done: after it come kPoll-1 loads and kPoll-1 re-arm stores
                 __builtin_amdgcn_s_waitcnt(vm_wait(2 * (kPoll - 1)));
                 int spins = 0;
+                const long long tw = TRACE ? (long long)__builtin_amdgcn_s_memtime() : 0;
                 while (!dead && !__all(v[u] != kSentinel)) {
                     __builtin_amdgcn_s_sleep(1);
                     v[u] = ld_agent(ga ? ga : dummy_ld);
@@ -418,6 +446,13 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                         if (lane == 0) atomicOr(err, 1);
                     }
                     __builtin_amdgcn_s_waitcnt(vm_wait(0));
+                }
+                if constexpr (TRACE) {
+                    bw_spins += spins;
+                    if (spins) bw_cyc += (long long)__builtin_amdgcn_s_memtime() - tw;
+                    if (lane == 0)
+                        trace[(long long)band * (3 * nbatch + 8) + 2 * nbatch + 8 + bi] =
+                            (long long)__builtin_amdgcn_s_memrealtime();
                 }
                 bring[(bi & 1) * 64 + lane] = __longlong_as_double((long long)v[u]);
                 st_agent(ga ? ga : dummy_st, kSentinel);       // re-arm for the next launch
@@ -428,16 +463,20 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
             }
         }
         raw_barrier();                      // final barrier (the writer drains the last batch)
+        if (TRACE && lane == 0) {
+            long long *trb = trace + (long long)band * (3 * nbatch + 8);
+            trb[nbatch + 5] = bw_spins;
+            trb[nbatch + 6] = bw_cyc;
+        }
         return;
     }
 
     // ---------------------------------------------------- compute wave
     constexpr int ctrl = FWD ? 0x138 : 0x130;   // wave_shr:1 / wave_shl:1
-    long long *tr = TRACE ? trace + (long long)band * (nbatch + 5) : nullptr;
+    long long *tr = TRACE ? trace + (long long)band * (3 * nbatch + 8) : nullptr;
     long long ph[4] = {0, 0, 0, 0};     // TRACE: barrier wait, top->step0, step0->last, last->end
     long long t_top = 0;
     double xp = 0.0;                        // this lane's previous step value
-    bool bad = false;                       // WD_RCP range guard
     // Register ring: operands of pair kk of the current batch, refilled from the
     // next batch right after use.  The last pair is fetched after the batch's
     // boundary values instead (LDS returns in order, and the boundary values
@@ -493,7 +532,6 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 } else if constexpr (DIV == WD_RCP) {
                     const double d = sx ? rg[kk][3].x : rg[kk][3].y;
                     const double y = sx ? rg[kk][4].x : rg[kk][4].y;
-                    bad |= (unsigned)(__builtin_amdgcn_frexp_exp(acc) + 900) > 1800u;
                     const double q0 = acc * y;
                     const double q1 = __builtin_fma(-__builtin_fma(q0, d, -acc), y, q0);
                     acc = __builtin_fma(-__builtin_fma(q1, d, -acc), y, q1);
@@ -525,9 +563,6 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();                          // final barrier: the writer drains the last batch
-    if constexpr (DIV == WD_RCP) {
-        if (__any(bad) && lane == 0) atomicOr(err, 2);
-    }
     if (TRACE && lane == 0) {
         tr[nbatch] = (long long)__builtin_amdgcn_s_memrealtime();
 #pragma unroll

@@ -12,7 +12,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libggmres.so")
+LIB_PATH = os.environ.get("GGMRES_LIB") or os.path.join(PKG_ROOT, "lib", "libggmres.so")
 
 GG_OK, GG_NOT_CONVERGED = 0, 1
 PRECOND_NONE, PRECOND_ILU0, PRECOND_ILUK, PRECOND_LU, PRECOND_SPLIT = range(5)
@@ -211,16 +211,14 @@ class Solver:
 
     def trace_precond(self, which=0, cap=1 << 20):
         """Per-band batch-start timestamps (100 MHz clock) of one wavefront
-        triangular solve: array [nbands, nbatch+5]: batch starts, end, then
-        core-cycle totals of four batch phases (barrier wait, top -> first
-        result, first -> last result, last result -> next barrier)."""
+        triangular solve: array [nbands, 3*nbatch+8] (layout in ggmres.h)."""
         import numpy as np
         buf = (ctypes.c_longlong * cap)()
         nb, nbt = ctypes.c_int(), ctypes.c_int()
         _check(lib().gg_trace_precond(self.h, int(which), buf, cap, ctypes.byref(nb),
                                       ctypes.byref(nbt)))
-        a = np.ctypeslib.as_array(buf)[: nb.value * (nbt.value + 5)].copy()
-        return a.reshape(nb.value, nbt.value + 5)
+        a = np.ctypeslib.as_array(buf)[: nb.value * (3 * nbt.value + 8)].copy()
+        return a.reshape(nb.value, 3 * nbt.value + 8)
 
     def time_precond(self, reps=20):
         ms = ctypes.c_double()

@@ -162,7 +162,10 @@ double gg_bytes_precond(gg_solver *s);
  * clock (100 MHz) at the start of each 8-step batch plus one end stamp, then
  * core-cycle totals of four phases of the compute wave's batches (barrier wait,
  * batch top to first result, first to last result, last result to the next
- * barrier): out[band * (nbatch + 5) + k].  GG_ESTATE unless the wavefront path is active. */
+ * barrier), the boundary wave's poll retries and the core cycles it spent
+ * retrying, one spare slot, then the real-time stamps at which the writer wave
+ * published each batch and at which the boundary wave saw each batch's
+ * values: out[band * (3 * nbatch + 8) + k].  GG_ESTATE unless the wavefront path is active. */
 int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int *nbands,
                      int *nbatch);
 

@@ -72,6 +72,26 @@ def test_ilu0_apply_bitexact(solver, name, force_level, monkeypatch):
     assert np.array_equal(z, O.lusolve(L, U, y))
 
 
+@pytest.mark.parametrize("name", sorted(WAVE))
+@pytest.mark.parametrize("scale", [1.0, 1e-250, 1e250])
+@pytest.mark.parametrize("hwdiv", [False, True])
+def test_wavefront_division_modes(solver, name, scale, hwdiv, monkeypatch):
+    """The U solve divides by the diagonal: IEEE division (GG_WAVE_HWDIV=1) or
+    the reciprocal + two FMA corrections (kernels.hip WD_RCP).  Both must give
+    RN(acc/d) bit for bit; right-hand sides at 1e-250 / 1e250 leave WD_RCP's
+    safe range, are flagged by the writer wave and redone with IEEE division."""
+    if hwdiv:
+        monkeypatch.setenv("GG_WAVE_HWDIV", "1")
+    A = MATS[name]()
+    L, U = O.ilu0(A)
+    y = np.random.default_rng(3).standard_normal(A.shape[0]) * scale
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert solver.uses_wavefront
+    for _ in range(2):      # the second apply runs after any fallback demotion
+        assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
+
+
 def test_lu_precond_user_factors(solver):
     A = M.laplacian_5pt(50, 70)
     L, U = O.iluk(A, 1)   # ILU(1) factors: not grid-structured -> level path
