@@ -103,11 +103,21 @@ __global__ __launch_bounds__(kBlock) void k_dot(Gate g, const double *a, const d
 {
     if (gated(g)) return;
     double acc = 0.0;
-    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units;
-         u += (long long)gridDim.x * kBlock) {
-        double2 x = ld2(a, u), y = ld2(b, u);
-        acc += x.x * y.x;
-        acc += x.y * y.y;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x; u0 < units; u0 += 4 * stride) {
+        double2 x[4], y[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const long long u = u0 + j * stride;
+            if (u < units) { x[j] = ld2(a, u); y[j] = ld2(b, u); }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (u0 + j * stride < units) {
+                acc += x[j].x * y[j].x;
+                acc += x[j].y * y[j].y;
+            }
+        }
     }
     acc = block_sum(acc);
     if (threadIdx.x == 0) part[blockIdx.x] = acc;
@@ -621,8 +631,16 @@ __global__ __launch_bounds__(kBlock) void k_init_cycle(DevState *ds, const doubl
 // One MGS step k of inner iteration i (src/gmres.cu:638-641):
 //   h = <w, v_k> (from the previous kernel's partials); H[k,i] = h;
 //   w = (-h) v_k + w;  partials of <w, vnext>  (vnext = v_{k+1}, or w for the norm)
-__global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m, double *w,
-                                                     const double *vk, const double *vnext,
+// Each thread owns units u = g*256 + t + j*G*256 (j = 0, 1, ...), accumulated in
+// ascending j (the oracle's blocked dot order); kUnroll of them are loaded
+// before any is used so a thread keeps several 16-B loads per stream in flight.
+constexpr int kUnroll = 4;
+
+template <bool NORM>
+__global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m,
+                                                     double *__restrict__ w,
+                                                     const double *__restrict__ vk,
+                                                     const double *__restrict__ vnext,
                                                      const double *part_in, double *part_out,
                                                      double *H, int G, long long units)
 {
@@ -631,15 +649,30 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
     if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
     const double a = -h;
     double acc = 0.0;
-    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units;
-         u += (long long)gridDim.x * kBlock) {
-        double2 wv = ld2(w, u), vv = ld2(vk, u);
-        wv.x = a * vv.x + wv.x;
-        wv.y = a * vv.y + wv.y;
-        st2(w, u, wv);
-        double2 nv = (vnext == w) ? wv : ld2(vnext, u);
-        acc += wv.x * nv.x;
-        acc += wv.y * nv.y;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x; u0 < units; u0 += kUnroll * stride) {
+        double2 wv[kUnroll], vv[kUnroll], nv[kUnroll];
+#pragma unroll
+        for (int j = 0; j < kUnroll; j++) {
+            const long long u = u0 + j * stride;
+            if (u < units) {
+                wv[j] = ld2(w, u);
+                vv[j] = ld2(vk, u);
+                if (!NORM) nv[j] = ld2(vnext, u);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kUnroll; j++) {
+            const long long u = u0 + j * stride;
+            if (u < units) {
+                wv[j].x = a * vv[j].x + wv[j].x;
+                wv[j].y = a * vv[j].y + wv[j].y;
+                st2(w, u, wv[j]);
+                if (NORM) nv[j] = wv[j];
+                acc += wv[j].x * nv[j].x;
+                acc += wv[j].y * nv[j].y;
+            }
+        }
     }
     acc = block_sum(acc);
     if (threadIdx.x == 0) part_out[blockIdx.x] = acc;
@@ -696,12 +729,20 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
     }
     // lucky breakdown (hn == 0): the reference divides by zero; v_{i+1} := 0
     const double inv = (hn != 0.0) ? 1.0 / hn : 0.0;
-    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units;
-         u += (long long)gridDim.x * kBlock) {
-        double2 a = ld2(w, u);
-        a.x = inv * a.x;
-        a.y = inv * a.y;
-        st2(vnext, u, a);
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x; u0 < units; u0 += 4 * stride) {
+        double2 a[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (u0 + j * stride < units) a[j] = ld2(w, u0 + j * stride);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (u0 + j * stride < units) {
+                a[j].x = inv * a[j].x;
+                a[j].y = inv * a[j].y;
+                st2(vnext, u0 + j * stride, a[j]);
+            }
+        }
     }
 }
 
@@ -883,7 +924,10 @@ void launch_mgs_step(Gate g, int i, int k, int m, double *w, const double *vk, c
                      const double *part_in, double *part_out, double *H, int G, long long Ppad,
                      hipStream_t st)
 {
-    k_mgs_step<<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, vnext, part_in, part_out, H, G, Ppad / 2);
+    if (vnext == w)
+        k_mgs_step<true><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, nullptr, part_in, part_out, H, G, Ppad / 2);
+    else
+        k_mgs_step<false><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, vnext, part_in, part_out, H, G, Ppad / 2);
 }
 void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *part, int G,
                              const double *w, double *vnext, double *H, double *cs, double *sn,

@@ -431,8 +431,10 @@ DevState read_state(gg_solver *s)
 struct RcpFallback {};
 void check_err(gg_solver *s)
 {
+    // on the solver's stream: a plain hipMemcpy would not wait for its kernels
     int err = 0;
-    GG_HIP(hipMemcpy(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost));
+    GG_HIP(hipMemcpyAsync(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
     GG_REQUIRE((err & 1) == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
     if (err & 2) throw RcpFallback{};
 }
