@@ -645,13 +645,11 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
                                                      double *H, int G, long long units)
 {
     if (gated(g)) return;
-    const double h = sum_partials(part_in, G);
-    if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
-    const double a = -h;
     double acc = 0.0;
     const long long stride = (long long)gridDim.x * kBlock;
-    for (long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x; u0 < units; u0 += kUnroll * stride) {
-        double2 wv[kUnroll], vv[kUnroll], nv[kUnroll];
+    long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x;
+    double2 wv[kUnroll], vv[kUnroll], nv[kUnroll];
+    auto load = [&]() {
 #pragma unroll
         for (int j = 0; j < kUnroll; j++) {
             const long long u = u0 + j * stride;
@@ -661,6 +659,12 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
                 if (!NORM) nv[j] = ld2(vnext, u);
             }
         }
+    };
+    load();                 // the first chunk is in flight while h is summed
+    const double h = sum_partials(part_in, G);
+    if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
+    const double a = -h;
+    while (u0 < units) {
 #pragma unroll
         for (int j = 0; j < kUnroll; j++) {
             const long long u = u0 + j * stride;
@@ -673,6 +677,8 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
                 acc += wv[j].y * nv[j].y;
             }
         }
+        u0 += kUnroll * stride;
+        load();
     }
     acc = block_sum(acc);
     if (threadIdx.x == 0) part_out[blockIdx.x] = acc;
