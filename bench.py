@@ -7,9 +7,10 @@ tol 1e-8, b = A*1, x0 = 0.  One step = one full solve (device-resident b, x;
 the ILU factorization and H2D copies are setup, outside the timed region).
 
 value = inner (Arnoldi) iterations of all ranks / max-over-ranks wall time.
-roofline: the dominant kernel family, timed live inside the timed region with
-hipEvent pairs on the solver's stream (gg_profile_*), algorithmic bytes from
-SURVEY.md 8(d).  cpu_baseline: the fp64 oracle restatement (oracle/, serial C)
+roofline: the single kernel with the most time in the step, timed live inside
+the timed region with hipEvent pairs on the solver's stream (gg_profile_*),
+algorithmic bytes from SURVEY.md 8(d) (DESIGN.md "Kernels"); traffic: HBM bytes
+per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json).  cpu_baseline: the fp64 oracle restatement (oracle/, serial C)
 on a bounded sample of the same workload, rank 0 only.
 
 Multi-GPU (torchrun, one rank per GPU): every rank solves its own C2 system
@@ -45,6 +46,28 @@ def parse():
                    help="oracle iterations timed for cpu_baseline (0 = skip)")
     p.add_argument("--no-profile", action="store_true", help="do not bracket kernels with events")
     return p.parse_args()
+
+
+# bench family -> the kernel it times (rocprofv3 kernel names in profiles/)
+KERNEL_NAMES = {
+    "spmv": "k_spmv_stream<false>",
+    "trsv_L": "k_trsv_wave2d<true, 0, false>",     # lower, unit diagonal (ILU(0) L)
+    "trsv_U": "k_trsv_wave2d<false, 2, false>",    # upper, reciprocal division (ILU(0) U)
+}
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by profiles/pmc_traffic.py: FETCH_SIZE
+    doubled for 16-B/lane streaming reads, + WRITE_SIZE; MI355X_MICROARCH.md HBM
+    section), or None when that file has no entry for it."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def mgs_bytes(n, m, inner_list):
@@ -123,6 +146,8 @@ def main():
     mgs_tot, mgs_it = mgs_bytes(n, a.restart, [r["inner"] for r in res])
     for name, kind, per in (("spmv", ggmres.PROF_SPMV, spmv_bytes),
                             ("ilu0_apply", ggmres.PROF_PRECOND, pre_bytes),
+                            ("trsv_L", ggmres.PROF_TRSV_L, s.bytes_trsv(0)),
+                            ("trsv_U", ggmres.PROF_TRSV_U, s.bytes_trsv(1)),
                             ("mgs_givens", ggmres.PROF_MGS, None)):
         cnt, ms = s.profile_get(kind)
         if cnt == 0:
@@ -133,13 +158,17 @@ def main():
                      "alg_bytes_per_launch": byt,
                      "achieved_gbs": round(byt / (avg_us * 1e-6) / 1e9, 1),
                      "share_of_step": round(ms / (el * 1e3), 4)}
-    dom = max(fam, key=lambda k: fam[k]["share_of_step"]) if fam else None
+    # the roofline entry is for ONE kernel: the single-kernel entry with the most
+    # time (ilu0_apply = trsv_L + trsv_U and mgs_givens are families of launches)
+    single = {k: v for k, v in fam.items() if k in KERNEL_NAMES}
+    dom = max(single, key=lambda k: single[k]["share_of_step"]) if single else None
     roof = None
     if dom:
         f = fam[dom]
-        roof = {"kernel": dom, "bound": "hbm", "achieved": f["achieved_gbs"],
+        roof = {"kernel": KERNEL_NAMES[dom], "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic(KERNEL_NAMES[dom]),
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"]}
     # isolated SpMV (4 rotating copies of A, x, y: > 256 MiB, not Infinity-Cache served)
     spmv_iso_ms = s.time_spmv(reps=100, nrot=4)

@@ -752,9 +752,36 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
     }
 }
 
-// y = H(0:k,0:k)^-1 s(0:k)  (Update, src/gmres.cu:93-116); k = conv_i or nit-1
-__global__ void k_update_y(Gate g, int m, DevState *ds, const double *H, const double *s,
-                           double *y)
+// y = H(0:k,0:k)^-1 s(0:k)  (Update, src/gmres.cu:93-116); k = conv_i or nit-1.
+// One wave: lane j keeps y[j] and row j of H in registers; for i = k..0 lane i
+// divides, the value is broadcast, lanes j < i subtract -- per element the same
+// operations in the same order as the serial back-substitution.
+constexpr int kMaxRestart = 64;
+__global__ __launch_bounds__(64) void k_update_y(Gate g, int m, DevState *ds, const double *H,
+                                                 const double *s, double *y)
+{
+    if (gated(g)) return;
+    const int lane = threadIdx.x;
+    const int k = (ds->done & DONE_INNER) ? ds->conv_i : ds->nit - 1;
+    if (lane == 0) ds->upd_k = k;
+    const int ld = m + 1;
+    double yj = lane <= k ? s[lane] : 0.0;
+    double hrow[kMaxRestart];
+#pragma unroll
+    for (int i = 0; i < kMaxRestart; i++) hrow[i] = (lane <= k && i <= k) ? H[lane + i * ld] : 0.0;
+#pragma unroll
+    for (int i = kMaxRestart - 1; i >= 0; i--) {
+        if (i > k) continue;                              // uniform
+        if (lane == i) yj = yj / hrow[i];
+        const double yi = __shfl(yj, i, 64);
+        if (lane < i) yj = yj - hrow[i] * yi;
+    }
+    if (lane <= k) y[lane] = yj;
+}
+
+// the same for restarts above kMaxRestart: one thread, serial
+__global__ void k_update_y_serial(Gate g, int m, DevState *ds, const double *H, const double *s,
+                                  double *y)
 {
     if (gated(g)) return;
     if (threadIdx.x != 0) return;
@@ -945,7 +972,8 @@ void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *p
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
                    const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st)
 {
-    k_update_y<<<1, 64, 0, st>>>(g, m, ds, H, s, ysmall);
+    if (m <= kMaxRestart) k_update_y<<<1, 64, 0, st>>>(g, m, ds, H, s, ysmall);
+    else k_update_y_serial<<<1, 64, 0, st>>>(g, m, ds, H, s, ysmall);
     k_update_x<<<G, kBlock, 0, st>>>(g, ds, ysmall, V, ldv, acc, Ppad / 2);
 }
 void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st)

@@ -148,8 +148,8 @@ struct gg_solver {
     size_t prof_used = 0;
     struct Mark { int kind, i, e0, e1; };
     std::vector<Mark> marks;
-    double prof_ms[GG_PROF_NKINDS] = {0, 0, 0};
-    long long prof_cnt[GG_PROF_NKINDS] = {0, 0, 0};
+    double prof_ms[GG_PROF_NKINDS] = {};
+    long long prof_cnt[GG_PROF_NKINDS] = {};
 };
 
 namespace {
@@ -268,8 +268,19 @@ void ensure_workspace(gg_solver *s, int m)
     s->m_alloc = m;
 }
 
+int prof_begin(gg_solver *s, int kind, int i);
+void prof_end(gg_solver *s, int mark);
+
+// one triangular solve, bracketed for in-solve timing when `i` >= 0
+void trsv(gg_solver *s, Gate g, DevTri &T, int kind, int i, const double *in, double *out)
+{
+    const int mk = i >= 0 ? prof_begin(s, kind, i) : -1;
+    launch_trsv(g, T, in, out, s->err.p, s->st);
+    prof_end(s, mk);
+}
+
 // ---- preconditioner operators (enqueue only; graph-capturable) ----------
-void apply_minv(gg_solver *s, Gate g, const double *in, double *out)
+void apply_minv(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 {
     if (s->pkind == GG_PRECOND_NONE) {
         Gate g2 = g;
@@ -277,22 +288,22 @@ void apply_minv(gg_solver *s, Gate g, const double *in, double *out)
         launch_copy(in, out, s->Ppad, s->st);   // copy is not gated: harmless
         return;
     }
-    launch_trsv(g, s->L, in, s->t1.p, s->err.p, s->st);
-    launch_trsv(g, s->U, s->t1.p, out, s->err.p, s->st);
+    trsv(s, g, s->L, GG_PROF_TRSV_L, i, in, s->t1.p);
+    trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, out);
 }
 // split: Ml(v) = L^-1 P_r D_l^-1 v   (DevPrecond_left, src/preconditioner.cu:1592-1626)
-void apply_left(gg_solver *s, Gate g, const double *in, double *out)
+void apply_left(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 {
     const int n = s->A.n;
     launch_gather_divsrc(g, in, s->lscale.p, s->prow.p, s->t1.p, n, s->st);
-    launch_trsv(g, s->L, s->t1.p, out, s->err.p, s->st);
+    trsv(s, g, s->L, GG_PROF_TRSV_L, i, s->t1.p, out);
 }
 // split: Mr(v) = D_r^-1 P_c U^-1 M v   (DevPrecond_right, :1629-1657)
-void apply_right(gg_solver *s, Gate g, const double *in, double *out)
+void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 {
     const int n = s->A.n;
     launch_mul(g, in, s->middle.p, s->t1.p, n, s->st);
-    launch_trsv(g, s->U, s->t1.p, s->t2.p, s->err.p, s->st);
+    trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
     launch_gather_divdst(g, s->t2.p, s->rscale.p, s->pcol.p, out, n, s->st);
 }
 // split: Mr^-1(x) = M^-1 U P_c^-1 D_r x   (DevPrecond_starting_value, :1561-1589)
@@ -320,15 +331,16 @@ int prof_event(gg_solver *s)
     GG_HIP(hipEventRecord(s->prof_pool[s->prof_used], s->st));
     return (int)s->prof_used++;
 }
-void prof_begin(gg_solver *s, int kind, int i)
+int prof_begin(gg_solver *s, int kind, int i)
 {
-    if (!s->prof_on) return;
+    if (!s->prof_on) return -1;
     s->marks.push_back({kind, i, prof_event(s), -1});
+    return (int)s->marks.size() - 1;
 }
-void prof_end(gg_solver *s)
+void prof_end(gg_solver *s, int mark)
 {
-    if (!s->prof_on) return;
-    s->marks.back().e1 = prof_event(s);
+    if (!s->prof_on || mark < 0) return;
+    s->marks[mark].e1 = prof_event(s);
 }
 // after a cycle has completed: account marks of iterations that really ran
 void prof_collect(gg_solver *s, int executed)
@@ -374,23 +386,24 @@ void enqueue_cycle(gg_solver *s, int m)
         gi.nit = &ds->nit;
         gi.i = i;
         double *vi = s->V.p + (long long)i * P;
+        int mk;
         if (!split) {
-            prof_begin(s, GG_PROF_SPMV, i);
+            mk = prof_begin(s, GG_PROF_SPMV, i);
             launch_spmv(gi, s->dA, vi, nullptr, s->ww.p, false, s->st);        // ww = A v_i
-            prof_end(s);
-            prof_begin(s, GG_PROF_PRECOND, i);
-            apply_minv(s, gi, s->ww.p, s->w.p);                                // w = M^-1 ww
-            prof_end(s);
+            prof_end(s, mk);
+            mk = prof_begin(s, GG_PROF_PRECOND, i);
+            apply_minv(s, gi, s->ww.p, s->w.p, i);                             // w = M^-1 ww
+            prof_end(s, mk);
         } else {
-            apply_right(s, gi, vi, s->z.p);                                    // z = Mr v_i
-            prof_begin(s, GG_PROF_SPMV, i);
+            apply_right(s, gi, vi, s->z.p, i);                                 // z = Mr v_i
+            mk = prof_begin(s, GG_PROF_SPMV, i);
             launch_spmv(gi, s->dA, s->z.p, nullptr, s->ww.p, false, s->st);    // ww = A z
-            prof_end(s);
-            prof_begin(s, GG_PROF_PRECOND, i);
-            apply_left(s, gi, s->ww.p, s->w.p);                                // w = Ml ww
-            prof_end(s);
+            prof_end(s, mk);
+            mk = prof_begin(s, GG_PROF_PRECOND, i);
+            apply_left(s, gi, s->ww.p, s->w.p, i);                             // w = Ml ww
+            prof_end(s, mk);
         }
-        prof_begin(s, GG_PROF_MGS, i);
+        mk = prof_begin(s, GG_PROF_MGS, i);
         double *pin = s->partA.p, *pout = s->partB.p;
         launch_dot(gi, s->w.p, s->V.p, pin, s->G, P, s->st);                   // <w, v_0>
         for (int k = 0; k <= i; k++) {
@@ -401,7 +414,7 @@ void enqueue_cycle(gg_solver *s, int m)
         }
         launch_arnoldi_finalize(gi, i, m, ds, pin, s->G, s->w.p, s->V.p + (long long)(i + 1) * P,
                                 s->H.p, s->cs.p, s->sn.p, s->s.p, s->hist.p, P, s->st);
-        prof_end(s);
+        prof_end(s, mk);
     }
     Gate gu;
     gu.done = &ds->done;
@@ -974,6 +987,12 @@ double gg_bytes_precond(gg_solver *s)
 {
     if (!s || s->pkind < 0) return 0.0;
     return s->L.bytes + s->U.bytes;
+}
+
+double gg_bytes_trsv(gg_solver *s, int which)
+{
+    if (!s || s->pkind < 0 || (which != 0 && which != 1)) return 0.0;
+    return which == 0 ? s->L.bytes : s->U.bytes;
 }
 
 }  // extern "C"

@@ -27,9 +27,9 @@ EXPORTS = [
     "gg_uses_wavefront", "gg_solve", "gg_solve_device", "gg_get_history", "gg_spmv",
     "gg_precond_apply", "gg_time_spmv", "gg_time_precond", "gg_bytes_spmv",
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
-    "gg_trace_precond",
+    "gg_trace_precond", "gg_bytes_trsv",
 ]
-PROF_SPMV, PROF_PRECOND, PROF_MGS = range(3)
+PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
 
 
 class Options(ctypes.Structure):
@@ -90,6 +90,8 @@ def lib():
         L.gg_bytes_spmv.restype = ctypes.c_double
         L.gg_bytes_precond.argtypes = [_VP]
         L.gg_bytes_precond.restype = ctypes.c_double
+        L.gg_bytes_trsv.argtypes = [_VP, ctypes.c_int]
+        L.gg_bytes_trsv.restype = ctypes.c_double
         L.gg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.gg_profile_enable.argtypes = [_VP, ctypes.c_int]
         L.gg_profile_reset.argtypes = [_VP]
@@ -240,6 +242,10 @@ class Solver:
 
     def bytes_precond(self):
         return lib().gg_bytes_precond(self.h)
+
+    def bytes_trsv(self, which):
+        """algorithmic bytes of one triangular solve (0 = L / Ml, 1 = U / Mr)"""
+        return lib().gg_bytes_trsv(self.h, int(which))
 
 
 def device_count():

@@ -147,7 +147,9 @@ enum gg_prof_kind {
     GG_PROF_SPMV = 0,      /* ww = A v_i                                  */
     GG_PROF_PRECOND = 1,   /* w = M^-1 ww (both triangular solves)        */
     GG_PROF_MGS = 2,       /* <w,v_0>, i+1 fused MGS steps, norm + Givens */
-    GG_PROF_NKINDS = 3
+    GG_PROF_TRSV_L = 3,    /* the lower triangular solve alone (L / Ml)   */
+    GG_PROF_TRSV_U = 4,    /* the upper triangular solve alone (U / Mr)   */
+    GG_PROF_NKINDS = 5
 };
 int gg_profile_enable(gg_solver *s, int on);
 int gg_profile_reset(gg_solver *s);
@@ -156,6 +158,7 @@ int gg_profile_get(gg_solver *s, int kind, int *launches, double *total_ms);
 /* bytes the solver moves per unit of work (algorithmic) */
 double gg_bytes_spmv(gg_solver *s);
 double gg_bytes_precond(gg_solver *s);
+double gg_bytes_trsv(gg_solver *s, int which);   /* 0 = L / Ml, 1 = U / Mr */
 
 /* Diagnostics: run one wavefront triangular solve (which: 0 = L / Ml, 1 = U / Mr)
  * on the current right-hand side and return, per band, the device real-time

@@ -1,0 +1,73 @@
+"""Turn rocprofv3 PMC passes into per-kernel HBM bytes per launch.
+
+    python profiles/pmc_traffic.py FETCH_DIR WRITE_DIR [out.json]
+
+FETCH_DIR / WRITE_DIR hold the csv output of
+    rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv ...
+    rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv ...
+(separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).
+Corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE is in KiB and on gfx950
+reports half the bytes of a 16-B/lane streaming read, so it is doubled;
+WRITE_SIZE (KiB) is exact for 16-B/lane streaming stores.  Infinity-Cache hits
+are counted by these memory-side counters, not excluded.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+
+def short(name):
+    """'void gg::(anonymous namespace)::k_trsv_wave2d<false, 2, false>(gg::Gate, ...)'
+    -> 'k_trsv_wave2d<false, 2, false>'"""
+    name = re.sub(r"^void ", "", name.strip())
+    name = name.split("(gg::")[0] if "(gg::" in name else name
+    m = re.search(r"(k_[A-Za-z0-9_]+(<[^()]*>)?)", name)
+    return m.group(1) if m else name
+
+
+def per_kernel(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    acc = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter:
+                    continue
+                k = short(row["Kernel_Name"])
+                v = float(row["Counter_Value"])
+                key = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                e = acc.setdefault(k, {})
+                e[key] = e.get(key, 0.0) + v          # sum over XCD / shader-engine instances
+    return {k: (sum(e.values()) / len(e), len(e)) for k, e in acc.items()}
+
+
+def main():
+    fdir, wdir = sys.argv[1], sys.argv[2]
+    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "pmc_traffic.json")
+    fetch = per_kernel(fdir, "FETCH_SIZE")
+    write = per_kernel(wdir, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        fk, fn = fetch.get(k, (0.0, 0))
+        wk, wn = write.get(k, (0.0, 0))
+        rd = 2.0 * fk * 1024.0
+        wr = wk * 1024.0
+        res[k] = {"fetch_kib_raw": round(fk, 3), "write_kib_raw": round(wk, 3),
+                  "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                  "hbm_bytes_per_launch": rd + wr, "dispatches": [fn, wn]}
+    doc = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (separate passes)",
+           "correction": "read = 2 x FETCH_SIZE KiB (gfx950 16-B/lane streaming reads); write = WRITE_SIZE KiB",
+           "kernels": res}
+    with open(out, "w") as f:
+        json.dump(doc, f, indent=1)
+    for k, v in res.items():
+        print(f"{k:45s} read {v['read_bytes_per_launch']/1e6:9.3f} MB  write {v['write_bytes_per_launch']/1e6:9.3f} MB")
+
+
+if __name__ == "__main__":
+    main()

@@ -244,8 +244,9 @@ def test_edge_cases(solver):
     o, ot = run(lambda: O.gmres_left(A, L, U, b, m=10, max_iter=0, tol=1e-10))
     check_gmres(g, o)
     check_exact(g, ot)
-    # restart m = 1 and a cycle cut short by max_iter (Update of the last filled column)
-    for m, mi in ((1, 17), (7, 25)):
+    # restart m = 1, a cycle cut short by max_iter (Update of the last filled
+    # column), and m = 80 (above the one-wave Update kernel: the serial one)
+    for m, mi in ((1, 17), (7, 25), (64, 100), (80, 170)):
         g = solver.solve(b, restart=m, max_iter=mi, tol=1e-300)
         o, ot = run(lambda: O.gmres_left(A, L, U, b, m=m, max_iter=mi, tol=1e-300))
         check_gmres(g, o)
