@@ -7,7 +7,7 @@ namespace gg {
 
 // Device-side GMRES control block (one per solver, lives in HBM).  Kernels of
 // a restart cycle read it to skip work once converged, so a whole cycle can be
-// enqueued (or replayed as a hipGraph) with a single host sync per cycle.
+// enqueued with a single host sync per cycle.
 struct DevState {
     double normb, beta, resid, tol;
     int done;       // bit flags: 1 inner-converged, 2 restart-converged, 4 converged at start

@@ -67,17 +67,13 @@ enum gg_precond_op {
     GG_APPLY_START = 3     /* split: Mr^-1 (DevPrecond_starting_value)                         */
 };
 
-/* solver flags */
-#define GG_FLAG_NO_GRAPH      0x1   /* launch eagerly instead of replaying a hipGraph per cycle */
-#define GG_FLAG_NO_WAVEFRONT  0x2   /* force the generic level-scheduled triangular solve      */
-
 typedef struct gg_solver gg_solver;
 
 typedef struct gg_options {
     int restart;       /* m  (reference default 32, src/defs.h:11)                 */
     int max_iter;      /* reference semantics: in = limit                          */
     double tol;        /* relative residual target on ||M r|| / ||M b||            */
-    int flags;         /* GG_FLAG_*                                               */
+    int flags;         /* reserved, 0                                             */
 } gg_options;
 
 typedef struct gg_result {
