@@ -259,15 +259,23 @@ constexpr int kSpinLimit = 1 << 20;
 #define GG_WAVE_RING 5
 #endif
 constexpr int kWaveRing = GG_WAVE_RING;
+// One loader wave streaming every array, or one per array.  Every wave with
+// loads in flight on a CU delays that CU's hand-off polls (MI355X_MICROARCH.md
+// handoff-1to1: the price sits in the consumer CU's memory queue).
+#ifndef GG_WAVE_LOADERS
+#define GG_WAVE_LOADERS 1
+#endif
+constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 
 template <int DIV>
 struct WaveCfg {
     static constexpr int A = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;   // streamed arrays
     static constexpr int SLOT = A * kWavePB * 64;                        // double2 per ring slot
     static constexpr int R = kWaveRing;                                  // ring slots
-    static constexpr int THREADS = (3 + A) * 64;                        // compute, boundary, writer, loaders
+    static constexpr int LOADERS = kWaveLoaders == 1 ? 1 : A;           // loader waves
+    static constexpr int THREADS = (3 + LOADERS) * 64;                  // compute, boundary, writer, loaders
     static constexpr int LDS2 = R * SLOT + 64 + 2 * kWavePB * 64;        // ring, boundary, x staging
-    static_assert(R >= 4 && (R - 3) * kWavePB <= 63, "ring depth vs vmcnt range");
+    static_assert(R >= 4 && (R - 3) * kWavePB * (LOADERS == 1 ? A : 1) <= 63, "ring depth vs vmcnt range");
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
 };
 
@@ -315,23 +323,27 @@ __device__ __forceinline__ bool rcp_safe(double v)
 }
 
 // loader wave: one array; batch j -> ring slot j % R; batches j, j+1 landed by barrier j
-template <bool FWD, int R, int SLOT>
-__device__ __forceinline__ void wave_loader(const double2 *src, double2 *lds, int np, int nbatch)
+template <bool FWD, int R, int SLOT, int NA>
+__device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *lds, int np, int nbatch)
 {
+    constexpr int PB = kWavePB * 64;            // double2 per array per slot
     auto issue = [&](int j) {
         double2 *slot = lds + (j % R) * SLOT;
 #pragma unroll
-        for (int kk = 0; kk < kWavePB; kk++) {
-            const int p = j * kWavePB + kk;
-            const long long q = (long long)(FWD ? p : np - 1 - p) * 64;
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + q), (lds_void_t *)(slot + kk * 64), 16, 0, 0);
-        }
+        for (int a = 0; a < NA; a++)
+#pragma unroll
+            for (int kk = 0; kk < kWavePB; kk++) {
+                const int p = j * kWavePB + kk;
+                const long long q = (long long)(FWD ? p : np - 1 - p) * 64;
+                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src[a] + q),
+                                                 (lds_void_t *)(slot + a * PB + kk * 64), 16, 0, 0);
+            }
     };
     for (int j = 0; j < R - 1 && j < nbatch; j++) issue(j);
     for (int j = 0; j < nbatch; j++) {
         // batches after j+1 may stay in flight
         const int issued = j + R - 1 < nbatch ? j + R - 1 : nbatch;
-        vm_wait_batches<R - 3, kWavePB>(issued - (j + 2));
+        vm_wait_batches<R - 3, NA * kWavePB>(issued - (j + 2));
         raw_barrier();                          // slot (j-1) % R is free from here on
         if (j + R - 1 < nbatch) issue(j + R - 1);
     }
@@ -363,10 +375,17 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
     constexpr int plane = FWD ? 63 : 0;     // lane whose values the next band needs
     unsigned long long *pub = bnd + (long long)band * T;
     if (wave >= 3) {
-        // ------------------------------------------------ loader waves
-        const double *arr = wave == 3 ? b : wave == 4 ? c1 : wave == 5 ? c2 : wave == 6 ? dv : rv;
-        wave_loader<FWD, C::R, C::SLOT>(reinterpret_cast<const double2 *>(arr) + boff,
-                                        lds + (wave - 3) * PB, np, nbatch);
+        // ------------------------------------------------ loader wave(s)
+        const double2 *src[5] = {reinterpret_cast<const double2 *>(b) + boff,
+                                 reinterpret_cast<const double2 *>(c1) + boff,
+                                 reinterpret_cast<const double2 *>(c2) + boff,
+                                 reinterpret_cast<const double2 *>(dv) + boff,
+                                 reinterpret_cast<const double2 *>(rv) + boff};
+        if constexpr (C::LOADERS == 1) {
+            wave_loader<FWD, C::R, C::SLOT, C::A>(src, lds, np, nbatch);
+        } else {
+            wave_loader<FWD, C::R, C::SLOT, 1>(src + (wave - 3), lds + (wave - 3) * PB, np, nbatch);
+        }
         raw_barrier();                      // final barrier (the writer drains the last batch)
         return;
     }
