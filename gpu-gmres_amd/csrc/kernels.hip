@@ -170,24 +170,64 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
                                                         double *y)
 {
     if (gated(g)) return;
+    constexpr int U = kSpmvCap / kBlock;        // products per thread
     __shared__ double prod[kSpmvCap];
+    __shared__ int srp[kBlock + 1];
+    const int tid = threadIdx.x;
     const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
-    const int e0 = rp[r0], e1 = rp[r1];
+    const int nr = r1 - r0;                     // <= kBlock rows
+    // the block's nr + 1 row pointers (nr <= kBlock: the last one by thread 0)
+    if (tid < nr) srp[tid] = rp[r0 + tid];
+    if (tid == 0) srp[nr] = rp[r1];
+    __syncthreads();
+    const int e0 = srp[0], e1 = srp[nr];
     const int cnt = e1 - e0;
     if (cnt > kSpmvCap) {   // one long row: strided partial sums + tree
         double acc = 0.0;
-        for (int e = e0 + threadIdx.x; e < e1; e += kBlock) acc += v[e] * x[ci[e]];
+        for (int e = e0 + tid; e < e1; e += kBlock) acc += v[e] * x[ci[e]];
         acc = block_sum(acc);
-        if (threadIdx.x == 0) y[r0] = RESID ? (-1.0 * acc + 1.0 * b[r0]) : acc;
+        if (tid == 0) y[r0] = RESID ? (-1.0 * acc + 1.0 * b[r0]) : acc;
         return;
     }
-    for (int e = threadIdx.x; e < cnt; e += kBlock) prod[e] = v[e0 + e] * x[ci[e0 + e]];
+    // entries in aligned pairs (8-B index and 16-B value loads) from the even
+    // entry at or below e0; all index/value loads first, then all gathers
+    constexpr int U2 = U / 2 + 1;               // pairs per thread (the alignment adds one)
+    const int ea = e0 & ~1;
+    const int npair = (e1 - ea + 1) >> 1;
+    int2 c[U2];
+    double2 vv[U2], xv[U2];
+#pragma unroll
+    for (int u = 0; u < U2; u++) {
+        const int p = tid + u * kBlock;
+        if (p < npair) {
+            c[u] = reinterpret_cast<const int2 *>(ci + ea)[p];
+            vv[u] = reinterpret_cast<const double2 *>(v + ea)[p];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U2; u++) {
+        const int p = tid + u * kBlock;
+        const int e = ea + 2 * p;
+        if (p < npair) {
+            if (e >= e0) xv[u].x = x[c[u].x];
+            if (e + 1 < e1) xv[u].y = x[c[u].y];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U2; u++) {
+        const int p = tid + u * kBlock;
+        const int e = ea + 2 * p;
+        if (p < npair) {
+            if (e >= e0) prod[e - e0] = vv[u].x * xv[u].x;
+            if (e + 1 < e1) prod[e + 1 - e0] = vv[u].y * xv[u].y;
+        }
+    }
     __syncthreads();
-    const int r = r0 + threadIdx.x;
-    if (r < r1) {
+    if (tid < nr) {
         double acc = 0.0;
-        const int a = rp[r] - e0, z = rp[r + 1] - e0;
+        const int a = srp[tid] - e0, z = srp[tid + 1] - e0;
         for (int e = a; e < z; e++) acc += prod[e];
+        const int r = r0 + tid;
         y[r] = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
     }
 }

@@ -29,8 +29,16 @@ void DevCsr::upload(const Csr &A, hipStream_t st)
     n = A.n;
     nnz = A.nnz();
     rp.upload(A.rp, st);
-    ci.upload(A.ci, st);
-    v.upload(A.v, st);
+    // two spare entries: the SpMV reads entries in aligned pairs and may touch
+    // the one after a block's last entry (never used)
+    ci.alloc(A.ci.size() + 2);
+    v.alloc(A.v.size() + 2);
+    GG_HIP(hipMemsetAsync(ci.p, 0, ci.n * sizeof(int), st));
+    GG_HIP(hipMemsetAsync(v.p, 0, v.n * sizeof(double), st));
+    if (!A.ci.empty()) {
+        GG_HIP(hipMemcpyAsync(ci.p, A.ci.data(), A.ci.size() * sizeof(int), hipMemcpyHostToDevice, st));
+        GG_HIP(hipMemcpyAsync(v.p, A.v.data(), A.v.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    }
     std::vector<int> lr;
     std::vector<int> b = spmv_blocks(A, lr);
     nblk = (int)b.size() - 1;
