@@ -38,6 +38,11 @@ int reduce_grid(long long units);  // blocks for the vector kernels (units = Ppa
 
 // ---- vector ops (lengths are Ppad, a multiple of 512) --------------------
 void launch_fill_u64(unsigned long long *p, long long n, unsigned long long v, hipStream_t st);
+// transient step: u = PULSE(it*h); w = B u + (C/h) x   (natural order, n rows)
+void launch_transient_step(int n, int nsrc, const double *pulse, int it, double h, double *u,
+                           const int *src_ptr, const int *src_idx, const double *cdiag,
+                           const double *x, double *w, hipStream_t st);
+void launch_gather_ports(int nport, const int *port, const double *x, double *out, hipStream_t st);
 void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st);  // out[i] = idx[i]<0 ? 0 : in[idx[i]]
 void launch_copy(const double *in, double *out, long long n, hipStream_t st);
 void launch_dot(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, hipStream_t st);

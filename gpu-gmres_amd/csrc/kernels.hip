@@ -639,6 +639,48 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
     }
 }
 
+// ================================================== transient step (C5)
+// PULSE source values at time index it (gen_PULSEut_kernel, src/kernels.cu:223-245);
+// pulse[k] = {vlo, vhi, td, tr, tf, tw, tp}
+__global__ void k_pulse(int nsrc, const double *pulse, int it, double h, double *u)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nsrc) return;
+    const double *q = pulse + 7 * k;
+    const double vlo = q[0], vhi = q[1], td = q[2], tr = q[3], tf = q[4], tw = q[5], tp = q[6];
+    double t = it * h;
+    t = t - floor(t / tp) * tp;
+    double value;
+    if (t < td) value = vlo;
+    else if (t < td + tr) value = vlo + (t - td) * (vhi - vlo) / tr;
+    else if (t < td + tr + tw) value = vhi;
+    else if (t < td + tr + tw + tf) value = vhi - (t - td - tr - tw) * (vhi - vlo) / tf;
+    else value = vlo;
+    u[k] = value;
+}
+
+// w = B u + (C/h) x_prev as the reference step driver forms it
+// (src/mna_solve_gpu_gmres.cpp:585-591): w = 0; w += B u (cs_dl_gaxpy, sources
+// of a row in column order); xnr = 0; xnr += (C/h) x; w += xnr.  B is an
+// incidence matrix (+1 per source), C/h diagonal.
+__global__ void k_transient_rhs(int n, const int *src_ptr, const int *src_idx, const double *u,
+                                const double *cdiag, const double *x, double *w)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    double bu = 0.0;
+    for (int q = src_ptr[r]; q < src_ptr[r + 1]; q++) bu = bu + 1.0 * u[src_idx[q]];
+    double xnr = 0.0;
+    xnr = xnr + cdiag[r] * x[r];
+    w[r] = bu + xnr;
+}
+
+__global__ void k_gather_ports(int nport, const int *port, const double *x, double *out)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < nport) out[j] = x[port[j]];
+}
+
 // ============================================================ GMRES kernels
 __global__ void k_set_normb(const double *part, int G, DevState *ds)
 {
@@ -914,6 +956,20 @@ void launch_fill_u64(unsigned long long *p, long long n, unsigned long long v, h
 {
     k_fill_u64<<<blocks_for(n, kBlock, 4096), kBlock, 0, st>>>(p, n, v);
 }
+void launch_transient_step(int n, int nsrc, const double *pulse, int it, double h, double *u,
+                           const int *src_ptr, const int *src_idx, const double *cdiag,
+                           const double *x, double *w, hipStream_t st)
+{
+    if (nsrc > 0) k_pulse<<<(nsrc + kBlock - 1) / kBlock, kBlock, 0, st>>>(nsrc, pulse, it, h, u);
+    if (n > 0)
+        k_transient_rhs<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, src_ptr, src_idx, u, cdiag, x, w);
+}
+
+void launch_gather_ports(int nport, const int *port, const double *x, double *out, hipStream_t st)
+{
+    if (nport > 0) k_gather_ports<<<(nport + kBlock - 1) / kBlock, kBlock, 0, st>>>(nport, port, x, out);
+}
+
 void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st)
 {
     k_gather<<<blocks_for(n, kBlock, 8192), kBlock, 0, st>>>(in, idx, out, n);

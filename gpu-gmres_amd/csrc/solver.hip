@@ -780,6 +780,68 @@ int gg_solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_optio
     GG_API_END
 }
 
+int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc,
+                 const int *src_node, const double *pulse, int nport, const int *port,
+                 double *x, const gg_options *opt, double *port_out, int *iters_total)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && opt && x && cdiag && iters_total, GG_EINVAL, "null argument");
+    GG_REQUIRE(nsteps >= 0 && nsrc >= 0 && nport >= 0, GG_EINVAL, "negative count");
+    GG_REQUIRE(nsrc == 0 || (src_node && pulse), GG_EINVAL, "null source arrays");
+    GG_REQUIRE(nport == 0 || (port && port_out), GG_EINVAL, "null port arrays");
+    GG_REQUIRE(s->have_A, GG_ESTATE, "gg_transient: no matrix");
+    set_device(s);
+    const int n = s->A.n;
+    // B^T by row: the sources of each row in ascending k (cs_dl_gaxpy column order)
+    std::vector<int> sptr(n + 1, 0), sidx(nsrc);
+    for (int k = 0; k < nsrc; k++) {
+        GG_REQUIRE(src_node[k] >= 0 && src_node[k] < n, GG_EINVAL, "source node out of range");
+        sptr[src_node[k] + 1]++;
+    }
+    for (int r = 0; r < n; r++) sptr[r + 1] += sptr[r];
+    {
+        std::vector<int> fill(sptr.begin(), sptr.end() - 1);
+        for (int k = 0; k < nsrc; k++) sidx[fill[src_node[k]]++] = k;
+    }
+    for (int j = 0; j < nport; j++) GG_REQUIRE(port[j] >= 0 && port[j] < n, GG_EINVAL, "port out of range");
+    DBuf<int> d_sptr, d_sidx, d_port;
+    DBuf<double> d_pulse, d_u, d_c, d_w, d_pv;
+    d_sptr.upload(sptr, s->st);
+    d_sidx.upload(sidx.data(), sidx.size(), s->st);
+    d_pulse.upload(pulse, (size_t)7 * nsrc, s->st);
+    d_u.alloc(std::max(nsrc, 1));
+    d_c.upload(cdiag, n, s->st);
+    d_w.alloc(std::max(n, 1));
+    d_port.upload(port, nport, s->st);
+    d_pv.alloc((size_t)std::max(nport, 1) * (nsteps + 1));
+    DBuf<double> xd;
+    xd.upload(x, n, s->st);
+    double *d_x = xd.p;
+    launch_gather_ports(nport, d_port.p, d_x, d_pv.p, s->st);
+    int total = 0, status = GG_OK;
+    for (int it = 1; it <= nsteps; it++) {
+        launch_transient_step(n, nsrc, d_pulse.p, it, h, d_u.p, d_sptr.p, d_sidx.p, d_c.p, d_x,
+                              d_w.p, s->st);
+        gg_result r{};
+        const int rc = solve_device(s, d_w.p, d_x, opt, &r);
+        if (rc != GG_OK) status = rc;
+        total += r.iters;
+        launch_gather_ports(nport, d_port.p, d_x, d_pv.p + (size_t)it * nport, s->st);
+    }
+    if (nport) {
+        std::vector<double> pv((size_t)nport * (nsteps + 1));
+        GG_HIP(hipMemcpyAsync(pv.data(), d_pv.p, pv.size() * sizeof(double), hipMemcpyDeviceToHost, s->st));
+        GG_HIP(hipStreamSynchronize(s->st));
+        for (int it = 0; it <= nsteps; it++)
+            for (int j = 0; j < nport; j++) port_out[(size_t)j * (nsteps + 1) + it] = pv[(size_t)it * nport + j];
+    }
+    GG_HIP(hipMemcpyAsync(x, d_x, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
+    *iters_total = total;
+    return status;
+    GG_API_END
+}
+
 int gg_solve(gg_solver *s, const double *b, double *x, const gg_options *opt, gg_result *res)
 {
     GG_API_BEGIN

@@ -27,7 +27,7 @@ EXPORTS = [
     "gg_uses_wavefront", "gg_solve", "gg_solve_device", "gg_get_history", "gg_spmv",
     "gg_precond_apply", "gg_time_spmv", "gg_time_precond", "gg_bytes_spmv",
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
-    "gg_trace_precond", "gg_bytes_trsv",
+    "gg_trace_precond", "gg_bytes_trsv", "gg_transient",
 ]
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
 
@@ -78,6 +78,9 @@ def lib():
         L.gg_solve_device.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options),
                                       ctypes.POINTER(Result)]
         L.gg_get_history.argtypes = [_VP, ctypes.c_void_p, ctypes.c_int]
+        L.gg_transient.argtypes = [_VP, ctypes.c_int, ctypes.c_double, _D, ctypes.c_int, _I, _D,
+                                   ctypes.c_int, _I, _D, ctypes.POINTER(Options), _D,
+                                   ctypes.POINTER(ctypes.c_int)]
         L.gg_spmv.argtypes = [_VP, _D, _D]
         L.gg_precond_apply.argtypes = [_VP, ctypes.c_int, _D, _D]
         L.gg_time_spmv.argtypes = [_VP, ctypes.c_int, ctypes.c_int,
@@ -188,6 +191,27 @@ class Solver:
                                           ctypes.byref(r)), allow_nc=True)
         return dict(ret=rc, iters=r.iters, inner=r.inner_iters, restarts=r.restarts,
                     relres=r.relres, solve_ms=r.solve_ms)
+
+    def transient(self, nsteps, h, cdiag, src_node, pulse, ports, x0, restart=32,
+                  max_iter=10000, tol=1e-7, flags=0):
+        """Backward-Euler loop on the device (gg_transient): returns dict(x, ports
+        [nport, nsteps+1], iters_total, ret)."""
+        n = self.n
+        x = np.array(x0, np.float64, copy=True)
+        src_node = np.ascontiguousarray(src_node, np.int32)
+        pulse = np.ascontiguousarray(pulse, np.float64).reshape(-1)
+        ports = np.ascontiguousarray(ports, np.int32)
+        pv = np.zeros(max(len(ports), 1) * (nsteps + 1))
+        tot = ctypes.c_int()
+        o = Options(int(restart), int(max_iter), float(tol), int(flags))
+        rc = _check(lib().gg_transient(self.h, int(nsteps), float(h),
+                                       np.ascontiguousarray(cdiag, np.float64), len(src_node),
+                                       src_node if len(src_node) else np.zeros(1, np.int32),
+                                       pulse if pulse.size else np.zeros(7), len(ports),
+                                       ports if len(ports) else np.zeros(1, np.int32), x,
+                                       ctypes.byref(o), pv, ctypes.byref(tot)), allow_nc=True)
+        return dict(x=x, ports=pv[: len(ports) * (nsteps + 1)].reshape(len(ports), nsteps + 1),
+                    iters_total=tot.value, ret=rc)
 
     def history(self):
         n = lib().gg_get_history(self.h, None, 0)

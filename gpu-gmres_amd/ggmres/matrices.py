@@ -78,6 +78,18 @@ def transient(G, c=1e-3, h=1e-2):
     return _finish(G + sp.identity(n, format="csr") * (c / h))
 
 
+def pulse_sources(n, frac=0.01, h=1e-2, seed=20261015):
+    """C5 sources: a seeded 1 % of the nodes each carry a PULSE
+    current, vlo 0, vhi 1e-3, td 0, tr = tf = 10 h, tw = 100 h, period 400 h.
+    Returns (src_node int32[nsrc], pulses float64[nsrc, 7] as
+    {vlo, vhi, td, tr, tf, tw, tp})."""
+    rng = np.random.default_rng(seed)
+    nsrc = max(1, int(round(frac * n)))
+    nodes = np.sort(rng.choice(n, size=nsrc, replace=False)).astype(np.int32)
+    q = np.array([0.0, 1e-3, 0.0, 10 * h, 10 * h, 100 * h, 400 * h])
+    return nodes, np.tile(q, (nsrc, 1))
+
+
 def read_mtx(path):
     import scipy.io
     return _finish(scipy.io.mmread(path))

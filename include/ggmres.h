@@ -156,6 +156,25 @@ double gg_bytes_spmv(gg_solver *s);
 double gg_bytes_precond(gg_solver *s);
 double gg_bytes_trsv(gg_solver *s, int which);   /* 0 = L / Ml, 1 = U / Mr */
 
+/* Backward-Euler transient loop on one factorization: the step driver of
+ * mna_solve_gpu_gmres (src/mna_solve_gpu_gmres.cpp:564-647) with PULSE sources
+ * evaluated as gen_PULSEut_kernel (src/kernels.cu:223-245), entirely on the
+ * device.  The matrix set by gg_set_matrix is A = G + C/h.  For it = 1..nsteps:
+ *   u_k = PULSE_k(it * h)                      pulse: 7 doubles per source
+ *                                              {vlo, vhi, td, tr, tf, tw, tp}
+ *   w   = B u + (C/h) x                        B: source k adds +1 * u_k at row
+ *                                              src_node[k]; cdiag = diag(C/h)
+ *   x   = GMRES(A, w; warm start x)            opt as gg_solve
+ *   port_out[j * (nsteps + 1) + it] = x[port[j]]   (column 0 = the initial x)
+ * All arrays are host arrays; x (n doubles) is the initial state in and the
+ * final state out, and stays in HBM between steps (only the right-hand side
+ * assembly, the solves and the port capture run per step, all on the device).
+ * *iters_total = sum of the per-step iteration counts (the reference's
+ * iterTotal); returns GG_OK, or the status of the last non-converged step. */
+int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc,
+                 const int *src_node, const double *pulse, int nport, const int *port,
+                 double *x, const gg_options *opt, double *port_out, int *iters_total);
+
 /* Diagnostics: run one wavefront triangular solve (which: 0 = L / Ml, 1 = U / Mr)
  * on the current right-hand side and return, per band, the device real-time
  * clock (100 MHz) at the start of each 8-step batch plus one end stamp, then

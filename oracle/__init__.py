@@ -226,3 +226,51 @@ def gmres_split(A, P, b, x0=None, m=32, max_iter=10000, tol=1e-7, hist_cap=None)
                                 ctypes.byref(mi), ctypes.byref(tl), hist, cap,
                                 ctypes.byref(hl), ctypes.byref(inner))
     return _gmres_out(ret, x, mi, tl, hist, hl, inner)
+
+
+# ---------------------------------------------------------------- transient (C5)
+def pulse(q, it, h):
+    """PULSE source value at time index it (gen_PULSEut_kernel, src/kernels.cu:223-245)."""
+    f = lib().orc_pulse
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_double]
+    q = np.ascontiguousarray(q, np.float64)
+    return f(q.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(it), float(h))
+
+
+def transient_rhs(cdiag, src_node, u, x):
+    """w = B u + (C/h) x as the reference step driver forms it."""
+    n = len(x)
+    w = np.zeros(n)
+    src_node = np.ascontiguousarray(src_node, np.int32)
+    f = lib().orc_transient_rhs
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    u = np.ascontiguousarray(u, np.float64)
+    c = np.ascontiguousarray(cdiag, np.float64)
+    xx = np.ascontiguousarray(x, np.float64)
+    f(n, len(src_node), src_node.ctypes.data, u.ctypes.data, c.ctypes.data, xx.ctypes.data,
+      w.ctypes.data)
+    return w
+
+
+def transient(A, L, U, nsteps, h, cdiag, src_node, pulses, ports, x0, m=32, max_iter=10000,
+              tol=1e-7):
+    """The reference's backward-Euler step driver (src/mna_solve_gpu_gmres.cpp:564-647)
+    with GMRES_leftILU0 per step, warm start x_{t-1}; returns dict(x, ports, iters_total)."""
+    x = np.array(x0, np.float64, copy=True)
+    pulses = np.asarray(pulses, np.float64).reshape(-1, 7)
+    ports = np.asarray(ports, np.int64)
+    pv = np.zeros((len(ports), nsteps + 1))
+    pv[:, 0] = x[ports]
+    total = 0
+    ret = 0
+    for it in range(1, nsteps + 1):
+        u = np.array([pulse(q, it, h) for q in pulses])
+        w = transient_rhs(cdiag, src_node, u, x)
+        o = gmres_left(A, L, U, w, x0=x, m=m, max_iter=max_iter, tol=tol)
+        x = o["x"]
+        total += o["iters"]
+        ret = ret or o["ret"]
+        pv[:, it] = x[ports]
+    return dict(x=x, ports=pv, iters_total=total, ret=ret)

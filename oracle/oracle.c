@@ -665,3 +665,28 @@ int orc_gmres_split(int n, const int *rp, const int *ci, const double *v,
     op_t op = {1, n, rp, ci, v, NULL, NULL, NULL, NULL, NULL, NULL, p};
     return gmres_core(&op, b, x, m, max_iter, tol, hist, hist_cap, hist_len, inner_iters);
 }
+
+/* ---------------------------------------------------------------- transient */
+double orc_pulse(const double *q, int it, double h)
+{
+    const double vlo = q[0], vhi = q[1], td = q[2], tr = q[3], tf = q[4], tw = q[5], tp = q[6];
+    double t = it * h;                         /* mytime = idxt * tstep */
+    t = t - floor(t / tp) * tp;
+    if (t < td) return vlo;
+    if (t < td + tr) return vlo + (t - td) * (vhi - vlo) / tr;
+    if (t < td + tr + tw) return vhi;
+    if (t < td + tr + tw + tf) return vhi - (t - td - tr - tw) * (vhi - vlo) / tf;
+    return vlo;
+}
+
+void orc_transient_rhs(int n, int nsrc, const int *src_node, const double *u,
+                       const double *cdiag, const double *x, double *w)
+{
+    for (int i = 0; i < n; i++) w[i] = 0.0;
+    for (int k = 0; k < nsrc; k++) w[src_node[k]] += 1.0 * u[k];   /* cs_dl_gaxpy(B, u, w) */
+    for (int i = 0; i < n; i++) {
+        double xnr = 0.0;
+        xnr += cdiag[i] * x[i];                                     /* cs_dl_gaxpy(right, xn, xnr) */
+        w[i] += xnr;                                                /* w += xnr */
+    }
+}

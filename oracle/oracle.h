@@ -94,6 +94,16 @@ int orc_gmres_split(int n, const int *rp, const int *ci, const double *v,
                     const double *b, double *x, int m, int *max_iter, double *tol,
                     double *hist, int hist_cap, int *hist_len, int *inner_iters);
 
+/* Transient step (src/mna_solve_gpu_gmres.cpp:564-647).  PULSE value of a
+ * source at time index it (gen_PULSEut_kernel, src/kernels.cu:223-245);
+ * q = {vlo, vhi, td, tr, tf, tw, tp}. */
+double orc_pulse(const double *q, int it, double h);
+/* w = B u + (C/h) x formed as the driver does: w = 0; w += B u (cs_dl_gaxpy,
+ * B incidence: source k adds +1 * u[k] at row src_node[k], k ascending);
+ * xnr = 0; xnr += diag(cdiag) x; w += xnr. */
+void orc_transient_rhs(int n, int nsrc, const int *src_node, const double *u,
+                       const double *cdiag, const double *x, double *w);
+
 #ifdef __cplusplus
 }
 #endif

@@ -272,3 +272,31 @@ def test_gmres_split_warm_start():
     r1 = O.gmres_split(A, P, b, m=32, max_iter=2000, tol=1e-10)
     r2 = O.gmres_split(A, P, b, x0=r1["x"], m=32, max_iter=2000, tol=1e-10)
     assert r2["ret"] == 0 and r2["iters"] <= 1
+
+
+def test_pulse_semantics():
+    """gen_PULSEut_kernel (src/kernels.cu:223-245): periodic trapezoid."""
+    q = [0.0, 1e-3, 0.0, 0.1, 0.1, 1.0, 4.0]     # vlo vhi td tr tf tw tp
+    h = 0.01
+    assert O.pulse(q, 0, h) == 0.0
+    assert O.pulse(q, 5, h) == 0.0 + (0.05 - 0.0) * (1e-3 - 0.0) / 0.1      # rising edge
+    assert O.pulse(q, 50, h) == 1e-3                                          # high
+    t = 115 * h
+    assert O.pulse(q, 115, h) == 1e-3 - (t - 0.0 - 0.1 - 1.0) * (1e-3 - 0.0) / 0.1
+    assert O.pulse(q, 300, h) == 0.0                                          # low
+    assert O.pulse(q, 405, h) == O.pulse(q, 5, h) or abs(O.pulse(q, 405, h) - 5e-4) < 1e-15
+
+
+def test_transient_rhs_order():
+    """w = B u + (C/h) x: sources of a row in ascending k, then + (0 + c x)."""
+    n = 6
+    src = np.array([4, 1, 4], np.int32)
+    u = np.array([1.0, 2.0, 1e-17])
+    c = np.full(n, 0.5)
+    x = np.arange(n, dtype=np.float64) - 2.0
+    w = O.transient_rhs(c, src, u, x)
+    ref = np.zeros(n)
+    ref[4] = (0.0 + 1.0) + 1e-17
+    ref[1] = 2.0
+    ref = ref + (0.0 + c * x)
+    assert np.array_equal(w, ref)
