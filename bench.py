@@ -13,9 +13,14 @@ algorithmic bytes from SURVEY.md 8(d) (DESIGN.md "Kernels"); traffic: HBM bytes
 per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json).  cpu_baseline: the fp64 oracle restatement (oracle/, serial C)
 on a bounded sample of the same workload, rank 0 only.
 
-Multi-GPU (torchrun, one rank per GPU): every rank solves its own C2 system
-(replicas, "scaling": "weak"); the arrow-partitioned sharded solve is DESIGN.md
-"Multi-GPU".
+--workload c5: the transient loop (gg_transient: A = G + C/h on the C2 grid, 1 %
+PULSE sources, --c5-steps backward-Euler steps per step, warm start); value =
+GMRES iterations of all steps / time.
+
+Multi-GPU (torchrun, one rank per GPU): every rank solves its own system (C2
+replicas, or its own C5 source scenario: independent many-RHS scenarios),
+"scaling": "weak", no collective on the data path; the arrow-partitioned
+sharded solve is DESIGN.md "Multi-GPU".
 """
 import argparse
 import json
@@ -45,6 +50,10 @@ def parse():
     p.add_argument("--cpu-iters", type=int, default=120,
                    help="oracle iterations timed for cpu_baseline (0 = skip)")
     p.add_argument("--no-profile", action="store_true", help="do not bracket kernels with events")
+    p.add_argument("--workload", choices=["c2", "c5"], default="c2",
+                   help="c2: one C2 solve per step (the headline); c5: a backward-Euler "
+                        "transient (A = G + C/h, 1%% PULSE sources) of --c5-steps time steps per step")
+    p.add_argument("--c5-steps", type=int, default=100)
     return p.parse_args()
 
 
@@ -98,7 +107,11 @@ def main():
     import ggmres
     from ggmres import matrices as M
 
+    c5 = a.workload == "c5"
+    h5 = 1e-2
     A = M.laplacian_5pt(a.grid)
+    if c5:
+        A = M.transient(A, c=1e-3, h=h5)
     n = A.shape[0]
     b = M.rhs_ones(A)
     s = ggmres.Solver(local)
@@ -108,8 +121,18 @@ def main():
     t_setup = time.perf_counter() - t_setup
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
+    if c5:
+        # scenario per rank: its own seeded source set (independent many-RHS scenarios)
+        nodes, pulses = M.pulse_sources(n, frac=0.01, h=h5, seed=20261015 + rank)
+        cdiag = np.full(n, 1e-3 / h5)
+        ports = np.array([0, n // 2, n - 1], np.int32)
 
     def step():
+        if c5:
+            r = s.transient(a.c5_steps, h5, cdiag, nodes, pulses, ports, np.zeros(n),
+                            restart=a.restart, max_iter=a.max_iter, tol=a.tol)
+            return dict(inner=r["iters_total"], iters=r["iters_total"], relres=None,
+                        ret=r["ret"])
         dx.zero_()
         torch.cuda.synchronize()
         return s.solve_device(db.data_ptr(), dx.data_ptr(), restart=a.restart,
@@ -143,7 +166,7 @@ def main():
     fam = {}
     spmv_bytes = s.bytes_spmv()
     pre_bytes = s.bytes_precond()
-    mgs_tot, mgs_it = mgs_bytes(n, a.restart, [r["inner"] for r in res])
+    mgs_tot, mgs_it = mgs_bytes(n, a.restart, [r["inner"] for r in res]) if not c5 else (0.0, 0)
     for name, kind, per in (("spmv", ggmres.PROF_SPMV, spmv_bytes),
                             ("ilu0_apply", ggmres.PROF_PRECOND, pre_bytes),
                             ("trsv_L", ggmres.PROF_TRSV_L, s.bytes_trsv(0)),
@@ -153,7 +176,7 @@ def main():
         if cnt == 0:
             continue
         avg_us = ms * 1e3 / cnt
-        byt = per if per is not None else mgs_tot / max(mgs_it, 1)
+        byt = per if per is not None else (mgs_tot / max(mgs_it, 1) if mgs_it else float("nan"))
         fam[name] = {"launches": cnt, "avg_us": round(avg_us, 3),
                      "alg_bytes_per_launch": byt,
                      "achieved_gbs": round(byt / (avg_us * 1e-6) / 1e9, 1),
@@ -178,7 +201,7 @@ def main():
 
     # ---- CPU baseline (rank 0, N=1): the oracle restatement -----------------------
     cpu = None
-    if rank == 0 and world == 1 and a.cpu_iters > 0:
+    if rank == 0 and world == 1 and a.cpu_iters > 0 and not c5:
         import oracle as O
         L, U = O.ilu0(A)
         t1 = time.perf_counter()
@@ -194,8 +217,12 @@ def main():
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el_max * 1e3 / a.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU(0) left, "
-                               f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step",
+        "config": {"workload": (f"C5: {a.grid}x{a.grid} 5-pt grid, A = G + C/h (c 1e-3, h 1e-2), "
+                                f"1% PULSE sources (own scenario per rank), ILU(0) left, "
+                                f"GMRES({a.restart}), tol {a.tol:g}, {a.c5_steps} backward-Euler "
+                                f"steps per step, warm start") if c5 else
+                               (f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU(0) left, "
+                                f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step"),
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
                    "wavefront_sptrsv": s.uses_wavefront,
