@@ -290,8 +290,19 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
 // needs every intermediate in the normal range: the host admits WD_RCP only for
 // 2^-100 <= |d| <= 2^100, and the writer wave flags results outside rcp_safe
 // (err bit 2), on which the caller repeats the work with WD_HW.
-constexpr int kWaveBatch = 8;              // steps per batch
-constexpr int kWavePB = kWaveBatch / 2;    // step pairs per batch
+// Steps per batch: one barrier, one boundary hand-over and one LDS-latency
+// exposure per batch, so longer is cheaper per step, as far as the LDS budget
+// lets the ring hold kWaveRing of them (GG_WAVE_BATCH_UNIT for the unit
+// triangle, 3 streams; the non-unit ones stream 4-5 arrays).
+#ifndef GG_WAVE_BATCH_UNIT
+#define GG_WAVE_BATCH_UNIT 16
+#endif
+#ifndef GG_WAVE_POLL
+#define GG_WAVE_POLL 2
+#endif
+#ifndef GG_WAVE_BATCH_HW
+#define GG_WAVE_BATCH_HW 8
+#endif
 constexpr int kSpinLimit = 1 << 20;
 // Ring depth: batches j and j+1 are in LDS at barrier j and kWaveRing-3 more are
 // in flight (enough to cover the HBM latency at this stream rate).
@@ -310,12 +321,18 @@ constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 template <int DIV>
 struct WaveCfg {
     static constexpr int A = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;   // streamed arrays
-    static constexpr int SLOT = A * kWavePB * 64;                        // double2 per ring slot
-    static constexpr int R = kWaveRing;                                  // ring slots
+    static constexpr int B = DIV == WD_UNIT ? GG_WAVE_BATCH_UNIT : DIV == WD_HW ? GG_WAVE_BATCH_HW : 8;
+    static constexpr int PBN = B / 2;                                     // step pairs per batch
+    static constexpr int SLOT = A * PBN * 64;                            // double2 per ring slot
+    // ring slots: kWaveRing, or what fits 150 KiB of LDS beside the boundary
+    // values and the x staging
+    static constexpr int RFIT = (150 * 1024 / 16 - 64 - 2 * PBN * 64) / SLOT;
+    static constexpr int R = kWaveRing < RFIT ? kWaveRing : RFIT;
     static constexpr int LOADERS = kWaveLoaders == 1 ? 1 : A;           // loader waves
     static constexpr int THREADS = (3 + LOADERS) * 64;                  // compute, boundary, writer, loaders
-    static constexpr int LDS2 = R * SLOT + 64 + 2 * kWavePB * 64;        // ring, boundary, x staging
-    static_assert(R >= 4 && (R - 3) * kWavePB * (LOADERS == 1 ? A : 1) <= 63, "ring depth vs vmcnt range");
+    static constexpr int LDS2 = R * SLOT + 64 + 2 * PBN * 64;            // ring, boundary, x staging
+    static_assert(R >= 4 && (R - 3) * PBN * (LOADERS == 1 ? A : 1) <= 63, "ring depth vs vmcnt range");
+    static_assert(B == 8 || B == 16, "batch");
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
 };
 
@@ -363,17 +380,17 @@ __device__ __forceinline__ bool rcp_safe(double v)
 }
 
 // loader wave: one array; batch j -> ring slot j % R; batches j, j+1 landed by barrier j
-template <bool FWD, int R, int SLOT, int NA>
+template <bool FWD, int R, int SLOT, int NA, int PBN>
 __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *lds, int np, int nbatch)
 {
-    constexpr int PB = kWavePB * 64;            // double2 per array per slot
+    constexpr int PB = PBN * 64;                // double2 per array per slot
     auto issue = [&](int j) {
         double2 *slot = lds + (j % R) * SLOT;
 #pragma unroll
         for (int a = 0; a < NA; a++)
 #pragma unroll
-            for (int kk = 0; kk < kWavePB; kk++) {
-                const int p = j * kWavePB + kk;
+            for (int kk = 0; kk < PBN; kk++) {
+                const int p = j * PBN + kk;
                 const long long q = (long long)(FWD ? p : np - 1 - p) * 64;
                 __builtin_amdgcn_global_load_lds((gbl_void_t *)(src[a] + q),
                                                  (lds_void_t *)(slot + a * PB + kk * 64), 16, 0, 0);
@@ -383,7 +400,7 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
     for (int j = 0; j < nbatch; j++) {
         // batches after j+1 may stay in flight
         const int issued = j + R - 1 < nbatch ? j + R - 1 : nbatch;
-        vm_wait_batches<R - 3, NA * kWavePB>(issued - (j + 2));
+        vm_wait_batches<R - 3, NA * PBN>(issued - (j + 2));
         raw_barrier();                          // slot (j-1) % R is free from here on
         if (j + R - 1 < nbatch) issue(j + R - 1);
     }
@@ -396,10 +413,10 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
     double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace)
 {
     using C = WaveCfg<DIV>;
-    constexpr int PB = kWavePB * 64;            // double2 per array per slot
+    constexpr int PB = C::PBN * 64;            // double2 per array per slot
     if (gated(g)) return;
-    // one LDS object: data ring [R][A][kWavePB][64] double2, 2 x 64 boundary values
-    // (lanes 0..kWaveBatch-1 of each half are used), x staging [2][kWavePB][64]
+    // one LDS object: data ring [R][A][C::PBN][64] double2, 2 x 64 boundary values
+    // (lanes 0..C::B-1 of each half are used), x staging [2][C::PBN][64]
     __shared__ double2 lds[C::LDS2];
     double *bring = reinterpret_cast<double *>(lds + C::R * C::SLOT);
     double2 *xbuf = lds + C::R * C::SLOT + 64;
@@ -407,7 +424,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int np = T / 2;                       // step pairs per band
-    const int nbatch = T / kWaveBatch;          // T is a multiple of 8 * kWaveBatch
+    const int nbatch = T / C::B;          // T is a multiple of 8 * C::B
     const bool has_src = FWD ? (band > 0) : (band < nbands - 1);
     const bool is_prod = FWD ? (band < nbands - 1) : (band > 0);
     const long long boff = (long long)band * np * 64 + lane;    // double2 units
@@ -422,9 +439,9 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                                  reinterpret_cast<const double2 *>(dv) + boff,
                                  reinterpret_cast<const double2 *>(rv) + boff};
         if constexpr (C::LOADERS == 1) {
-            wave_loader<FWD, C::R, C::SLOT, C::A>(src, lds, np, nbatch);
+            wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN>(src, lds, np, nbatch);
         } else {
-            wave_loader<FWD, C::R, C::SLOT, 1>(src + (wave - 3), lds + (wave - 3) * PB, np, nbatch);
+            wave_loader<FWD, C::R, C::SLOT, 1, C::PBN>(src + (wave - 3), lds + (wave - 3) * PB, np, nbatch);
         }
         raw_barrier();                      // final barrier (the writer drains the last batch)
         return;
@@ -433,7 +450,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
         // ------------------------------------------------ writer wave
         // After barrier bi+1 the compute wave's x of batch bi sits in xbuf[bi & 1]:
         // store it to HBM and publish the edge lane's values of the batch as
-        // hand-off granules (lanes 0..kWaveBatch-1, one coalesced sc1 store).
+        // hand-off granules (lanes 0..C::B-1, one coalesced sc1 store).
         double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
         [[maybe_unused]] bool bad = false;  // WD_RCP range guard (see rcp_safe)
         for (int bi = 0; bi <= nbatch; bi++) {
@@ -442,19 +459,19 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
             const int pb = bi - 1;
             const double2 *xb = xbuf + (pb & 1) * PB;
             // the hand-off granules first: they are on the critical path, x is not
-            const int tt = lane & (kWaveBatch - 1);
+            const int tt = lane & (C::B - 1);
             const double e = reinterpret_cast<const double *>(xb + (tt >> 1) * 64 + plane)
                 [FWD ? (tt & 1) : 1 - (tt & 1)];
-            if (is_prod && lane < kWaveBatch) {
-                const int t = FWD ? pb * kWaveBatch + tt : (T - 1) - (pb * kWaveBatch + tt);
+            if (is_prod && lane < C::B) {
+                const int t = FWD ? pb * C::B + tt : (T - 1) - (pb * C::B + tt);
                 st_agent(pub + t, (unsigned long long)__double_as_longlong(e));
             }
-            double2 v[kWavePB];
+            double2 v[C::PBN];
 #pragma unroll
-            for (int kk = 0; kk < kWavePB; kk++) v[kk] = xb[kk * 64 + lane];
+            for (int kk = 0; kk < C::PBN; kk++) v[kk] = xb[kk * 64 + lane];
 #pragma unroll
-            for (int kk = 0; kk < kWavePB; kk++) {
-                const int p = pb * kWavePB + kk;
+            for (int kk = 0; kk < C::PBN; kk++) {
+                const int p = pb * C::PBN + kk;
                 X2[(long long)(FWD ? p : np - 1 - p) * 64] = v[kk];
                 if constexpr (DIV == WD_RCP) bad |= !rcp_safe(v[kk].x) || !rcp_safe(v[kk].y);
             }
@@ -477,14 +494,14 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
         // Every memory op is issued by all lanes (lanes with nothing to do use
         // the dummy granules after the bands: 64 zeros to read, 64 to write),
         // which keeps the vmcnt arithmetic exact.
-        constexpr int kPoll = 4;
+        constexpr int kPoll = GG_WAVE_POLL;
         unsigned long long *src = bnd + (long long)(FWD ? band - 1 : band + 1) * T;
         unsigned long long *dummy_ld = bnd + (long long)nbands * T + lane;
         unsigned long long *dummy_st = dummy_ld + 64;
         auto gaddr = [&](int bj) {
-            const int t = FWD ? bj * kWaveBatch + lane : (T - 1) - (bj * kWaveBatch + lane);
+            const int t = FWD ? bj * C::B + lane : (T - 1) - (bj * C::B + lane);
             const int gi = FWD ? t + 63 : t - 63;
-            const bool need = has_src && lane < kWaveBatch && bj < nbatch && gi >= 0 && gi < T;
+            const bool need = has_src && lane < C::B && bj < nbatch && gi >= 0 && gi < T;
             return need ? src + gi : (unsigned long long *)nullptr;
         };
         // the prologue mirrors the steady-state issue order (re-arm store, poll)
@@ -550,10 +567,10 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
     // next batch right after use.  The last pair is fetched after the batch's
     // boundary values instead (LDS returns in order, and the boundary values
     // are needed first).
-    double2 rg[kWavePB][C::A];
+    double2 rg[C::PBN][C::A];
     raw_barrier();                          // barrier 0: batches 0 and 1 are in LDS
 #pragma unroll
-    for (int kk = 0; kk < kWavePB - 1; kk++)
+    for (int kk = 0; kk < C::PBN - 1; kk++)
 #pragma unroll
         for (int a = 0; a < C::A; a++) rg[kk][a] = lds[a * PB + kk * 64 + lane];
     for (int bi = 0; bi < nbatch; bi++) {
@@ -573,18 +590,18 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
             if (lane == 0) tr[bi] = (long long)__builtin_amdgcn_s_memrealtime();
         }
         const double2 *br = reinterpret_cast<const double2 *>(bring + (bi & 1) * 64);
-        double2 bv[kWavePB];
+        double2 bv[C::PBN];
 #pragma unroll
-        for (int kk = 0; kk < kWavePB; kk++) bv[kk] = br[kk];    // broadcast reads
+        for (int kk = 0; kk < C::PBN; kk++) bv[kk] = br[kk];    // broadcast reads
         if constexpr (TRACE) t_top = (long long)__builtin_amdgcn_s_memtime();
         const double2 *sc = lds + (bi % C::R) * C::SLOT + lane;
 #pragma unroll
-        for (int a = 0; a < C::A; a++) rg[kWavePB - 1][a] = sc[a * PB + (kWavePB - 1) * 64];
+        for (int a = 0; a < C::A; a++) rg[C::PBN - 1][a] = sc[a * PB + (C::PBN - 1) * 64];
         __builtin_amdgcn_sched_barrier(0);          // boundary values first, then the last pair
         const double2 *sn = lds + ((bi + 1) % C::R) * C::SLOT + lane;
-        double xv[kWaveBatch];
+        double xv[C::B];
 #pragma unroll
-        for (int kk = 0; kk < kWavePB; kk++) {
+        for (int kk = 0; kk < C::PBN; kk++) {
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int tt = 2 * kk + h;
@@ -608,7 +625,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 xp = acc;
                 xv[tt] = acc;
                 if constexpr (TRACE) {      // phase stamps at the first and last step
-                    if (tt == 0 || tt == kWaveBatch - 1) {
+                    if (tt == 0 || tt == C::B - 1) {
                         const int f = __builtin_amdgcn_readfirstlane(__double2hiint(acc));
                         asm volatile("; use %0" ::"s"(f));
                         const long long now = (long long)__builtin_amdgcn_s_memtime();
@@ -623,7 +640,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
             // all inside this pair, in the recurrence's latency bubbles
             xbuf[(bi & 1) * PB + kk * 64 + lane] =
                 FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
-            if (kk < kWavePB - 1) {
+            if (kk < C::PBN - 1) {
 #pragma unroll
                 for (int a = 0; a < C::A; a++) rg[kk][a] = sn[a * PB + kk * 64];
             }
@@ -1016,6 +1033,11 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
         k_spmv_stream<true><<<A.nblk, kBlock, 0, st>>>(g, A.blk.p, A.rp.p, A.ci.p, A.v.p, x, b, y);
     else
         k_spmv_stream<false><<<A.nblk, kBlock, 0, st>>>(g, A.blk.p, A.rp.p, A.ci.p, A.v.p, x, b, y);
+}
+
+int wave_batch_steps(int div)
+{
+    return div == WD_UNIT ? WaveCfg<WD_UNIT>::B : div == WD_HW ? WaveCfg<WD_HW>::B : WaveCfg<WD_RCP>::B;
 }
 
 void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st)

@@ -1003,7 +1003,7 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     GG_REQUIRE(T.kind == DevTri::WAVE2D, GG_ESTATE, "wavefront path not active");
     set_device(s);
     ensure_workspace(s, std::max(s->m_alloc, 1));
-    const int nb = T.wl.nbands, nbt = T.wl.T / 8;   // kernels.hip kWaveBatch
+    const int nb = T.wl.nbands, nbt = T.wl.T / wave_batch_steps(T.div);
     const long long need = (long long)nb * (3 * nbt + 8);
     GG_REQUIRE(cap >= need, GG_EINVAL, "trace buffer too small");
     DBuf<long long> buf;

@@ -177,7 +177,7 @@ int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int ns
 
 /* Diagnostics: run one wavefront triangular solve (which: 0 = L / Ml, 1 = U / Mr)
  * on the current right-hand side and return, per band, the device real-time
- * clock (100 MHz) at the start of each 8-step batch plus one end stamp, then
+ * clock (100 MHz) at the start of each batch (8 or 16 steps) plus one end stamp, then
  * core-cycle totals of four phases of the compute wave's batches (barrier wait,
  * batch top to first result, first to last result, last result to the next
  * barrier), the boundary wave's poll retries and the core cycles it spent

@@ -23,12 +23,12 @@ s.set_precond_ilu0()
 b = np.ones(A.shape[0])
 s.precond_apply(0, b)
 print("precond apply avg ms", s.time_precond(20))
-KB = 8
 for which in (0, 1):
     for rep in range(2):
         raw = s.trace_precond(which)
     nb = raw.shape[0]
     nbt = (raw.shape[1] - 8) // 3
+    KB = (args.grid + 63 + 63) // 64 * 64 // nbt      # steps per batch
     t0 = raw[:, 0].min()
     comp = (raw[:, :nbt + 1] - t0) * 0.01           # us
     ph = raw[:, nbt + 1:nbt + 5].astype(np.float64)
