@@ -74,6 +74,14 @@ void launch_mgs_step(Gate g, int i, int k, int m, double *w, const double *vk, c
 void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *part, int G,
                              const double *w, double *vnext, double *H, double *cs, double *sn,
                              double *s, double *hist, long long Ppad, hipStream_t st);
+// persistent Arnoldi orthogonalization (one launch per inner iteration):
+// units per thread (1/2/4/8, 0 = too many), how many blocks can be resident
+int arnoldi_persist_units(int G, long long Ppad);
+int arnoldi_persist_max_blocks();
+void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
+                            long long ldv, double *H, double *cs, double *sn, double *s,
+                            double *hist, unsigned long long *gran, int G, long long Ppad, int *err,
+                            hipStream_t st);
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
                    const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st);
 void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st);

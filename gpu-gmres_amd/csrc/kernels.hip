@@ -870,6 +870,128 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
     }
 }
 
+// ---- persistent Arnoldi orthogonalization: <w,v_0>, the i+1 MGS steps, the
+// norm, Givens and v_{i+1} = w/||w|| of inner iteration i in ONE launch.
+// Block g owns the same units as in the per-step kernels (u = g*256 + t +
+// j*G*256) and keeps them of w and of the current basis vector in registers
+// across the steps, so a step reads one basis vector from HBM instead of
+// w, v_k, v_{k+1} and writing w.  The per-step global sum is an all-gather of
+// the G block partials through 8-byte granules (sentinel = not ready, relaxed
+// agent-scope stores and polls, one row of G per step, re-armed per cycle);
+// every block sums them in sum_partials' fixed order, so h is bit-identical to
+// the per-step kernels'.  Needs all G blocks resident (checked on the host);
+// every spin is bounded (err bit 0).
+__device__ __forceinline__ double gather_sum(const unsigned long long *row, int G, int *err)
+{
+    double v = 0.0;
+    for (int q = threadIdx.x; q < G; q += kBlock) {
+        unsigned long long b = ld_agent(row + q);
+        int spins = 0;
+        while (b == kSentinel) {
+            __builtin_amdgcn_s_sleep(1);
+            b = ld_agent(row + q);
+            if (++spins > kSpinLimit) {
+                atomicOr(err, 1);
+                break;
+            }
+        }
+        v += __longlong_as_double((long long)b);
+    }
+    return block_sum(v);
+}
+
+template <int J>
+__global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m, DevState *ds,
+                                                            const double *__restrict__ w_in,
+                                                            double *__restrict__ V, long long ldv,
+                                                            double *H, double *cs, double *sn,
+                                                            double *s, double *hist,
+                                                            unsigned long long *gran, long long units,
+                                                            int *err)
+{
+    if (gated(g)) return;
+    const int G = gridDim.x;
+    const long long stride = (long long)G * kBlock;
+    const long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x;
+    double2 w[J], vk[J], vn[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const long long u = u0 + j * stride;
+        if (u < units) {
+            w[j] = ld2(w_in, u);
+            vk[j] = ld2(V, u);
+        }
+    }
+    auto publish = [&](int k, double acc) {
+        acc = block_sum(acc);
+        if (threadIdx.x == 0) st_agent(gran + (long long)k * G + blockIdx.x, (unsigned long long)__double_as_longlong(acc));
+    };
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < J; j++)
+        if (u0 + j * stride < units) {
+            acc += w[j].x * vk[j].x;
+            acc += w[j].y * vk[j].y;
+        }
+    publish(0, acc);                                          // <w, v_0>
+    for (int k = 0; k <= i; k++) {
+        if (k < i) {                                          // v_{k+1}, in flight during the sum
+            const double *vnp = V + (long long)(k + 1) * ldv;
+#pragma unroll
+            for (int j = 0; j < J; j++)
+                if (u0 + j * stride < units) vn[j] = ld2(vnp, u0 + j * stride);
+        }
+        const double h = gather_sum(gran + (long long)k * G, G, err);
+        if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
+        const double a = -h;
+        acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (u0 + j * stride < units) {
+                w[j].x = a * vk[j].x + w[j].x;
+                w[j].y = a * vk[j].y + w[j].y;
+                const double2 o = (k < i) ? vn[j] : w[j];     // next dot: v_{k+1}, or the norm
+                acc += w[j].x * o.x;
+                acc += w[j].y * o.y;
+                vk[j] = vn[j];
+            }
+        }
+        publish(k + 1, acc);
+    }
+    const double hn = sqrt(gather_sum(gran + (long long)(i + 1) * G, G, err));
+    if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
+        const int ld = m + 1;
+        double *Hc = H + i * ld;
+        Hc[i + 1] = hn;
+        for (int k = 0; k < i; k++) apply_rot(Hc[k], Hc[k + 1], cs[k], sn[k]);
+        double c, sv;
+        gen_rot(Hc[i], Hc[i + 1], c, sv);
+        cs[i] = c;
+        sn[i] = sv;
+        apply_rot(Hc[i], Hc[i + 1], c, sv);
+        apply_rot(s[i], s[i + 1], c, sv);
+        const double resid = fabs(s[i + 1]) / ds->normb;
+        hist[ds->hist_len + i] = resid;
+        ds->resid = resid;
+        if (resid < ds->tol) {
+            ds->conv_i = i;
+            ds->done = DONE_INNER;
+        }
+    }
+    const double inv = (hn != 0.0) ? 1.0 / hn : 0.0;
+    double *vout = V + (long long)(i + 1) * ldv;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const long long u = u0 + j * stride;
+        if (u < units) {
+            double2 a = w[j];
+            a.x = inv * a.x;
+            a.y = inv * a.y;
+            st2(vout, u, a);
+        }
+    }
+}
+
 // y = H(0:k,0:k)^-1 s(0:k)  (Update, src/gmres.cu:93-116); k = conv_i or nit-1.
 // One wave: lane j keeps y[j] and row j of H in registers; for i = k..0 lane i
 // divides, the value is broadcast, lanes j < i subtract -- per element the same
@@ -1106,6 +1228,39 @@ void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *p
     k_arnoldi_finalize<<<G, kBlock, 0, st>>>(g, i, m, ds, part, G, w, vnext, H, cs, sn, s, hist,
                                               Ppad / 2);
 }
+int arnoldi_persist_units(int G, long long Ppad)
+{
+    const long long units = Ppad / 2, per = (long long)G * kBlock;
+    const int J = (int)((units + per - 1) / per);
+    return J <= 1 ? 1 : J <= 2 ? 2 : J <= 4 ? 4 : J <= 8 ? 8 : 0;
+}
+
+int arnoldi_persist_max_blocks()
+{
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_arnoldi_persist<8>, kBlock, 0) != hipSuccess)
+        return 0;
+    return cus * per;
+}
+
+void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
+                            long long ldv, double *H, double *cs, double *sn, double *s,
+                            double *hist, unsigned long long *gran, int G, long long Ppad, int *err,
+                            hipStream_t st)
+{
+    const int J = arnoldi_persist_units(G, Ppad);
+#define GG_PERSIST(JJ)                                                                       \
+    k_arnoldi_persist<JJ><<<G, kBlock, 0, st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, \
+                                                 Ppad / 2, err)
+    if (J == 1) GG_PERSIST(1);
+    else if (J == 2) GG_PERSIST(2);
+    else if (J == 4) GG_PERSIST(4);
+    else GG_PERSIST(8);
+#undef GG_PERSIST
+}
+
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
                    const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st)
 {

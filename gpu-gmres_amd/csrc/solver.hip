@@ -143,6 +143,9 @@ struct gg_solver {
     int m_alloc = -1;
     DBuf<double> V, w, ww, r, rr, bb, t1, t2, z, xv, bv, y;
     DBuf<double> partA, partB, H, s, cs, sn, ysm;
+    // persistent Arnoldi orthogonalization (kernels.hip k_arnoldi_persist)
+    bool persist = false;
+    DBuf<unsigned long long> gran;      // m * (m+2) * G hand-off granules, re-armed per cycle
     DBuf<double> hist;
     long long hist_cap = 0;
     DBuf<DevState> ds;
@@ -265,6 +268,12 @@ void ensure_workspace(gg_solver *s, int m)
     }
     s->partA.alloc(1024);
     s->partB.alloc(1024);
+    {
+        const char *e = std::getenv("GG_NO_PERSIST");
+        s->persist = !(e && e[0] == '1') && arnoldi_persist_units(s->G, s->Ppad) != 0 &&
+                     s->G <= arnoldi_persist_max_blocks();
+        if (s->persist) s->gran.alloc((size_t)m * (m + 2) * s->G);
+    }
     s->H.alloc((size_t)(m + 1) * m);
     GG_HIP(hipMemsetAsync(s->H.p, 0, (size_t)(m + 1) * m * sizeof(double), s->st));
     s->s.alloc(m + 1);
@@ -387,6 +396,7 @@ void enqueue_cycle(gg_solver *s, int m)
     const long long P = s->Ppad;
     const bool split = s->pkind == GG_PRECOND_SPLIT;
     launch_init_cycle(ds, s->r.p, s->V.p, s->s.p, s->G, P, s->st);
+    if (s->persist) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
     for (int i = 0; i < m; i++) {
         Gate gi;
         gi.done = &ds->done;
@@ -412,16 +422,23 @@ void enqueue_cycle(gg_solver *s, int m)
             prof_end(s, mk);
         }
         mk = prof_begin(s, GG_PROF_MGS, i);
-        double *pin = s->partA.p, *pout = s->partB.p;
-        launch_dot(gi, s->w.p, s->V.p, pin, s->G, P, s->st);                   // <w, v_0>
-        for (int k = 0; k <= i; k++) {
-            const double *vk = s->V.p + (long long)k * P;
-            const double *vn = (k < i) ? s->V.p + (long long)(k + 1) * P : s->w.p;
-            launch_mgs_step(gi, i, k, m, s->w.p, vk, vn, pin, pout, s->H.p, s->G, P, s->st);
-            std::swap(pin, pout);
+        if (s->persist) {
+            launch_arnoldi_persist(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
+                                   s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, s->G, P,
+                                   s->err.p, s->st);
+        } else {
+            double *pin = s->partA.p, *pout = s->partB.p;
+            launch_dot(gi, s->w.p, s->V.p, pin, s->G, P, s->st);               // <w, v_0>
+            for (int k = 0; k <= i; k++) {
+                const double *vk = s->V.p + (long long)k * P;
+                const double *vn = (k < i) ? s->V.p + (long long)(k + 1) * P : s->w.p;
+                launch_mgs_step(gi, i, k, m, s->w.p, vk, vn, pin, pout, s->H.p, s->G, P, s->st);
+                std::swap(pin, pout);
+            }
+            launch_arnoldi_finalize(gi, i, m, ds, pin, s->G, s->w.p,
+                                    s->V.p + (long long)(i + 1) * P, s->H.p, s->cs.p, s->sn.p,
+                                    s->s.p, s->hist.p, P, s->st);
         }
-        launch_arnoldi_finalize(gi, i, m, ds, pin, s->G, s->w.p, s->V.p + (long long)(i + 1) * P,
-                                s->H.p, s->cs.p, s->sn.p, s->s.p, s->hist.p, P, s->st);
         prof_end(s, mk);
     }
     Gate gu;

@@ -152,7 +152,12 @@ def oracle_both(run, n, nx=None):
 
 @pytest.mark.parametrize("m", [30, 32])
 @pytest.mark.parametrize("rhs", ["ones", "uniform"])
-def test_gmres_left_c1_parity(solver, m, rhs):
+@pytest.mark.parametrize("persist", [True, False])
+def test_gmres_left_c1_parity(solver, m, rhs, persist, monkeypatch):
+    """persist: one persistent launch per inner iteration for the orthogonalization
+    (default) or the per-step kernels (GG_NO_PERSIST=1): both bit-identical."""
+    if not persist:
+        monkeypatch.setenv("GG_NO_PERSIST", "1")
     A = M.laplacian_5pt(100)
     b = M.rhs_ones(A) if rhs == "ones" else M.rhs_uniform(A.shape[0])
     L, U = O.ilu0(A)
