@@ -7,11 +7,13 @@ tol 1e-8, b = A*1, x0 = 0.  One step = one full solve (device-resident b, x;
 the ILU factorization and H2D copies are setup, outside the timed region).
 
 value = inner (Arnoldi) iterations of all ranks / max-over-ranks wall time.
-roofline: the single kernel with the most time in the step, timed live inside
-the timed region with hipEvent pairs on the solver's stream (gg_profile_*),
-algorithmic bytes from SURVEY.md 8(d) (DESIGN.md "Kernels"); traffic: HBM bytes
-per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json).  cpu_baseline: the fp64 oracle restatement (oracle/, serial C)
-on a bounded sample of the same workload, rank 0 only.
+roofline: the single kernel with the most time in the step (found in a
+profiled warmup step that brackets every kernel family), timed live inside the
+timed region with hipEvent pairs around its launches only, on the solver's
+stream (gg_profile_*); algorithmic bytes from SURVEY.md 8(d) (DESIGN.md
+"Kernels"); traffic: HBM bytes per launch from the committed rocprofv3 PMC
+passes (profiles/pmc_traffic.json).  cpu_baseline: the fp64 oracle restatement
+(oracle/, serial C) on a bounded sample of the same workload, rank 0 only.
 
 --workload c5: the transient loop (gg_transient: A = G + C/h on the C2 grid, 1 %
 PULSE sources, --c5-steps backward-Euler steps per step, warm start); value =
@@ -144,14 +146,66 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
-        step()
-    s.profile(not a.no_profile)
+    FAMS = (("spmv", ggmres.PROF_SPMV, lambda: s.bytes_spmv()),
+            ("ilu0_apply", ggmres.PROF_PRECOND, lambda: s.bytes_precond()),
+            ("trsv_L", ggmres.PROF_TRSV_L, lambda: s.bytes_trsv(0)),
+            ("trsv_U", ggmres.PROF_TRSV_U, lambda: s.bytes_trsv(1)),
+            ("mgs_givens", ggmres.PROF_MGS, None))
+
+    def families(res, el):
+        """per-family event timing of the solves in `res` (elapsed el seconds)"""
+        fam = {}
+        mgs_tot, mgs_it = mgs_bytes(n, a.restart, [r["inner"] for r in res]) if not c5 else (0.0, 0)
+        for name, kind, per in FAMS:
+            cnt, ms = s.profile_get(kind)
+            if cnt == 0:
+                continue
+            avg_us = ms * 1e3 / cnt
+            byt = per() if per is not None else (mgs_tot / max(mgs_it, 1) if mgs_it else float("nan"))
+            fam[name] = {"launches": cnt, "avg_us": round(avg_us, 3),
+                         "alg_bytes_per_launch": byt,
+                         "achieved_gbs": round(byt / (avg_us * 1e-6) / 1e9, 1),
+                         "share_of_step": round(ms / (el * 1e3), 4)}
+        return fam
+
+    def profiled_pass():
+        """one step with every kernel family bracketed (events cost ~10 us per
+        iteration, so this pass is kept out of the timed region)"""
+        s.profile(True)
+        barrier()
+        t1 = time.perf_counter()
+        r = step()
+        barrier()
+        fam = families([r], time.perf_counter() - t1)
+        s.profile(False)
+        return fam
+
+    # breakdown pass in the last warmup step (or after the timed region when W = 0)
+    fam = {}
+    for w in range(a.warmup):
+        if w == a.warmup - 1 and not a.no_profile:
+            fam = profiled_pass()
+        else:
+            step()
+    # the roofline entry is for ONE kernel: the single-kernel family with the most
+    # time (ilu0_apply = trsv_L + trsv_U and mgs_givens are families of launches);
+    # inside the timed region only its launches are bracketed with events
+    dom = None
+    if not a.no_profile:
+        if not fam:
+            dom = "trsv_U"
+        else:
+            single = {k: v for k, v in fam.items() if k in KERNEL_NAMES}
+            dom = max(single, key=lambda k: single[k]["share_of_step"]) if single else None
+        if dom:
+            s.profile(True, kinds=[dict((f[0], f[1]) for f in FAMS)[dom]])
     barrier()
     t0 = time.perf_counter()
     res = [step() for _ in range(a.steps)]
     barrier()
     el = time.perf_counter() - t0
+    timed = families(res, el) if dom else {}
+    s.profile(False)
 
     inner = sum(r["inner"] for r in res)
     t = torch.tensor([el], dtype=torch.float64, device="cuda")
@@ -161,38 +215,19 @@ def main():
         dist.all_reduce(it, op=dist.ReduceOp.SUM)
     el_max, inner_all = float(t.item()), float(it.item())
     value = inner_all / el_max
+    if not a.no_profile and not fam:
+        fam = profiled_pass()
 
-    # ---- per-kernel-family timing from the timed region -----------------------
-    fam = {}
-    spmv_bytes = s.bytes_spmv()
-    pre_bytes = s.bytes_precond()
-    mgs_tot, mgs_it = mgs_bytes(n, a.restart, [r["inner"] for r in res]) if not c5 else (0.0, 0)
-    for name, kind, per in (("spmv", ggmres.PROF_SPMV, spmv_bytes),
-                            ("ilu0_apply", ggmres.PROF_PRECOND, pre_bytes),
-                            ("trsv_L", ggmres.PROF_TRSV_L, s.bytes_trsv(0)),
-                            ("trsv_U", ggmres.PROF_TRSV_U, s.bytes_trsv(1)),
-                            ("mgs_givens", ggmres.PROF_MGS, None)):
-        cnt, ms = s.profile_get(kind)
-        if cnt == 0:
-            continue
-        avg_us = ms * 1e3 / cnt
-        byt = per if per is not None else (mgs_tot / max(mgs_it, 1) if mgs_it else float("nan"))
-        fam[name] = {"launches": cnt, "avg_us": round(avg_us, 3),
-                     "alg_bytes_per_launch": byt,
-                     "achieved_gbs": round(byt / (avg_us * 1e-6) / 1e9, 1),
-                     "share_of_step": round(ms / (el * 1e3), 4)}
-    # the roofline entry is for ONE kernel: the single-kernel entry with the most
-    # time (ilu0_apply = trsv_L + trsv_U and mgs_givens are families of launches)
-    single = {k: v for k, v in fam.items() if k in KERNEL_NAMES}
-    dom = max(single, key=lambda k: single[k]["share_of_step"]) if single else None
     roof = None
-    if dom:
-        f = fam[dom]
+    if dom and dom in timed:
+        f = timed[dom]
         roof = {"kernel": KERNEL_NAMES[dom], "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(KERNEL_NAMES[dom]),
-                "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"]}
+                "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
+                "launches_timed": f["launches"]}
+    spmv_bytes = s.bytes_spmv()
     # isolated SpMV (4 rotating copies of A, x, y: > 256 MiB, not Infinity-Cache served)
     spmv_iso_ms = s.time_spmv(reps=100, nrot=4)
     spmv_iso = {"avg_us": round(spmv_iso_ms * 1e3, 3),
@@ -230,6 +265,7 @@ def main():
                    "setup_s": round(t_setup, 3)},
         "roofline": roof,
         "kernels": fam,
+        "kernels_from": "one profiled warmup step, every family bracketed by hipEvents",
         "spmv_isolated": spmv_iso,
         "cpu_baseline": cpu,
     }

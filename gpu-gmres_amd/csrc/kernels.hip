@@ -260,15 +260,14 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
 //    previous value (same line, column i-+1) and the neighbour line's value
 //    from the previous step, moved in-register with DPP wave_shr/wave_shl; the
 //    edge lane keeps the DPP "old" operand, which holds the neighbouring band's
-//    value.  Its operands come from LDS one batch ahead (a register ring of
-//    step pairs refilled right after use), so the recurrence never waits on
-//    memory; its results go to LDS staging (a global store costs the issuing
+//    value.  Its operands come from LDS a few step pairs ahead of their use,
+//    so the recurrence waits on memory at most once per batch; its results go to LDS staging (a global store costs the issuing
 //    wave ~50 cycles, an LDS write a few);
 //  * wave 2 (writer) stores the compute wave's x from LDS staging to HBM and
 //    publishes the band's edge values, one batch behind;
 //  * waves 3.. (loaders, one array each) stream HBM -> LDS with LDS-DMA
 //    (global_load_lds_dwordx4) into an R-slot ring, each retiring batches with
-//    its own counted vmcnt before the barrier (batches j and j+1 by barrier j);
+//    its own counted vmcnt before the barrier (batch j by barrier j);
 //  * wave 1 (boundary) polls the neighbouring band's edge values and hands
 //    them over through LDS.
 // All waves meet at one raw s_barrier per batch (no fence, no drain).
@@ -301,8 +300,17 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
 #define GG_WAVE_POLL 2
 #endif
 #ifndef GG_WAVE_BATCH_HW
-#define GG_WAVE_BATCH_HW 8
+#define GG_WAVE_BATCH_HW 16
 #endif
+#ifndef GG_WAVE_BATCH_RCP
+#define GG_WAVE_BATCH_RCP 16
+#endif
+// the compute wave reads a batch's operands after that batch's barrier, kWaveLook
+// step pairs ahead of their use
+#ifndef GG_WAVE_LOOK
+#define GG_WAVE_LOOK 3
+#endif
+constexpr int kWaveLook = GG_WAVE_LOOK;
 constexpr int kSpinLimit = 1 << 20;
 // Ring depth: batches j and j+1 are in LDS at barrier j and kWaveRing-3 more are
 // in flight (enough to cover the HBM latency at this stream rate).
@@ -321,18 +329,23 @@ constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 template <int DIV>
 struct WaveCfg {
     static constexpr int A = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;   // streamed arrays
-    static constexpr int B = DIV == WD_UNIT ? GG_WAVE_BATCH_UNIT : DIV == WD_HW ? GG_WAVE_BATCH_HW : 8;
+    static constexpr int B = DIV == WD_UNIT ? GG_WAVE_BATCH_UNIT
+                           : DIV == WD_HW   ? GG_WAVE_BATCH_HW
+                                            : GG_WAVE_BATCH_RCP;       // steps per batch
     static constexpr int PBN = B / 2;                                     // step pairs per batch
     static constexpr int SLOT = A * PBN * 64;                            // double2 per ring slot
-    // ring slots: kWaveRing, or what fits 150 KiB of LDS beside the boundary
-    // values and the x staging
-    static constexpr int RFIT = (150 * 1024 / 16 - 64 - 2 * PBN * 64) / SLOT;
-    static constexpr int R = kWaveRing < RFIT ? kWaveRing : RFIT;
     static constexpr int LOADERS = kWaveLoaders == 1 ? 1 : A;           // loader waves
+    static constexpr int NPER = (LOADERS == 1 ? A : 1) * PBN;           // DMA instructions per batch per loader
+    // ring slots: kWaveRing, at most what fits 150 KiB of LDS beside the boundary
+    // values and the x staging, and at most what the 6-bit vmcnt can count
+    static constexpr int RFIT = (150 * 1024 / 16 - 64 - 2 * PBN * 64) / SLOT;
+    static constexpr int RVM = 2 + 63 / NPER;
+    static constexpr int R = kWaveRing < RFIT ? (kWaveRing < RVM ? kWaveRing : RVM) : (RFIT < RVM ? RFIT : RVM);
     static constexpr int THREADS = (3 + LOADERS) * 64;                  // compute, boundary, writer, loaders
     static constexpr int LDS2 = R * SLOT + 64 + 2 * PBN * 64;            // ring, boundary, x staging
-    static_assert(R >= 4 && (R - 3) * PBN * (LOADERS == 1 ? A : 1) <= 63, "ring depth vs vmcnt range");
+    static_assert(R >= 3 && (R - 2) * NPER <= 63, "ring depth vs vmcnt range");
     static_assert(B == 8 || B == 16, "batch");
+    static_assert(kWaveLook >= 1 && kWaveLook <= PBN, "lookahead");
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
 };
 
@@ -379,7 +392,7 @@ __device__ __forceinline__ bool rcp_safe(double v)
     return v == 0.0 || (a >= 0x1p-800 && a <= 0x1p800);
 }
 
-// loader wave: one array; batch j -> ring slot j % R; batches j, j+1 landed by barrier j
+// loader wave: batch j -> ring slot j % R; batch j landed by barrier j
 template <bool FWD, int R, int SLOT, int NA, int PBN>
 __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *lds, int np, int nbatch)
 {
@@ -398,9 +411,9 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
     };
     for (int j = 0; j < R - 1 && j < nbatch; j++) issue(j);
     for (int j = 0; j < nbatch; j++) {
-        // batches after j+1 may stay in flight
+        // batch j must have landed; the ones after it may stay in flight
         const int issued = j + R - 1 < nbatch ? j + R - 1 : nbatch;
-        vm_wait_batches<R - 3, NA * PBN>(issued - (j + 2));
+        vm_wait_batches<R - 2, NA * PBN>(issued - (j + 1));
         raw_barrier();                          // slot (j-1) % R is free from here on
         if (j + R - 1 < nbatch) issue(j + R - 1);
     }
@@ -563,16 +576,11 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
     long long ph[4] = {0, 0, 0, 0};     // TRACE: barrier wait, top->step0, step0->last, last->end
     long long t_top = 0;
     double xp = 0.0;                        // this lane's previous step value
-    // Register ring: operands of pair kk of the current batch, refilled from the
-    // next batch right after use.  The last pair is fetched after the batch's
-    // boundary values instead (LDS returns in order, and the boundary values
-    // are needed first).
+    // Operands of the current batch in registers, read kWaveLook step pairs
+    // ahead of their use; the boundary values are read first (LDS returns in
+    // order and they are needed at the batch's first step).
     double2 rg[C::PBN][C::A];
-    raw_barrier();                          // barrier 0: batches 0 and 1 are in LDS
-#pragma unroll
-    for (int kk = 0; kk < C::PBN - 1; kk++)
-#pragma unroll
-        for (int a = 0; a < C::A; a++) rg[kk][a] = lds[a * PB + kk * 64 + lane];
+    raw_barrier();                          // barrier 0: batch 0 is in LDS
     for (int bi = 0; bi < nbatch; bi++) {
         if (bi > 0) {
             // x staging writes of batch bi-1 complete before the barrier (writer)
@@ -583,22 +591,30 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 raw_barrier();
                 ph[0] += (long long)__builtin_amdgcn_s_memtime() - ta;
             } else {
-                raw_barrier();              // batch bi's boundary values, batch bi+1's data
+                raw_barrier();              // batch bi's data and boundary values
             }
         }
         if constexpr (TRACE) {
             if (lane == 0) tr[bi] = (long long)__builtin_amdgcn_s_memrealtime();
         }
         const double2 *br = reinterpret_cast<const double2 *>(bring + (bi & 1) * 64);
+        // issue order = need order: the first pair's boundary values and
+        // operands, then the look-ahead pairs, then the remaining boundary
+        // values (LDS returns in order, so the first step waits on ~A+1 reads)
         double2 bv[C::PBN];
-#pragma unroll
-        for (int kk = 0; kk < C::PBN; kk++) bv[kk] = br[kk];    // broadcast reads
-        if constexpr (TRACE) t_top = (long long)__builtin_amdgcn_s_memtime();
         const double2 *sc = lds + (bi % C::R) * C::SLOT + lane;
+        bv[0] = br[0];
 #pragma unroll
-        for (int a = 0; a < C::A; a++) rg[C::PBN - 1][a] = sc[a * PB + (C::PBN - 1) * 64];
-        __builtin_amdgcn_sched_barrier(0);          // boundary values first, then the last pair
-        const double2 *sn = lds + ((bi + 1) % C::R) * C::SLOT + lane;
+        for (int a = 0; a < C::A; a++) rg[0][a] = sc[a * PB];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 1; kk < kWaveLook; kk++)
+#pragma unroll
+            for (int a = 0; a < C::A; a++) rg[kk][a] = sc[a * PB + kk * 64];
+#pragma unroll
+        for (int kk = 1; kk < C::PBN; kk++) bv[kk] = br[kk];    // broadcast reads
+        if constexpr (TRACE) t_top = (long long)__builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
         double xv[C::B];
 #pragma unroll
         for (int kk = 0; kk < C::PBN; kk++) {
@@ -635,14 +651,14 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 }
             }
             // the pair's results go to LDS staging (the writer wave stores them
-            // and publishes the edge values), then pair kk is refilled from the
-            // next batch (landed by barrier bi); the scheduling fence keeps it
-            // all inside this pair, in the recurrence's latency bubbles
+            // and publishes the edge values), then the pair kWaveLook ahead is
+            // read; the scheduling fence keeps it all inside this pair, in the
+            // recurrence's latency bubbles
             xbuf[(bi & 1) * PB + kk * 64 + lane] =
                 FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
-            if (kk < C::PBN - 1) {
+            if (kk + kWaveLook < C::PBN) {
 #pragma unroll
-                for (int a = 0; a < C::A; a++) rg[kk][a] = sn[a * PB + kk * 64];
+                for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
             }
             __builtin_amdgcn_sched_barrier(0);
         }

@@ -154,7 +154,7 @@ struct gg_solver {
     std::vector<double> last_hist;
 
     // in-solve kernel timing (gg_profile_*)
-    bool prof_on = false;
+    int prof_mask = 0;                  // (1 << GG_PROF_*) bits being timed
     std::vector<hipEvent_t> prof_pool;
     size_t prof_used = 0;
     struct Mark { int kind, i, e0, e1; };
@@ -342,7 +342,7 @@ int prof_event(gg_solver *s)
 {
     if (s->prof_used == s->prof_pool.size()) {
         hipEvent_t e;
-        GG_HIP(hipEventCreate(&e));
+        GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));   // timing only
         s->prof_pool.push_back(e);
     }
     GG_HIP(hipEventRecord(s->prof_pool[s->prof_used], s->st));
@@ -350,19 +350,19 @@ int prof_event(gg_solver *s)
 }
 int prof_begin(gg_solver *s, int kind, int i)
 {
-    if (!s->prof_on) return -1;
+    if (!((s->prof_mask >> kind) & 1)) return -1;
     s->marks.push_back({kind, i, prof_event(s), -1});
     return (int)s->marks.size() - 1;
 }
 void prof_end(gg_solver *s, int mark)
 {
-    if (!s->prof_on || mark < 0) return;
+    if (mark < 0) return;
     s->marks[mark].e1 = prof_event(s);
 }
 // after a cycle has completed: account marks of iterations that really ran
 void prof_collect(gg_solver *s, int executed)
 {
-    if (!s->prof_on) return;
+    if (!s->prof_mask) return;
     for (const auto &mk : s->marks) {
         if (mk.i >= executed || mk.e1 < 0) continue;
         float ms = 0.f;
@@ -1038,10 +1038,10 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     GG_API_END
 }
 
-int gg_profile_enable(gg_solver *s, int on)
+int gg_profile_enable(gg_solver *s, int kinds)
 {
-    if (!s) return GG_EINVAL;
-    s->prof_on = on != 0;
+    if (!s || (kinds & ~GG_PROF_ALL)) return GG_EINVAL;
+    s->prof_mask = kinds;
     return GG_OK;
 }
 

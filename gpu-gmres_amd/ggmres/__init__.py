@@ -30,6 +30,7 @@ EXPORTS = [
     "gg_trace_precond", "gg_bytes_trsv", "gg_transient",
 ]
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
+PROF_NKINDS = 5
 
 
 class Options(ctypes.Structure):
@@ -251,8 +252,12 @@ class Solver:
         _check(lib().gg_time_precond(self.h, int(reps), ctypes.byref(ms)))
         return ms.value
 
-    def profile(self, on=True):
-        _check(lib().gg_profile_enable(self.h, int(bool(on))))
+    def profile(self, on=True, kinds=None):
+        """Time kernel families inside solves: kinds = iterable of PROF_* (default all)."""
+        mask = 0
+        if on:
+            mask = (1 << PROF_NKINDS) - 1 if kinds is None else sum(1 << int(k) for k in set(kinds))
+        _check(lib().gg_profile_enable(self.h, mask))
         _check(lib().gg_profile_reset(self.h))
 
     def profile_get(self, kind):

@@ -136,9 +136,11 @@ int gg_time_spmv(gg_solver *s, int reps, int nrot, double *avg_ms);
 /* average device time of one preconditioner application (L then U solve) */
 int gg_time_precond(gg_solver *s, int reps, double *avg_ms);
 
-/* In-solve kernel timing: when enabled, every inner iteration brackets each
- * kernel family below with a hipEvent pair on the solver's stream; totals
- * accumulate over gg_solve* calls until gg_profile_reset. */
+/* In-solve kernel timing: every inner iteration brackets each selected kernel
+ * family below with a hipEvent pair (timing-only events, no system fence) on
+ * the solver's stream; totals accumulate over gg_solve* calls until
+ * gg_profile_reset.  gg_profile_enable(s, kinds): kinds is a bit mask of
+ * (1 << GG_PROF_*), GG_PROF_ALL for every family, 0 to switch timing off. */
 enum gg_prof_kind {
     GG_PROF_SPMV = 0,      /* ww = A v_i                                  */
     GG_PROF_PRECOND = 1,   /* w = M^-1 ww (both triangular solves)        */
@@ -147,7 +149,8 @@ enum gg_prof_kind {
     GG_PROF_TRSV_U = 4,    /* the upper triangular solve alone (U / Mr)   */
     GG_PROF_NKINDS = 5
 };
-int gg_profile_enable(gg_solver *s, int on);
+#define GG_PROF_ALL ((1 << GG_PROF_NKINDS) - 1)
+int gg_profile_enable(gg_solver *s, int kinds);
 int gg_profile_reset(gg_solver *s);
 int gg_profile_get(gg_solver *s, int kind, int *launches, double *total_ms);
 

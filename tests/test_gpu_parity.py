@@ -321,3 +321,23 @@ def test_transient_c5(solver, grid):
     assert rel_err(g["x"], o["x"]) <= 1e-10
     assert np.max(np.abs(g["ports"] - o["ports"])) <= 1e-10 * np.max(np.abs(o["ports"]))
     assert np.max(np.abs(o["ports"])) > 0      # the sources did drive the grid
+
+
+@pytest.mark.gpu
+def test_profile_kind_mask():
+    """gg_profile_enable(kinds): only the selected families are bracketed."""
+    A = M.laplacian_5pt(40)
+    b = M.rhs_ones(A)
+    s = ggmres.Solver()
+    s.set_matrix(A)
+    s.set_precond_ilu0()
+    s.profile(True, kinds=[ggmres.PROF_TRSV_U])
+    r = s.solve(b, np.zeros(A.shape[0]), restart=30, max_iter=200, tol=1e-8)
+    n_u = s.profile_get(ggmres.PROF_TRSV_U)[0]
+    assert r["inner"] <= n_u <= r["inner"] + r["restarts"] + 1
+    for k in (ggmres.PROF_SPMV, ggmres.PROF_PRECOND, ggmres.PROF_MGS, ggmres.PROF_TRSV_L):
+        assert s.profile_get(k)[0] == 0
+    s.profile(True)
+    s.solve(b, np.zeros(A.shape[0]), restart=30, max_iter=200, tol=1e-8)
+    assert all(s.profile_get(k)[0] > 0 for k in range(ggmres.PROF_NKINDS))
+    s.close()

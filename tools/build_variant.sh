@@ -1,0 +1,12 @@
+#!/bin/bash
+# tools/build_variant.sh NAME -DMACRO=V ...  -> variants/libggmres_NAME.so
+# (kernels.hip rebuilt with the given macros, other objects from the main build;
+# select at run time with GGMRES_LIB=variants/libggmres_NAME.so)
+set -e
+cd "$(dirname "$0")/../gpu-gmres_amd"
+name=$1; shift
+mkdir -p ../variants build/var
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -I../include/compat -I../include -Icsrc \
+    "$@" -c csrc/kernels.hip -o build/var/kernels_$name.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../variants/libggmres_$name.so build/var/kernels_$name.o \
+    build/solver.o build/host/factor.o build/host/analysis.o build/host/host_abi.o build/compat/interface_pg.o -L/opt/rocm/lib -lamdhip64
