@@ -311,6 +311,11 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
 #define GG_WAVE_LOOK 3
 #endif
 constexpr int kWaveLook = GG_WAVE_LOOK;
+// the compute wave's LDS traffic is issued in the shadow of each step's DPP shift
+#ifndef GG_WAVE_SHADOW
+#define GG_WAVE_SHADOW 1
+#endif
+constexpr bool kWaveShadow = GG_WAVE_SHADOW != 0;
 constexpr int kSpinLimit = 1 << 20;
 // Ring depth: batches j and j+1 are in LDS at barrier j and kWaveRing-3 more are
 // in flight (enough to cover the HBM latency at this stream rate).
@@ -626,9 +631,26 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 const double e1 = sx ? rg[kk][1].x : rg[kk][1].y;
                 const double e2 = sx ? rg[kk][2].x : rg[kk][2].y;
                 const double old = h ? bv[kk].y : bv[kk].x;
+                const double p2 = e2 * xp;
                 const double xs = dpp_shift_old<ctrl>(xp, old);
+                if constexpr (kWaveShadow) {
+                    // LDS work of the pair in the cross-lane shift's latency:
+                    // the look-ahead reads at the first step, the previous
+                    // pair's x staging at the second
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (h == 0 && kk + kWaveLook < C::PBN) {
+#pragma unroll
+                        for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
+                    }
+                    if (h == 1 && kk > 0) {
+                        xbuf[(bi & 1) * PB + (kk - 1) * 64 + lane] =
+                            FWD ? make_double2(xv[2 * kk - 2], xv[2 * kk - 1])
+                                : make_double2(xv[2 * kk - 1], xv[2 * kk - 2]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
                 double acc = bb - e1 * xs;      // line neighbour first (|offset| = nx)
-                acc = acc - e2 * xp;            // then the in-line neighbour (|offset| = 1)
+                acc = acc - p2;                 // then the in-line neighbour (|offset| = 1)
                 if constexpr (DIV == WD_HW) {
                     acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
                 } else if constexpr (DIV == WD_RCP) {
@@ -654,9 +676,11 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
             // and publishes the edge values), then the pair kWaveLook ahead is
             // read; the scheduling fence keeps it all inside this pair, in the
             // recurrence's latency bubbles
-            xbuf[(bi & 1) * PB + kk * 64 + lane] =
-                FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
-            if (kk + kWaveLook < C::PBN) {
+            if (!kWaveShadow || kk == C::PBN - 1)
+                xbuf[(bi & 1) * PB + kk * 64 + lane] =
+                    FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
+
+            if (!kWaveShadow && kk + kWaveLook < C::PBN) {
 #pragma unroll
                 for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
             }
