@@ -10,7 +10,7 @@ gap = collections.defaultdict(list)
 dur = collections.defaultdict(list)
 prev = None
 for r in rows:
-    n = r["Kernel_Name"].split("(")[0][-48:]
+    n = r["Kernel_Name"].replace("(anonymous namespace)", "").split("(")[0][-48:]
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     dur[n].append(e - s)
     if prev is not None:
