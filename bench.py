@@ -15,6 +15,11 @@ stream (gg_profile_*); algorithmic bytes from SURVEY.md 8(d) (DESIGN.md
 passes (profiles/pmc_traffic.json).  cpu_baseline: the fp64 oracle restatement
 (oracle/, serial C) on a bounded sample of the same workload, rank 0 only.
 
+--workload c3: SpMV on the circuit5M stand-in (seeded power-law CSR with
+circuit5M's n = 5,558,326 and nnz ~ 59.5M; the SuiteSparse file
+is not available offline): one step = --c3-spmvs SpMV launches, value =
+algorithmic SpMV bytes / time in GB/s (no parity claim on this matrix).
+
 --workload c5: the transient loop (gg_transient: A = G + C/h on the C2 grid, 1 %
 PULSE sources, --c5-steps backward-Euler steps per step, warm start); value =
 GMRES iterations of all steps / time.
@@ -52,7 +57,8 @@ def parse():
     p.add_argument("--cpu-iters", type=int, default=120,
                    help="oracle iterations timed for cpu_baseline (0 = skip)")
     p.add_argument("--no-profile", action="store_true", help="do not bracket kernels with events")
-    p.add_argument("--workload", choices=["c2", "c5"], default="c2",
+    p.add_argument("--c3-spmvs", type=int, default=20, help="SpMV launches per c3 step")
+    p.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
                    help="c2: one C2 solve per step (the headline); c5: a backward-Euler "
                         "transient (A = G + C/h, 1%% PULSE sources) of --c5-steps time steps per step")
     p.add_argument("--c5-steps", type=int, default=100)
@@ -68,13 +74,15 @@ KERNEL_NAMES = {
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, workload=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, written by profiles/pmc_traffic.py: FETCH_SIZE
-    doubled for 16-B/lane streaming reads, + WRITE_SIZE; MI355X_MICROARCH.md HBM
-    section), or None when that file has no entry for it."""
+    (profiles/pmc_traffic.json, or profiles/pmc_traffic_<workload>.json; written
+    by profiles/pmc_traffic.py: FETCH_SIZE doubled for 16-B/lane streaming
+    reads, + WRITE_SIZE; MI355X_MICROARCH.md HBM section), or None when that
+    file has no entry for it."""
+    path = PMC_FILE if workload is None else PMC_FILE.replace(".json", f"_{workload}.json")
     try:
-        with open(PMC_FILE) as f:
+        with open(path) as f:
             d = json.load(f)
         return d["kernels"][kernel]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
@@ -94,6 +102,64 @@ def mgs_bytes(n, m, inner_list):
     return tot, iters
 
 
+def bench_c3(a, torch, dist, world, rank, local):
+    """SpMV roofline on the C3 stand-in (one matrix per rank, weak scaling)."""
+    import ggmres
+    from ggmres import matrices as M
+    t_setup = time.perf_counter()
+    A = M.power_law(seed=20261015 + rank)
+    s = ggmres.Solver(local)
+    s.set_matrix(A)
+    s.set_precond_none()
+    t_setup = time.perf_counter() - t_setup
+    byt = s.bytes_spmv()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        s.time_spmv(reps=a.c3_spmvs, nrot=1)
+    barrier()
+    t0 = time.perf_counter()
+    ev_ms = [s.time_spmv(reps=a.c3_spmvs, nrot=1) for _ in range(a.steps)]
+    barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    tot = torch.tensor([byt * a.c3_spmvs * a.steps], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    value = float(tot.item()) / float(t.item()) / 1e9
+    avg_us = sum(ev_ms) / len(ev_ms) * 1e3                 # events around each launch
+    ach = byt / (avg_us * 1e-6) / 1e9
+    rl = np.diff(A.indptr)
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "GB/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el * 1e3 / a.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"C3 stand-in: seeded power-law CSR (circuit5M n and nnz), "
+                               f"y = A x, {a.c3_spmvs} SpMVs per step",
+                   "n": int(A.shape[0]), "nnz": int(A.nnz), "max_row": int(rl.max()),
+                   "mean_row": round(float(rl.mean()), 2),
+                   "parallelism": "single" if world == 1 else f"replicas{world}",
+                   "setup_s": round(t_setup, 3)},
+        "roofline": {"kernel": "k_spmv_stream<false>", "bound": "hbm", "achieved": round(ach, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic("k_spmv_stream<false>", "c3"),
+                     "alg_bytes_per_launch": byt, "avg_us": round(avg_us, 3)},
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    s.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,6 +175,8 @@ def main():
     import ggmres
     from ggmres import matrices as M
 
+    if a.workload == "c3":
+        return bench_c3(a, torch, dist, world, rank, local)
     c5 = a.workload == "c5"
     h5 = 1e-2
     A = M.laplacian_5pt(a.grid)

@@ -943,6 +943,22 @@ int gg_time_spmv(gg_solver *s, int reps, int nrot, double *avg_ms)
     GG_REQUIRE(s && avg_ms && reps > 0 && nrot > 0, GG_EINVAL, "bad argument");
     GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner / layout");
     set_device(s);
+    if (nrot == 1) {
+        // the solver's own A and workspace vectors: no copies (for matrices
+        // far larger than the Infinity Cache, e.g. the C3 stand-in)
+        ensure_workspace(s, std::max(s->m_alloc, 1));
+        launch_fill_u64(reinterpret_cast<unsigned long long *>(s->xv.p), s->Ppad,
+                        0x3FF0000000000000ull, s->st);              // x = 1.0
+        launch_spmv(Gate{}, s->dA, s->xv.p, nullptr, s->ww.p, false, s->st);   // warm-up
+        GG_HIP(hipEventRecord(s->ev0, s->st));
+        for (int r = 0; r < reps; r++) launch_spmv(Gate{}, s->dA, s->xv.p, nullptr, s->ww.p, false, s->st);
+        GG_HIP(hipEventRecord(s->ev1, s->st));
+        GG_HIP(hipEventSynchronize(s->ev1));
+        float ms = 0.f;
+        GG_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        *avg_ms = ms / reps;
+        return GG_OK;
+    }
     // nrot independent copies of (A, x, y) so repeats are not served on-die
     std::vector<std::unique_ptr<DevCsr>> As;
     std::vector<std::unique_ptr<DBuf<double>>> xs, ys;

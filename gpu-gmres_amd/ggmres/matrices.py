@@ -3,6 +3,8 @@
 Configs:
   C1  100x100 5-pt Dirichlet Laplacian (diag 4, off -1), natural order, n=10,000
   C2  1000x1000 5-pt, n=1,000,000, nnz=4,996,000
+  C3  circuit5M stand-in (the SuiteSparse file is not available offline):
+      seeded power-law CSR with circuit5M's n and nnz (power_law)
   C4  7-pt 3D thermal grid, kx=ky=1, kz=10, diag = sum|off| + 1e-3
   C5  A = G + C/h with C = c*I
 
@@ -136,6 +138,28 @@ def read_rua(path):
     assert len(ptr) == ncol + 1 and len(ind) == nnz and len(val) == nnz
     A = sp.csc_matrix((val, ind, ptr), shape=(nrow, ncol))
     return _finish(A.tocsr())
+
+
+def power_law(n=5_558_326, nnz=59_524_291, alpha=1.5, cap=100_000, seed=20261015):
+    """Synthetic stand-in for C3: off-diagonal counts per row
+    ~ Zipf(alpha) clipped to [1, cap], rescaled (stochastic rounding) so the
+    matrix holds about `nnz` entries; columns uniform; values -U(0,1); the
+    diagonal is the row's sum of |off| + 1 (strictly diagonally dominant).
+    Heavy-tailed rows (a few thousand entries) exercise the long-row path."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k = np.minimum(rng.zipf(alpha, n), cap).astype(np.float64)
+    k *= (nnz - n) / k.sum()
+    k = np.floor(k + rng.random(n)).astype(np.int64)
+    k = np.minimum(k, n - 1)
+    tot = int(k.sum())
+    rows = np.repeat(np.arange(n, dtype=np.int64), k)
+    cols = rng.integers(0, n - 1, tot, dtype=np.int64)
+    cols += cols >= rows                       # skip the diagonal
+    vals = -rng.random(tot)
+    A = sp.coo_matrix((vals, (rows, cols)), shape=(n, n)).tocsr()
+    A.sum_duplicates()
+    d = np.asarray(abs(A).sum(axis=1)).ravel() + 1.0
+    return _finish(A + sp.diags(d))
 
 
 def rhs_ones(A):

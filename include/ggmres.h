@@ -131,7 +131,8 @@ int gg_precond_apply(gg_solver *s, int op, const double *in, double *out);
 
 /* device-timed kernel measurements on the solver's stream (hipEvents).
  * gg_time_spmv: y = A x over nrot rotating copies of (x, y) so the Infinity
- * Cache cannot serve repeats when nrot * footprint > 256 MiB; avg_ms per launch. */
+ * Cache cannot serve repeats when nrot * footprint > 256 MiB; avg_ms per launch.
+ * nrot == 1 runs on the solver's own A and workspace (no copies, x = 1). */
 int gg_time_spmv(gg_solver *s, int reps, int nrot, double *avg_ms);
 /* average device time of one preconditioner application (L then U solve) */
 int gg_time_precond(gg_solver *s, int reps, double *avg_ms);

@@ -41,6 +41,7 @@ MATS = {
     "3pt_100": lambda: load("3pt_100.mtx"),
     "sherman1": lambda: load("sherman1.rua"),
     "thermal_7pt_12": lambda: M.grid_7pt(12),
+    "powerlaw_3000": lambda: M.power_law(3000, 33000, seed=7),    # C3 stand-in, small
 }
 WAVE = {"c1_5pt_100x100", "5pt_37x64"}
 
@@ -55,6 +56,23 @@ def test_spmv_bitexact(solver, name):
     solver.set_precond_ilu0()   # wavefront layout where it applies
     assert solver.uses_wavefront == (name in WAVE)
     assert np.array_equal(solver.spmv(x), O.spmv(A, x))
+
+
+def test_spmv_long_rows(solver):
+    """Rows above the block capacity (2048 entries) are summed by a strided
+    block reduction: within 1e-13 of the serial sum (scale |A||x|); every
+    other row stays bit-exact."""
+    A = M.power_law(6000, 600000, seed=3)
+    rl = np.diff(A.indptr)
+    assert (rl > 2048).sum() > 0
+    x = np.random.default_rng(4).standard_normal(A.shape[0])
+    solver.set_matrix(A)
+    solver.set_precond_none()
+    y, ref = solver.spmv(x), O.spmv(A, x)
+    short = rl <= 2048
+    assert np.array_equal(y[short], ref[short])
+    scale = abs(A) @ abs(x)
+    assert np.all(np.abs(y - ref) <= 1e-13 * scale)
 
 
 @pytest.mark.parametrize("name", sorted(MATS))
@@ -186,7 +204,8 @@ def test_gmres_left_fixed_iterations(solver):
     check_exact(g, ot)
 
 
-@pytest.mark.parametrize("name", ["7pt_10x10x10", "sherman1", "thermal_7pt_12", "5pt_37x64"])
+@pytest.mark.parametrize("name", ["7pt_10x10x10", "sherman1", "thermal_7pt_12", "5pt_37x64",
+                                  "powerlaw_3000"])
 def test_gmres_left_other_matrices(solver, name):
     A = MATS[name]()
     b = M.rhs_uniform(A.shape[0])
