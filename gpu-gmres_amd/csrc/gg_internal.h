@@ -49,6 +49,12 @@ struct CanonTri {
 
 // host-side factorization (host/factor.cpp)
 void ilu0_left(const Csr &A, Csr &L, Csr &U);                 // leftILU semantics
+// splitLU_csr (src/leftILU.cu:481-541): drop |v| < 1e-9, unit diagonal LAST in L
+void split_lu_drop(const Csr &F, Csr &L, Csr &U);
+// CSC pattern of a square CSR (rows ascending per column) and the position maps
+// csc2csr[k] = CSR position of CSC entry k, csr2csc its inverse
+void csc_pattern(const Csr &A, std::vector<int> &cp, std::vector<int> &ri,
+                 std::vector<long long> &csc2csr, std::vector<long long> &csr2csc);
 int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U);        // lofC + ilukC, 0 or GG_EZEROPIVOT
 
 // canonical forms (host/analysis.cpp)

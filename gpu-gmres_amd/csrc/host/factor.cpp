@@ -87,26 +87,52 @@ void ilu0_left(const Csr &A, Csr &L, Csr &U)
     }
 
     // back to CSR, split with the 1e-9 drop, unit diagonal appended LAST in L
-    std::vector<int> rp2, ci2;
-    std::vector<double> v2;
-    transpose(n, cp, ri, cv, rp2, ci2, v2);
+    Csr F;
+    F.n = n;
+    transpose(n, cp, ri, cv, F.rp, F.ci, F.v);
+    split_lu_drop(F, L, U);
+}
+
+void split_lu_drop(const Csr &F, Csr &L, Csr &U)
+{
+    const int n = F.n;
     L.n = U.n = n;
     L.rp.assign(n + 1, 0);
     U.rp.assign(n + 1, 0);
     L.ci.clear(); L.v.clear(); U.ci.clear(); U.v.clear();
-    L.ci.reserve(rp2[n] / 2 + n); L.v.reserve(rp2[n] / 2 + n);
-    U.ci.reserve(rp2[n] / 2 + n); U.v.reserve(rp2[n] / 2 + n);
+    L.ci.reserve(F.rp[n] / 2 + n); L.v.reserve(F.rp[n] / 2 + n);
+    U.ci.reserve(F.rp[n] / 2 + n); U.v.reserve(F.rp[n] / 2 + n);
     for (int r = 0; r < n; r++) {
-        for (int k = rp2[r]; k < rp2[r + 1]; k++) {
-            if (near_zero(v2[k])) continue;
-            if (ci2[k] < r) { L.ci.push_back(ci2[k]); L.v.push_back(v2[k]); }
-            else { U.ci.push_back(ci2[k]); U.v.push_back(v2[k]); }
+        for (int k = F.rp[r]; k < F.rp[r + 1]; k++) {
+            if (near_zero(F.v[k])) continue;
+            if (F.ci[k] < r) { L.ci.push_back(F.ci[k]); L.v.push_back(F.v[k]); }
+            else { U.ci.push_back(F.ci[k]); U.v.push_back(F.v[k]); }
         }
         L.ci.push_back(r);
         L.v.push_back(1.0);
         L.rp[r + 1] = (int)L.ci.size();
         U.rp[r + 1] = (int)U.ci.size();
     }
+}
+
+void csc_pattern(const Csr &A, std::vector<int> &cp, std::vector<int> &ri,
+                 std::vector<long long> &csc2csr, std::vector<long long> &csr2csc)
+{
+    const int n = A.n, nnz = A.rp[n];
+    cp.assign(n + 1, 0);
+    ri.resize(nnz);
+    csc2csr.resize(nnz);
+    csr2csc.resize(nnz);
+    for (int k = 0; k < nnz; k++) cp[A.ci[k] + 1]++;
+    for (int c = 0; c < n; c++) cp[c + 1] += cp[c];
+    std::vector<int> pos(cp.begin(), cp.end() - 1);
+    for (int r = 0; r < n; r++)
+        for (int k = A.rp[r]; k < A.rp[r + 1]; k++) {
+            const int p = pos[A.ci[k]]++;
+            ri[p] = r;
+            csc2csr[p] = k;
+            csr2csc[k] = p;
+        }
 }
 
 int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U)

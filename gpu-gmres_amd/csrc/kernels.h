@@ -43,6 +43,10 @@ void launch_transient_step(int n, int nsrc, const double *pulse, int it, double 
                            const int *src_ptr, const int *src_idx, const double *cdiag,
                            const double *x, double *w, hipStream_t st);
 void launch_gather_ports(int nport, const int *port, const double *x, double *out, hipStream_t st);
+// device ILU(0) column elimination (co-resident grid of at most ilu0_columns_max_blocks())
+int ilu0_columns_max_blocks();
+void launch_ilu0_columns(int n, const int *cp, const int *ri, const double *cv0, double *cv, int *level,
+                         int *done, int *err, int blocks, hipStream_t st);
 void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st);  // out[i] = idx[i]<0 ? 0 : in[idx[i]]
 void launch_copy(const double *in, double *out, long long n, hipStream_t st);
 void launch_dot(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, hipStream_t st);

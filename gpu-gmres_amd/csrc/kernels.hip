@@ -696,6 +696,122 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
     }
 }
 
+// ================================================ ILU(0) factorization (device)
+// leftILU's column elimination (src/leftILU.cu:27-336: cpuSequentialTriSolve
+// :769-825 per column, columns in generateLevel :339-368 order) as a dataflow
+// kernel.  Lane = column c; a wave takes 64 consecutive columns, the grid
+// strides over the columns in ascending order (all blocks co-resident, so the
+// smallest unfinished column can always progress).  Per column:
+//  1. its level: max(level[r] + 1) over the rows r < c of its U part whose
+//     ORIGINAL value is not |a| < 1e-9 (generateLevel), published in level[c];
+//  2. the serial order of the reference processes columns by (level, index),
+//     so a source column r < c (a U-part row of c) was finished before c iff
+//     level[r] <= level[c]: then wait for done[r] and read r's factored
+//     values, otherwise read r's ORIGINAL values (r had not been processed);
+//  3. the column update in the reference's order (ascending U-part rows, then
+//     the L part divided by the diagonal, 0 when |diag| < 1e-9), written with
+//     agent-scope stores, drained, then done[c] published.
+// Lanes of one wave can depend on each other, so every lane retries inside a
+// wave-uniform loop instead of spinning alone.  Spins are bounded (err bit 0).
+__device__ __forceinline__ int ld_agent_i(const int *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent_i(int *p, int v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent_d(const double *p)
+{
+    return __longlong_as_double((long long)ld_agent(reinterpret_cast<const unsigned long long *>(p)));
+}
+__device__ __forceinline__ void st_agent_d(double *p, double v)
+{
+    st_agent(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v));
+}
+__device__ __forceinline__ bool ilu_zero(double a) { return __builtin_fabs(a) < 1e-9; }   // Equal(a, 0)
+
+__global__ __launch_bounds__(kBlock) void k_ilu0_columns(int n, const int *__restrict__ cp,
+                                                         const int *__restrict__ ri,
+                                                         const double *__restrict__ cv0, double *cv,
+                                                         int *level, int *done, int *err)
+{
+    const int lane = threadIdx.x & 63;
+    const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
+    for (long long base = wid * 64; base < n; base += nw * 64) {
+        const int c = (int)(base + lane);
+        int state = c < n ? 0 : 2;             // 0: level, 1: factor, 2: finished
+        int lev = 0;
+        int spins = 0;
+        const int lb = c < n ? cp[c] : 0, ub = c < n ? cp[c + 1] : 0;
+        while (__any(state != 2)) {
+            bool moved = false;
+            if (state == 0) {
+                bool ready = true;
+                int l = 0;
+                for (int k = lb; k < ub; k++) {
+                    const int r = ri[k];
+                    if (r >= c) break;
+                    const int lr = ld_agent_i(level + r);
+                    if (lr < 0) { ready = false; break; }
+                    if (!ilu_zero(cv0[k]) && lr + 1 > l) l = lr + 1;
+                }
+                if (ready) {
+                    lev = l;
+                    st_agent_i(level + c, l);
+                    state = 1;
+                    moved = true;
+                }
+            }
+            if (state == 1) {
+                bool ready = true;
+                for (int k = lb; k < ub; k++) {
+                    const int r = ri[k];
+                    if (r >= c) break;
+                    if (ld_agent_i(level + r) <= lev && ld_agent_i(done + r) == 0) { ready = false; break; }
+                }
+                if (ready) {
+                    double u_diag = 0.0;
+                    for (int k = lb; k < ub - 1; k++) {
+                        const int cr = ri[k];
+                        if (cr > c) break;
+                        if (cr == c) { u_diag = ld_agent_d(cv + k); break; }
+                        const bool fin = ld_agent_i(level + cr) <= lev;
+                        int q = cp[cr];
+                        const int qe = cp[cr + 1];
+                        const double ukt = ld_agent_d(cv + k);
+                        for (int p = k + 1; p < ub; p++) {
+                            const int r2 = ri[p];
+                            while (q < qe && ri[q] < r2) q++;
+                            if (q == qe) break;
+                            if (ri[q] == r2) {
+                                const double lq = fin ? ld_agent_d(cv + q) : cv0[q];
+                                st_agent_d(cv + p, ld_agent_d(cv + p) - lq * ukt);
+                            }
+                        }
+                    }
+                    for (int k = lb; k < ub; k++) {
+                        if (ri[k] <= c) continue;
+                        st_agent_d(cv + k, ilu_zero(u_diag) ? 0.0 : ld_agent_d(cv + k) / u_diag);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // values out before the flag
+                    st_agent_i(done + c, 1);
+                    state = 2;
+                    moved = true;
+                }
+            }
+            if (!moved && state != 2) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > kSpinLimit) {
+                    atomicOr(err, 1);
+                    state = 2;
+                }
+            }
+        }
+    }
+}
+
 // ================================================== transient step (C5)
 // PULSE source values at time index it (gen_PULSEut_kernel, src/kernels.cu:223-245);
 // pulse[k] = {vlo, vhi, td, tr, tf, tw, tp}
@@ -1149,6 +1265,19 @@ void launch_gather_ports(int nport, const int *port, const double *x, double *ou
     if (nport > 0) k_gather_ports<<<(nport + kBlock - 1) / kBlock, kBlock, 0, st>>>(nport, port, x, out);
 }
 
+int ilu0_columns_max_blocks()
+{
+    int dev = 0, per = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ilu0_columns, kBlock, 0) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return per * cus;
+}
+void launch_ilu0_columns(int n, const int *cp, const int *ri, const double *cv0, double *cv, int *level,
+                         int *done, int *err, int blocks, hipStream_t st)
+{
+    k_ilu0_columns<<<blocks, kBlock, 0, st>>>(n, cp, ri, cv0, cv, level, done, err);
+}
 void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st)
 {
     k_gather<<<blocks_for(n, kBlock, 8192), kBlock, 0, st>>>(in, idx, out, n);

@@ -724,6 +724,84 @@ int gg_set_precond_ilu0(gg_solver *s)
     GG_API_END
 }
 
+// ILU(0) numeric factorization on the device (k_ilu0_columns): the factored
+// matrix in A's CSR order, bit-identical to ilu0_left before its split.  The
+// CSC pattern and position maps are built on the host (O(nnz)), as leftILU
+// builds its CSC and level lists on the host before its device kernels.
+void ilu0_device_values(gg_solver *s, std::vector<double> &fv, double *ms)
+{
+    const Csr &A = s->A;
+    const int n = A.n, nnz = A.rp[n];
+    std::vector<int> cp, ri;
+    std::vector<long long> c2r, r2c;
+    csc_pattern(A, cp, ri, c2r, r2c);
+    DBuf<int> dcp, dri, dlev, ddone;
+    DBuf<long long> dc2r, dr2c;
+    DBuf<double> dv, dcv0, dcv, dout;
+    dcp.upload(cp, s->st);
+    dri.upload(ri, s->st);
+    dc2r.upload(c2r, s->st);
+    dr2c.upload(r2c, s->st);
+    dv.upload(A.v, s->st);
+    dcv0.alloc(nnz);
+    dcv.alloc(nnz);
+    dout.alloc(nnz);
+    dlev.alloc(n);
+    ddone.alloc(n);
+    if (!s->err.p) s->err.alloc(1);
+    GG_HIP(hipMemsetAsync(dlev.p, 0xFF, (size_t)n * sizeof(int), s->st));     // level -1: not known
+    GG_HIP(hipMemsetAsync(ddone.p, 0, (size_t)n * sizeof(int), s->st));
+    GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
+    const int maxb = ilu0_columns_max_blocks();
+    GG_REQUIRE(maxb > 0, GG_EHIP, "ILU(0) device: occupancy query failed");
+    const long long need = ((long long)n + kBlock - 1) / kBlock;
+    const int blocks = (int)std::max<long long>(1, std::min<long long>(maxb, need));
+    GG_HIP(hipEventRecord(s->ev0, s->st));
+    launch_gather(dv.p, dc2r.p, dcv0.p, nnz, s->st);
+    launch_gather(dv.p, dc2r.p, dcv.p, nnz, s->st);
+    launch_ilu0_columns(n, dcp.p, dri.p, dcv0.p, dcv.p, dlev.p, ddone.p, s->err.p, blocks, s->st);
+    launch_gather(dcv.p, dr2c.p, dout.p, nnz, s->st);
+    GG_HIP(hipEventRecord(s->ev1, s->st));
+    fv.resize(nnz);
+    GG_HIP(hipMemcpyAsync(fv.data(), dout.p, (size_t)nnz * sizeof(double), hipMemcpyDeviceToHost, s->st));
+    int err = 0;
+    GG_HIP(hipMemcpyAsync(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
+    GG_REQUIRE(err == 0, GG_ETIMEOUT, "ILU(0) device: a column wait timed out");
+    float t = 0.f;
+    GG_HIP(hipEventElapsedTime(&t, s->ev0, s->ev1));
+    if (ms) *ms = t;
+}
+
+int gg_ilu0_device_values(gg_solver *s, double *val, double *ms)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A && val, GG_ESTATE, "gg_ilu0_device_values: call gg_set_matrix first");
+    set_device(s);
+    std::vector<double> fv;
+    ilu0_device_values(s, fv, ms);
+    std::copy(fv.begin(), fv.end(), val);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_set_precond_ilu0_device(gg_solver *s)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "set_precond before set_matrix");
+    set_device(s);
+    Csr F;
+    F.n = s->A.n;
+    F.rp = s->A.rp;
+    F.ci = s->A.ci;
+    ilu0_device_values(s, F.v, nullptr);
+    Csr Lf, Uf;
+    split_lu_drop(F, Lf, Uf);
+    setup_left(s, Lf, Uf, GG_PRECOND_ILU0);
+    return GG_OK;
+    GG_API_END
+}
+
 int gg_set_precond_iluk(gg_solver *s, int level)
 {
     GG_API_BEGIN

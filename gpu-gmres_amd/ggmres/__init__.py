@@ -27,7 +27,8 @@ EXPORTS = [
     "gg_uses_wavefront", "gg_solve", "gg_solve_device", "gg_get_history", "gg_spmv",
     "gg_precond_apply", "gg_time_spmv", "gg_time_precond", "gg_bytes_spmv",
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
-    "gg_trace_precond", "gg_bytes_trsv", "gg_transient",
+    "gg_trace_precond", "gg_bytes_trsv", "gg_transient", "gg_set_precond_ilu0_device",
+    "gg_ilu0_device_values",
 ]
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
 PROF_NKINDS = 5
@@ -70,9 +71,10 @@ def lib():
         L.gg_destroy.argtypes = [_VP]
         L.gg_set_matrix.argtypes = [_VP, ctypes.c_int, _I, _I, _D]
         for f in ("gg_set_precond_none", "gg_set_precond_ilu0", "gg_precond_kind",
-                  "gg_uses_wavefront"):
+                  "gg_uses_wavefront", "gg_set_precond_ilu0_device"):
             getattr(L, f).argtypes = [_VP]
         L.gg_set_precond_iluk.argtypes = [_VP, ctypes.c_int]
+        L.gg_ilu0_device_values.argtypes = [_VP, _D, ctypes.POINTER(ctypes.c_double)]
         L.gg_set_precond_lu.argtypes = [_VP, _I, _I, _D, _I, _I, _D]
         L.gg_set_precond_split.argtypes = [_VP, _I, _I, _D, _I, _I, _D, _D, _I, _I, _D, _D]
         L.gg_solve.argtypes = [_VP, _D, _D, ctypes.POINTER(Options), ctypes.POINTER(Result)]
@@ -130,6 +132,7 @@ class Solver:
         _check(lib().gg_create(int(device), ctypes.byref(h)))
         self.h = h
         self.n = 0
+        self.nnz = 0
 
     def close(self):
         if self.h:
@@ -146,6 +149,7 @@ class Solver:
     def set_matrix(self, A):
         n, rp, ci, v = _csr_arrays(A)
         self.n = n
+        self.nnz = int(rp[n])
         _check(lib().gg_set_matrix(self.h, n, rp, ci, v))
 
     def set_precond_none(self):
@@ -153,6 +157,17 @@ class Solver:
 
     def set_precond_ilu0(self):
         _check(lib().gg_set_precond_ilu0(self.h))
+
+    def set_precond_ilu0_device(self):
+        """ILU(0) factored on the GPU (bit-identical factors to set_precond_ilu0)."""
+        _check(lib().gg_set_precond_ilu0_device(self.h))
+
+    def ilu0_device_values(self):
+        """(factored values in A's CSR order before the drop/split, device ms)."""
+        out = np.zeros(self.nnz)
+        ms = ctypes.c_double()
+        _check(lib().gg_ilu0_device_values(self.h, out, ctypes.byref(ms)))
+        return out, ms.value
 
     def set_precond_iluk(self, level):
         _check(lib().gg_set_precond_iluk(self.h, int(level)))

@@ -7,6 +7,9 @@
  *
  *   gg_set_matrix          MySpMatrix / gpuMallocCpyCSRmySpM  src/SpMV.h:57-84, src/SpMV_alloc.cu:121-165
  *   gg_set_precond_ilu0    MyILU0::Initilize / leftILU        src/preconditioner.h:119-144, src/leftILU.cu:27-336
+ *   gg_set_precond_ilu0_device, gg_ilu0_device_values
+ *                          leftILU's device path (sparseTriSolve_V2 per level)
+ *                                                               src/leftILU.cu:188-262, 650-702
  *   gg_set_precond_iluk    MyILUK::Initilize (ilukC, lofC)     src/preconditioner.cu:1659-1753, src/iluk.cpp:56-334
  *   gg_set_precond_lu      GMRES_GPU_leftILU0 L/U arguments     src/gmres.h:206-213 (src/gmres.cu:1438-1444)
  *   gg_set_precond_split   MyILUPPfloat::Initilize              src/preconditioner.cu:1205-1334
@@ -98,6 +101,14 @@ int gg_set_matrix(gg_solver *s, int n, const int *row_ptr, const int *col_idx,
 
 int gg_set_precond_none(gg_solver *s);
 int gg_set_precond_ilu0(gg_solver *s);
+/* the same ILU(0) with its numeric factorization on the GPU: leftILU
+ * (src/leftILU.cu:27-336) factors level by level on the device; here one
+ * dataflow launch processes every column once its sources are done.
+ * Factors bit-identical to gg_set_precond_ilu0. */
+int gg_set_precond_ilu0_device(gg_solver *s);
+/* the device-factored matrix (L strict part divided by the pivots, U part) in
+ * A's CSR order, before the 1e-9 drop / split; ms = device time (may be NULL) */
+int gg_ilu0_device_values(gg_solver *s, double *val, double *ms);
 int gg_set_precond_iluk(gg_solver *s, int level);
 /* L: unit lower (strict entries + unit diagonal LAST in each row; the diagonal is
  *    not applied, LUSolve_ignoreZero semantics); U: upper, diagonal first. */

@@ -50,6 +50,7 @@ def lib():
                           _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
                           _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD)]
             f.restype = ctypes.c_int
+        L.orc_ilu0_values.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p]
         L.orc_iluk.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p,
                                _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
                                _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD)]
@@ -120,6 +121,14 @@ def ilu0(A):
                         u_rp, ctypes.byref(uci), ctypes.byref(uv))
     assert rc == 0
     return _take(n, l_rp, lci, lv), _take(n, u_rp, uci, uv)
+
+
+def ilu0_values(A):
+    """leftILU's factored matrix before the split (A's sorted CSR order)."""
+    A = csr(A)
+    out = np.zeros(max(int(A.rp[A.n]), 1))
+    assert lib().orc_ilu0_values(A.n, A.rp, A.ci, A.v, out) == 0
+    return out[:int(A.rp[A.n])]
 
 
 def iluk(A, k):

@@ -122,9 +122,10 @@ static void split_lu(int n, const int *rp, const int *ci, const double *v,
     }
 }
 
-int orc_ilu0(int n, const int *rp, const int *ci, const double *v,
-             int *l_rp, int **l_ci, double **l_v,
-             int *u_rp, int **u_ci, double **u_v)
+/* leftILU's factorization up to (excluding) the split: the factored matrix in
+ * CSR form (crp/cci/cvv, malloc'd; same pattern and order as a sorted A) */
+static void ilu0_factor_csr(int n, const int *rp, const int *ci, const double *v,
+                            int **crp_out, int **cci_out, double **cvv_out)
 {
     int nnz = rp[n];
     size_t cap = (size_t)(nnz > 0 ? nnz : 1);
@@ -159,11 +160,30 @@ int orc_ilu0(int n, const int *rp, const int *ci, const double *v,
     int *cci = (int *)malloc(cap * sizeof(int));
     double *cvv = (double *)malloc(cap * sizeof(double));
     csr_to_csc(n, cp, ri, cv, crp, cci, cvv); /* transpose of CSC == CSR */
-    split_lu(n, crp, cci, cvv, l_rp, l_ci, l_v, u_rp, u_ci, u_v);
-
-    free(crp); free(cci); free(cvv);
+    *crp_out = crp; *cci_out = cci; *cvv_out = cvv;
     free(cp); free(ri); free(cv);
     free(order); free(lcnt); free(level);
+}
+
+int orc_ilu0(int n, const int *rp, const int *ci, const double *v,
+             int *l_rp, int **l_ci, double **l_v,
+             int *u_rp, int **u_ci, double **u_v)
+{
+    int *crp, *cci;
+    double *cvv;
+    ilu0_factor_csr(n, rp, ci, v, &crp, &cci, &cvv);
+    split_lu(n, crp, cci, cvv, l_rp, l_ci, l_v, u_rp, u_ci, u_v);
+    free(crp); free(cci); free(cvv);
+    return 0;
+}
+
+int orc_ilu0_values(int n, const int *rp, const int *ci, const double *v, double *out)
+{
+    int *crp, *cci;
+    double *cvv;
+    ilu0_factor_csr(n, rp, ci, v, &crp, &cci, &cvv);
+    memcpy(out, cvv, (size_t)rp[n] * sizeof(double));
+    free(crp); free(cci); free(cvv);
     return 0;
 }
 

@@ -36,6 +36,8 @@ void orc_residual(int n, const int *rp, const int *ci, const double *v,
  * final split splitLU_csr :481-541).  L: strictly-lower entries + unit diag
  * stored LAST per row; U: entries col>=row (diag first for sorted input).
  * Outputs are malloc'd; release with orc_free.  Returns 0. */
+/* the factored matrix of orc_ilu0 before its split (A's sorted CSR order) */
+int orc_ilu0_values(int n, const int *rp, const int *ci, const double *v, double *out);
 int orc_ilu0(int n, const int *rp, const int *ci, const double *v,
              int *l_rp, int **l_ci, double **l_v,
              int *u_rp, int **u_ci, double **u_v);

@@ -300,3 +300,20 @@ def test_transient_rhs_order():
     ref[1] = 2.0
     ref = ref + (0.0 + c * x)
     assert np.array_equal(w, ref)
+
+
+def test_ilu0_values_split_consistent():
+    """orc_ilu0_values (the factored matrix before the split) splits into
+    exactly orc_ilu0's L and U (drop |v| < 1e-9, unit diagonal last in L)."""
+    for A in (M.laplacian_5pt(12, 9), M.power_law(400, 4000, seed=5), M.grid_7pt(5)):
+        A = O.csr(A)
+        fv = O.ilu0_values(A)
+        L, U = O.ilu0(A)
+        lv, uv = [], []
+        for r in range(A.n):
+            for k in range(A.rp[r], A.rp[r + 1]):
+                if abs(fv[k]) < 1e-9:
+                    continue
+                (lv if A.ci[k] < r else uv).append(fv[k])
+            lv.append(1.0)
+        assert np.array_equal(np.array(lv), L.v) and np.array_equal(np.array(uv), U.v)
