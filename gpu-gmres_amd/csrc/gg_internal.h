@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "ggmres.h"
+#include "ggmres_host.h"
 
 namespace gg {
 
@@ -49,6 +50,15 @@ struct CanonTri {
 
 // host-side factorization (host/factor.cpp)
 void ilu0_left(const Csr &A, Csr &L, Csr &U);                 // leftILU semantics
+// domain decomposition setup (host/partition.cpp): partition4 with a recursive
+// BFS bisection (or contiguous blocks) in place of METIS, the arrow permutation,
+// dd_form's block extraction
+void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &node_part,
+                     std::vector<int> &part_size, std::vector<int> &pinv, std::vector<int> &q);
+Csr arrow_permute(const Csr &A, const std::vector<int> &pinv, const std::vector<int> &q);
+Csr csr_block(const Csr &A, int r0, int r1, int c0, int c1);
+// Matrix Market reader (host/mtx.cpp; readSparseMatrix semantics, fp64)
+bool read_mtx(const char *path, bool expand_symmetric, int &nrows, int &ncols, Csr &A);
 // splitLU_csr (src/leftILU.cu:481-541): drop |v| < 1e-9, unit diagonal LAST in L
 void split_lu_drop(const Csr &F, Csr &L, Csr &U);
 // CSC pattern of a square CSR (rows ascending per column) and the position maps

@@ -1,0 +1,87 @@
+"""Host-only entry points of libggmres.so (include/ggmres_host.h): domain
+decomposition setup and Matrix Market input.  No GPU is needed."""
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _check, _csr_arrays, lib
+
+PART_BISECT, PART_BLOCKS = 0, 1
+_PI = ctypes.POINTER(ctypes.c_int)
+_PD = ctypes.POINTER(ctypes.c_double)
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _take_csr(nrows, ncols, rp, ci_p, v_p):
+    L = lib()
+    nnz = int(rp[nrows])
+    ci = np.ctypeslib.as_array(ci_p, (max(nnz, 1),))[:nnz].copy()
+    v = np.ctypeslib.as_array(v_p, (max(nnz, 1),))[:nnz].copy()
+    L.gg_host_free(ctypes.cast(ci_p, ctypes.c_void_p))
+    L.gg_host_free(ctypes.cast(v_p, ctypes.c_void_p))
+    return sp.csr_matrix((v, ci, np.asarray(rp, np.int32)), shape=(nrows, ncols))
+
+
+def partition(A, nparts, method=PART_BISECT):
+    """partition4 (src/partition3.cpp:122-194) -> dict(node_part, part_size,
+    pinv, q, begin): nparts interiors, separator part nparts last."""
+    n, rp, ci, _ = _csr_arrays(A)
+    node_part = np.zeros(n, np.int32)
+    part_size = np.zeros(nparts + 1, np.int32)
+    pinv = np.zeros(n, np.int32)
+    q = np.zeros(n, np.int32)
+    _check(lib().gg_host_partition(ctypes.c_int(n), _ptr(rp, _PI), _ptr(ci, _PI), ctypes.c_int(nparts),
+                                   ctypes.c_int(method), _ptr(node_part, _PI), _ptr(part_size, _PI),
+                                   _ptr(pinv, _PI), _ptr(q, _PI)))
+    begin = np.concatenate([[0], np.cumsum(part_size)]).astype(np.int64)
+    return dict(node_part=node_part, part_size=part_size, pinv=pinv, q=q, begin=begin)
+
+
+def permute(A, pinv, q):
+    """P A P^T for (pinv, q) of partition()."""
+    n, rp, ci, v = _csr_arrays(A)
+    pinv = np.ascontiguousarray(pinv, np.int32)
+    q = np.ascontiguousarray(q, np.int32)
+    brp = np.zeros(n + 1, np.int32)
+    bci, bv = _PI(), _PD()
+    _check(lib().gg_host_permute(ctypes.c_int(n), _ptr(rp, _PI), _ptr(ci, _PI), _ptr(v, _PD),
+                                 _ptr(pinv, _PI), _ptr(q, _PI), _ptr(brp, _PI), ctypes.byref(bci),
+                                 ctypes.byref(bv)))
+    return _take_csr(n, n, brp, bci, bv)
+
+
+def block(A, r0, r1, c0, c1):
+    """rows [r0, r1) x cols [c0, c1) (dd_form's As / E / F / At, src/form_dd.cpp:32-110)."""
+    n, rp, ci, v = _csr_arrays(A)
+    brp = np.zeros(r1 - r0 + 1, np.int32)
+    bci, bv = _PI(), _PD()
+    _check(lib().gg_host_block(ctypes.c_int(n), _ptr(rp, _PI), _ptr(ci, _PI), _ptr(v, _PD),
+                               ctypes.c_int(r0), ctypes.c_int(r1), ctypes.c_int(c0), ctypes.c_int(c1),
+                               _ptr(brp, _PI), ctypes.byref(bci), ctypes.byref(bv)))
+    return _take_csr(r1 - r0, c1 - c0, brp, bci, bv)
+
+
+def dd_form(B, begin, nparts):
+    """dd_form's blocks of the permuted matrix B: As[k], E[k] (interior k x
+    separator), F[k] (separator x interior k), At (separator x separator)."""
+    s0, s1 = int(begin[nparts]), int(begin[nparts + 1])
+    As = [block(B, int(begin[k]), int(begin[k + 1]), int(begin[k]), int(begin[k + 1])) for k in range(nparts)]
+    E = [block(B, int(begin[k]), int(begin[k + 1]), s0, s1) for k in range(nparts)]
+    F = [block(B, s0, s1, int(begin[k]), int(begin[k + 1])) for k in range(nparts)]
+    return As, E, F, block(B, s0, s1, s0, s1)
+
+
+def read_mtx(path, expand_symmetric=False):
+    """Matrix Market -> scipy CSR (readSparseMatrix, src_thermal/SpMV_gen.cpp:93-187)."""
+    nr, nc = ctypes.c_int(), ctypes.c_int()
+    rp_p, ci_p, v_p = _PI(), _PI(), _PD()
+    _check(lib().gg_host_read_mtx(str(path).encode(), ctypes.c_int(int(expand_symmetric)),
+                                  ctypes.byref(nr), ctypes.byref(nc), ctypes.byref(rp_p),
+                                  ctypes.byref(ci_p), ctypes.byref(v_p)))
+    rp = np.ctypeslib.as_array(rp_p, (nr.value + 1,)).copy()
+    lib().gg_host_free(ctypes.cast(rp_p, ctypes.c_void_p))
+    return _take_csr(nr.value, nc.value, rp, ci_p, v_p)

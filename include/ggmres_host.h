@@ -8,6 +8,11 @@
  *   gg_host_iluk   ilukC + lofC       src/iluk.cpp:56-334
  *   gg_host_wave2d structured-grid detection for the wavefront SpTRSV
  *                  (replaces cusparseScsrsv_analysis, src/gmres.cu:1516-1517)
+ *   gg_host_partition  partition4      src/partition3.cpp:122-194 (METIS is not
+ *                  available: recursive BFS bisection or contiguous blocks)
+ *   gg_host_permute    the arrow permutation P A P^T of the DD solve
+ *   gg_host_block      dd_form block extraction  src/form_dd.cpp:32-110
+ *   gg_host_read_mtx   readSparseMatrix (Matrix Market)  src_thermal/SpMV_gen.cpp:93-187
  * Output arrays are malloc'd by the library; release them with gg_host_free.
  */
 #ifndef GGMRES_HOST_H_
@@ -28,6 +33,34 @@ int gg_host_iluk(int level, int n, const int *row_ptr, const int *col_idx, const
 int gg_host_wave2d(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,
                    const int *u_row_ptr, const int *u_col_idx, const double *u_val,
                    int *nx, int *ny);
+enum gg_part_method {
+    GG_PART_BISECT = 0,    /* recursive BFS bisection of the node graph (METIS stand-in) */
+    GG_PART_BLOCKS = 1     /* contiguous index ranges (strips / slabs of a natural-order grid) */
+};
+/* nparts interiors + the separator part `nparts` (every endpoint of a cut edge
+ * of the symmetrized pattern).  node_part[n]; part_size[nparts + 1];
+ * pinv[j] = new index of node j; q[i] = node at new index i (interiors first,
+ * separator last, ascending original index inside a part). */
+int gg_host_partition(int n, const int *row_ptr, const int *col_idx, int nparts, int method,
+                      int *node_part, int *part_size, int *pinv, int *q);
+/* B = P A P^T for (pinv, q) of gg_host_partition; a row's entries sorted by
+ * new column (stable) */
+int gg_host_permute(int n, const int *row_ptr, const int *col_idx, const double *val,
+                    const int *pinv, const int *q,
+                    int *b_row_ptr, int **b_col_idx, double **b_val);
+/* rows [r0, r1) x columns [c0, c1) of a CSR (As_k, E_k, F_k, At of dd_form
+ * are the blocks of B at the part boundaries); b_row_ptr has r1 - r0 + 1 slots */
+int gg_host_block(int n, const int *row_ptr, const int *col_idx, const double *val,
+                  int r0, int r1, int c0, int c1,
+                  int *b_row_ptr, int **b_col_idx, double **b_val);
+/* Matrix Market coordinate file -> CSR (0-based, entries sorted by (row, col),
+ * stable: duplicates kept in file order, as readSparseMatrix keeps them).
+ * The reference reads every file as general; expand_symmetric != 0 mirrors
+ * the strict triangle of symmetric / skew-symmetric files (an extension).
+ * 'pattern' files get value 1.  Values are parsed as fp64 (the reference
+ * narrows to float).  Returns GG_OK or GG_EINVAL (unreadable / malformed). */
+int gg_host_read_mtx(const char *path, int expand_symmetric, int *nrows, int *ncols,
+                     int **row_ptr, int **col_idx, double **val);
 void gg_host_free(void *p);
 
 #ifdef __cplusplus

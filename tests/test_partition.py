@@ -1,0 +1,112 @@
+"""Domain decomposition setup and Matrix Market input on the host (no GPU):
+gg_host_partition / gg_host_permute / gg_host_block / gg_host_read_mtx against
+the restatement in oracle/partition.py (integer work: exact)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import fixture_path
+from ggmres import host as H
+from ggmres import matrices as M
+from oracle import partition as OP
+
+GRIDS = {
+    "5pt_40x30": lambda: M.laplacian_5pt(40, 30),
+    "7pt_12": lambda: M.grid_7pt(12),
+    "powerlaw_800": lambda: M.power_law(800, 6000, seed=9),
+    "sherman1": lambda: M.read_rua(fixture_path("sherman1.rua")),
+}
+
+
+@pytest.mark.parametrize("name", sorted(GRIDS))
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+def test_partition4_blocks_exact(name, nparts):
+    """contiguous base partition -> partition4's adjustment, sizes, pinv, q exactly"""
+    A = GRIDS[name]()
+    n = A.shape[0]
+    got = H.partition(A, nparts, H.PART_BLOCKS)
+    ref = OP.partition4_adjust(A.indptr, A.indices, n, nparts, OP.blocks_base(n, nparts))
+    for k, r in zip(("node_part", "part_size", "pinv", "q"), ref):
+        assert np.array_equal(got[k], r), k
+
+
+@pytest.mark.parametrize("name", sorted(GRIDS))
+@pytest.mark.parametrize("method", [H.PART_BLOCKS, H.PART_BISECT])
+@pytest.mark.parametrize("nparts", [2, 4, 8])
+def test_arrow_structure(name, method, nparts):
+    """interiors are mutually uncoupled; the separator is last; dd_form's blocks
+    reassemble the permuted matrix; P A P^T matches the dense permutation"""
+    A = GRIDS[name]()
+    n = A.shape[0]
+    P = H.partition(A, nparts, method)
+    pinv, q, begin = P["pinv"], P["q"], P["begin"]
+    assert np.array_equal(np.sort(q), np.arange(n)) and np.array_equal(pinv[q], np.arange(n))
+    assert P["part_size"].sum() == n
+    B = H.permute(A, pinv, q)
+    assert np.array_equal(B.toarray(), OP.permute_dense(A, pinv))
+    for r in range(n):     # entries of a row sorted by new column
+        cols = B.indices[B.indptr[r]:B.indptr[r + 1]]
+        assert np.all(np.diff(cols) >= 0)
+    for a in range(nparts):
+        for b in range(nparts):
+            if a != b:
+                blk = H.block(B, int(begin[a]), int(begin[a + 1]), int(begin[b]), int(begin[b + 1]))
+                assert blk.nnz == 0
+    As, E, F, At = H.dd_form(B, begin, nparts)
+    s0 = int(begin[nparts])
+    R = sp.lil_matrix((n, n))
+    for k in range(nparts):
+        b0, b1 = int(begin[k]), int(begin[k + 1])
+        R[b0:b1, b0:b1] = As[k]
+        R[b0:b1, s0:] = E[k]
+        R[s0:, b0:b1] = F[k]
+    R[s0:, s0:] = At
+    assert np.array_equal(R.toarray(), B.toarray())
+
+
+@pytest.mark.parametrize("nparts", [2, 4, 8])
+def test_bisection_balance(nparts):
+    """the METIS stand-in splits a grid into parts of equal size (+-1) before
+    the separator is taken out, and its separator is a small fraction"""
+    A = M.laplacian_5pt(64, 64)
+    n = A.shape[0]
+    P = H.partition(A, nparts, H.PART_BISECT)
+    sizes = P["part_size"][:nparts]
+    sep = int(P["part_size"][nparts])
+    assert sep < 0.2 * n
+    # recover the base sizes: separator nodes belong to some base part; the
+    # interiors alone must still be roughly balanced
+    assert sizes.min() > 0.5 * sizes.max()
+
+
+def test_read_mtx_fixtures_exact():
+    for f in ("3pt_100.mtx", "5pt_10x10.mtx", "7pt_10x10x10.mtx", "9pt_10x10.mtx"):
+        A = H.read_mtx(fixture_path(f))
+        nr, nc, rows, cols, vals = OP.read_mtx(fixture_path(f))
+        assert A.shape == (nr, nc)
+        coo = A.tocoo()
+        assert np.array_equal(coo.row, rows) and np.array_equal(coo.col, cols)
+        assert np.array_equal(coo.data, vals)
+        assert np.array_equal(A.toarray(), M.read_mtx(fixture_path(f)).toarray())
+
+
+def test_read_mtx_variants(tmp_path):
+    p = tmp_path / "s.mtx"
+    p.write_text("%%MatrixMarket matrix coordinate real symmetric\n% c\n3 3 4\n1 1 2.5\n2 1 -1\n"
+                 "3.0 2.0 -0.5\n3 3 4\n")
+    A = H.read_mtx(p)                       # the reference reads every file as general
+    assert A.nnz == 4 and A[0, 1] == 0 and A[1, 0] == -1
+    S = H.read_mtx(p, expand_symmetric=True)
+    assert S.nnz == 6 and S[0, 1] == -1 and S[1, 2] == -0.5
+    q = tmp_path / "p.mtx"
+    q.write_text("%%MatrixMarket matrix coordinate pattern general\n2 2 2\n2 1\n1 2\n")
+    P = H.read_mtx(q)
+    assert P.toarray().tolist() == [[0, 1], [1, 0]]
+    d = tmp_path / "d.mtx"                  # duplicates kept, in file order
+    d.write_text("%%MatrixMarket matrix coordinate real general\n2 2 3\n1 1 1\n1 1 2\n2 2 3\n")
+    D = H.read_mtx(d)
+    assert D.indptr.tolist() == [0, 2, 3] and D.data.tolist() == [1.0, 2.0, 3.0]
+    bad = tmp_path / "b.mtx"
+    bad.write_text("%%MatrixMarket matrix coordinate real general\n2 2 1\n3 1 1\n")
+    with pytest.raises(Exception):
+        H.read_mtx(bad)
