@@ -65,6 +65,7 @@ __device__ __forceinline__ void st2(double *p, long long u, double2 v)
 }
 
 // ---- relaxed agent-scope loads/stores for the band hand-off --------------------
+constexpr int kSpinLimit = 1 << 20;
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -249,6 +250,77 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
     x[r] = acc / d[r];
 }
 
+// Sync-free (dataflow) form of the same solve, one launch per triangle: x is
+// pre-filled with the sentinel and a row's value is its own ready flag.  Rows
+// are taken in level order (lev_rows), a wave 64 consecutive ones, the
+// co-resident grid striding over the list; a lane loads all its sources with
+// agent-scope loads, and if none is the sentinel finishes the row with the
+// same operations as k_trsv_level (canonical order, then / d[r]) and stores it
+// with an agent-scope store; otherwise it retries inside a wave-uniform loop
+// (sources of one wave's rows may be other lanes of the wave).  The smallest
+// unfinished row in level order always has its sources done, so the grid
+// drains; spins are bounded (err bit 0).
+__global__ void k_fill_gated(Gate g, unsigned long long *p, long long n, unsigned long long v)
+{
+    if (gated(g)) return;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int n, const int *__restrict__ rows,
+                                                      const int *__restrict__ rp, const int *__restrict__ ci,
+                                                      const double *__restrict__ v,
+                                                      const double *__restrict__ d,
+                                                      const double *__restrict__ b, double *x, int *err)
+{
+    if (gated(g)) return;
+    const int lane = threadIdx.x & 63;
+    const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
+    unsigned long long *xu = reinterpret_cast<unsigned long long *>(x);
+    for (long long base = wid * 64; base < n; base += nw * 64) {
+        const long long idx = base + lane;
+        const int r = idx < n ? rows[idx] : -1;
+        bool pending = r >= 0;
+        int k = pending ? rp[r] : 0;
+        const int k1 = pending ? rp[r + 1] : 0;
+        double acc = pending ? b[r] : 0.0;
+        const double dr = pending ? d[r] : 1.0;
+        int spins = 0;
+        while (__any(pending)) {
+            if (pending) {
+                // consume the sources in canonical order as far as they are
+                // ready (one outstanding poll per waiting lane); a source
+                // once seen stays final, so acc is built incrementally
+                bool stop = false;
+                while (!stop && k < k1) {
+                    unsigned long long u[4];            // up to 4 polls in flight
+#pragma unroll
+                    for (int j = 0; j < 4; j++) u[j] = k + j < k1 ? ld_agent(xu + ci[k + j]) : 0ull;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        if (stop || k >= k1) break;
+                        if (u[j] == kSentinel) { stop = true; break; }
+                        acc = acc - v[k] * __longlong_as_double((long long)u[j]);
+                        k++;
+                    }
+                }
+                if (k == k1) {
+                    st_agent(xu + r, (unsigned long long)__double_as_longlong(acc / dr));
+                    pending = false;
+                }
+            }
+            if (__any(pending)) {
+                __builtin_amdgcn_s_sleep(4);
+                if (++spins > kSpinLimit) {
+                    if (pending) atomicOr(err, 1);
+                    pending = false;
+                }
+            }
+        }
+    }
+}
+
 // 2D structured-grid wavefront solve.  Layout (gg_internal.h Wave2D): band =
 // 64 grid lines, lane l = line 64*band+l, step t = column i + l; a lane's two
 // consecutive steps are adjacent in memory (16 B per array per step pair, 1 KiB
@@ -316,7 +388,6 @@ constexpr int kWaveLook = GG_WAVE_LOOK;
 #define GG_WAVE_SHADOW 1
 #endif
 constexpr bool kWaveShadow = GG_WAVE_SHADOW != 0;
-constexpr int kSpinLimit = 1 << 20;
 // Ring depth: batches j and j+1 are in LDS at barrier j and kWaveRing-3 more are
 // in flight (enough to cover the HBM latency at this stream rate).
 #ifndef GG_WAVE_RING
@@ -1265,6 +1336,14 @@ void launch_gather_ports(int nport, const int *port, const double *x, double *ou
     if (nport > 0) k_gather_ports<<<(nport + kBlock - 1) / kBlock, kBlock, 0, st>>>(nport, port, x, out);
 }
 
+int trsv_flow_max_blocks()
+{
+    int dev = 0, per = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_trsv_flow, kBlock, 0) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return per * cus;
+}
 int ilu0_columns_max_blocks()
 {
     int dev = 0, per = 0, cus = 0;
@@ -1335,6 +1414,29 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
 {
     if (T.kind == DevTri::LEVEL) {
         const int nlev = (int)T.lev_ptr.size() - 1;
+        static const int flow_blocks = trsv_flow_max_blocks();
+        const char *lv = getenv("GG_TRSV_LEVELS");         // 1: one launch per level
+        const bool per_level = lv && atoi(lv) != 0;
+        const int nrows = T.lev_ptr[nlev];
+        if (!per_level && b != x && flow_blocks > 0 && nlev > 1 && nrows > 0) {
+            // few resident waves: every waiting lane polls, so the grid is
+            // capped at GG_FLOW_BPC blocks per CU (default 1)
+            static const int cus = [] {
+                int dev = 0, c = 0;
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+                return c;
+            }();
+            const char *bpc_s = getenv("GG_FLOW_BPC");
+            const int bpc = bpc_s ? std::max(1, atoi(bpc_s)) : 1;
+            const long long need = ((long long)nrows + kBlock - 1) / kBlock;
+            const int blocks = (int)std::min<long long>(std::min(flow_blocks, bpc * std::max(cus, 1)), need);
+            k_fill_gated<<<blocks_for(nrows, kBlock, 8192), kBlock, 0, st>>>(
+                g, reinterpret_cast<unsigned long long *>(x), nrows, kSentinel);
+            k_trsv_flow<<<blocks, kBlock, 0, st>>>(g, nrows, T.lev_rows.p, T.off.rp.p, T.off.ci.p, T.off.v.p,
+                                                   T.d.p, b, x, err);
+            return;
+        }
         for (int l = 0; l < nlev; l++) {
             const int cnt = T.lev_ptr[l + 1] - T.lev_ptr[l];
             if (cnt == 0) continue;

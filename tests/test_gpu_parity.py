@@ -76,10 +76,14 @@ def test_spmv_long_rows(solver):
 
 
 @pytest.mark.parametrize("name", sorted(MATS))
-@pytest.mark.parametrize("force_level", [False, True])
+@pytest.mark.parametrize("force_level", [False, True, "per_level"])
 def test_ilu0_apply_bitexact(solver, name, force_level, monkeypatch):
+    """wavefront kernel where it applies; force_level: the dataflow level kernel
+    (k_trsv_flow); "per_level": one k_trsv_level launch per level"""
     if force_level:
         monkeypatch.setenv("GG_NO_WAVEFRONT", "1")
+    if force_level == "per_level":
+        monkeypatch.setenv("GG_TRSV_LEVELS", "1")
     A = MATS[name]()
     L, U = O.ilu0(A)
     y = np.random.default_rng(2).standard_normal(A.shape[0])
