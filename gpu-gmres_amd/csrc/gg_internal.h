@@ -86,16 +86,23 @@ Levels level_sets(const CanonTri &T);
 //   T = nx + 63 rounded up to a multiple of 64 (four 16-step kernel batches)
 struct Wave2D {
     bool ok = false;
-    int nx = 0, ny = 0, nbands = 0, T = 0;
-    long long P = 0;         // padded layout length
-    long long slot(int r) const {
-        int j = r / nx, i = r % nx, l = j & 63, t = i + l;
-        return (((long long)(j >> 6) * (T / 2) + t / 2) * 64 + l) * 2 + (t & 1);
+    int nx = 0, ny = 0, nz = 1, nbands = 0, T = 0;
+    long long P2 = 0;        // one plane's layout length (nbands * T * 64)
+    long long P = 0;         // padded layout length (nz * P2)
+    long long ngran() const { return (long long)nz * nbands * T; }   // hand-off granules
+    long long slot(long long r) const {
+        const long long nxy = (long long)nx * ny;
+        const long long k = r / nxy, q = r % nxy;
+        const int j = (int)(q / nx), i = (int)(q % nx), l = j & 63, t = i + l;
+        return k * P2 + ((((long long)(j >> 6) * (T / 2) + t / 2) * 64 + l) * 2 + (t & 1));
     }
 };
 // detect: L off-diagonals only at offsets {nx (first), 1 (second)} and U only at
 // {nx (first), 1 (second)}, no wrap-around entries.  Returns ok=false otherwise.
 Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U);
+// 3D: offsets {nx*ny, nx, 1} in this order in L and in U (canonical orders),
+// no wrap-around; nz >= 2 planes of the 2D layout
+Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U);
 
 // SpMV row blocks: each block <= 256 rows and <= kSpmvCap nnz (CSR-stream)
 constexpr int kSpmvCap = 2048;
@@ -160,6 +167,8 @@ struct DevTri {
     // WAVE2D (layout arrays, length P)
     Wave2D wl;
     DBuf<double> c1, c2, dw, rw; // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor, rw: RN(1/dw)
+    DBuf<double> c0;             // 3D: |offset| = nx*ny coefficient
+    DBuf<unsigned long long> prog;   // 3D: per (plane, band) batches stored (0 between launches)
     int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
     bool rcp_ok = false;         // every divisor admits WD_RCP
     DBuf<unsigned long long> bnd;  // nbands * T hand-off granules (sentinel = not ready) + 128 dummies

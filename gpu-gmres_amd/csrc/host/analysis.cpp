@@ -144,7 +144,52 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
     w.ny = n / nx;
     w.nbands = (w.ny + 63) / 64;
     w.T = (nx + 63 + 63) / 64 * 64;   // whole 16-step batches, batch count a multiple of 4
-    w.P = (long long)w.nbands * w.T * 64;
+    w.P2 = (long long)w.nbands * w.T * 64;
+    w.P = w.P2;
+    return w;
+}
+
+Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U)
+{
+    Wave2D w;
+    const int n = L.off.n;
+    if (n < 128 || U.off.n != n) return w;
+    long long nxy = 0;
+    for (int r = 0; r < n; r++)
+        for (int k = L.off.rp[r]; k < L.off.rp[r + 1]; k++) nxy = std::max<long long>(nxy, r - L.off.ci[k]);
+    long long nx = 0;
+    for (int r = 0; r < n; r++)
+        for (int k = L.off.rp[r]; k < L.off.rp[r + 1]; k++) {
+            const long long o = r - L.off.ci[k];
+            if (o < nxy) nx = std::max(nx, o);
+        }
+    if (nx < 2 || nxy <= nx || nxy % nx != 0 || nxy / nx < 2 || n % nxy != 0 || n / nxy < 2) return w;
+    // L rows: [r-nxy][r-nx][r-1] in this order (each may be absent), no wrap
+    for (int r = 0; r < n; r++) {
+        int k = L.off.rp[r];
+        const int ub = L.off.rp[r + 1];
+        if (k < ub && L.off.ci[k] == r - nxy) k++;
+        if (k < ub && L.off.ci[k] == r - nx && (r % nxy) >= nx) k++;
+        if (k < ub && L.off.ci[k] == r - 1 && (r % nx) != 0) k++;
+        if (k != ub) return w;
+    }
+    // U rows (LUSolve_ignoreZero walks from the row end): [r+nxy][r+nx][r+1]
+    for (int r = 0; r < n; r++) {
+        int k = U.off.rp[r];
+        const int ub = U.off.rp[r + 1];
+        if (k < ub && U.off.ci[k] == r + nxy) k++;
+        if (k < ub && U.off.ci[k] == r + nx && (r % nxy) + nx < nxy) k++;
+        if (k < ub && U.off.ci[k] == r + 1 && (r % nx) != nx - 1) k++;
+        if (k != ub) return w;
+    }
+    w.ok = true;
+    w.nx = (int)nx;
+    w.ny = (int)(nxy / nx);
+    w.nz = (int)(n / nxy);
+    w.nbands = (w.ny + 63) / 64;
+    w.T = (w.nx + 63 + 63) / 64 * 64;
+    w.P2 = (long long)w.nbands * w.T * 64;
+    w.P = w.P2 * w.nz;
     return w;
 }
 

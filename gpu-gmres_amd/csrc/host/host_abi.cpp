@@ -80,6 +80,21 @@ int gg_host_wave2d(int n, const int *l_rp, const int *l_ci, const double *l_v, c
     }
 }
 
+int gg_host_wave3d(int n, const int *l_rp, const int *l_ci, const double *l_v, const int *u_rp,
+                   const int *u_ci, const double *u_v, int *nx, int *ny, int *nz)
+{
+    try {
+        Wave2D w = detect_wave3d(canon_lower_unit(wrap(n, l_rp, l_ci, l_v)),
+                                 canon_upper_ignorezero(wrap(n, u_rp, u_ci, u_v)));
+        if (nx) *nx = w.nx;
+        if (ny) *ny = w.ny;
+        if (nz) *nz = w.nz;
+        return w.ok ? 1 : 0;
+    } catch (...) {
+        return GG_EINVAL;
+    }
+}
+
 int gg_host_partition(int n, const int *rp, const int *ci, int nparts, int method, int *node_part,
                       int *part_size, int *pinv, int *q)
 {

@@ -75,6 +75,16 @@ __device__ __forceinline__ void st_agent(unsigned long long *p, unsigned long lo
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// 16 bytes stored write-through (two agent-scope 8-byte stores, sc1): visible
+// to other XCDs once drained.  (Not inline asm: the compiler does not guard an
+// asm store's data registers against the VALU write hazard that follows it.)
+__device__ __forceinline__ void st_sc1_16(double2 *p, double2 v)
+{
+    unsigned long long *q = reinterpret_cast<unsigned long long *>(p);
+    __hip_atomic_store(q, (unsigned long long)__double_as_longlong(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (unsigned long long)__double_as_longlong(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ============================================================== vector ops
 __global__ void k_fill_u64(unsigned long long *p, long long n, unsigned long long v)
 {
@@ -402,12 +412,17 @@ constexpr int kWaveRing = GG_WAVE_RING;
 #endif
 constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 
-template <int DIV>
+template <int DIV, bool D3 = false>
 struct WaveCfg {
-    static constexpr int A = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;   // streamed arrays
-    static constexpr int B = DIV == WD_UNIT ? GG_WAVE_BATCH_UNIT
-                           : DIV == WD_HW   ? GG_WAVE_BATCH_HW
-                                            : GG_WAVE_BATCH_RCP;       // steps per batch
+    // streamed arrays: b, c1, c2 (, d (, RN(1/d))); a 3D grid adds the plane
+    // coefficient c0 and the previous plane's x
+    static constexpr int A2 = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;
+    static constexpr int A = A2 + (D3 ? 2 : 0);
+    static constexpr int B16 = DIV == WD_UNIT ? GG_WAVE_BATCH_UNIT
+                             : DIV == WD_HW   ? GG_WAVE_BATCH_HW
+                                              : GG_WAVE_BATCH_RCP;
+    // steps per batch: 8 where 16-step slots of A arrays would not leave room for 3 slots
+    static constexpr int B = (B16 == 16 && 3 * A * 8 * 64 + 64 + 2 * 8 * 64 > 150 * 1024 / 16) ? 8 : B16;
     static constexpr int PBN = B / 2;                                     // step pairs per batch
     static constexpr int SLOT = A * PBN * 64;                            // double2 per ring slot
     static constexpr int LOADERS = kWaveLoaders == 1 ? 1 : A;           // loader waves
@@ -421,6 +436,7 @@ struct WaveCfg {
     static constexpr int LDS2 = R * SLOT + 64 + 2 * PBN * 64;            // ring, boundary, x staging
     static_assert(R >= 3 && (R - 2) * NPER <= 63, "ring depth vs vmcnt range");
     static_assert(B == 8 || B == 16, "batch");
+    static_assert(!D3 || LOADERS == 1, "3D grids stream every array from one loader wave");
     static_assert(kWaveLook >= 1 && kWaveLook <= PBN, "lookahead");
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
 };
@@ -469,14 +485,17 @@ __device__ __forceinline__ bool rcp_safe(double v)
 }
 
 // loader wave: batch j -> ring slot j % R; batch j landed by barrier j
-template <bool FWD, int R, int SLOT, int NA, int PBN>
+template <bool FWD, int R, int SLOT, int NA, int PBN, int SC1 = -1>
 __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *lds, int np, int nbatch)
 {
+    // array SC1 (a 3D grid's previous-plane x, written by another workgroup in
+    // this launch) is read write-through coherent (sc1: cache policy 16)
     constexpr int PB = PBN * 64;                // double2 per array per slot
     auto issue = [&](int j) {
         double2 *slot = lds + (j % R) * SLOT;
 #pragma unroll
-        for (int a = 0; a < NA; a++)
+        for (int a = 0; a < NA; a++) {
+            if (a == SC1) continue;
 #pragma unroll
             for (int kk = 0; kk < PBN; kk++) {
                 const int p = j * PBN + kk;
@@ -484,6 +503,16 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
                 __builtin_amdgcn_global_load_lds((gbl_void_t *)(src[a] + q),
                                                  (lds_void_t *)(slot + a * PB + kk * 64), 16, 0, 0);
             }
+        }
+        if constexpr (SC1 >= 0) {
+#pragma unroll
+            for (int kk = 0; kk < PBN; kk++) {
+                const int p = j * PBN + kk;
+                const long long q = (long long)(FWD ? p : np - 1 - p) * 64;
+                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src[SC1] + q),
+                                                 (lds_void_t *)(slot + SC1 * PB + kk * 64), 16, 0, 16);
+            }
+        }
     };
     for (int j = 0; j < R - 1 && j < nbatch; j++) issue(j);
     for (int j = 0; j < nbatch; j++) {
@@ -495,57 +524,100 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
     }
 }
 
-template <bool FWD, int DIV, bool TRACE>
-__global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
+template <bool FWD, int DIV, bool TRACE, bool D3 = false>
+__global__ __launch_bounds__((WaveCfg<DIV, D3>::THREADS)) void k_trsv_wave2d(
     Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
     const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
-    double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace)
+    double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace,
+    int nz, long long P2, const double *__restrict__ c0, unsigned long long *prog)
 {
-    using C = WaveCfg<DIV>;
+    using C = WaveCfg<DIV, D3>;
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
+    static_assert(!(D3 && TRACE), "no trace for 3D grids");
     if (gated(g)) return;
     // one LDS object: data ring [R][A][C::PBN][64] double2, 2 x 64 boundary values
     // (lanes 0..C::B-1 of each half are used), x staging [2][C::PBN][64]
     __shared__ double2 lds[C::LDS2];
     double *bring = reinterpret_cast<double *>(lds + C::R * C::SLOT);
     double2 *xbuf = lds + C::R * C::SLOT + 64;
-    const int band = FWD ? blockIdx.x : (nbands - 1 - blockIdx.x);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int np = T / 2;                       // step pairs per band
     const int nbatch = T / C::B;          // T is a multiple of 8 * C::B
+    constexpr int plane = FWD ? 63 : 0;     // lane whose values the next band needs
+    // Tasks: (plane, band) in dependency order, a workgroup takes every
+    // gridDim.x-th (2D: one band per workgroup, nz = 1).  A 3D task also needs
+    // the previous plane's x (same band): its writer publishes prog[] =
+    // batches stored, the boundary wave polls it, the loader streams it.
+    const int ntask = nz * nbands;
+    for (int task = blockIdx.x; task < ntask; task += gridDim.x) {
+    const int kq = task / nbands, bq = task % nbands;
+    const int band = FWD ? bq : (nbands - 1 - bq);
+    const int kp = FWD ? kq : (nz - 1 - kq);    // plane
     const bool has_src = FWD ? (band > 0) : (band < nbands - 1);
     const bool is_prod = FWD ? (band < nbands - 1) : (band > 0);
-    const long long boff = (long long)band * np * 64 + lane;    // double2 units
-
-    constexpr int plane = FWD ? 63 : 0;     // lane whose values the next band needs
-    unsigned long long *pub = bnd + (long long)band * T;
+    const bool has_prev = D3 && (FWD ? kp > 0 : kp < nz - 1);
+    const long long boff = (long long)band * np * 64 + lane + (long long)kp * (P2 / 2);   // double2 units
+    const long long prev_off = (FWD ? -1 : 1) * (P2 / 2);                                // previous plane
+    unsigned long long *pub = bnd + ((long long)kp * nbands + band) * T;
+    unsigned long long *prog_mine = D3 ? prog + (long long)kp * nbands + band : nullptr;
+    unsigned long long *prog_prev = has_prev ? prog + (long long)(FWD ? kp - 1 : kp + 1) * nbands + band : nullptr;
     if (wave >= 3) {
         // ------------------------------------------------ loader wave(s)
-        const double2 *src[5] = {reinterpret_cast<const double2 *>(b) + boff,
+        const double2 *src[7] = {reinterpret_cast<const double2 *>(b) + boff,
                                  reinterpret_cast<const double2 *>(c1) + boff,
                                  reinterpret_cast<const double2 *>(c2) + boff,
                                  reinterpret_cast<const double2 *>(dv) + boff,
-                                 reinterpret_cast<const double2 *>(rv) + boff};
+                                 reinterpret_cast<const double2 *>(rv) + boff,
+                                 nullptr, nullptr};
+        if constexpr (D3) {
+            // the plane coefficient and the previous plane's x (zeros on the
+            // first plane, where c0 is 0) follow the 2D arrays
+            src[C::A2] = reinterpret_cast<const double2 *>(c0) + boff;
+            src[C::A2 + 1] = reinterpret_cast<const double2 *>(has_prev ? x : c0) + boff + (has_prev ? prev_off : 0);
+        }
+        if constexpr (D3) {
+            // the prologue streams batches 0..R-2 before the boundary wave has
+            // checked anything: wait here for the previous plane to store them
+            // (no DMA is in flight yet, so a blocking poll is free)
+            if (has_prev) {
+                const unsigned long long need = (unsigned long long)(C::R - 1 < nbatch ? C::R - 1 : nbatch);
+                int spins = 0;
+                while (ld_agent(prog_prev) < need) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > kSpinLimit) {
+                        if (lane == 0) atomicOr(err, 1);
+                        break;
+                    }
+                }
+            }
+        }
         if constexpr (C::LOADERS == 1) {
-            wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN>(src, lds, np, nbatch);
+            wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN, D3 ? C::A2 + 1 : -1>(src, lds, np, nbatch);
         } else {
             wave_loader<FWD, C::R, C::SLOT, 1, C::PBN>(src + (wave - 3), lds + (wave - 3) * PB, np, nbatch);
         }
         raw_barrier();                      // final barrier (the writer drains the last batch)
-        return;
+        continue;
     }
     if (wave == 2) {
         // ------------------------------------------------ writer wave
         // After barrier bi+1 the compute wave's x of batch bi sits in xbuf[bi & 1]:
         // store it to HBM and publish the edge lane's values of the batch as
         // hand-off granules (lanes 0..C::B-1, one coalesced sc1 store).
+        // 3D: x is stored write-through (sc1) and, once a batch's stores have
+        // drained (checked one batch later, off the critical path), counted in
+        // prog_mine for the next plane.
         double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
         [[maybe_unused]] bool bad = false;  // WD_RCP range guard (see rcp_safe)
         for (int bi = 0; bi <= nbatch; bi++) {
             raw_barrier();
             if (bi == 0) continue;
             const int pb = bi - 1;
+            if constexpr (D3) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // batches < pb stored
+                if (lane == 0 && pb > 0) st_agent(prog_mine, (unsigned long long)pb);
+            }
             const double2 *xb = xbuf + (pb & 1) * PB;
             // the hand-off granules first: they are on the critical path, x is not
             const int tt = lane & (C::B - 1);
@@ -561,17 +633,26 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
 #pragma unroll
             for (int kk = 0; kk < C::PBN; kk++) {
                 const int p = pb * C::PBN + kk;
-                X2[(long long)(FWD ? p : np - 1 - p) * 64] = v[kk];
+                double2 *dst = X2 + (long long)(FWD ? p : np - 1 - p) * 64;
+                if constexpr (D3) {
+                    st_sc1_16(dst, v[kk]);
+                } else {
+                    *dst = v[kk];
+                }
                 if constexpr (DIV == WD_RCP) bad |= !rcp_safe(v[kk].x) || !rcp_safe(v[kk].y);
             }
             if (TRACE && lane == 0)
                 trace[(long long)band * (3 * nbatch + 8) + nbatch + 8 + pb] =
                     (long long)__builtin_amdgcn_s_memrealtime();
         }
+        if constexpr (D3) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) st_agent(prog_mine, (unsigned long long)nbatch);
+        }
         if constexpr (DIV == WD_RCP) {
             if (__any(bad) && lane == 0) atomicOr(err, 2);
         }
-        return;
+        continue;
     }
     if (wave == 1) {
         // ------------------------------------------------ boundary wave
@@ -584,14 +665,29 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
         // the dummy granules after the bands: 64 zeros to read, 64 to write),
         // which keeps the vmcnt arithmetic exact.
         constexpr int kPoll = GG_WAVE_POLL;
-        unsigned long long *src = bnd + (long long)(FWD ? band - 1 : band + 1) * T;
-        unsigned long long *dummy_ld = bnd + (long long)nbands * T + lane;
+        // 3D: lane 32 polls the previous plane's progress instead: before
+        // barrier bi it must have stored the batches the loader streams after
+        // it (up to bi + R - 1); its word is never re-armed here, but reset to
+        // 0 when this task is done (the producer has finished by then).
+        unsigned long long *src = bnd + ((long long)kp * nbands + (FWD ? band - 1 : band + 1)) * T;
+        unsigned long long *dummy_ld = bnd + (long long)nz * nbands * T + lane;
         unsigned long long *dummy_st = dummy_ld + 64;
+        constexpr int kProgLane = 32;
+        const bool prog_lane = has_prev && lane == kProgLane;
         auto gaddr = [&](int bj) {
             const int t = FWD ? bj * C::B + lane : (T - 1) - (bj * C::B + lane);
             const int gi = FWD ? t + 63 : t - 63;
             const bool need = has_src && lane < C::B && bj < nbatch && gi >= 0 && gi < T;
             return need ? src + gi : (unsigned long long *)nullptr;
+        };
+        auto poll_addr = [&](int bj) -> unsigned long long * {
+            if (prog_lane) return prog_prev;
+            unsigned long long *ga = gaddr(bj);
+            return ga ? ga : dummy_ld;
+        };
+        auto ready = [&](unsigned long long w, int bj) {
+            if (prog_lane) return w >= (unsigned long long)(bj + C::R < nbatch ? bj + C::R : nbatch);
+            return w != kSentinel;
         };
         // the prologue mirrors the steady-state issue order (re-arm store, poll)
         // so the same vmcnt holds in every iteration
@@ -599,8 +695,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
 #pragma unroll
         for (int u = 0; u < kPoll; u++) {
             if (u > 0) st_agent(dummy_st, kSentinel);
-            unsigned long long *ga = gaddr(u);
-            v[u] = ld_agent(ga ? ga : dummy_ld);
+            v[u] = ld_agent(poll_addr(u));
         }
         bool dead = false;
         long long bw_spins = 0, bw_cyc = 0;     // TRACE: poll retries, cycles in retry loops
@@ -613,9 +708,9 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 __builtin_amdgcn_s_waitcnt(vm_wait(2 * (kPoll - 1)));
                 int spins = 0;
                 const long long tw = TRACE ? (long long)__builtin_amdgcn_s_memtime() : 0;
-                while (!dead && !__all(v[u] != kSentinel)) {
+                while (!dead && !__all(ready(v[u], bi))) {
                     __builtin_amdgcn_s_sleep(1);
-                    v[u] = ld_agent(ga ? ga : dummy_ld);
+                    v[u] = ld_agent(poll_addr(bi));
                     if (++spins > kSpinLimit) {
                         dead = true;
                         if (lane == 0) atomicOr(err, 1);
@@ -631,8 +726,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 }
                 bring[(bi & 1) * 64 + lane] = __longlong_as_double((long long)v[u]);
                 st_agent(ga ? ga : dummy_st, kSentinel);       // re-arm for the next launch
-                unsigned long long *gn = gaddr(bi + kPoll);
-                v[u] = ld_agent(gn ? gn : dummy_ld);
+                v[u] = ld_agent(poll_addr(bi + kPoll));
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 raw_barrier();
             }
@@ -643,7 +737,11 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
             trb[nbatch + 5] = bw_spins;
             trb[nbatch + 6] = bw_cyc;
         }
-        return;
+        if (prog_lane) {
+            __builtin_amdgcn_s_waitcnt(vm_wait(0));
+            st_agent(prog_prev, 0ull);              // re-arm for the next launch
+        }
+        continue;
     }
 
     // ---------------------------------------------------- compute wave
@@ -703,6 +801,14 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                 const double e2 = sx ? rg[kk][2].x : rg[kk][2].y;
                 const double old = h ? bv[kk].y : bv[kk].x;
                 const double p2 = e2 * xp;
+                // 3D: the plane neighbour comes first in the canonical order
+                // (|offset| = nx*ny); its term is off the recurrence
+                double bz = bb;
+                if constexpr (D3) {
+                    const double e0 = sx ? rg[kk][C::A2].x : rg[kk][C::A2].y;
+                    const double xz = sx ? rg[kk][C::A2 + 1].x : rg[kk][C::A2 + 1].y;
+                    bz = bb - e0 * xz;
+                }
                 const double xs = dpp_shift_old<ctrl>(xp, old);
                 if constexpr (kWaveShadow) {
                     // LDS work of the pair in the cross-lane shift's latency:
@@ -720,7 +826,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                double acc = bb - e1 * xs;      // line neighbour first (|offset| = nx)
+                double acc = bz - e1 * xs;      // line neighbour next (|offset| = nx)
                 acc = acc - p2;                 // then the in-line neighbour (|offset| = 1)
                 if constexpr (DIV == WD_HW) {
                     acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
@@ -765,6 +871,7 @@ __global__ __launch_bounds__(WaveCfg<DIV>::THREADS) void k_trsv_wave2d(
 #pragma unroll
         for (int k = 0; k < 4; k++) tr[nbatch + 1 + k] = ph[k];
     }
+    }   // task loop
 }
 
 // ================================================ ILU(0) factorization (device)
@@ -1405,8 +1512,26 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
         k_spmv_stream<false><<<A.nblk, kBlock, 0, st>>>(g, A.blk.p, A.rp.p, A.ci.p, A.v.p, x, b, y);
 }
 
-int wave_batch_steps(int div)
+template <bool FWD, int DIV>
+int wave3d_max_blocks()
 {
+    static int cached = -1;
+    if (cached < 0) {
+        int dev = 0, per = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_trsv_wave2d<FWD, DIV, false, true>,
+                                                         WaveCfg<DIV, true>::THREADS, 0) != hipSuccess)
+            per = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        cached = std::max(1, per * cus);
+    }
+    return cached;
+}
+
+int wave_batch_steps(int div, bool d3)
+{
+    if (d3) return div == WD_UNIT ? WaveCfg<WD_UNIT, true>::B : div == WD_HW ? WaveCfg<WD_HW, true>::B
+                                                                              : WaveCfg<WD_RCP, true>::B;
     return div == WD_UNIT ? WaveCfg<WD_UNIT>::B : div == WD_HW ? WaveCfg<WD_HW>::B : WaveCfg<WD_RCP>::B;
 }
 
@@ -1445,28 +1570,52 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         }
     } else if (T.kind == DevTri::WAVE2D) {
         const Wave2D &w = T.wl;
-        dim3 grid(w.nbands);
         const double *dv = T.div == WD_UNIT ? nullptr : T.dw.p;
         const double *rv = T.div == WD_RCP ? T.rw.p : nullptr;
-#define GG_WAVE_LAUNCH(FWD, DIV)                                                             \
-    do {                                                                                     \
-        if (T.trace)                                                                         \
-            k_trsv_wave2d<FWD, DIV, true><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(           \
-                g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, T.trace);      \
-        else                                                                                 \
-            k_trsv_wave2d<FWD, DIV, false><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(          \
-                g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr);      \
+        if (w.nz == 1) {
+            dim3 grid(w.nbands);
+#define GG_WAVE_LAUNCH(FWD, DIV)                                                                   \
+    do {                                                                                           \
+        if (T.trace)                                                                               \
+            k_trsv_wave2d<FWD, DIV, true><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                 \
+                g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, T.trace, 1, w.P2,     \
+                nullptr, nullptr);                                                                 \
+        else                                                                                       \
+            k_trsv_wave2d<FWD, DIV, false><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                \
+                g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2,     \
+                nullptr, nullptr);                                                                 \
     } while (0)
-        if (T.lower) {
-            if (T.div == WD_UNIT) GG_WAVE_LAUNCH(true, WD_UNIT);
-            else if (T.div == WD_HW) GG_WAVE_LAUNCH(true, WD_HW);
-            else GG_WAVE_LAUNCH(true, WD_RCP);
-        } else {
-            if (T.div == WD_UNIT) GG_WAVE_LAUNCH(false, WD_UNIT);
-            else if (T.div == WD_HW) GG_WAVE_LAUNCH(false, WD_HW);
-            else GG_WAVE_LAUNCH(false, WD_RCP);
-        }
+            if (T.lower) {
+                if (T.div == WD_UNIT) GG_WAVE_LAUNCH(true, WD_UNIT);
+                else if (T.div == WD_HW) GG_WAVE_LAUNCH(true, WD_HW);
+                else GG_WAVE_LAUNCH(true, WD_RCP);
+            } else {
+                if (T.div == WD_UNIT) GG_WAVE_LAUNCH(false, WD_UNIT);
+                else if (T.div == WD_HW) GG_WAVE_LAUNCH(false, WD_HW);
+                else GG_WAVE_LAUNCH(false, WD_RCP);
+            }
 #undef GG_WAVE_LAUNCH
+        } else {
+            // 3D: persistent, every workgroup co-resident (tasks wait on tasks)
+            const int ntask = w.nz * w.nbands;
+#define GG_WAVE_LAUNCH3(FWD, DIV)                                                                  \
+    do {                                                                                           \
+        const int grid = std::min(ntask, wave3d_max_blocks<FWD, DIV>());                           \
+        k_trsv_wave2d<FWD, DIV, false, true><<<grid, WaveCfg<DIV, true>::THREADS, 0, st>>>(        \
+            g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, w.nz, w.P2,      \
+            T.c0.p, T.prog.p);                                                                     \
+    } while (0)
+            if (T.lower) {
+                if (T.div == WD_UNIT) GG_WAVE_LAUNCH3(true, WD_UNIT);
+                else if (T.div == WD_HW) GG_WAVE_LAUNCH3(true, WD_HW);
+                else GG_WAVE_LAUNCH3(true, WD_RCP);
+            } else {
+                if (T.div == WD_UNIT) GG_WAVE_LAUNCH3(false, WD_UNIT);
+                else if (T.div == WD_HW) GG_WAVE_LAUNCH3(false, WD_HW);
+                else GG_WAVE_LAUNCH3(false, WD_RCP);
+            }
+#undef GG_WAVE_LAUNCH3
+        }
     }
 }
 

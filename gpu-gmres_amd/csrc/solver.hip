@@ -62,14 +62,18 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
     if (wl && wl->ok) {
         T.kind = DevTri::WAVE2D;
         T.wl = *wl;
+        const bool d3 = wl->nz > 1;
         std::vector<double> c1(Ppad, 0.0), c2(Ppad, 0.0), dv(Ppad, 1.0), rv(Ppad, 1.0);
+        std::vector<double> c0(d3 ? Ppad : 0, 0.0);
         bool unit = true, rcp_ok = true;
         const int nx = wl->nx;
+        const long long nxy = (long long)wl->nx * wl->ny;
         for (int r = 0; r < n; r++) {
             const long long p = (*nat2lay)[r];
             for (int k = C.off.rp[r]; k < C.off.rp[r + 1]; k++) {
-                const int off = std::abs(C.off.ci[k] - r);
-                (off == nx ? c1 : c2)[p] = C.off.v[k];
+                const long long off = std::abs((long long)C.off.ci[k] - r);
+                if (d3 && off == nxy) c0[p] = C.off.v[k];
+                else (off == nx ? c1 : c2)[p] = C.off.v[k];
             }
             const double d = C.d[r];
             dv[p] = d;
@@ -80,6 +84,11 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         }
         T.c1.upload(c1, st);
         T.c2.upload(c2, st);
+        if (d3) {
+            T.c0.upload(c0, st);
+            T.prog.alloc((size_t)wl->nz * wl->nbands);
+            GG_HIP(hipMemsetAsync(T.prog.p, 0, T.prog.n * sizeof(unsigned long long), st));
+        }
         T.rcp_ok = false;
         if (unit) {
             T.div = WD_UNIT;
@@ -92,12 +101,12 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         }
         // one hand-off granule per band and step, then 64 zero granules (dummy
         // reads) and 64 write-only ones (dummy re-arms); kernels.hip k_trsv_wave2d
-        const long long ngran = (long long)wl->nbands * wl->T;
+        const long long ngran = wl->ngran();
         T.bnd.alloc((size_t)ngran + 128);
         launch_fill_u64(T.bnd.p, ngran, kSentinel, st);
         launch_fill_u64(T.bnd.p + ngran, 128, 0ull, st);
         // algorithmic bytes: b, two coefficients, (divisor (, reciprocal)), x per grid point
-        T.bytes = (double)n * (8.0 * (unit ? 4 : T.rcp_ok ? 6 : 5));
+        T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? 2 : 0)));
     } else {
         T.kind = DevTri::LEVEL;
         T.off.upload(C.off, st);
@@ -464,6 +473,13 @@ DevState read_state(gg_solver *s)
     return h;
 }
 
+// re-arm a wavefront triangle's hand-off state (granules, 3D progress words)
+void reset_wave(DevTri *T, hipStream_t st)
+{
+    launch_fill_u64(T->bnd.p, T->wl.ngran(), kSentinel, st);
+    if (T->prog.p) GG_HIP(hipMemsetAsync(T->prog.p, 0, T->prog.n * sizeof(unsigned long long), st));
+}
+
 // Device error word: bit 0 = wavefront boundary wait timed out, bit 1 = a
 // WD_RCP step saw a numerator outside its safe range (repeat with WD_HW).
 struct RcpFallback {};
@@ -507,7 +523,7 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
         GG_HIP(hipMemsetAsync(s->y.p, 0, s->Ppad * sizeof(double), s->st));
     for (DevTri *T : {&s->L, &s->U})
         if (T->kind == DevTri::WAVE2D)
-            launch_fill_u64(T->bnd.p, (long long)T->wl.nbands * T->wl.T, kSentinel, s->st);
+            reset_wave(T, s->st);
     DevState h{};
     h.tol = opt->tol;
     h.max_iter = opt->max_iter;
@@ -703,8 +719,12 @@ static void setup_left(gg_solver *s, const Csr &Lf, const Csr &Uf, int kind)
     CanonTri cu = canon_upper_ignorezero(Uf);
     Wave2D wl;
     const char *env = std::getenv("GG_NO_WAVEFRONT");
-    if (!(env && env[0] == '1')) wl = detect_wave2d(cl, cu);
-    if (wl.ok && wl.nbands > 512) wl.ok = false;   // every band must be co-resident
+    if (!(env && env[0] == '1')) {
+        wl = detect_wave2d(cl, cu);
+        if (wl.ok && wl.nbands > 512) wl.ok = false;   // every band must be co-resident
+        const char *e3 = std::getenv("GG_NO_WAVE3D");
+        if (!wl.ok && !(e3 && e3[0] == '1')) wl = detect_wave3d(cl, cu);
+    }
     setup_space(s, &wl);
     build_tri(s->L, cl, &wl, &s->nat2lay_h, s->Ppad, s->st);
     build_tri(s->U, cu, &wl, &s->nat2lay_h, s->Ppad, s->st);
@@ -988,7 +1008,7 @@ int gg_precond_apply(gg_solver *s, int op, const double *in, double *out)
     ensure_workspace(s, std::max(s->m_alloc, 1));
     for (DevTri *T : {&s->L, &s->U})
         if (T->kind == DevTri::WAVE2D)
-            launch_fill_u64(T->bnd.p, (long long)T->wl.nbands * T->wl.T, kSentinel, s->st);
+            reset_wave(T, s->st);
     stage_in(s, in, s->nat_in);
     launch_gather(s->nat_in.p, s->lay2nat.p, s->xv.p, s->Ppad, s->st);
     auto run = [&]() {
@@ -1111,7 +1131,7 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     GG_REQUIRE(s && out && nbands && nbatch && (which == 0 || which == 1), GG_EINVAL, "bad argument");
     GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner");
     DevTri &T = which == 0 ? s->L : s->U;
-    GG_REQUIRE(T.kind == DevTri::WAVE2D, GG_ESTATE, "wavefront path not active");
+    GG_REQUIRE(T.kind == DevTri::WAVE2D && T.wl.nz == 1, GG_ESTATE, "2D wavefront path not active");
     set_device(s);
     ensure_workspace(s, std::max(s->m_alloc, 1));
     const int nb = T.wl.nbands, nbt = T.wl.T / wave_batch_steps(T.div);

@@ -6,7 +6,8 @@
  * without a device:
  *   gg_host_ilu0   leftILU            src/leftILU.cu:27-336
  *   gg_host_iluk   ilukC + lofC       src/iluk.cpp:56-334
- *   gg_host_wave2d structured-grid detection for the wavefront SpTRSV
+ *   gg_host_wave2d / gg_host_wave3d
+ *                  structured-grid detection for the wavefront SpTRSV
  *                  (replaces cusparseScsrsv_analysis, src/gmres.cu:1516-1517)
  *   gg_host_partition  partition4      src/partition3.cpp:122-194 (METIS is not
  *                  available: recursive BFS bisection or contiguous blocks)
@@ -61,6 +62,11 @@ int gg_host_block(int n, const int *row_ptr, const int *col_idx, const double *v
  * narrows to float).  Returns GG_OK or GG_EINVAL (unreadable / malformed). */
 int gg_host_read_mtx(const char *path, int expand_symmetric, int *nrows, int *ncols,
                      int **row_ptr, int **col_idx, double **val);
+/* the same for a 3D 7-point grid (offsets nx*ny, nx, 1): 1 and the grid
+ * dimensions if the 3D wavefront path applies, else 0 */
+int gg_host_wave3d(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,
+                   const int *u_row_ptr, const int *u_col_idx, const double *u_val,
+                   int *nx, int *ny, int *nz);
 void gg_host_free(void *p);
 
 #ifdef __cplusplus

@@ -43,7 +43,10 @@ MATS = {
     "thermal_7pt_12": lambda: M.grid_7pt(12),
     "powerlaw_3000": lambda: M.power_law(3000, 33000, seed=7),    # C3 stand-in, small
 }
-WAVE = {"c1_5pt_100x100", "5pt_37x64"}
+# wavefront path: 2D grids (line length) and 3D grids (line length, lines per plane)
+GRID = {"c1_5pt_100x100": (100, None), "5pt_37x64": (37, None), "7pt_10x10x10": (10, 10),
+        "thermal_7pt_12": (12, 12), "sherman1": (10, 10)}
+WAVE = set(GRID)
 
 
 @pytest.mark.parametrize("name", sorted(MATS))
@@ -160,10 +163,10 @@ def check_exact(g, o):
     assert np.array_equal(g["x"], o["x"]), rel_err(g["x"], o["x"])
 
 
-def oracle_both(run, n, nx=None):
+def oracle_both(run, n, nx=None, ny=None):
     """run() under serial and under order-matched dot products."""
     o_serial = run()
-    lay, G = device_layout(n, nx)
+    lay, G = device_layout(n, nx, ny)
     O.set_dot_order(lay, G)
     try:
         o_tree = run()
@@ -215,7 +218,7 @@ def test_gmres_left_other_matrices(solver, name):
     b = M.rhs_uniform(A.shape[0])
     L, U = O.ilu0(A)
     o, ot = oracle_both(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=2000, tol=1e-10),
-                        A.shape[0], nx=37 if name in WAVE else None)
+                        A.shape[0], *(GRID[name] if name in GRID else (None, None)))
     solver.set_matrix(A)
     solver.set_precond_ilu0()
     g = solver.solve(b, restart=30, max_iter=2000, tol=1e-10)
@@ -394,3 +397,26 @@ def test_ilu0_device_factor_bitexact(solver, name):
     L, U = O.ilu0(A)
     y = np.random.default_rng(5).standard_normal(A.shape[0])
     assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
+
+
+@pytest.mark.parametrize("dims", [(20, 30, 7), (16, 70, 5), (8, 8, 300), (130, 3, 4)])
+def test_wave3d_apply_and_gmres(solver, dims):
+    """3D 7-point grids on the pipelined (plane, band) wavefront kernel: several
+    bands per plane (16x70), more tasks than co-resident workgroups (8x8x300),
+    several batches per line (130): apply and GMRES bit-exact vs the oracle."""
+    nx, ny, nz = dims
+    A = M.grid_7pt(nx, ny, nz, upwind=0.1)
+    n = A.shape[0]
+    L, U = O.ilu0(A)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert solver.uses_wavefront
+    y = np.random.default_rng(8).standard_normal(n)
+    assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
+    b = M.rhs_uniform(n)
+    # 120 iterations: long enough for several restarts, short enough that the
+    # serial-order history stays within 1e-10 on the slowest case (130x3x4)
+    o, ot = oracle_both(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=120, tol=1e-10), n, nx, ny)
+    g = solver.solve(b, restart=30, max_iter=120, tol=1e-10)
+    check_gmres(g, o)
+    check_exact(g, ot)
