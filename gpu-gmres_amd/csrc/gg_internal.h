@@ -84,6 +84,9 @@ Levels level_sets(const CanonTri &T);
 //   natural row r = j*nx + i, band = j/64, lane l = j%64, step t = i + l:
 //   slot = ((band*(T/2) + t/2)*64 + l)*2 + t%2     (a lane's step pair adjacent)
 //   T = nx + 63 rounded up to a multiple of 64 (four 16-step kernel batches)
+// steps per band are padded to a multiple of this (whole batches, an even
+// number of them for the two-deep boundary polls; kernels.hip checks it)
+constexpr int kWaveTAlign = 32;
 struct Wave2D {
     bool ok = false;
     int nx = 0, ny = 0, nz = 1, nbands = 0, T = 0;

@@ -143,7 +143,7 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
     w.nx = nx;
     w.ny = n / nx;
     w.nbands = (w.ny + 63) / 64;
-    w.T = (nx + 63 + 63) / 64 * 64;   // whole 16-step batches, batch count a multiple of 4
+    w.T = (nx + 63 + kWaveTAlign - 1) / kWaveTAlign * kWaveTAlign;   // the 63-step lane skew
     w.P2 = (long long)w.nbands * w.T * 64;
     w.P = w.P2;
     return w;
@@ -187,7 +187,7 @@ Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U)
     w.ny = (int)(nxy / nx);
     w.nz = (int)(n / nxy);
     w.nbands = (w.ny + 63) / 64;
-    w.T = (w.nx + 63 + 63) / 64 * 64;
+    w.T = (w.nx + 63 + kWaveTAlign - 1) / kWaveTAlign * kWaveTAlign;
     w.P2 = (long long)w.nbands * w.T * 64;
     w.P = w.P2 * w.nz;
     return w;

@@ -436,6 +436,7 @@ struct WaveCfg {
     static constexpr int LDS2 = R * SLOT + 64 + 2 * PBN * 64;            // ring, boundary, x staging
     static_assert(R >= 3 && (R - 2) * NPER <= 63, "ring depth vs vmcnt range");
     static_assert(B == 8 || B == 16, "batch");
+    static_assert(kWaveTAlign % (B * GG_WAVE_POLL) == 0, "batches per band must be a multiple of the poll depth");
     static_assert(!D3 || LOADERS == 1, "3D grids stream every array from one loader wave");
     static_assert(kWaveLook >= 1 && kWaveLook <= PBN, "lookahead");
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
@@ -543,7 +544,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3>::THREADS)) void k_trsv_wave2d(
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int np = T / 2;                       // step pairs per band
-    const int nbatch = T / C::B;          // T is a multiple of 8 * C::B
+    const int nbatch = T / C::B;          // T is a multiple of kWaveTAlign
     constexpr int plane = FWD ? 63 : 0;     // lane whose values the next band needs
     // Tasks: (plane, band) in dependency order, a workgroup takes every
     // gridDim.x-th (2D: one band per workgroup, nz = 1).  A 3D task also needs

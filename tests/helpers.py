@@ -61,7 +61,7 @@ def device_layout(n, nx=None, ny=None):
     """(lay2nat, G) of the solver's vector space: natural order, or -- for a 2D
     grid of line length nx on the wavefront path -- band = j//64, lane l = j%64,
     step t = i + l, slot ((band*T/2 + t//2)*64 + l)*2 + t%2 with
-    T = roundup(nx+63, 64); for a 3D grid (ny given) the planes of that layout
+    T = roundup(nx+63, 32); for a 3D grid (ny given) the planes of that layout
     one after the other; padded to a multiple of 512 slots;
     G = min(1024, ceil(Ppad/2 / 1024)) reduction blocks."""
     if nx is None:
@@ -71,7 +71,7 @@ def device_layout(n, nx=None, ny=None):
         nxy = n if ny is None else nx * ny
         ny = nxy // nx
         nz = n // nxy
-        T = (nx + 63 + 63) // 64 * 64
+        T = (nx + 63 + 31) // 32 * 32
         nb = (ny + 63) // 64
         P2 = nb * T * 64
         P = nz * P2

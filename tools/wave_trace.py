@@ -28,7 +28,7 @@ for which in (0, 1):
         raw = s.trace_precond(which)
     nb = raw.shape[0]
     nbt = (raw.shape[1] - 8) // 3
-    KB = (args.grid + 63 + 63) // 64 * 64 // nbt      # steps per batch
+    KB = (args.grid + 63 + 31) // 32 * 32 // nbt      # steps per batch
     t0 = raw[:, 0].min()
     comp = (raw[:, :nbt + 1] - t0) * 0.01           # us
     ph = raw[:, nbt + 1:nbt + 5].astype(np.float64)
