@@ -14,6 +14,7 @@
  *   gg_host_permute    the arrow permutation P A P^T of the DD solve
  *   gg_host_block      dd_form block extraction  src/form_dd.cpp:32-110
  *   gg_host_read_mtx   readSparseMatrix (Matrix Market)  src_thermal/SpMV_gen.cpp:93-187
+ *   gg_host_coo2csr_in coo2csrDouble_in  src/formatConvert.cpp:165-216
  * Output arrays are malloc'd by the library; release them with gg_host_free.
  */
 #ifndef GGMRES_HOST_H_
@@ -67,6 +68,11 @@ int gg_host_read_mtx(const char *path, int expand_symmetric, int *nrows, int *nc
 int gg_host_wave3d(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,
                    const int *u_row_ptr, const int *u_col_idx, const double *u_val,
                    int *nx, int *ny, int *nz);
+/* coo2csrDouble_in (src/formatConvert.cpp:165-216): COO -> CSR in place;
+ * on return row_idx[0..nrows] holds the row pointers (row_idx needs
+ * max(nz, nrows + 1) slots), entries of a row bubble-sorted by column.
+ * The reference's C++ boundary-feed symbols are in include/compat/format_convert.h. */
+int gg_host_coo2csr_in(int nrows, int nz, double *val, int *row_idx, int *col_idx);
 void gg_host_free(void *p);
 
 #ifdef __cplusplus
