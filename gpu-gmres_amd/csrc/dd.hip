@@ -1,0 +1,789 @@
+// dd.hip -- sharded GMRES(m) + ILU(0) over P GPUs (include/ggmres_dd.h).
+//
+// Shard p's vector space (identical offsets on every shard):
+//   [0, S0)        interior p rows in its own layout (3D/2D wavefront when the
+//                  interior triangles are grid-shaped, else natural), zero padded
+//   [S0, H0)       separator replica, in its own layout
+//   [H0, Pl)       halo: P slots of maxI interface values (slot q = shard q's)
+// Ops run over [0, H0); the dot range is [0, H0) on shard 0 (which counts the
+// separator replica) and [0, S0) on the others, so the all-gathered block
+// partials sum to the global dot, in one fixed order on every shard.
+//
+// Per Arnoldi iteration: pack+all-gather of v_i's interface (SpMV), of the
+// forward solve's interface, and one 8*G-byte all-gather per MGS dot.
+// Everything is enqueued on one stream per process; RCCL collectives run on
+// that stream in between the (gated) kernels, so a whole restart cycle is
+// enqueued with one host read of the control block per cycle, as solver.hip.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+
+#include "ggmres_dd.h"
+#include "kernels.h"
+
+using namespace gg;
+
+#define GG_NCCL(call)                                                                       \
+    do {                                                                                    \
+        ncclResult_t r_ = (call);                                                           \
+        if (r_ != ncclSuccess)                                                              \
+            throw ::gg::Error{GG_ECOMM, std::string(#call) + ": " + ncclGetErrorString(r_)}; \
+    } while (0)
+
+namespace {
+
+struct Shard {
+    int p = 0, nI = 0, nS = 0;
+    Wave2D wI, wS;
+    std::vector<long long> slotI, slotS;    // region-local row -> region slot (host)
+    long long PIr = 0, PSr = 0;             // region slot counts (multiples of 512)
+    DevCsr A, LSH, UIS;
+    DevTri LI, LS, UI, US;
+    DBuf<long long> iface_slot;             // maxI: own interface slots (-1 pad)
+    DBuf<long long> slot2nat;               // H0: natural row of each slot (-1 pad)
+    DBuf<long long> own_slot, own_nat;      // rows this process writes back
+    long long nown = 0;
+    // workspace
+    DBuf<double> V, w, ww, r, rr, bb, t1, t2, xv, bv, partA, partB, H, s, cs, sn, ysm, hist;
+    long long hist_cap = 0;
+    DBuf<DevState> ds;
+    DBuf<int> err;                          // P words (slot p is this shard's)
+    double bytes_spmv = 0, bytes_trsv = 0;
+    std::vector<long long> slot2perm;       // host: slot -> permuted global row (-1 pad), H0
+};
+
+using Get = std::function<double *(Shard &)>;
+
+}  // namespace
+
+struct gg_dd {
+    int device = 0, P = 1, kind = GG_DD_LOCAL, rank = 0;
+    ncclComm_t comm = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool have = false;
+    int n = 0, nsep = 0, maxI = 0;
+    std::vector<int> pinv, q;
+    long long S0 = 0, H0 = 0, Pl = 0;
+    int G = 1;
+    std::vector<std::unique_ptr<Shard>> sh;
+    int m_alloc = -1;
+    std::vector<double> last_hist;
+    DBuf<double> nat_a, nat_b;
+    DBuf<long long> dtmp;
+};
+
+namespace {
+
+int fail(const Error &e)
+{
+    set_error(e.msg);
+    return e.code;
+}
+#define GG_API_BEGIN try {
+#define GG_API_END                                                                          \
+    }                                                                                       \
+    catch (const gg::Error &e) { return fail(e); }                                          \
+    catch (const std::bad_alloc &) { return fail({GG_ENOMEM, "host allocation failed"}); } \
+    catch (const std::exception &e) { return fail({GG_EINVAL, e.what()}); }
+
+void set_dev(gg_dd *d) { GG_HIP(hipSetDevice(d->device)); }
+
+Gate gate_i(Shard &s, int i)
+{
+    Gate g;
+    g.done = &s.ds.p->done;
+    g.mask = ~0;
+    g.nit = &s.ds.p->nit;
+    g.i = i;
+    return g;
+}
+Gate gate_mask(Shard &s, int mask)
+{
+    Gate g;
+    g.done = &s.ds.p->done;
+    g.mask = mask;
+    return g;
+}
+
+// max over all shards of all processes (setup only: host-synchronous)
+long long agree_max(gg_dd *d, long long v)
+{
+    if (d->kind != GG_DD_RCCL || d->P == 1) return v;
+    DBuf<long long> b;
+    b.alloc(1);
+    GG_HIP(hipMemcpyAsync(b.p, &v, sizeof(v), hipMemcpyHostToDevice, d->st));
+    GG_NCCL(ncclAllReduce(b.p, b.p, 1, ncclInt64, ncclMax, d->comm, d->st));
+    GG_HIP(hipMemcpyAsync(&v, b.p, sizeof(v), hipMemcpyDeviceToHost, d->st));
+    GG_HIP(hipStreamSynchronize(d->st));
+    return v;
+}
+
+// all-gather of the slot each shard owns in buf(s) + off: slot q at off + q*cnt
+void exchange(gg_dd *d, const Get &buf, long long off, long long cnt)
+{
+    if (d->P == 1 || cnt == 0) return;
+    if (d->kind == GG_DD_RCCL) {
+        Shard &s = *d->sh[0];
+        double *b = buf(s) + off;
+        GG_NCCL(ncclAllGather(b + (long long)s.p * cnt, b, (size_t)cnt, ncclDouble, d->comm, d->st));
+    } else {
+        ShardPtrs ptr{};
+        for (int q = 0; q < d->P; q++) ptr.p[q] = buf(*d->sh[q]);
+        launch_allgather_local(ptr, d->P, off, cnt, d->st);
+    }
+}
+// own interface values of vector x -> halo slot p, then the all-gather
+void halo(gg_dd *d, const Get &x)
+{
+    if (d->maxI == 0 || d->P == 1) return;
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        double *v = x(s);
+        launch_gather(v, s.iface_slot.p, v + d->H0 + (long long)s.p * d->maxI, d->maxI, d->st);
+    }
+    exchange(d, x, d->H0, d->maxI);
+}
+
+Get vec(DBuf<double> Shard::*m) { return [m](Shard &s) { return (s.*m).p; }; }
+
+// gate of a phase: inner iteration gi (>= 0), else the done-mask (0 = ungated)
+Gate gate_of(Shard &s, int gi, int mask)
+{
+    return gi >= 0 ? gate_i(s, gi) : (mask ? gate_mask(s, mask) : Gate{});
+}
+
+// z = (LU)^-1 y of the arrow-ordered ILU(0), per shard (module comment of host/dd_setup.cpp)
+void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
+{
+    const long long S0 = d->S0;
+    auto gate = [&](Shard &s) { return gate_of(s, gi, mask); };
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        launch_trsv(gate(s), s.LI, in(s), s.t1.p, s.err.p + s.p, d->st);          // y_I
+    }
+    halo(d, vec(&Shard::t1));                                                      // interface y
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        Gate g = gate(s);
+        launch_sub_seq(g, s.LSH, s.t1.p, in(s) + S0, s.t2.p + S0, d->st);         // b_S - L_SI y_I
+        launch_trsv(g, s.LS, s.t2.p + S0, s.t1.p + S0, s.err.p + s.p, d->st);     // y_S
+        launch_trsv(g, s.US, s.t1.p + S0, out(s) + S0, s.err.p + s.p, d->st);     // x_S
+        launch_sub_seq(g, s.UIS, out(s), s.t1.p, s.t2.p, d->st);                  // y_I - U_IS x_S
+        launch_trsv(g, s.UI, s.t2.p, out(s), s.err.p + s.p, d->st);               // x_I
+    }
+}
+
+void spmv(gg_dd *d, int gi, const Get &x, const Get &y)   // y = A x
+{
+    halo(d, x);
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        launch_spmv(gate_of(s, gi, 0), s.A, x(s), nullptr, y(s), false, d->st);
+    }
+}
+void resid(gg_dd *d, int mask)   // rr = b - A x
+{
+    halo(d, vec(&Shard::xv));
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        launch_spmv(gate_of(s, -1, mask), s.A, s.xv.p, s.bv.p, s.rr.p, true, d->st);
+    }
+}
+long long dot_len(gg_dd *d, const Shard &s) { return s.p == 0 ? d->H0 : d->S0; }
+
+// block partials of <a, b> into part slot p, then the all-gather
+void dot(gg_dd *d, int gi, int mask, const Get &a, const Get &b, DBuf<double> Shard::*part)
+{
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        launch_dot(gate_of(s, gi, mask), a(s), b(s), (s.*part).p + (long long)s.p * d->G, d->G, dot_len(d, s), d->st);
+    }
+    exchange(d, vec(part), 0, d->G);
+}
+
+void ensure_workspace(gg_dd *d, int m)
+{
+    if (d->m_alloc == m) return;
+    const long long Pl = d->Pl;
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        s.V.alloc((size_t)(m + 1) * Pl);
+        GG_HIP(hipMemsetAsync(s.V.p, 0, (size_t)(m + 1) * Pl * sizeof(double), d->st));
+        for (DBuf<double> *b : {&s.w, &s.ww, &s.r, &s.rr, &s.bb, &s.t1, &s.t2, &s.xv, &s.bv}) {
+            b->alloc(Pl);
+            GG_HIP(hipMemsetAsync(b->p, 0, Pl * sizeof(double), d->st));
+        }
+        for (DBuf<double> *b : {&s.partA, &s.partB}) {
+            b->alloc((size_t)d->P * d->G);
+            GG_HIP(hipMemsetAsync(b->p, 0, (size_t)d->P * d->G * sizeof(double), d->st));
+        }
+        s.H.alloc((size_t)(m + 1) * m);
+        GG_HIP(hipMemsetAsync(s.H.p, 0, (size_t)(m + 1) * m * sizeof(double), d->st));
+        s.s.alloc(m + 1);
+        s.cs.alloc(m + 1);
+        s.sn.alloc(m + 1);
+        s.ysm.alloc(m + 1);
+        if (!s.ds.p) s.ds.alloc(1);
+        if (!s.err.p) s.err.alloc(d->P);
+    }
+    d->m_alloc = m;
+}
+
+void enqueue_init(gg_dd *d)
+{
+    apply_minv(d, -1, 0, vec(&Shard::bv), vec(&Shard::bb));                    // bb = M b
+    dot(d, -1, 0, vec(&Shard::bb), vec(&Shard::bb), &Shard::partA);
+    for (auto &sp : d->sh) launch_set_normb(sp->partA.p, d->P * d->G, sp->ds.p, d->st);
+    resid(d, 0);                                                                // rr = b - A x
+    apply_minv(d, -1, 0, vec(&Shard::rr), vec(&Shard::r));                     // r = M rr
+    dot(d, -1, 0, vec(&Shard::r), vec(&Shard::r), &Shard::partA);
+    for (auto &sp : d->sh) launch_init_beta(sp->partA.p, d->P * d->G, sp->ds.p, sp->hist.p, d->st);
+}
+
+void enqueue_cycle(gg_dd *d, int m)
+{
+    const long long Pl = d->Pl, H0 = d->H0;
+    const int NP = d->P * d->G;
+    for (auto &sp : d->sh) launch_init_cycle(sp->ds.p, sp->r.p, sp->V.p, sp->s.p, d->G, H0, d->st);
+    for (int i = 0; i < m; i++) {
+        const Get vi = [i, Pl](Shard &s) { return s.V.p + (long long)i * Pl; };
+        spmv(d, i, vi, vec(&Shard::ww));                                        // ww = A v_i
+        apply_minv(d, i, 0, vec(&Shard::ww), vec(&Shard::w));                   // w = M^-1 ww
+        dot(d, i, 0, vec(&Shard::w), [](Shard &s) { return s.V.p; }, &Shard::partA);
+        DBuf<double> Shard::*pin = &Shard::partA, Shard::*pout = &Shard::partB;
+        for (int k = 0; k <= i; k++) {
+            for (auto &sp : d->sh) {
+                Shard &s = *sp;
+                const double *vk = s.V.p + (long long)k * Pl;
+                const double *vn = (k < i) ? s.V.p + (long long)(k + 1) * Pl : s.w.p;
+                launch_mgs_step_r(gate_i(s, i), i, k, m, s.w.p, vk, vn, (s.*pin).p, NP,
+                                  (s.*pout).p + (long long)s.p * d->G, s.H.p, d->G, H0,
+                                  dot_len(d, s), d->st);
+            }
+            exchange(d, vec(pout), 0, d->G);
+            std::swap(pin, pout);
+        }
+        for (auto &sp : d->sh) {
+            Shard &s = *sp;
+            launch_arnoldi_finalize_r(gate_i(s, i), i, m, s.ds.p, (s.*pin).p, NP, d->G, s.w.p,
+                                      s.V.p + (long long)(i + 1) * Pl, s.H.p, s.cs.p, s.sn.p, s.s.p,
+                                      s.hist.p, H0, d->st);
+        }
+    }
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        launch_update(gate_mask(s, DONE_RESTART | DONE_INIT), m, s.ds.p, s.H.p, s.s.p, s.ysm.p, s.V.p,
+                      Pl, s.xv.p, d->G, H0, d->st);
+    }
+    resid(d, ~0);                                                               // rr = b - A x
+    apply_minv(d, -1, ~0, vec(&Shard::rr), vec(&Shard::r));
+    dot(d, -1, ~0, vec(&Shard::r), vec(&Shard::r), &Shard::partA);
+    for (auto &sp : d->sh) launch_end_cycle(sp->partA.p, NP, sp->ds.p, sp->hist.p, d->st);
+}
+
+DevState read_state(gg_dd *d)
+{
+    std::vector<DevState> h(d->sh.size());
+    for (size_t k = 0; k < d->sh.size(); k++)
+        GG_HIP(hipMemcpyAsync(&h[k], d->sh[k]->ds.p, sizeof(DevState), hipMemcpyDeviceToHost, d->st));
+    GG_HIP(hipStreamSynchronize(d->st));
+    for (size_t k = 1; k < h.size(); k++)     // the replicas must agree bit for bit
+        GG_REQUIRE(std::memcmp(&h[k].resid, &h[0].resid, sizeof(double)) == 0 &&
+                       h[k].done == h[0].done && h[k].j == h[0].j,
+                   GG_EINVAL, "dd: shard control blocks diverged");
+    return h[0];
+}
+
+struct RcpFallback {};
+void check_err(gg_dd *d)
+{
+    if (d->kind == GG_DD_RCCL && d->P > 1) {
+        Shard &s = *d->sh[0];
+        GG_NCCL(ncclAllGather(s.err.p + s.p, s.err.p, 1, ncclInt32, d->comm, d->st));
+    }
+    int any = 0;
+    for (auto &sp : d->sh) {
+        std::vector<int> e(d->P, 0);
+        GG_HIP(hipMemcpyAsync(e.data(), sp->err.p, d->P * sizeof(int), hipMemcpyDeviceToHost, d->st));
+        GG_HIP(hipStreamSynchronize(d->st));
+        for (int v : e) any |= v;
+    }
+    GG_REQUIRE((any & 1) == 0, GG_ETIMEOUT, "dd: wavefront triangular solve: boundary wait timed out");
+    if (any & 2) throw RcpFallback{};
+}
+void demote_rcp(gg_dd *d)
+{
+    for (auto &sp : d->sh)
+        for (DevTri *T : {&sp->LI, &sp->LS, &sp->UI, &sp->US})
+            if (T->kind == DevTri::WAVE2D && T->div == WD_RCP) T->div = WD_HW;
+}
+void reset_waves(gg_dd *d)
+{
+    for (auto &sp : d->sh) {
+        for (DevTri *T : {&sp->LI, &sp->LS, &sp->UI, &sp->US}) {
+            if (T->kind != DevTri::WAVE2D) continue;
+            launch_fill_u64(T->bnd.p, T->wl.ngran(), kSentinel, d->st);
+            if (T->prog.p) GG_HIP(hipMemsetAsync(T->prog.p, 0, T->prog.n * sizeof(unsigned long long), d->st));
+        }
+        GG_HIP(hipMemsetAsync(sp->err.p, 0, d->P * sizeof(int), d->st));
+    }
+}
+
+// natural global vector (device, length n) -> every shard's slots of `dst`
+void gather_in(gg_dd *d, const double *nat, DBuf<double> Shard::*dst)
+{
+    for (auto &sp : d->sh) launch_gather(nat, sp->slot2nat.p, (sp.get()->*dst).p, d->H0, d->st);
+}
+void scatter_out(gg_dd *d, DBuf<double> Shard::*src, double *nat)
+{
+    for (auto &sp : d->sh) launch_scatter_idx((sp.get()->*src).p, sp->own_slot.p, sp->own_nat.p, nat, sp->nown, d->st);
+}
+
+int solve_once(gg_dd *d, const double *d_b, double *d_x, const gg_options *opt, gg_result *res)
+{
+    GG_REQUIRE(d->have, GG_ESTATE, "gg_dd_solve: no system (call gg_dd_set_system)");
+    GG_REQUIRE(opt, GG_EINVAL, "gg_dd_solve: null options");
+    const int m = opt->restart;
+    GG_REQUIRE(m >= 1 && m <= 512, GG_EINVAL, "gg_dd_solve: restart must be in [1, 512]");
+    GG_REQUIRE(opt->max_iter >= 0, GG_EINVAL, "gg_dd_solve: negative max_iter");
+    set_dev(d);
+    ensure_workspace(d, m);
+    const long long need = (long long)opt->max_iter + opt->max_iter / m + 4;
+    for (auto &sp : d->sh)
+        if (need > sp->hist_cap) {
+            sp->hist.alloc(need);
+            sp->hist_cap = need;
+        }
+    gather_in(d, d_b, &Shard::bv);
+    gather_in(d, d_x, &Shard::xv);
+    reset_waves(d);
+    DevState h{};
+    h.tol = opt->tol;
+    h.max_iter = opt->max_iter;
+    h.m = m;
+    h.j = 1;
+    for (auto &sp : d->sh)
+        GG_HIP(hipMemcpyAsync(sp->ds.p, &h, sizeof(DevState), hipMemcpyHostToDevice, d->st));
+    GG_HIP(hipEventRecord(d->ev0, d->st));
+    enqueue_init(d);
+    h = read_state(d);
+    int ret = 1, iters = 0, inner = 0, restarts = 0;
+    long long hist_len = 1;
+    double relres = h.resid;
+    if (h.done & DONE_INIT) {
+        ret = 0;
+    } else {
+        while (true) {
+            if (h.j > opt->max_iter) {
+                ret = 1;
+                relres = h.resid;
+                iters = opt->max_iter;
+                hist_len = h.hist_len;
+                break;
+            }
+            restarts++;
+            enqueue_cycle(d, m);
+            DevState prev = h;
+            h = read_state(d);
+            check_err(d);
+            if (h.done & DONE_INNER) {
+                ret = 0;
+                iters = prev.j + h.conv_i;
+                inner += h.conv_i + 1;
+                relres = h.resid;
+                hist_len = h.hist_len + h.conv_i + 1;
+                break;
+            }
+            inner += h.nit;
+            if (h.done & DONE_RESTART) {
+                ret = 0;
+                iters = h.j;
+                relres = h.resid;
+                hist_len = h.hist_len;
+                break;
+            }
+            hist_len = h.hist_len;
+            relres = h.resid;
+        }
+    }
+    GG_HIP(hipEventRecord(d->ev1, d->st));
+    check_err(d);
+    scatter_out(d, &Shard::xv, d_x);
+    GG_HIP(hipStreamSynchronize(d->st));
+    float ms = 0.f;
+    GG_HIP(hipEventElapsedTime(&ms, d->ev0, d->ev1));
+    d->last_hist.resize(hist_len);
+    if (hist_len)
+        GG_HIP(hipMemcpy(d->last_hist.data(), d->sh[0]->hist.p, hist_len * sizeof(double),
+                         hipMemcpyDeviceToHost));
+    if (res) {
+        res->status = ret;
+        res->iters = iters;
+        res->inner_iters = inner;
+        res->restarts = restarts;
+        res->relres = relres;
+        res->solve_ms = ms;
+    }
+    return ret;
+}
+
+int solve_dev(gg_dd *d, const double *d_b, double *d_x, const gg_options *opt, gg_result *res)
+{
+    try {
+        return solve_once(d, d_b, d_x, opt, res);
+    } catch (RcpFallback &) {
+        demote_rcp(d);
+        return solve_once(d, d_b, d_x, opt, res);
+    }
+}
+
+// ---------------------------------------------------------------- setup
+Wave2D region_wave(const CanonTri &L, const CanonTri &U)
+{
+    Wave2D wl;
+    const char *env = std::getenv("GG_NO_WAVEFRONT");
+    if (env && env[0] == '1') return wl;
+    wl = detect_wave2d(L, U);
+    if (wl.ok && wl.nbands > 512) wl.ok = false;
+    const char *e3 = std::getenv("GG_NO_WAVE3D");
+    if (!wl.ok && !(e3 && e3[0] == '1')) wl = detect_wave3d(L, U);
+    return wl;
+}
+
+// rows of a region CSR (region-local row -> slot), columns mapped by `col`
+template <class F>
+Csr slot_csr(const Csr &C, const std::vector<long long> &slot, long long nslots, F col)
+{
+    std::vector<long long> row_of(nslots, -1);
+    for (size_t r = 0; r < slot.size(); r++) row_of[slot[r]] = (long long)r;
+    Csr O;
+    O.n = (int)nslots;
+    O.rp.assign(nslots + 1, 0);
+    O.ci.reserve(C.nnz());
+    O.v.reserve(C.nnz());
+    for (long long t = 0; t < nslots; t++) {
+        const long long r = row_of[t];
+        if (r >= 0)
+            for (int k = C.rp[r]; k < C.rp[r + 1]; k++) {
+                O.ci.push_back((int)col(C.ci[k]));
+                O.v.push_back(C.v[k]);
+            }
+        O.rp[t + 1] = (int)O.ci.size();
+    }
+    return O;
+}
+
+void set_system(gg_dd *d, const Csr &A, int method)
+{
+    DDPlan plan = dd_plan(A, d->P, method);
+    d->n = plan.n;
+    d->nsep = plan.part_size[d->P];
+    d->maxI = plan.maxI;
+    d->pinv = plan.pinv;
+    d->q = plan.q;
+    // pass 1: host pieces and region layouts of this process's shards
+    std::vector<int> mine;
+    if (d->kind == GG_DD_RCCL) mine.push_back(d->rank);
+    else for (int p = 0; p < d->P; p++) mine.push_back(p);
+    std::vector<DDShardHost> hs;
+    d->sh.clear();
+    long long pi_max = 0, ps = 0;
+    for (int p : mine) {
+        hs.push_back(dd_shard(plan, p));
+        DDShardHost &H = hs.back();
+        auto s = std::make_unique<Shard>();
+        s->p = p;
+        s->nI = H.nI;
+        s->nS = H.nS;
+        s->wI = region_wave(H.LI, H.UI);
+        s->wS = region_wave(H.LS, H.US);
+        s->slotI.resize(H.nI);
+        for (int r = 0; r < H.nI; r++) s->slotI[r] = s->wI.ok ? s->wI.slot(r) : r;
+        s->slotS.resize(H.nS);
+        for (int r = 0; r < H.nS; r++) s->slotS[r] = s->wS.ok ? s->wS.slot(r) : r;
+        s->PIr = round_up(std::max<long long>(s->wI.ok ? s->wI.P : H.nI, 1), 512);
+        s->PSr = H.nS ? round_up(s->wS.ok ? s->wS.P : H.nS, 512) : 0;
+        pi_max = std::max(pi_max, s->PIr);
+        ps = s->PSr;            // the separator (and its layout) is the same on every shard
+        d->sh.push_back(std::move(s));
+    }
+    plan.B = Csr{};             // the rest of the plan is not needed any more
+    d->S0 = agree_max(d, pi_max);
+    d->H0 = d->S0 + ps;
+    d->Pl = round_up(d->H0 + (long long)d->P * d->maxI, 512);
+    d->G = reduce_grid(d->H0 / 2);
+    // pass 2: device structures in the shard's slot space
+    for (size_t k = 0; k < d->sh.size(); k++) {
+        Shard &s = *d->sh[k];
+        DDShardHost &H = hs[k];
+        const long long S0 = d->S0, H0 = d->H0;
+        const int nI = H.nI, nS = H.nS;
+        std::vector<long long> lslot(nI + nS);
+        for (int r = 0; r < nI; r++) lslot[r] = s.slotI[r];
+        for (int r = 0; r < nS; r++) lslot[nI + r] = S0 + s.slotS[r];
+        auto lcol = [&](int c) -> long long {
+            if (c < nI) return s.slotI[c];
+            if (c < nI + nS) return S0 + s.slotS[c - nI];
+            return H0 + (c - nI - nS);
+        };
+        Csr As = slot_csr(H.A, lslot, H0, lcol);
+        s.A.upload(As, d->st);
+        s.bytes_spmv = 12.0 * H.A.nnz() + 4.0 * (H0 + 1) + 16.0 * (nI + nS);
+        // triangles on their regions
+        build_tri(s.LI, H.LI, &s.wI, &s.slotI, s.PIr, d->st);
+        build_tri(s.UI, H.UI, &s.wI, &s.slotI, s.PIr, d->st);
+        if (nS) {
+            build_tri(s.LS, H.LS, &s.wS, &s.slotS, s.PSr, d->st);
+            build_tri(s.US, H.US, &s.wS, &s.slotS, s.PSr, d->st);
+        }
+        s.bytes_trsv = s.LI.bytes + s.UI.bytes + s.LS.bytes + s.US.bytes;
+        // coupling terms: separator L rows' interface terms, interior U rows' separator terms
+        Csr lsh = slot_csr(H.LSH, s.slotS, s.PSr, [&](int h) { return H0 + h; });
+        s.LSH.upload(lsh, d->st);
+        Csr uis = slot_csr(H.UIS, s.slotI, s.PIr, [&](int c) { return S0 + s.slotS[c]; });
+        s.UIS.upload(uis, d->st);
+        // interface slots, natural rows of the slots, rows written back
+        std::vector<long long> ifs(std::max(d->maxI, 1), -1);
+        for (size_t t = 0; t < H.iface.size(); t++) ifs[t] = s.slotI[H.iface[t]];
+        s.iface_slot.upload(ifs, d->st);
+        std::vector<long long> s2n(H0, -1), os, on;
+        s.slot2perm.assign(H0, -1);
+        for (int r = 0; r < nI + nS; r++) {
+            s2n[lslot[r]] = plan.q[H.rows[r]];
+            s.slot2perm[lslot[r]] = H.rows[r];
+        }
+        s.slot2nat.upload(s2n, d->st);
+        const bool own_sep = d->kind == GG_DD_RCCL || s.p == 0;
+        for (int r = 0; r < nI + (own_sep ? nS : 0); r++) {
+            os.push_back(lslot[r]);
+            on.push_back(plan.q[H.rows[r]]);
+        }
+        s.nown = (long long)os.size();
+        s.own_slot.upload(os, d->st);
+        s.own_nat.upload(on, d->st);
+        GG_HIP(hipStreamSynchronize(d->st));
+        H = DDShardHost{};
+    }
+    d->m_alloc = -1;
+    d->have = true;
+}
+
+void stage_nat(gg_dd *d, DBuf<double> &buf, const double *h)
+{
+    if (buf.n < (size_t)std::max(d->n, 1)) buf.alloc(std::max(d->n, 1));
+    GG_HIP(hipMemcpyAsync(buf.p, h, sizeof(double) * d->n, hipMemcpyHostToDevice, d->st));
+}
+void fetch_nat(gg_dd *d, const DBuf<double> &buf, double *h)
+{
+    GG_HIP(hipMemcpyAsync(h, buf.p, sizeof(double) * d->n, hipMemcpyDeviceToHost, d->st));
+    GG_HIP(hipStreamSynchronize(d->st));
+}
+
+}  // namespace
+
+extern "C" {
+
+int gg_dd_unique_id(unsigned char *id)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(id, GG_EINVAL, "null id");
+    static_assert(sizeof(ncclUniqueId) == GG_DD_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    GG_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char *id, gg_dd **out)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(out, GG_EINVAL, "null out");
+    GG_REQUIRE(nparts >= 1 && nparts <= kMaxShards, GG_EINVAL, "dd: nparts must be in [1, 16]");
+    GG_REQUIRE(comm == GG_DD_LOCAL || comm == GG_DD_RCCL, GG_EINVAL, "dd: unknown communicator");
+    GG_REQUIRE(comm == GG_DD_LOCAL || (id && rank >= 0 && rank < nparts), GG_EINVAL,
+               "dd: RCCL needs an id and 0 <= rank < nparts");
+    auto d = std::make_unique<gg_dd>();
+    d->device = device;
+    d->P = nparts;
+    d->kind = comm;
+    d->rank = comm == GG_DD_RCCL ? rank : 0;
+    set_dev(d.get());
+    GG_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
+    GG_HIP(hipEventCreate(&d->ev0));
+    GG_HIP(hipEventCreate(&d->ev1));
+    if (comm == GG_DD_RCCL) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        GG_NCCL(ncclCommInitRank(&d->comm, nparts, u, rank));
+    }
+    *out = d.release();
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_destroy(gg_dd *d)
+{
+    if (!d) return GG_OK;
+    (void)hipSetDevice(d->device);
+    if (d->st) (void)hipStreamSynchronize(d->st);
+    d->sh.clear();
+    d->nat_a.release();
+    d->nat_b.release();
+    if (d->comm) (void)ncclCommDestroy(d->comm);
+    if (d->ev0) (void)hipEventDestroy(d->ev0);
+    if (d->ev1) (void)hipEventDestroy(d->ev1);
+    if (d->st) (void)hipStreamDestroy(d->st);
+    delete d;
+    return GG_OK;
+}
+
+int gg_dd_set_system(gg_dd *d, int n, const int *rp, const int *ci, const double *val, int method)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && rp && (n == 0 || (ci && val)), GG_EINVAL, "null argument");
+    GG_REQUIRE(n >= 1 && rp[0] == 0, GG_EINVAL, "dd: bad CSR");
+    for (int r = 0; r < n; r++) {
+        GG_REQUIRE(rp[r + 1] >= rp[r], GG_EINVAL, "dd: row_ptr not monotone");
+        for (int k = rp[r]; k < rp[r + 1]; k++)
+            GG_REQUIRE(ci[k] >= 0 && ci[k] < n, GG_EINVAL, "dd: column index out of range");
+    }
+    set_dev(d);
+    Csr A;
+    A.n = n;
+    A.rp.assign(rp, rp + n + 1);
+    A.ci.assign(ci, ci + rp[n]);
+    A.v.assign(val, val + rp[n]);
+    d->have = false;
+    set_system(d, A, method);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_info(gg_dd *d, int *info)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && info, GG_EINVAL, "null argument");
+    GG_REQUIRE(d->have, GG_ESTATE, "dd: no system");
+    const Shard &s = *d->sh[0];
+    info[0] = d->n;
+    info[1] = d->P;
+    info[2] = d->nsep;
+    info[3] = d->maxI;
+    info[4] = s.nI;
+    info[5] = s.wI.ok ? (s.wI.nz > 1 ? 3 : 2) : 0;
+    info[6] = s.wS.ok ? (s.wS.nz > 1 ? 3 : 2) : 0;
+    info[7] = (int)d->Pl;
+    info[8] = (int)d->sh.size();
+    info[9] = d->P * d->maxI;
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_perm(gg_dd *d, int *pinv, int *q)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && d->have, GG_ESTATE, "dd: no system");
+    if (pinv) std::memcpy(pinv, d->pinv.data(), sizeof(int) * d->n);
+    if (q) std::memcpy(q, d->q.data(), sizeof(int) * d->n);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_dot_layout(gg_dd *d, int part, long long *out, long long cap, int *G)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && d->have, GG_ESTATE, "dd: no system");
+    for (auto &sp : d->sh) {
+        if (sp->p != part) continue;
+        const long long len = dot_len(d, *sp);
+        if (out) std::memcpy(out, sp->slot2perm.data(), sizeof(long long) * std::min(len, cap));
+        if (G) *G = d->G;
+        return (int)len;
+    }
+    GG_REQUIRE(false, GG_EINVAL, "dd: part not held by this process");
+    return GG_EINVAL;
+    GG_API_END
+}
+
+int gg_dd_solve_device(gg_dd *d, const double *d_b, double *d_x, const gg_options *opt, gg_result *res)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && d_b && d_x, GG_EINVAL, "null argument");
+    return solve_dev(d, d_b, d_x, opt, res);
+    GG_API_END
+}
+
+int gg_dd_solve(gg_dd *d, const double *b, double *x, const gg_options *opt, gg_result *res)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && b && x, GG_EINVAL, "null argument");
+    GG_REQUIRE(d->have, GG_ESTATE, "gg_dd_solve: no system");
+    set_dev(d);
+    stage_nat(d, d->nat_a, b);
+    stage_nat(d, d->nat_b, x);
+    int rc = solve_dev(d, d->nat_a.p, d->nat_b.p, opt, res);
+    if (rc >= 0) fetch_nat(d, d->nat_b, x);
+    return rc;
+    GG_API_END
+}
+
+int gg_dd_get_history(gg_dd *d, double *out, int cap)
+{
+    if (!d) return GG_EINVAL;
+    const int len = (int)d->last_hist.size();
+    if (out && cap > 0) std::memcpy(out, d->last_hist.data(), sizeof(double) * std::min(len, cap));
+    return len;
+}
+
+int gg_dd_spmv(gg_dd *d, const double *x, double *y)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && x && y, GG_EINVAL, "null argument");
+    GG_REQUIRE(d->have, GG_ESTATE, "dd: no system");
+    set_dev(d);
+    ensure_workspace(d, std::max(d->m_alloc, 1));
+    stage_nat(d, d->nat_a, x);
+    stage_nat(d, d->nat_b, y);
+    gather_in(d, d->nat_a.p, &Shard::xv);
+    spmv(d, -1, vec(&Shard::xv), vec(&Shard::ww));
+    scatter_out(d, &Shard::ww, d->nat_b.p);
+    fetch_nat(d, d->nat_b, y);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_precond_apply(gg_dd *d, const double *in, double *out)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && in && out, GG_EINVAL, "null argument");
+    GG_REQUIRE(d->have, GG_ESTATE, "dd: no system");
+    set_dev(d);
+    ensure_workspace(d, std::max(d->m_alloc, 1));
+    stage_nat(d, d->nat_a, in);
+    stage_nat(d, d->nat_b, out);
+    gather_in(d, d->nat_a.p, &Shard::xv);
+    auto run = [&]() {
+        reset_waves(d);
+        apply_minv(d, -1, 0, vec(&Shard::xv), vec(&Shard::ww));
+        check_err(d);
+    };
+    try {
+        run();
+    } catch (RcpFallback &) {
+        demote_rcp(d);
+        run();
+    }
+    scatter_out(d, &Shard::ww, d->nat_b.p);
+    fetch_nat(d, d->nat_b, out);
+    return GG_OK;
+    GG_API_END
+}
+
+}  // extern "C"

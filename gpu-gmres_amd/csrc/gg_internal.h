@@ -73,6 +73,30 @@ CanonTri canon_upper_ignorezero(const Csr &U);  // LUSolve_ignoreZero backward
 CanonTri canon_lower_lastdiag(const Csr &L);    // MyILUPP HostPrecond_left (divide by last)
 CanonTri canon_upper_firstdiag(const Csr &U);   // MyILUPP HostPrecond_right (divide by first)
 
+// ---- sharded (domain-decomposed) solve: host plan (host/dd_setup.cpp) ----
+constexpr int kMaxShards = 16;
+struct DDPlan {
+    int n = 0, P = 0;
+    std::vector<int> part_size, pinv, q, begin;   // partition4 sizes / permutation, part offsets (P+2)
+    Csr B;                                        // arrow-permuted A
+    CanonTri cl, cu;                              // canonical ILU(0) triangles of B
+    std::vector<std::vector<int>> iface;          // per part: interface nodes (permuted index)
+    std::vector<int> hidx;                        // permuted index -> halo index, -1 if none
+    int maxI = 0;
+};
+// one part's pieces in its local index space [interior | separator | halo]
+struct DDShardHost {
+    int p = 0, nI = 0, nS = 0;
+    Csr A;                      // nI + nS rows, local columns
+    CanonTri LI, LS, UI, US;    // region triangles (region-local indices)
+    Csr LSH;                    // nS rows: interior terms of separator L rows (cols = halo index)
+    Csr UIS;                    // nI rows: separator terms of interior U rows (cols = separator index)
+    std::vector<int> iface;     // own interface nodes, interior-local, ascending
+    std::vector<int> rows;      // permuted global index of each local row
+};
+DDPlan dd_plan(const Csr &A, int P, int method);
+DDShardHost dd_shard(const DDPlan &D, int p);
+
 // level sets for a canonical triangle: rows grouped by dependency depth
 struct Levels {
     std::vector<int> ptr;    // nlev+1
@@ -178,6 +202,12 @@ struct DevTri {
     long long *trace = nullptr;  // diagnostics: per band, nbatch+1 timestamps (gg_trace_precond)
     double bytes = 0;            // algorithmic bytes per solve
 };
+
+// device triangle from a canonical one: WAVE2D when `wl` is an active grid
+// layout (nat2lay: row -> slot, arrays of length Ppad), else LEVEL (solver.hip)
+void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector<long long> *nat2lay,
+               long long Ppad, hipStream_t st);
+long long round_up(long long a, long long b);
 
 struct DevState;   // device-side GMRES control block (kernels.h)
 

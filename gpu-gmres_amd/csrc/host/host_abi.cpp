@@ -1,6 +1,8 @@
 // host_abi.cpp -- include/ggmres_host.h: setup-phase entry points (no device).
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <memory>
 
 #include "../gg_internal.h"
 #include "ggmres_host.h"
@@ -170,5 +172,121 @@ int gg_host_read_mtx(const char *path, int expand_symmetric, int *nrows, int *nc
 }
 
 void gg_host_free(void *p) { std::free(p); }
+
+}  // extern "C"
+
+struct gg_dd_plan {
+    DDPlan plan;
+    std::map<int, std::unique_ptr<DDShardHost>> shards;
+    DDShardHost &shard(int p)
+    {
+        auto it = shards.find(p);
+        if (it == shards.end()) it = shards.emplace(p, std::make_unique<DDShardHost>(dd_shard(plan, p))).first;
+        return *it->second;
+    }
+};
+
+extern "C" {
+
+int gg_host_dd_plan(int n, const int *rp, const int *ci, const double *v, int nparts, int method,
+                    gg_dd_plan **out)
+{
+    if (n < 1 || !rp || !ci || !v || !out) return GG_EINVAL;
+    try {
+        auto pl = std::make_unique<gg_dd_plan>();
+        pl->plan = dd_plan(wrap(n, rp, ci, v), nparts, method);
+        *out = pl.release();
+        return GG_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    } catch (...) {
+        return GG_EINVAL;
+    }
+}
+
+int gg_host_dd_plan_sizes(const gg_dd_plan *pl, int *sizes)
+{
+    if (!pl || !sizes) return GG_EINVAL;
+    sizes[0] = pl->plan.n;
+    sizes[1] = pl->plan.P;
+    sizes[2] = pl->plan.part_size[pl->plan.P];
+    sizes[3] = pl->plan.maxI;
+    return GG_OK;
+}
+
+int gg_host_dd_plan_perm(const gg_dd_plan *pl, int *part_size, int *pinv, int *q)
+{
+    if (!pl) return GG_EINVAL;
+    const DDPlan &D = pl->plan;
+    if (part_size) std::memcpy(part_size, D.part_size.data(), sizeof(int) * (D.P + 1));
+    if (pinv) std::memcpy(pinv, D.pinv.data(), sizeof(int) * D.n);
+    if (q) std::memcpy(q, D.q.data(), sizeof(int) * D.n);
+    return GG_OK;
+}
+
+int gg_host_dd_shard_sizes(gg_dd_plan *pl, int part, int *sizes)
+{
+    if (!pl || !sizes || part < 0 || part >= pl->plan.P) return GG_EINVAL;
+    try {
+        DDShardHost &S = pl->shard(part);
+        sizes[0] = S.nI;
+        sizes[1] = S.nS;
+        sizes[2] = (int)S.iface.size();
+        return GG_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    }
+}
+
+int gg_host_dd_shard_csr(gg_dd_plan *pl, int part, int piece, int *nrows, int **rp, int **ci,
+                         double **v)
+{
+    if (!pl || !nrows || !rp || !ci || !v || part < 0 || part >= pl->plan.P) return GG_EINVAL;
+    try {
+        DDShardHost &S = pl->shard(part);
+        const Csr *C = nullptr;
+        switch (piece) {
+        case GG_DD_A: C = &S.A; break;
+        case GG_DD_LI: C = &S.LI.off; break;
+        case GG_DD_LS: C = &S.LS.off; break;
+        case GG_DD_LSH: C = &S.LSH; break;
+        case GG_DD_UI: C = &S.UI.off; break;
+        case GG_DD_US: C = &S.US.off; break;
+        case GG_DD_UIS: C = &S.UIS; break;
+        default: return GG_EINVAL;
+        }
+        *nrows = C->n;
+        *rp = (int *)std::malloc(sizeof(int) * (C->n + 1));
+        emit(*C, *rp, ci, v);
+        return GG_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    }
+}
+
+int gg_host_dd_shard_div(gg_dd_plan *pl, int part, int piece, double *d)
+{
+    if (!pl || !d || part < 0 || part >= pl->plan.P) return GG_EINVAL;
+    DDShardHost &S = pl->shard(part);
+    const CanonTri *T = piece == GG_DD_LI ? &S.LI : piece == GG_DD_LS ? &S.LS
+                      : piece == GG_DD_UI ? &S.UI : piece == GG_DD_US ? &S.US : nullptr;
+    if (!T) return GG_EINVAL;
+    if (!T->d.empty()) std::memcpy(d, T->d.data(), sizeof(double) * T->d.size());
+    return GG_OK;
+}
+
+int gg_host_dd_shard_index(gg_dd_plan *pl, int part, int *iface, int *rows)
+{
+    if (!pl || part < 0 || part >= pl->plan.P) return GG_EINVAL;
+    DDShardHost &S = pl->shard(part);
+    if (iface && !S.iface.empty()) std::memcpy(iface, S.iface.data(), sizeof(int) * S.iface.size());
+    if (rows && !S.rows.empty()) std::memcpy(rows, S.rows.data(), sizeof(int) * S.rows.size());
+    return GG_OK;
+}
+
+void gg_host_dd_plan_free(gg_dd_plan *pl) { delete pl; }
 
 }  // extern "C"

@@ -51,6 +51,16 @@ void launch_gather(const double *in, const long long *idx, double *out, long lon
 void launch_copy(const double *in, double *out, long long n, hipStream_t st);
 void launch_dot(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, hipStream_t st);
 
+// ---- sharded solve (dd.hip) --------------------------------------------------
+// out[r] = in[r] - sum_k C.v[k] * x[C.ci[k]] (sequential, listed order), r < C.n
+void launch_sub_seq(Gate g, const DevCsr &C, const double *x, const double *in, double *out,
+                    hipStream_t st);
+struct ShardPtrs { double *p[kMaxShards]; };
+// every shard's slot (b.p[s] + off + s*cnt, cnt doubles) copied to every other shard
+void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long cnt, hipStream_t st);
+void launch_scatter_idx(const double *in, const long long *src, const long long *dst, double *out,
+                        long long n, hipStream_t st);   // out[dst[i]] = in[src[i]]
+
 // ---- split (PG) elementwise maps -------------------------------------------
 void launch_mul(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in*s
 void launch_div(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in/s
@@ -75,6 +85,14 @@ void launch_init_cycle(DevState *ds, const double *r, double *v0, double *s, int
 void launch_mgs_step(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
                      const double *part_in, double *part_out, double *H, int G, long long Ppad,
                      hipStream_t st);
+// the same with a separate dot range [0, Pdot) and nparts_in input partials
+// (the sharded solve: every shard's block partials after the all-gather)
+void launch_mgs_step_r(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
+                       const double *part_in, int nparts_in, double *part_out, double *H, int G,
+                       long long Ppad, long long Pdot, hipStream_t st);
+void launch_arnoldi_finalize_r(Gate g, int i, int m, DevState *ds, const double *part, int nparts_in,
+                               int G, const double *w, double *vnext, double *H, double *cs,
+                               double *sn, double *s, double *hist, long long Ppad, hipStream_t st);
 void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *part, int G,
                              const double *w, double *vnext, double *H, double *cs, double *sn,
                              double *s, double *hist, long long Ppad, hipStream_t st);

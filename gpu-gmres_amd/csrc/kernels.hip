@@ -112,6 +112,8 @@ __global__ void k_copy(const double *in, double *out, long long units)
 __global__ __launch_bounds__(kBlock) void k_dot(Gate g, const double *a, const double *b,
                                                 double *part, long long units)
 {
+    // units: the dot range (a prefix of the vector space; the sharded solve
+    // counts its separator replica on one shard only)
     if (gated(g)) return;
     double acc = 0.0;
     const long long stride = (long long)gridDim.x * kBlock;
@@ -132,6 +134,41 @@ __global__ __launch_bounds__(kBlock) void k_dot(Gate g, const double *a, const d
     }
     acc = block_sum(acc);
     if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+// ---- sharded solve (dd.hip) helpers ---------------------------------------------
+// out[r] = in[r] - v_0 x[c_0] - v_1 x[c_1] - ...  in the listed (reference) order:
+// the coupling terms a triangular row subtracts before its own triangle's terms
+// (separator rows' interior terms, interior rows' separator terms)
+__global__ void k_sub_seq(Gate g, int n, const int *rp, const int *ci, const double *v,
+                          const double *x, const double *in, double *out)
+{
+    if (gated(g)) return;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        double acc = in[r];
+        for (int k = rp[r]; k < rp[r + 1]; k++) acc -= v[k] * x[ci[k]];
+        out[r] = acc;
+    }
+}
+// all shards of one process: slot s of shard s' buffer (at off + s*cnt) -> every other shard
+__global__ void k_allgather_local(ShardPtrs b, int P, long long off, long long cnt)
+{
+    const long long tot = P * cnt;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot;
+         e += (long long)gridDim.x * blockDim.x) {
+        const int src = (int)(e / cnt);
+        const double v = b.p[src][off + e];
+        for (int q = 0; q < P; q++)
+            if (q != src) b.p[q][off + e] = v;
+    }
+}
+// out[dst[i]] = in[src[i]]
+__global__ void k_scatter_idx(const double *in, const long long *src, const long long *dst,
+                              double *out, long long n)
+{
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[dst[i]] = in[src[i]];
 }
 
 // ------------------------------------------------------- split (PG) maps
@@ -1095,8 +1132,12 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
                                                      const double *__restrict__ vk,
                                                      const double *__restrict__ vnext,
                                                      const double *part_in, double *part_out,
-                                                     double *H, int G, long long units)
+                                                     double *H, int G, long long units,
+                                                     long long dunits)
 {
+    // the AXPY runs over [0, units); the next dot accumulates over [0, dunits)
+    // (dunits < units on the shards of a sharded solve that do not own the
+    // separator replica); part_in holds G partials (all shards' in that case)
     if (gated(g)) return;
     double acc = 0.0;
     const long long stride = (long long)gridDim.x * kBlock;
@@ -1126,8 +1167,10 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
                 wv[j].y = a * vv[j].y + wv[j].y;
                 st2(w, u, wv[j]);
                 if (NORM) nv[j] = wv[j];
-                acc += wv[j].x * nv[j].x;
-                acc += wv[j].y * nv[j].y;
+                if (u < dunits) {
+                    acc += wv[j].x * nv[j].x;
+                    acc += wv[j].y * nv[j].y;
+                }
             }
         }
         u0 += kUnroll * stride;
@@ -1478,6 +1521,23 @@ void launch_dot(Gate g, const double *a, const double *b, double *part, int G, l
 {
     k_dot<<<G, kBlock, 0, st>>>(g, a, b, part, Ppad / 2);
 }
+void launch_sub_seq(Gate g, const DevCsr &C, const double *x, const double *in, double *out,
+                    hipStream_t st)
+{
+    if (C.n == 0) return;
+    k_sub_seq<<<blocks_for(C.n, kBlock, 1 << 30), kBlock, 0, st>>>(g, C.n, C.rp.p, C.ci.p, C.v.p, x, in, out);
+}
+void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long cnt, hipStream_t st)
+{
+    if (P <= 1 || cnt == 0) return;
+    k_allgather_local<<<blocks_for(P * cnt, kBlock, 8192), kBlock, 0, st>>>(b, P, off, cnt);
+}
+void launch_scatter_idx(const double *in, const long long *src, const long long *dst, double *out,
+                        long long n, hipStream_t st)
+{
+    if (n == 0) return;
+    k_scatter_idx<<<blocks_for(n, kBlock, 8192), kBlock, 0, st>>>(in, src, dst, out, n);
+}
 
 void launch_mul(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st)
 {
@@ -1637,17 +1697,31 @@ void launch_mgs_step(Gate g, int i, int k, int m, double *w, const double *vk, c
                      const double *part_in, double *part_out, double *H, int G, long long Ppad,
                      hipStream_t st)
 {
+    launch_mgs_step_r(g, i, k, m, w, vk, vnext, part_in, G, part_out, H, G, Ppad, Ppad, st);
+}
+void launch_mgs_step_r(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
+                       const double *part_in, int nparts_in, double *part_out, double *H, int G,
+                       long long Ppad, long long Pdot, hipStream_t st)
+{
     if (vnext == w)
-        k_mgs_step<true><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, nullptr, part_in, part_out, H, G, Ppad / 2);
+        k_mgs_step<true><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, nullptr, part_in, part_out, H,
+                                                nparts_in, Ppad / 2, Pdot / 2);
     else
-        k_mgs_step<false><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, vnext, part_in, part_out, H, G, Ppad / 2);
+        k_mgs_step<false><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, vnext, part_in, part_out, H,
+                                                 nparts_in, Ppad / 2, Pdot / 2);
 }
 void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *part, int G,
                              const double *w, double *vnext, double *H, double *cs, double *sn,
                              double *s, double *hist, long long Ppad, hipStream_t st)
 {
-    k_arnoldi_finalize<<<G, kBlock, 0, st>>>(g, i, m, ds, part, G, w, vnext, H, cs, sn, s, hist,
-                                              Ppad / 2);
+    launch_arnoldi_finalize_r(g, i, m, ds, part, G, G, w, vnext, H, cs, sn, s, hist, Ppad, st);
+}
+void launch_arnoldi_finalize_r(Gate g, int i, int m, DevState *ds, const double *part, int nparts_in,
+                               int G, const double *w, double *vnext, double *H, double *cs,
+                               double *sn, double *s, double *hist, long long Ppad, hipStream_t st)
+{
+    k_arnoldi_finalize<<<G, kBlock, 0, st>>>(g, i, m, ds, part, nparts_in, w, vnext, H, cs, sn, s,
+                                              hist, Ppad / 2);
 }
 int arnoldi_persist_units(int G, long long Ppad)
 {

@@ -47,8 +47,6 @@ void DevCsr::upload(const Csr &A, hipStream_t st)
     long_rows.upload(lr, st);
 }
 
-namespace {
-
 long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
 
 // Build a device triangular solve from a canonical triangle.  WAVE2D when a
@@ -117,8 +115,6 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         T.bytes = 12.0 * C.off.nnz() + 4.0 * (n + 1) + 24.0 * n;
     }
 }
-
-}  // namespace
 
 }  // namespace gg
 

@@ -85,3 +85,77 @@ def read_mtx(path, expand_symmetric=False):
     rp = np.ctypeslib.as_array(rp_p, (nr.value + 1,)).copy()
     lib().gg_host_free(ctypes.cast(rp_p, ctypes.c_void_p))
     return _take_csr(nr.value, nc.value, rp, ci_p, v_p)
+
+
+# ---- sharded-solve plan (gg_host_dd_*): the pieces each shard of
+# include/ggmres_dd.h runs on, in the shard's local index space
+# [interior (nI) | separator (nS) | halo (nparts * max_iface)]
+DD_A, DD_LI, DD_LS, DD_LSH, DD_UI, DD_US, DD_UIS = range(7)
+
+
+class DDPlan:
+    def __init__(self, A, nparts, method=PART_BLOCKS):
+        n, rp, ci, v = _csr_arrays(A)
+        h = ctypes.c_void_p()
+        L = lib()
+        L.gg_host_dd_plan.argtypes = [ctypes.c_int, _PI, _PI, _PD, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_void_p)]
+        for f in ("gg_host_dd_plan_sizes", "gg_host_dd_plan_perm", "gg_host_dd_shard_sizes",
+                  "gg_host_dd_shard_csr", "gg_host_dd_shard_div", "gg_host_dd_shard_index",
+                  "gg_host_dd_plan_free"):
+            getattr(L, f).restype = ctypes.c_int if f != "gg_host_dd_plan_free" else None
+        _check(L.gg_host_dd_plan(ctypes.c_int(n), _ptr(rp, _PI), _ptr(ci, _PI), _ptr(v, _PD),
+                                 ctypes.c_int(nparts), ctypes.c_int(method), ctypes.byref(h)))
+        self.h = h
+        s = np.zeros(4, np.int32)
+        _check(L.gg_host_dd_plan_sizes(h, _ptr(s, _PI)))
+        self.n, self.P, self.nsep, self.max_iface = (int(x) for x in s)
+        self.part_size = np.zeros(self.P + 1, np.int32)
+        self.pinv = np.zeros(self.n, np.int32)
+        self.q = np.zeros(self.n, np.int32)
+        _check(L.gg_host_dd_plan_perm(h, _ptr(self.part_size, _PI), _ptr(self.pinv, _PI),
+                                      _ptr(self.q, _PI)))
+        self.begin = np.concatenate([[0], np.cumsum(self.part_size)]).astype(np.int64)
+
+    def close(self):
+        if self.h:
+            lib().gg_host_dd_plan_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def shard(self, p):
+        """dict: nI, nS, A, LI, LS, LSH, UI, US, UIS (scipy CSR, entries in the
+        reference's summation order), dLI/dLS/dUI/dUS (divisors), iface, rows."""
+        L = lib()
+        sz = np.zeros(3, np.int32)
+        _check(L.gg_host_dd_shard_sizes(self.h, ctypes.c_int(p), _ptr(sz, _PI)))
+        nI, nS, ni = (int(x) for x in sz)
+        ncols = {DD_A: nI + nS + self.P * self.max_iface, DD_LI: nI, DD_LS: nS,
+                 DD_LSH: self.P * self.max_iface, DD_UI: nI, DD_US: nS, DD_UIS: nS}
+        out = dict(nI=nI, nS=nS)
+        for name, piece in (("A", DD_A), ("LI", DD_LI), ("LS", DD_LS), ("LSH", DD_LSH),
+                            ("UI", DD_UI), ("US", DD_US), ("UIS", DD_UIS)):
+            nr = ctypes.c_int()
+            rp_p, ci_p, v_p = _PI(), _PI(), _PD()
+            _check(L.gg_host_dd_shard_csr(self.h, ctypes.c_int(p), ctypes.c_int(piece),
+                                          ctypes.byref(nr), ctypes.byref(rp_p), ctypes.byref(ci_p),
+                                          ctypes.byref(v_p)))
+            rp = np.ctypeslib.as_array(rp_p, (nr.value + 1,)).copy()
+            L.gg_host_free(ctypes.cast(rp_p, ctypes.c_void_p))
+            out[name] = _take_csr(nr.value, max(ncols[piece], 1), rp, ci_p, v_p)
+        for name, piece, nr in (("dLI", DD_LI, nI), ("dLS", DD_LS, nS), ("dUI", DD_UI, nI),
+                                ("dUS", DD_US, nS)):
+            d = np.zeros(max(nr, 1))
+            _check(L.gg_host_dd_shard_div(self.h, ctypes.c_int(p), ctypes.c_int(piece), _ptr(d, _PD)))
+            out[name] = d[:nr]
+        iface = np.zeros(max(ni, 1), np.int32)
+        rows = np.zeros(max(nI + nS, 1), np.int32)
+        _check(L.gg_host_dd_shard_index(self.h, ctypes.c_int(p), _ptr(iface, _PI), _ptr(rows, _PI)))
+        out["iface"] = iface[:ni]
+        out["rows"] = rows[:nI + nS]
+        return out

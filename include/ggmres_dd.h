@@ -1,0 +1,87 @@
+/*
+ * ggmres_dd.h -- C ABI of the sharded (domain-decomposed) GMRES solve, SURVEY.md 8(e).
+ *
+ * Replaces the reference's multi-domain path: partition4 (src/partition3.cpp:122-194,
+ * METIS_PartGraphRecursive -> our recursive BFS bisection / contiguous blocks),
+ * dd_form's arrow-matrix blocks (src/form_dd.cpp:32-110) and the per-domain
+ * solves of etbr_dd (src/etbr_dd.cpp), here as ONE GMRES(m) + ILU(0) solve of
+ * the arrow-permuted system B = P A P^T sharded over nparts GPUs:
+ *
+ *   - shard p holds interior p's rows and a replica of the separator rows;
+ *   - SpMV and the forward triangular solve need the "interface" values
+ *     (interior nodes the separator rows reference) of every shard: one
+ *     all-gather each (RCCL over xGMI); the backward solve needs nothing;
+ *   - every MGS dot is an all-gather of the shards' block partials, summed in
+ *     one fixed order on every shard (identical Hessenberg on every shard);
+ *   - the ILU(0) factors are those of B (factored on the host), and each row
+ *     of every triangular solve runs the reference's operations in the
+ *     reference's order (LUSolve_ignoreZero, src/SpMV_compute.cpp:92-136):
+ *     the operators are bit-identical to the single-GPU solve of B.
+ *
+ * Two communicators:
+ *   GG_DD_RCCL   one process per GPU (torchrun), shard = rank, RCCL collectives
+ *                on the solver's stream; the 128-byte id comes from
+ *                gg_dd_unique_id on rank 0 and is broadcast by the caller.
+ *   GG_DD_LOCAL  all nparts shards in this process on one device (the same
+ *                kernels, the exchanges done by a copy kernel): tests and
+ *                single-GPU studies of the decomposition.
+ *
+ * Vectors are global, natural (unpermuted) order, length n, identical on every
+ * rank on input.  On output a process writes the rows it holds (GG_DD_LOCAL:
+ * all rows; GG_DD_RCCL: interior p and the separator); other entries are left
+ * untouched.  Status codes as ggmres.h; GG_ECOMM for RCCL failures.
+ */
+#ifndef GGMRES_DD_H_
+#define GGMRES_DD_H_
+
+#include "ggmres.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GG_DD_ID_BYTES 128
+
+enum gg_dd_comm {
+    GG_DD_LOCAL = 0,
+    GG_DD_RCCL = 1
+};
+
+typedef struct gg_dd gg_dd;
+
+/* ncclGetUniqueId: call on rank 0, broadcast the bytes to every rank */
+int gg_dd_unique_id(unsigned char *id);
+int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char *id, gg_dd **out);
+int gg_dd_destroy(gg_dd *d);
+
+/* the global system (identical on every rank): partition (gg_part_method of
+ * ggmres_host.h), arrow permutation, ILU(0) of the permuted matrix, shards */
+int gg_dd_set_system(gg_dd *d, int n, const int *row_ptr, const int *col_idx, const double *val,
+                     int method);
+/* info[0..9]: n, nparts, separator rows, max interface per shard, this
+ * process's first shard: interior rows, wavefront interior (0/1), wavefront
+ * separator (0/1), local vector length (slots), shards in this process, halo
+ * doubles exchanged per all-gather (received, per shard) */
+int gg_dd_info(gg_dd *d, int *info);
+/* the arrow permutation in use: pinv[j] = new index of node j; q = its inverse */
+int gg_dd_perm(gg_dd *d, int *pinv, int *q);
+
+/* the reduction order of the shard's dots (for order-matched parity checks):
+ * out[slot] = permuted row of each slot of the part's dot range (-1 = padding),
+ * G = block partials per shard; returns the range length (part must be held
+ * by this process) */
+int gg_dd_dot_layout(gg_dd *d, int part, long long *out, long long cap, int *G);
+
+int gg_dd_solve(gg_dd *d, const double *b, double *x, const gg_options *opt, gg_result *res);
+int gg_dd_solve_device(gg_dd *d, const double *d_b, double *d_x, const gg_options *opt,
+                       gg_result *res);
+int gg_dd_get_history(gg_dd *d, double *out, int cap);
+
+/* single operators (host vectors, natural order) for parity tests */
+int gg_dd_spmv(gg_dd *d, const double *x, double *y);
+int gg_dd_precond_apply(gg_dd *d, const double *in, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

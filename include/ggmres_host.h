@@ -73,6 +73,38 @@ int gg_host_wave3d(int n, const int *l_row_ptr, const int *l_col_idx, const doub
  * max(nz, nrows + 1) slots), entries of a row bubble-sorted by column.
  * The reference's C++ boundary-feed symbols are in include/compat/format_convert.h. */
 int gg_host_coo2csr_in(int nrows, int nz, double *val, int *row_idx, int *col_idx);
+/* Sharded-solve plan (the host half of include/ggmres_dd.h, exposed for CPU
+ * checks of the decomposition): partition4 + arrow permutation B = P A P^T +
+ * ILU(0) of B + per-part pieces in the part's local index space
+ * [interior (nI) | separator (nS) | halo (nparts * max_iface)]. */
+typedef struct gg_dd_plan gg_dd_plan;
+enum gg_dd_piece {
+    GG_DD_A = 0,      /* local rows of B, local columns                          */
+    GG_DD_LI = 1,     /* interior triangle L_II (canonical order, off-diagonals)  */
+    GG_DD_LS = 2,     /* separator triangle L_SS                                  */
+    GG_DD_LSH = 3,    /* separator rows' interior terms of L (cols: halo index)   */
+    GG_DD_UI = 4,     /* interior triangle U_II                                   */
+    GG_DD_US = 5,     /* separator triangle U_SS                                  */
+    GG_DD_UIS = 6     /* interior rows' separator terms of U (cols: separator idx)*/
+};
+int gg_host_dd_plan(int n, const int *row_ptr, const int *col_idx, const double *val, int nparts,
+                    int method, gg_dd_plan **out);
+/* sizes[4]: n, nparts, separator rows, max interface nodes per part */
+int gg_host_dd_plan_sizes(const gg_dd_plan *pl, int *sizes);
+/* part_size[nparts + 1], pinv[n], q[n] (any may be NULL) */
+int gg_host_dd_plan_perm(const gg_dd_plan *pl, int *part_size, int *pinv, int *q);
+/* sizes[3]: nI, nS, number of own interface nodes */
+int gg_host_dd_shard_sizes(gg_dd_plan *pl, int part, int *sizes);
+/* a piece as CSR (row_ptr malloc'd too); triangles list the off-diagonal
+ * terms in the reference's summation order */
+int gg_host_dd_shard_csr(gg_dd_plan *pl, int part, int piece, int *nrows, int **row_ptr,
+                         int **col_idx, double **val);
+/* divisors of a triangle piece (GG_DD_LI/LS/UI/US), nrows doubles */
+int gg_host_dd_shard_div(gg_dd_plan *pl, int part, int piece, double *d);
+/* own interface nodes (interior-local, ascending) and the permuted global index
+ * of every local row (nI + nS) (either may be NULL) */
+int gg_host_dd_shard_index(gg_dd_plan *pl, int part, int *iface, int *rows);
+void gg_host_dd_plan_free(gg_dd_plan *pl);
 void gg_host_free(void *p);
 
 #ifdef __cplusplus

@@ -62,6 +62,11 @@ def lib():
             f.argtypes = [ctypes.POINTER(SplitT), _f64p, _f64p]
         L.orc_set_dot_order.argtypes = [ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
                                         ctypes.c_void_p]
+        L.orc_set_dot_order_shards.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                               ctypes.c_void_p]
+        L.orc_canon_trsv.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, _f64p,
+                                     _f64p, _f64p]
+        L.orc_sub_seq.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
         L.orc_gen_rot.argtypes = [ctypes.c_double, ctypes.c_double, _PD, _PD]
         L.orc_apply_rot.argtypes = [_PD, _PD, ctypes.c_double, ctypes.c_double]
         common = [_f64p, _f64p, ctypes.c_int, _PI, _PD, _f64p, ctypes.c_int, _PI, _PI]
@@ -196,6 +201,18 @@ def set_dot_order(lay2nat=None, G=1):
     else:
         _dot_keep = np.ascontiguousarray(lay2nat, np.int64)
         lib().orc_set_dot_order(1, len(_dot_keep), int(G), _dot_keep.ctypes.data)
+
+
+def set_dot_order_shards(segments, G):
+    """The sharded solve's tree (gpu-gmres_amd/csrc/dd.hip): segments = per
+    shard, its dot range's slot -> index map (int64, -1 = padding); each shard
+    sums its range into G block partials, then all shards' partials are summed
+    shard-major as in the single-device tree."""
+    global _dot_keep
+    seglen = np.array([len(s) for s in segments], np.int64)
+    cat = np.ascontiguousarray(np.concatenate(segments), np.int64)
+    _dot_keep = (seglen, cat)
+    lib().orc_set_dot_order_shards(len(segments), seglen.ctypes.data, int(G), cat.ctypes.data)
 
 
 def gen_rot(dx, dy):

@@ -437,6 +437,11 @@ static int g_blocked = 0;
 static long long g_ppad = 0;
 static int g_G = 1;
 static const long long *g_lay2nat = NULL;
+/* the sharded solve (gpu-gmres_amd/csrc/dd.hip): nseg shards, shard s summing
+ * its own dot range of seglen[s] slots (lay2nat segments concatenated) into G
+ * block partials; the nseg*G partials (shard-major) are then summed as above */
+static int g_nseg = 1;
+static const long long *g_seglen = NULL;
 
 void orc_set_dot_order(int blocked, long long ppad, int G, const long long *lay2nat)
 {
@@ -444,6 +449,18 @@ void orc_set_dot_order(int blocked, long long ppad, int G, const long long *lay2
     g_ppad = ppad;
     g_G = G > 0 ? G : 1;
     g_lay2nat = lay2nat;
+    g_nseg = 1;
+    g_seglen = NULL;
+}
+
+void orc_set_dot_order_shards(int nseg, const long long *seglen, int G, const long long *lay2nat)
+{
+    g_blocked = nseg > 0;
+    g_nseg = nseg > 0 ? nseg : 1;
+    g_seglen = seglen;
+    g_G = G > 0 ? G : 1;
+    g_lay2nat = lay2nat;
+    g_ppad = 0;
 }
 
 static double block_sum256(double *v)
@@ -459,26 +476,33 @@ static double block_sum256(double *v)
 
 static double dot_blocked(const double *x, const double *y)
 {
-    const long long units = g_ppad / 2;
-    double *part = (double *)malloc((size_t)g_G * sizeof(double));
+    const int nparts = g_nseg * g_G;
+    double *part = (double *)malloc((size_t)nparts * sizeof(double));
     double v[256];
-    for (int blk = 0; blk < g_G; blk++) {
-        for (int t = 0; t < 256; t++) {
-            double acc = 0.0;
-            for (long long u = (long long)blk * 256 + t; u < units; u += (long long)g_G * 256) {
-                long long p0 = g_lay2nat[2 * u], p1 = g_lay2nat[2 * u + 1];
-                double a0 = p0 >= 0 ? x[p0] : 0.0, b0 = p0 >= 0 ? y[p0] : 0.0;
-                double a1 = p1 >= 0 ? x[p1] : 0.0, b1 = p1 >= 0 ? y[p1] : 0.0;
-                acc += a0 * b0;
-                acc += a1 * b1;
+    long long base = 0;
+    for (int sg = 0; sg < g_nseg; sg++) {
+        const long long len = g_seglen ? g_seglen[sg] : g_ppad;
+        const long long units = len / 2;
+        const long long *l2n = g_lay2nat + base;
+        for (int blk = 0; blk < g_G; blk++) {
+            for (int t = 0; t < 256; t++) {
+                double acc = 0.0;
+                for (long long u = (long long)blk * 256 + t; u < units; u += (long long)g_G * 256) {
+                    long long p0 = l2n[2 * u], p1 = l2n[2 * u + 1];
+                    double a0 = p0 >= 0 ? x[p0] : 0.0, b0 = p0 >= 0 ? y[p0] : 0.0;
+                    double a1 = p1 >= 0 ? x[p1] : 0.0, b1 = p1 >= 0 ? y[p1] : 0.0;
+                    acc += a0 * b0;
+                    acc += a1 * b1;
+                }
+                v[t] = acc;
             }
-            v[t] = acc;
+            part[sg * g_G + blk] = block_sum256(v);
         }
-        part[blk] = block_sum256(v);
+        base += len;
     }
     for (int t = 0; t < 256; t++) {
         double acc = 0.0;
-        for (int k = t; k < g_G; k += 256) acc += part[k];
+        for (int k = t; k < nparts; k += 256) acc += part[k];
         v[t] = acc;
     }
     double r = block_sum256(v);
@@ -708,5 +732,33 @@ void orc_transient_rhs(int n, int nsrc, const int *src_node, const double *u,
         double xnr = 0.0;
         xnr += cdiag[i] * x[i];                                     /* cs_dl_gaxpy(right, xn, xnr) */
         w[i] += xnr;                                                /* w += xnr */
+    }
+}
+
+/* ------------------------------------------------ sharded solve (oracle/dd.py)
+ * One row of a triangular solve in the reference's arithmetic
+ * (LUSolve_ignoreZero, src/SpMV_compute.cpp:92-136): x[r] = b[r], then
+ * x[r] -= v_k * x[c_k] for the listed terms in order, then x[r] /= d[r]
+ * (d = 1 for the unit / skipped diagonal: exact).  Rows ascending (lower) or
+ * descending (upper).  sub_seq: the same subtraction without the division,
+ * for the coupling terms a row subtracts before its own triangle's. */
+void orc_canon_trsv(int n, int lower, const int *rp, const int *ci, const double *v,
+                    const double *d, const double *b, double *x)
+{
+    for (int t = 0; t < n; t++) {
+        const int r = lower ? t : n - 1 - t;
+        double acc = b[r];
+        for (int k = rp[r]; k < rp[r + 1]; k++) acc -= v[k] * x[ci[k]];
+        x[r] = acc / d[r];
+    }
+}
+
+void orc_sub_seq(int n, const int *rp, const int *ci, const double *v, const double *x,
+                 const double *in, double *out)
+{
+    for (int r = 0; r < n; r++) {
+        double acc = in[r];
+        for (int k = rp[r]; k < rp[r + 1]; k++) acc -= v[k] * x[ci[k]];
+        out[r] = acc;
     }
 }

@@ -73,6 +73,7 @@ void orc_split_start(const orc_split_t *p, const double *in, double *out);
  * is the reference CPU engine's serial loop (default); blocked = 1 restates
  * the device kernels' reduction tree over a laid-out vector (see oracle.c). */
 void orc_set_dot_order(int blocked, long long ppad, int G, const long long *lay2nat);
+void orc_set_dot_order_shards(int nseg, const long long *seglen, int G, const long long *lay2nat);
 
 /* Givens (src/gmres.cu:192-216) */
 void orc_apply_rot(double *dx, double *dy, double cs, double sn);
@@ -105,6 +106,12 @@ double orc_pulse(const double *q, int it, double h);
  * xnr = 0; xnr += diag(cdiag) x; w += xnr. */
 void orc_transient_rhs(int n, int nsrc, const int *src_node, const double *u,
                        const double *cdiag, const double *x, double *w);
+
+/* sharded solve pieces (oracle/dd.py) */
+void orc_canon_trsv(int n, int lower, const int *rp, const int *ci, const double *v,
+                    const double *d, const double *b, double *x);
+void orc_sub_seq(int n, const int *rp, const int *ci, const double *v, const double *x,
+                 const double *in, double *out);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,7 @@ import oracle as O
 from conftest import PKG, REPO, fixture_path
 from ggmres import matrices as M
 
-HEADERS = ["ggmres.h", "ggmres_host.h"]
+HEADERS = ["ggmres.h", "ggmres_host.h", "ggmres_dd.h"]
 
 
 def declared(header):
@@ -37,7 +37,9 @@ def test_library_exports_every_declared_symbol(ggmres_lib):
         assert not missing, f"{h}: not exported: {missing}"
     import ggmres
     assert set(ggmres.EXPORTS) == set(declared("ggmres.h"))
-    for name in ggmres.EXPORTS:
+    from ggmres import dd
+    assert set(dd.EXPORTS) == set(declared("ggmres_dd.h"))
+    for name in ggmres.EXPORTS + dd.EXPORTS:
         getattr(ggmres_lib, name)   # resolvable through ctypes
 
 
@@ -56,7 +58,7 @@ def test_reference_boundary_classes_exported(ggmres_lib):
 
 def test_headers_compile_as_c_and_cpp(tmp_path):
     c = tmp_path / "t.c"
-    c.write_text('#include "ggmres.h"\n#include "ggmres_host.h"\nint main(void){gg_options o; (void)o; return 0;}\n')
+    c.write_text('#include "ggmres.h"\n#include "ggmres_host.h"\n#include "ggmres_dd.h"\nint main(void){gg_options o; (void)o; return 0;}\n')
     subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only",
                            f"-I{REPO}/include", str(c)])
     cc = tmp_path / "t.cpp"

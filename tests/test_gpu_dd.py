@@ -1,0 +1,127 @@
+"""GPU parity of the sharded solve (include/ggmres_dd.h).
+
+All shards of a P-way decomposition run in one process on one GPU
+(GG_DD_LOCAL: the same kernels and the same exchange points as one process
+per GPU over RCCL; the exchanges are done by a copy kernel), checked against
+the oracle on the arrow-permuted matrix B = P A P^T:
+  * SpMV and the ILU(0) apply: bit-exact vs oracle.spmv(B) / lusolve(ilu0(B));
+  * GMRES: bit-identical history, iteration count and solution vs the oracle
+    run with the sharded reduction order (oracle.set_dot_order_shards), and
+    within 1e-10 (north_star) of the serial-order oracle.
+The RCCL communicator is exercised with one rank (the GPU box has one GPU).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import fixture_path
+from ggmres import host, matrices as M
+from ggmres.dd import DD, unique_id
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    # name: (matrix, parts, method, expect wavefront interior / separator (0, 2 or 3))
+    "5pt_200x160_P2": (lambda: M.laplacian_5pt(200, 160), 2, host.PART_BLOCKS, 2, 2),
+    "5pt_200x160_P4": (lambda: M.laplacian_5pt(200, 160), 4, host.PART_BLOCKS, 2, 2),
+    "7pt_24_P4": (lambda: M.grid_7pt(24), 4, host.PART_BLOCKS, 3, 3),
+    "7pt_16x16x32_P8_upwind": (lambda: M.grid_7pt(16, 16, 32, upwind=0.1), 8, host.PART_BLOCKS, 3, 3),
+    "7pt_16_P4_bisect": (lambda: M.grid_7pt(16), 4, host.PART_BISECT, None, None),
+    "sherman1_P4": (lambda: M.read_rua(fixture_path("sherman1.rua")), 4, host.PART_BISECT, None, None),
+    "5pt_60x60_P1": (lambda: M.laplacian_5pt(60, 60), 1, host.PART_BLOCKS, 2, 0),
+}
+
+_cache = {}
+
+
+def setup(name):
+    if name not in _cache:
+        make, P, method, wi, ws = CASES[name]
+        A = make()
+        d = DD(P, device=0)
+        d.set_system(A, method)
+        pinv, q = d.perm()
+        B = host.permute(A, pinv, q)
+        L, U = O.ilu0(B)
+        _cache[name] = (A, d, q, B, L, U)
+    return _cache[name]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_dd_layout(name):
+    A, d, q, B, L, U = setup(name)
+    inf = d.info()
+    _, P, _, wi, ws = CASES[name]
+    assert inf["nparts"] == P and inf["shards_here"] == P
+    if wi is not None:
+        assert inf["wave_interior"] == wi, inf
+        assert inf["wave_separator"] == ws, inf
+    plan = host.DDPlan(A, P, CASES[name][2])          # the host plan agrees with the solver's
+    assert np.array_equal(plan.q, q) and inf["nsep"] == plan.nsep
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_dd_spmv_and_apply_bitexact(name):
+    A, d, q, B, L, U = setup(name)
+    n = A.shape[0]
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(n)
+    y = d.spmv(x)
+    assert np.array_equal(y[q], O.spmv(B, x[q]))
+    for scale in (1.0, 1e-250, 1e250):                  # WD_RCP range fallback on the U solves
+        v = rng.standard_normal(n) * scale
+        z = d.precond_apply(v)
+        assert np.array_equal(z[q], O.lusolve(L, U, v[q])), scale
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_dd_gmres_bitexact_order_matched(name):
+    A, d, q, B, L, U = setup(name)
+    P = CASES[name][1]
+    b = M.rhs_ones(A)
+    g = d.solve(b, restart=30, max_iter=1500, tol=1e-10)
+    segs, G = zip(*[d.dot_layout(p) for p in range(P)])
+    O.set_dot_order_shards(list(segs), G[0])
+    try:
+        ref_t = O.gmres_left(B, L, U, b[q], m=30, max_iter=1500, tol=1e-10)
+    finally:
+        O.set_dot_order(None)
+    ref = O.gmres_left(B, L, U, b[q], m=30, max_iter=1500, tol=1e-10)
+    assert g["ret"] == ref_t["ret"] == 0
+    assert g["iters"] == ref_t["iters"]
+    assert np.array_equal(g["hist"], ref_t["hist"])
+    assert np.array_equal(g["x"][q], ref_t["x"])
+    # the serial-order restatement: same iteration count, history within 1e-10
+    assert g["iters"] == ref["iters"] and g["hist"].shape == ref["hist"].shape
+    assert np.max(np.abs(g["hist"] - ref["hist"])) <= 1e-10 * np.max(np.abs(ref["hist"]))
+    assert np.linalg.norm(g["x"][q] - ref["x"]) <= 1e-10 * np.linalg.norm(ref["x"])
+
+
+def test_dd_restart_and_max_iter_semantics():
+    A, d, q, B, L, U = setup("7pt_24_P4")
+    b = M.rhs_uniform(A.shape[0])
+    x0 = np.random.default_rng(9).standard_normal(A.shape[0])
+    g = d.solve(b, x0=x0, restart=7, max_iter=40, tol=1e-14)       # cut by max_iter mid-cycle
+    segs, G = zip(*[d.dot_layout(p) for p in range(4)])
+    O.set_dot_order_shards(list(segs), G[0])
+    try:
+        ref = O.gmres_left(B, L, U, b[q], x0=x0[q], m=7, max_iter=40, tol=1e-14)
+    finally:
+        O.set_dot_order(None)
+    assert g["ret"] == ref["ret"] == 1 and g["iters"] == ref["iters"] == 40
+    assert np.array_equal(g["hist"], ref["hist"]) and np.array_equal(g["x"][q], ref["x"])
+
+
+def test_dd_rccl_single_rank_matches_local():
+    A = M.laplacian_5pt(64, 64)
+    b = M.rhs_ones(A)
+    loc = DD(1, device=0)
+    loc.set_system(A, host.PART_BLOCKS)
+    r0 = loc.solve(b, restart=30, max_iter=500, tol=1e-10)
+    rc = DD(1, device=0, rank=0, uid=unique_id())
+    rc.set_system(A, host.PART_BLOCKS)
+    r1 = rc.solve(b, restart=30, max_iter=500, tol=1e-10)
+    assert r0["iters"] == r1["iters"] and np.array_equal(r0["hist"], r1["hist"])
+    assert np.array_equal(r0["x"], r1["x"])
+    rc.close()
+    loc.close()
