@@ -59,7 +59,11 @@ def parse():
     p.add_argument("--no-profile", action="store_true", help="do not bracket kernels with events")
     p.add_argument("--c3-spmvs", type=int, default=20, help="SpMV launches per c3 step")
     p.add_argument("--c4-grid", type=int, default=216, help="C4: grid points per side (216^3 = 10.1M rows)")
-    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
+    p.add_argument("--dd-parts", type=int, default=8,
+                   help="dd workload on one process: shards held by this process (GG_DD_LOCAL)")
+    p.add_argument("--dd-grid", choices=["c4", "c2"], default="c4",
+                   help="dd workload system: c4 (216^3 7-pt) or c2 (1000^2 5-pt)")
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "dd"], default="c2",
                    help="c2: one C2 solve per step (the headline); c5: a backward-Euler "
                         "transient (A = G + C/h, 1%% PULSE sources) of --c5-steps time steps per step")
     p.add_argument("--c5-steps", type=int, default=100)
@@ -161,6 +165,81 @@ def bench_c3(a, torch, dist, world, rank, local):
         dist.destroy_process_group()
 
 
+def bench_dd(a, torch, dist, world, rank, local):
+    """The sharded solve (include/ggmres_dd.h): ONE system split over the ranks
+    (torchrun: one shard per GPU, RCCL exchanges; one process: --dd-parts
+    shards on this GPU, in-process exchanges).  value = inner iterations of
+    the one solve / max-over-ranks wall time ("scaling": "strong")."""
+    from ggmres import host, matrices as M
+    from ggmres.dd import DD, unique_id
+    A = M.grid_7pt(a.c4_grid) if a.dd_grid == "c4" else M.laplacian_5pt(a.grid)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    t_setup = time.perf_counter()
+    if world > 1:
+        uid = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        d = DD(world, device=local, rank=rank, uid=uid[0])
+    else:
+        d = DD(a.dd_parts, device=local)
+    d.set_system(A, host.PART_BLOCKS)
+    t_setup = time.perf_counter() - t_setup
+    info = d.info()
+    db = torch.from_numpy(b).cuda()
+    dx = torch.zeros(n, dtype=torch.float64, device="cuda")
+
+    def step():
+        dx.zero_()
+        torch.cuda.synchronize()
+        return d.solve_device(db.data_ptr(), dx.data_ptr(), restart=a.restart,
+                              max_iter=a.max_iter, tol=a.tol)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    res = [step() for _ in range(a.steps)]
+    barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el_max = float(t.item())
+    inner = sum(r["inner"] for r in res)          # one system: every rank counts the same
+    parts = world if world > 1 else a.dd_parts
+    out = {
+        "metric": METRIC, "value": round(inner / el_max, 3), "unit": "iterations/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(el_max * 1e3 / a.steps, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": (f"sharded solve: {'C4 %d^3 7-pt' % a.c4_grid if a.dd_grid == 'c4' else 'C2 %dx%d 5-pt' % (a.grid, a.grid)}"
+                                f", {parts}-way partition4 (contiguous slabs) arrow ordering, ILU(0) of "
+                                f"the permuted matrix, GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, "
+                                f"one solve per step"),
+                   "n": n, "nnz": int(A.nnz), "parts": parts,
+                   "exchange": "RCCL all-gather over xGMI" if world > 1 else
+                               f"in-process ({parts} shards on one GPU)",
+                   "separator_rows": info["nsep"], "max_interface": info["max_iface"],
+                   "wavefront_interior": info["wave_interior"],
+                   "wavefront_separator": info["wave_separator"],
+                   "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
+                   "parallelism": f"dd{parts}", "setup_s": round(t_setup, 3)},
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    d.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,6 +257,8 @@ def main():
 
     if a.workload == "c3":
         return bench_c3(a, torch, dist, world, rank, local)
+    if a.workload == "dd":
+        return bench_dd(a, torch, dist, world, rank, local)
     c5 = a.workload == "c5"
     c4 = a.workload == "c4"
     h5 = 1e-2
