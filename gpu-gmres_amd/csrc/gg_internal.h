@@ -175,7 +175,14 @@ struct DevCsr {
     DBuf<int> blk;           // nblk+1 row boundaries
     int nlong = 0;
     DBuf<int> long_rows;     // rows too long for one block (vector-per-row path)
+    // sliced ELL (one 64-row slice per wave, entry k of the slice's lane l at
+    // sptr[s] + 64 k + l, padding col -1), used when rows are short and even
+    bool sell = false;
+    int nslice = 0;
+    DBuf<int> sptr, sci;
+    DBuf<double> sv;
     void upload(const Csr &A, hipStream_t st);
+    void copy_from(const DevCsr &o, hipStream_t st);   // device-side duplicate
 };
 
 // wavefront division modes: unit diagonal, IEEE division, reciprocal + FMA corrections

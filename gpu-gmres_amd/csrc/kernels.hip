@@ -280,6 +280,47 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
     }
 }
 
+// Sliced ELL: one wave per 64-row slice, lane = row; the slice's entries are
+// read k-major (each load instruction is one coalesced 256-B / 512-B line per
+// wave), up to 8 index/value pairs in flight before their gathers; each row is
+// summed serially in CSR order from 0.0, skipping the padding (col -1): the
+// same operations as k_spmv_stream (computeSpMV order).
+template <bool RESID>
+__global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice, const int *sptr,
+                                                      const int *__restrict__ ci,
+                                                      const double *__restrict__ v,
+                                                      const double *__restrict__ x,
+                                                      const double *__restrict__ b,
+                                                      double *__restrict__ y)
+{
+    if (gated(g)) return;
+    const int s = blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (s >= nslice) return;
+    const int lane = threadIdx.x & 63;
+    const int off = sptr[s], w = (sptr[s + 1] - off) >> 6;
+    const int *cp = ci + off + lane;
+    const double *vp = v + off + lane;
+    double acc = 0.0;
+    for (int k0 = 0; k0 < w; k0 += 8) {
+        int c[8];
+        double a[8], xv[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k0 + k < w) {
+                c[k] = __builtin_nontemporal_load(cp + (k0 + k) * 64);
+                a[k] = __builtin_nontemporal_load(vp + (k0 + k) * 64);
+            }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k0 + k < w && c[k] >= 0) xv[k] = x[c[k]];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k0 + k < w && c[k] >= 0) acc += a[k] * xv[k];
+    }
+    const int r = s * 64 + lane;
+    if (r < n) y[r] = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
+}
+
 // ======================================================= triangular solves
 // Level-scheduled row solve (one launch per dependency level):
 //   x[r] = (b[r] - sum_k off[k] * x[col[k]]) / d[r]   in canonical order
@@ -1567,6 +1608,14 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
                  hipStream_t st)
 {
     if (A.nblk == 0) return;
+    if (A.sell) {
+        const int grid = (A.nslice + kBlock / 64 - 1) / (kBlock / 64);
+        if (resid)
+            k_spmv_sell<true><<<grid, kBlock, 0, st>>>(g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, b, y);
+        else
+            k_spmv_sell<false><<<grid, kBlock, 0, st>>>(g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, b, y);
+        return;
+    }
     if (resid)
         k_spmv_stream<true><<<A.nblk, kBlock, 0, st>>>(g, A.blk.p, A.rp.p, A.ci.p, A.v.p, x, b, y);
     else

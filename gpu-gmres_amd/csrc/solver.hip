@@ -45,6 +45,65 @@ void DevCsr::upload(const Csr &A, hipStream_t st)
     blk.upload(b, st);
     nlong = (int)lr.size();
     long_rows.upload(lr, st);
+    // sliced ELL when every 64-row slice is short and evenly filled (grids,
+    // banded / stencil matrices): padded entries <= 1.25 nnz + one slice
+    sell = false;
+    const char *force_csr = std::getenv("GG_SPMV_CSR");
+    if (n > 0 && !(force_csr && force_csr[0] == '1')) {
+        nslice = (n + 63) / 64;
+        std::vector<int> sp(nslice + 1, 0);
+        long long tot = 0;
+        int wmax = 0;
+        for (int s_ = 0; s_ < nslice; s_++) {
+            int w = 0;
+            for (int r = s_ * 64; r < std::min(n, s_ * 64 + 64); r++) w = std::max(w, A.rp[r + 1] - A.rp[r]);
+            wmax = std::max(wmax, w);
+            tot += 64LL * w;
+            GG_REQUIRE(tot < (1LL << 31), GG_EINVAL, "matrix too large for int32 entry offsets");
+            sp[s_ + 1] = (int)tot;
+        }
+        if (wmax <= 64 && tot <= (long long)(1.25 * nnz) + 64LL * wmax) {
+            std::vector<int> c(tot, -1);
+            std::vector<double> vv(tot, 0.0);
+            for (int r = 0; r < n; r++) {
+                const int s_ = r / 64, l = r % 64;
+                for (int k = A.rp[r]; k < A.rp[r + 1]; k++) {
+                    const long long e = sp[s_] + 64LL * (k - A.rp[r]) + l;
+                    c[e] = A.ci[k];
+                    vv[e] = A.v[k];
+                }
+            }
+            sptr.upload(sp, st);
+            sci.upload(c, st);
+            sv.upload(vv, st);
+            sell = true;
+            GG_HIP(hipStreamSynchronize(st));   // the host staging vectors go out of scope
+        }
+    }
+}
+
+void DevCsr::copy_from(const DevCsr &o, hipStream_t st)
+{
+    n = o.n;
+    nnz = o.nnz;
+    nblk = o.nblk;
+    nlong = o.nlong;
+    sell = o.sell;
+    nslice = o.nslice;
+    auto dup = [&](auto &dst, const auto &src) {
+        dst.alloc(src.n);
+        GG_HIP(hipMemcpyAsync(dst.p, src.p, src.n * sizeof(*src.p), hipMemcpyDeviceToDevice, st));
+    };
+    dup(rp, o.rp);
+    dup(ci, o.ci);
+    dup(v, o.v);
+    dup(blk, o.blk);
+    dup(long_rows, o.long_rows);
+    if (sell) {
+        dup(sptr, o.sptr);
+        dup(sci, o.sci);
+        dup(sv, o.sv);
+    }
 }
 
 long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
@@ -1058,13 +1117,7 @@ int gg_time_spmv(gg_solver *s, int reps, int nrot, double *avg_ms)
     std::vector<std::unique_ptr<DBuf<double>>> xs, ys;
     for (int k = 0; k < nrot; k++) {
         auto A = std::make_unique<DevCsr>();
-        DevCsr &src = s->dA;
-        A->n = src.n; A->nnz = src.nnz; A->nblk = src.nblk; A->nlong = src.nlong;
-        A->rp.alloc(src.rp.n); A->ci.alloc(src.ci.n); A->v.alloc(src.v.n); A->blk.alloc(src.blk.n);
-        GG_HIP(hipMemcpyAsync(A->rp.p, src.rp.p, src.rp.n * 4, hipMemcpyDeviceToDevice, s->st));
-        GG_HIP(hipMemcpyAsync(A->ci.p, src.ci.p, src.ci.n * 4, hipMemcpyDeviceToDevice, s->st));
-        GG_HIP(hipMemcpyAsync(A->v.p, src.v.p, src.v.n * 8, hipMemcpyDeviceToDevice, s->st));
-        GG_HIP(hipMemcpyAsync(A->blk.p, src.blk.p, src.blk.n * 4, hipMemcpyDeviceToDevice, s->st));
+        A->copy_from(s->dA, s->st);
         As.push_back(std::move(A));
         auto x = std::make_unique<DBuf<double>>();
         auto y = std::make_unique<DBuf<double>>();
