@@ -72,9 +72,10 @@ def parse():
 
 # bench family -> the kernel it times (rocprofv3 kernel names in profiles/)
 KERNEL_NAMES = {
-    "spmv": "k_spmv_stream<false>",
-    "trsv_L": "k_trsv_wave2d<true, 0, false>",     # lower, unit diagonal (ILU(0) L)
-    "trsv_U": "k_trsv_wave2d<false, 2, false>",    # upper, reciprocal division (ILU(0) U)
+    # sliced-ELL SpMV on short even rows (grids); GG_SPMV_CSR=1 keeps the CSR-stream kernel
+    "spmv": "k_spmv_stream<false>" if os.environ.get("GG_SPMV_CSR") == "1" else "k_spmv_sell<false>",
+    "trsv_L": "k_trsv_wave2d<true, 0, false, false>",     # lower, unit diagonal (ILU(0) L), 2D grid
+    "trsv_U": "k_trsv_wave2d<false, 2, false, false>",    # upper, reciprocal division (ILU(0) U), 2D grid
 }
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
