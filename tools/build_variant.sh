@@ -9,4 +9,4 @@ mkdir -p ../variants build/var
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -I../include/compat -I../include -Icsrc \
     "$@" -c csrc/kernels.hip -o build/var/kernels_$name.o
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../variants/libggmres_$name.so build/var/kernels_$name.o \
-    build/solver.o build/host/factor.o build/host/analysis.o build/host/partition.o build/host/mtx.o build/host/host_abi.o build/compat/interface_pg.o build/compat/format_convert.o -L/opt/rocm/lib -lamdhip64
+    $(find build -name "*.o" ! -path "build/var/*" ! -name kernels.o | sort) -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
