@@ -66,6 +66,13 @@ void split_lu_drop(const Csr &F, Csr &L, Csr &U);
 void csc_pattern(const Csr &A, std::vector<int> &cp, std::vector<int> &ri,
                  std::vector<long long> &csc2csr, std::vector<long long> &csr2csc);
 int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U);        // lofC + ilukC, 0 or GG_EZEROPIVOT
+// its pieces: lofC's patterns (L part in leftmost-pivot order, U part in
+// insertion order) and the emission of ilukC's factors in the solver's forms
+void iluk_symbolic(const Csr &A, int lof, std::vector<std::vector<int>> &Lja,
+                   std::vector<std::vector<int>> &Uja);
+void iluk_emit(const std::vector<std::vector<int>> &Lja, const std::vector<std::vector<int>> &Uja,
+               const std::vector<std::vector<double>> &Lma, const std::vector<std::vector<double>> &Uma,
+               const std::vector<double> &Draw, Csr &L, Csr &U);
 
 // canonical forms (host/analysis.cpp)
 CanonTri canon_lower_unit(const Csr &L);        // LUSolve_ignoreZero forward (diag never applied)

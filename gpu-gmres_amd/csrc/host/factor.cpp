@@ -135,12 +135,15 @@ void csc_pattern(const Csr &A, std::vector<int> &cp, std::vector<int> &ri,
         }
 }
 
-int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U)
+void iluk_symbolic(const Csr &A, int lof, std::vector<std::vector<int>> &Lja,
+                   std::vector<std::vector<int>> &Uja)
 {
     const int n = A.n;
     // ---- symbolic (lofC): per row, L part in leftmost-pivot order, U part in
     //      insertion order, with levels of fill
-    std::vector<std::vector<int>> Lja(n), Uja(n), ulvl(n);
+    Lja.assign(n, {});
+    Uja.assign(n, {});
+    std::vector<std::vector<int>> ulvl(n);
     std::vector<int> jbuf(n + 1), levls(n + 1), iw(n, -1);
     for (int i = 0; i < n; i++) {
         int incl = 0, incu = i;
@@ -181,12 +184,18 @@ int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U)
         Uja[i].assign(jbuf.begin() + i, jbuf.begin() + incu);
         ulvl[i].assign(levls.begin() + i, levls.begin() + incu);
     }
-    for (auto &u : ulvl) std::vector<int>().swap(u);
+}
+
+int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U)
+{
+    const int n = A.n;
+    std::vector<std::vector<int>> Lja, Uja;
+    iluk_symbolic(A, lof, Lja, Uja);
 
     // ---- numeric (ilukC): D kept inverted, multipliers scaled by D[jrow]
     std::vector<std::vector<double>> Lma(n), Uma(n);
     std::vector<double> D(n), Draw(n);
-    std::vector<int> &jw = iw;
+    std::vector<int> jw(n, -1);
     for (int i = 0; i < n; i++) {
         Lma[i].assign(Lja[i].size(), 0.0);
         Uma[i].assign(Uja[i].size(), 0.0);
@@ -220,6 +229,15 @@ int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U)
         D[i] = 1.0 / D[i];
     }
 
+    iluk_emit(Lja, Uja, Lma, Uma, Draw, L, U);
+    return 0;
+}
+
+void iluk_emit(const std::vector<std::vector<int>> &Lja, const std::vector<std::vector<int>> &Uja,
+               const std::vector<std::vector<double>> &Lma, const std::vector<std::vector<double>> &Uma,
+               const std::vector<double> &Draw, Csr &L, Csr &U)
+{
+    const int n = (int)Lja.size();
     // ---- emit: L strict ascending + unit diag last; U diag (un-inverted)
     //      first + strict upper ascending
     L.n = U.n = n;
@@ -240,7 +258,6 @@ int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U)
         for (int t : idx) { U.ci.push_back(Uja[i][t]); U.v.push_back(Uma[i][t]); }
         U.rp[i + 1] = (int)U.ci.size();
     }
-    return 0;
 }
 
 }  // namespace gg

@@ -47,6 +47,11 @@ void launch_gather_ports(int nport, const int *port, const double *x, double *ou
 int ilu0_columns_max_blocks();
 void launch_ilu0_columns(int n, const int *cp, const int *ri, const double *cv0, double *cv, int *level,
                          int *done, int *err, int blocks, hipStream_t st);
+// device ILU(k) numeric factorization on lofC's pattern (k_iluk_rows; co-resident grid)
+int iluk_rows_max_blocks();
+void launch_iluk_rows(int n, const long long *prow, const int *nl, const int *pcol, const long long *uptr,
+                      const long long *usrc, const long long *udst, double *val, double *dinv, double *draw,
+                      int *done, int *err, int blocks, hipStream_t st);
 void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st);  // out[i] = idx[i]<0 ? 0 : in[idx[i]]
 void launch_copy(const double *in, double *out, long long n, hipStream_t st);
 void launch_dot(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, hipStream_t st);

@@ -1069,6 +1069,71 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_columns(int n, const int *__res
     }
 }
 
+// ILU(k) numeric factorization (ilukC, src/iluk.cpp:108-188) on lofC's pattern
+// (built on the host, src/iluk.cpp:193-334).  Row i's entries: its L part in
+// lofC's order, the diagonal, its U part (prow[i] .. prow[i+1]; nl[i] L
+// entries; pcol = column).  For L entry t (column jrow) the host lists, in the
+// reference's loop order, the (source U entry of row jrow, destination entry of
+// row i) pairs whose column is in row i's pattern (jw[col] != -1).  Lane = row;
+// a row is ready when every row of its L part is done; then, per L entry in
+// order: l = val[t] * Dinv[jrow]; val[dst] = val[dst] - l * val[src] for its
+// pairs; then Draw[i] = val[diag], Dinv[i] = 1 / Draw[i] (err bit 2 on a zero
+// pivot, src/iluk.cpp:175-185), every store drained, done[i] published.  Same
+// wave-uniform retry loop and co-resident grid as k_ilu0_columns.
+__global__ __launch_bounds__(kBlock) void k_iluk_rows(int n, const long long *__restrict__ prow,
+                                                      const int *__restrict__ nl,
+                                                      const int *__restrict__ pcol,
+                                                      const long long *__restrict__ uptr,
+                                                      const long long *__restrict__ usrc,
+                                                      const long long *__restrict__ udst, double *val,
+                                                      double *dinv, double *draw, int *done, int *err)
+{
+    const int lane = threadIdx.x & 63;
+    const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
+    for (long long base = wid * 64; base < n; base += nw * 64) {
+        const int i = (int)(base + lane);
+        bool fin = i >= n;
+        int spins = 0;
+        const long long p0 = fin ? 0 : prow[i];
+        const int nli = fin ? 0 : nl[i];
+        while (__any(!fin)) {
+            bool moved = false;
+            if (!fin) {
+                bool ready = true;
+                for (int t = 0; t < nli; t++)
+                    if (ld_agent_i(done + pcol[p0 + t]) == 0) { ready = false; break; }
+                if (ready) {
+                    for (int t = 0; t < nli; t++) {
+                        const long long e = p0 + t;
+                        const double l = ld_agent_d(val + e) * ld_agent_d(dinv + pcol[e]);
+                        st_agent_d(val + e, l);
+                        for (long long q = uptr[e]; q < uptr[e + 1]; q++) {
+                            const long long d = udst[q];
+                            st_agent_d(val + d, ld_agent_d(val + d) - l * ld_agent_d(val + usrc[q]));
+                        }
+                    }
+                    const double dg = ld_agent_d(val + p0 + nli);
+                    if (dg == 0.0) atomicOr(err, 2);
+                    st_agent_d(draw + i, dg);
+                    st_agent_d(dinv + i, 1.0 / dg);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // values out before the flag
+                    st_agent_i(done + i, 1);
+                    fin = true;
+                    moved = true;
+                }
+            }
+            if (!moved && !fin) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > kSpinLimit) {
+                    atomicOr(err, 1);
+                    fin = true;
+                }
+            }
+        }
+    }
+}
+
 // ================================================== transient step (C5)
 // PULSE source values at time index it (gen_PULSEut_kernel, src/kernels.cu:223-245);
 // pulse[k] = {vlo, vhi, td, tr, tf, tw, tp}
@@ -1548,6 +1613,20 @@ void launch_ilu0_columns(int n, const int *cp, const int *ri, const double *cv0,
                          int *done, int *err, int blocks, hipStream_t st)
 {
     k_ilu0_columns<<<blocks, kBlock, 0, st>>>(n, cp, ri, cv0, cv, level, done, err);
+}
+int iluk_rows_max_blocks()
+{
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_iluk_rows, kBlock, 0) != hipSuccess) return 0;
+    return cus * per;
+}
+void launch_iluk_rows(int n, const long long *prow, const int *nl, const int *pcol, const long long *uptr,
+                      const long long *usrc, const long long *udst, double *val, double *dinv, double *draw,
+                      int *done, int *err, int blocks, hipStream_t st)
+{
+    k_iluk_rows<<<blocks, kBlock, 0, st>>>(n, prow, nl, pcol, uptr, usrc, udst, val, dinv, draw, done, err);
 }
 void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st)
 {

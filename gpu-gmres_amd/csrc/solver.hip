@@ -877,6 +877,136 @@ int gg_set_precond_ilu0_device(gg_solver *s)
     GG_API_END
 }
 
+// ILU(k) with the numeric phase on the device (k_iluk_rows): lofC's pattern
+// and the per-row update lists built on the host (the reference runs lofC on
+// the host too), A's values gathered into the pattern and factored on the
+// device, the factors emitted as iluk_itsol does; bit-identical to iluk_itsol.
+void iluk_device_factor(gg_solver *s, int level, Csr &L, Csr &U, double *ms)
+{
+    const Csr &A = s->A;
+    const int n = A.n;
+    std::vector<std::vector<int>> Lja, Uja;
+    iluk_symbolic(A, level, Lja, Uja);
+    std::vector<long long> prow(n + 1, 0);
+    std::vector<int> nl(n);
+    for (int i = 0; i < n; i++) {
+        nl[i] = (int)Lja[i].size();
+        prow[i + 1] = prow[i] + nl[i] + 1 + (long long)Uja[i].size();
+    }
+    const long long np = prow[n];
+    std::vector<int> pcol(np);
+    std::vector<long long> p2a(np, -1), uptr(np + 1, 0), usrc, udst;
+    std::vector<int> jw(n, -1);
+    for (int i = 0; i < n; i++) {
+        const long long p0 = prow[i], d0 = p0 + nl[i];
+        for (int j = 0; j < nl[i]; j++) { pcol[p0 + j] = Lja[i][j]; jw[Lja[i][j]] = (int)(p0 + j - p0); }
+        pcol[d0] = i;
+        jw[i] = nl[i];
+        for (size_t j = 0; j < Uja[i].size(); j++) { pcol[d0 + 1 + j] = Uja[i][j]; jw[Uja[i][j]] = nl[i] + 1 + (int)j; }
+        for (int k = A.rp[i]; k < A.rp[i + 1]; k++) p2a[p0 + jw[A.ci[k]]] = k;   // A's entries are in lofC's pattern
+        for (int j = 0; j < nl[i]; j++) {
+            const int jrow = Lja[i][j];
+            const long long s0 = prow[jrow] + nl[jrow] + 1;
+            for (size_t k = 0; k < Uja[jrow].size(); k++) {
+                const int jp = jw[Uja[jrow][k]];
+                if (jp < 0) continue;
+                usrc.push_back(s0 + (long long)k);
+                udst.push_back(p0 + jp);
+            }
+            uptr[p0 + j + 1] = (long long)usrc.size();
+        }
+        for (long long e = p0 + nl[i]; e < prow[i + 1]; e++) uptr[e + 1] = (long long)usrc.size();
+        for (int j = 0; j < nl[i]; j++) jw[Lja[i][j]] = -1;
+        jw[i] = -1;
+        for (int c : Uja[i]) jw[c] = -1;
+    }
+    DBuf<long long> dprow, dp2a, duptr, dusrc, dudst;
+    DBuf<int> dnl, dpcol, ddone;
+    DBuf<double> dav, dval, ddinv, ddraw;
+    dprow.upload(prow, s->st);
+    dp2a.upload(p2a, s->st);
+    duptr.upload(uptr, s->st);
+    if (usrc.empty()) { usrc.push_back(0); udst.push_back(0); }   // no updates (diagonal L parts)
+    dusrc.upload(usrc, s->st);
+    dudst.upload(udst, s->st);
+    dnl.upload(nl, s->st);
+    dpcol.upload(pcol, s->st);
+    dav.upload(A.v, s->st);
+    dval.alloc(np);
+    ddinv.alloc(n);
+    ddraw.alloc(n);
+    ddone.alloc(n);
+    if (!s->err.p) s->err.alloc(1);
+    GG_HIP(hipMemsetAsync(ddone.p, 0, (size_t)n * sizeof(int), s->st));
+    GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
+    const int maxb = iluk_rows_max_blocks();
+    GG_REQUIRE(maxb > 0, GG_EHIP, "ILU(k) device: occupancy query failed");
+    const long long need = ((long long)n + kBlock - 1) / kBlock;
+    const int blocks = (int)std::max<long long>(1, std::min<long long>(maxb, need));
+    GG_HIP(hipEventRecord(s->ev0, s->st));
+    launch_gather(dav.p, dp2a.p, dval.p, np, s->st);                    // A into the pattern, fill = 0
+    launch_iluk_rows(n, dprow.p, dnl.p, dpcol.p, duptr.p, dusrc.p, dudst.p, dval.p, ddinv.p, ddraw.p,
+                     ddone.p, s->err.p, blocks, s->st);
+    GG_HIP(hipEventRecord(s->ev1, s->st));
+    std::vector<double> val(np), draw(n);
+    GG_HIP(hipMemcpyAsync(val.data(), dval.p, (size_t)np * sizeof(double), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipMemcpyAsync(draw.data(), ddraw.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s->st));
+    int err = 0;
+    GG_HIP(hipMemcpyAsync(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
+    GG_REQUIRE((err & 1) == 0, GG_ETIMEOUT, "ILU(k) device: a row wait timed out");
+    GG_REQUIRE((err & 2) == 0, GG_EZEROPIVOT, "ILU(k): zero pivot (src/iluk.cpp:175-185)");
+    float t = 0.f;
+    GG_HIP(hipEventElapsedTime(&t, s->ev0, s->ev1));
+    if (ms) *ms = t;
+    std::vector<std::vector<double>> Lma(n), Uma(n);
+    for (int i = 0; i < n; i++) {
+        const long long p0 = prow[i];
+        Lma[i].assign(val.begin() + p0, val.begin() + p0 + nl[i]);
+        Uma[i].assign(val.begin() + p0 + nl[i] + 1, val.begin() + prow[i + 1]);
+    }
+    iluk_emit(Lja, Uja, Lma, Uma, draw, L, U);
+}
+
+int gg_set_precond_iluk_device(gg_solver *s, int level)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "set_precond before set_matrix");
+    GG_REQUIRE(level >= 0, GG_EINVAL, "ILU(k): negative level");
+    set_device(s);
+    Csr Lf, Uf;
+    iluk_device_factor(s, level, Lf, Uf, nullptr);
+    setup_left(s, Lf, Uf, GG_PRECOND_ILUK);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_iluk_device_factors(gg_solver *s, int level, int *l_row_ptr, int **l_col_idx, double **l_val,
+                           int *u_row_ptr, int **u_col_idx, double **u_val, double *ms)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "gg_iluk_device_factors: call gg_set_matrix first");
+    GG_REQUIRE(level >= 0, GG_EINVAL, "ILU(k): negative level");
+    GG_REQUIRE(l_row_ptr && l_col_idx && l_val && u_row_ptr && u_col_idx && u_val, GG_EINVAL,
+               "gg_iluk_device_factors: null output");
+    set_device(s);
+    Csr Lf, Uf;
+    iluk_device_factor(s, level, Lf, Uf, ms);
+    auto out = [](const Csr &F, int *rp, int **ci, double **v) {
+        std::copy(F.rp.begin(), F.rp.end(), rp);
+        const size_t nz = F.ci.size();
+        *ci = static_cast<int *>(std::malloc(std::max<size_t>(nz, 1) * sizeof(int)));
+        *v = static_cast<double *>(std::malloc(std::max<size_t>(nz, 1) * sizeof(double)));
+        GG_REQUIRE(*ci && *v, GG_ENOMEM, "gg_iluk_device_factors: out of host memory");
+        std::copy(F.ci.begin(), F.ci.end(), *ci);
+        std::copy(F.v.begin(), F.v.end(), *v);
+    };
+    out(Lf, l_row_ptr, l_col_idx, l_val);
+    out(Uf, u_row_ptr, u_col_idx, u_val);
+    return GG_OK;
+    GG_API_END
+}
+
 int gg_set_precond_iluk(gg_solver *s, int level)
 {
     GG_API_BEGIN

@@ -28,7 +28,7 @@ EXPORTS = [
     "gg_precond_apply", "gg_time_spmv", "gg_time_precond", "gg_bytes_spmv",
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
     "gg_trace_precond", "gg_bytes_trsv", "gg_transient", "gg_set_precond_ilu0_device",
-    "gg_ilu0_device_values",
+    "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
 ]
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
 PROF_NKINDS = 5
@@ -74,6 +74,10 @@ def lib():
                   "gg_uses_wavefront", "gg_set_precond_ilu0_device"):
             getattr(L, f).argtypes = [_VP]
         L.gg_set_precond_iluk.argtypes = [_VP, ctypes.c_int]
+        L.gg_set_precond_iluk_device.argtypes = [_VP, ctypes.c_int]
+        _PI, _PD = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)
+        L.gg_iluk_device_factors.argtypes = [_VP, ctypes.c_int, _I, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
+                                             _I, ctypes.POINTER(_PI), ctypes.POINTER(_PD), _PD]
         L.gg_ilu0_device_values.argtypes = [_VP, _D, ctypes.POINTER(ctypes.c_double)]
         L.gg_set_precond_lu.argtypes = [_VP, _I, _I, _D, _I, _I, _D]
         L.gg_set_precond_split.argtypes = [_VP, _I, _I, _D, _I, _I, _D, _D, _I, _I, _D, _D]
@@ -171,6 +175,30 @@ class Solver:
 
     def set_precond_iluk(self, level):
         _check(lib().gg_set_precond_iluk(self.h, int(level)))
+
+    def set_precond_iluk_device(self, level):
+        """ILU(k) with the numeric phase on the GPU (bit-identical factors)."""
+        _check(lib().gg_set_precond_iluk_device(self.h, int(level)))
+
+    def iluk_device_factors(self, level):
+        """((L rp, ci, v), (U rp, ci, v), device ms) of the device ILU(k)."""
+        n = self.n
+        lrp = np.zeros(n + 1, np.int32)
+        urp = np.zeros(n + 1, np.int32)
+        PI, PD = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)
+        lci, lv, uci, uv = PI(), PD(), PI(), PD()
+        ms = ctypes.c_double()
+        _check(lib().gg_iluk_device_factors(self.h, int(level), lrp, ctypes.byref(lci), ctypes.byref(lv),
+                                            urp, ctypes.byref(uci), ctypes.byref(uv), ctypes.byref(ms)))
+        out = []
+        for rp, ci, v in ((lrp, lci, lv), (urp, uci, uv)):
+            nz = int(rp[n])
+            c = np.ctypeslib.as_array(ci, shape=(max(nz, 1),))[:nz].copy()
+            x = np.ctypeslib.as_array(v, shape=(max(nz, 1),))[:nz].copy()
+            lib().gg_host_free(ctypes.cast(ci, ctypes.c_void_p))
+            lib().gg_host_free(ctypes.cast(v, ctypes.c_void_p))
+            out.append((rp, c, x))
+        return out[0], out[1], ms.value
 
     def set_precond_lu(self, L, U):
         _, lrp, lci, lv = _csr_arrays(L)

@@ -11,6 +11,8 @@
  *                          leftILU's device path (sparseTriSolve_V2 per level)
  *                                                               src/leftILU.cu:188-262, 650-702
  *   gg_set_precond_iluk    MyILUK::Initilize (ilukC, lofC)     src/preconditioner.cu:1659-1753, src/iluk.cpp:56-334
+ *   gg_set_precond_iluk_device, gg_iluk_device_factors
+ *                          the same with ilukC's numeric phase on the device  src/iluk.cpp:108-188
  *   gg_set_precond_lu      GMRES_GPU_leftILU0 L/U arguments     src/gmres.h:206-213 (src/gmres.cu:1438-1444)
  *   gg_set_precond_split   MyILUPPfloat::Initilize              src/preconditioner.cu:1205-1334
  *                          gmresInterfacePGfloat::setPrecondPG  src/gmres_interface_pg.cu:30-60
@@ -110,6 +112,16 @@ int gg_set_precond_ilu0_device(gg_solver *s);
  * A's CSR order, before the 1e-9 drop / split; ms = device time (may be NULL) */
 int gg_ilu0_device_values(gg_solver *s, double *val, double *ms);
 int gg_set_precond_iluk(gg_solver *s, int level);
+/* ILU(k) with ilukC's numeric elimination on the device (lofC's pattern and the
+ * update lists built on the host, the reference's lofC is host code too); one
+ * dataflow launch processes every row once the rows of its L part are done.
+ * Factors bit-identical to gg_set_precond_iluk. GG_EZEROPIVOT as ilukC. */
+int gg_set_precond_iluk_device(gg_solver *s, int level);
+/* those device factors in the solver's forms (L unit lower, diagonal LAST; U
+ * diagonal first); col/val arrays malloc'd by the library, release with
+ * gg_host_free (ggmres_host.h); ms = device time (may be NULL) */
+int gg_iluk_device_factors(gg_solver *s, int level, int *l_row_ptr, int **l_col_idx, double **l_val,
+                           int *u_row_ptr, int **u_col_idx, double **u_val, double *ms);
 /* L: unit lower (strict entries + unit diagonal LAST in each row; the diagonal is
  *    not applied, LUSolve_ignoreZero semantics); U: upper, diagonal first. */
 int gg_set_precond_lu(gg_solver *s,

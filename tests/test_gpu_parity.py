@@ -239,6 +239,48 @@ def test_gmres_iluk_parity(solver):
     check_exact(g, ot)
 
 
+@pytest.mark.parametrize("name,k", [("5pt_10x10", 1), ("7pt_10x10x10", 1), ("9pt_10x10", 2),
+                                    ("sherman1", 1), ("c1_5pt_100x100", 0), ("c1_5pt_100x100", 2),
+                                    ("thermal_7pt_12", 1), ("powerlaw_3000", 1)])
+def test_iluk_device_factors_bitexact(solver, name, k):
+    """ILU(k) with ilukC's numeric phase on the GPU: the same factors, bit for bit,
+    as the oracle's lofC + ilukC restatement (and hence as the host path)."""
+    A = MATS[name]()
+    solver.set_matrix(A)
+    try:
+        Lo, Uo = O.iluk(A, k)
+    except ZeroDivisionError:
+        with pytest.raises(ggmres.GGError):
+            solver.iluk_device_factors(k)
+        return
+    (lrp, lci, lv), (urp, uci, uv), ms = solver.iluk_device_factors(k)
+    assert ms > 0
+    for (rp, ci, v), o in (((lrp, lci, lv), Lo), ((urp, uci, uv), Uo)):
+        assert np.array_equal(rp, o.rp) and np.array_equal(ci, o.ci)
+        assert np.array_equal(v, o.v)
+
+
+def test_gmres_iluk_device_parity(solver):
+    """GMRES with the device-factored ILU(1): identical to the host-factored run."""
+    A = M.grid_7pt(10, 10, 8)
+    b = M.rhs_uniform(A.shape[0])
+    L, U = O.iluk(A, 1)
+    o, ot = oracle_both(lambda: O.gmres_left(A, L, U, b, m=20, max_iter=1000, tol=1e-10),
+                        A.shape[0])
+    solver.set_matrix(A)
+    solver.set_precond_iluk_device(1)
+    g = solver.solve(b, restart=20, max_iter=1000, tol=1e-10)
+    check_gmres(g, o)
+    check_exact(g, ot)
+
+
+def test_iluk_device_zero_pivot(solver):
+    import scipy.sparse as sp
+    solver.set_matrix(sp.csr_matrix(np.array([[0.0, 1.0], [1.0, 1.0]])))
+    with pytest.raises(ggmres.GGError):
+        solver.set_precond_iluk_device(1)
+
+
 def test_gmres_split_parity(solver):
     A = M.laplacian_5pt(40)
     P = make_split(A, seed=9)
