@@ -78,6 +78,11 @@ KERNEL_NAMES = {
     "trsv_U": "k_trsv_wave2d<false, 2, false, false>",    # upper, reciprocal division (ILU(0) U), 2D grid
 }
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
+# bare dependent-chain latency of one wavefront step (cycles, tools/lat_probe.hip:
+# "step(dpp)" = unit L, "U step (WD_RCP)" = U with the reciprocal-FMA division)
+# and the shader clock it ran at (profiles/r01_lat_probe.txt)
+CHAIN_CYCLES = {"trsv_L": 39.2, "trsv_U": 63.4}
+SHADER_GHZ = 2.396
 
 
 def pmc_traffic(kernel, workload=None):
@@ -382,6 +387,17 @@ def main():
                 else None,
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
                 "launches_timed": f["launches"]}
+    # the triangular solves are latency-bound: their other roofline is the
+    # dependency chain, nx + ny - 1 wavefront steps at the bare per-step chain
+    # latency (tools/lat_probe.hip on MI355X, profiles/r01_lat_probe.txt)
+    lat = None
+    if roof and dom in ("trsv_L", "trsv_U") and s.uses_wavefront and not c4 and not c5:
+        cyc = CHAIN_CYCLES["trsv_L" if dom == "trsv_L" else "trsv_U"]
+        steps = 2 * a.grid - 1
+        floor_us = steps * cyc / (SHADER_GHZ * 1e3)
+        lat = {"kernel": roof["kernel"], "bound": "dependency chain", "critical_steps": steps,
+               "cycles_per_step": cyc, "clock_ghz": SHADER_GHZ, "floor_us": round(floor_us, 2),
+               "achieved_us": roof["avg_us"], "frac": round(floor_us / roof["avg_us"], 4)}
     spmv_bytes = s.bytes_spmv()
     # isolated SpMV (4 rotating copies of A, x, y: > 256 MiB, not Infinity-Cache served)
     spmv_iso_ms = s.time_spmv(reps=100, nrot=4)
@@ -421,7 +437,7 @@ def main():
                    "wavefront_sptrsv": s.uses_wavefront,
                    "parallelism": "single" if world == 1 else f"replicas{world}",
                    "setup_s": round(t_setup, 3)},
-        "roofline": roof,
+        "roofline": roof, "latency_roofline": lat,
         "kernels": fam,
         "kernels_from": "one profiled warmup step, every family bracketed by hipEvents",
         "spmv_isolated": spmv_iso,

@@ -18,6 +18,17 @@ __device__ __forceinline__ double dpp_zero_rowshr(double v)
     return __hiloint2double(hi, lo);
 }
 
+// the same shift with bound_ctrl (out-of-range lanes read 0) and the edge lane's
+// value selected afterwards: no `old` operand tied into the DPP move
+template <int CTRL, int EDGE>
+__device__ __forceinline__ double dpp_sel(double v, double old)
+{
+    int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
+    int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
+    const double t = __hiloint2double(hi, lo);
+    return (threadIdx.x & 63) == EDGE ? old : t;
+}
+
 constexpr int N = 256;
 
 __global__ void k_probe(const double *in, double *out, long long *cyc)
@@ -56,6 +67,32 @@ __global__ void k_probe(const double *in, double *out, long long *cyc)
     TIMED(16, x = dpp_old<0x13C>(x, d))
     TIMED(17, x = dpp_zero_rowshr(x) + b)
     TIMED(18, x = __shfl_up(x, 1, 64) + b)
+    // the wavefront U step exactly (k_trsv_wave2d WD_RCP): DPP, mul, two subs,
+    // q0 = acc*y and the two FMA corrections
+    TIMED(19, { double acc = (c - b * dpp_old<0x130>(x, d)) - d * x; double q0 = acc * c;
+                double q1 = __builtin_fma(-__builtin_fma(q0, a, -acc), c, q0);
+                x = __builtin_fma(-__builtin_fma(q1, a, -acc), c, q1); })
+    TIMED(20, x = (dpp_sel<0x138, 0>(x, d)))
+    TIMED(21, x = (c - b * dpp_sel<0x138, 0>(x, d)) - d * x)
+    TIMED(22, { double acc = (c - b * dpp_sel<0x130, 63>(x, d)) - d * x; double q0 = acc * c;
+                double q1 = __builtin_fma(-__builtin_fma(q0, a, -acc), c, q0);
+                x = __builtin_fma(-__builtin_fma(q1, a, -acc), c, q1); })
+}
+
+// shader clock vs the constant 100 MHz real-time counter over a long chain
+__global__ void k_clock(const double *in, double *out, long long *cyc)
+{
+    const int l = threadIdx.x;
+    double x = in[l], b = in[64 + l];
+    long long t0, t1, r0, r1;
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+    asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(r0)::"memory");
+    for (int i = 0; i < (1 << 20); i++) x = x * b;
+    { int f = __builtin_amdgcn_readfirstlane(__double2hiint(x)); asm volatile("; use %0" ::"s"(f)); }
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+    out[l] = x;
+    if (l == 0) { cyc[0] = t1 - t0; cyc[1] = r1 - r0; }
 }
 
 // same dependent step chain, wave 0 only, other waves of the block parked
@@ -101,8 +138,9 @@ int main()
     const char *names[] = {"add", "mul", "fma", "step(no dpp)", "step(dpp)", "div", "markstein div",
                            "dpp only", "step+div", "step+markstein", "add x2 indep", "rcp",
                            "row_shr:1", "row_bcast:15", "quad_perm", "step(row_shr)", "wave_ror:1",
-                           "row_shr+add", "shfl_up+add"};
-    for (int i = 0; i < 19; i++) printf("%-16s %7.2f cycles/iter\n", names[i], (double)hc[i] / N);
+                           "row_shr+add", "shfl_up+add", "U step (WD_RCP)",
+                           "wave_shr sel", "step(wave_shr sel)", "U step (sel)"};
+    for (int i = 0; i < 23; i++) printf("%-16s %7.2f cycles/iter\n", names[i], (double)hc[i] / N);
     for (int nw : {1, 5, 7}) {
         for (int mode = 0; mode < 3; mode++) {
             for (int rep = 0; rep < 3; rep++) {
@@ -119,5 +157,9 @@ int main()
         hipMemcpy(hc, dc, sizeof(long long), hipMemcpyDeviceToHost);
         printf("grid %d blocks x 5 waves, mode 2: step(dpp) %7.2f cycles/iter\n", nb, (double)hc[0] / N);
     }
+    for (int rep = 0; rep < 2; rep++) k_clock<<<1, 64>>>(din, dout, dc);
+    hipMemcpy(hc, dc, 2 * sizeof(long long), hipMemcpyDeviceToHost);
+    printf("shader clock %.3f GHz (s_memtime / s_memrealtime at 100 MHz, one wave)\n",
+           (double)hc[0] / (double)hc[1] * 0.1);
     return 0;
 }
