@@ -33,6 +33,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -67,6 +68,9 @@ def parse():
                    help="c2: one C2 solve per step (the headline); c5: a backward-Euler "
                         "transient (A = G + C/h, 1%% PULSE sources) of --c5-steps time steps per step")
     p.add_argument("--c5-steps", type=int, default=100)
+    p.add_argument("--c5-scenarios", type=int, default=1,
+                   help="c5: independent source scenarios per GPU, solved concurrently (one solver, "
+                        "stream and host thread each; GG_SOLVE_SHARED_DEVICE)")
     return p.parse_args()
 
 
@@ -281,17 +285,40 @@ def main():
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
     if c5:
-        # scenario per rank: its own seeded source set (independent many-RHS scenarios)
-        nodes, pulses = M.pulse_sources(n, frac=0.01, h=h5, seed=20261015 + rank)
+        # independent many-RHS scenarios, each its own seeded source set: S per
+        # rank, solved concurrently on the rank's GPU when S > 1
+        S = max(1, a.c5_scenarios)
+        scen = [M.pulse_sources(n, frac=0.01, h=h5, seed=20261015 + rank * S + k) for k in range(S)]
         cdiag = np.full(n, 1e-3 / h5)
         ports = np.array([0, n // 2, n - 1], np.int32)
+        solvers = [s]
+        for _ in range(S - 1):
+            s2 = ggmres.Solver(local)
+            s2.set_matrix(A)
+            s2.set_precond_ilu0()
+            solvers.append(s2)
+        flags = ggmres.SOLVE_SHARED_DEVICE if S > 1 else 0
 
     def step():
         if c5:
-            r = s.transient(a.c5_steps, h5, cdiag, nodes, pulses, ports, np.zeros(n),
-                            restart=a.restart, max_iter=a.max_iter, tol=a.tol)
-            return dict(inner=r["iters_total"], iters=r["iters_total"], relres=None,
-                        ret=r["ret"])
+            out = [None] * len(solvers)
+
+            def run(k):
+                nodes, pulses = scen[k]
+                out[k] = solvers[k].transient(a.c5_steps, h5, cdiag, nodes, pulses, ports, np.zeros(n),
+                                              restart=a.restart, max_iter=a.max_iter, tol=a.tol,
+                                              flags=flags)
+
+            if len(solvers) == 1:
+                run(0)
+            else:
+                th = [threading.Thread(target=run, args=(k,)) for k in range(len(solvers))]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join()
+            tot = sum(r["iters_total"] for r in out)
+            return dict(inner=tot, iters=tot, relres=None, ret=max(r["ret"] for r in out))
         dx.zero_()
         torch.cuda.synchronize()
         return s.solve_device(db.data_ptr(), dx.data_ptr(), restart=a.restart,
@@ -427,9 +454,10 @@ def main():
                                 f"sum|off| + 1e-3), ILU(0) left, GMRES({a.restart}), tol {a.tol:g}, "
                                 f"b=A*1, x0=0, one solve per step, one GPU") if c4 else
                                (f"C5: {a.grid}x{a.grid} 5-pt grid, A = G + C/h (c 1e-3, h 1e-2), "
-                                f"1% PULSE sources (own scenario per rank), ILU(0) left, "
+                                f"1% PULSE sources (own seeded scenarios), ILU(0) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, {a.c5_steps} backward-Euler "
-                                f"steps per step, warm start") if c5 else
+                                f"steps per step, warm start, {a.c5_scenarios} concurrent scenario(s) "
+                                f"per GPU") if c5 else
                                (f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU(0) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step"),
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
@@ -445,7 +473,8 @@ def main():
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    s.close()
+    for s_ in (solvers if c5 else [s]):
+        s_.close()
     if dist:
         dist.destroy_process_group()
 

@@ -209,6 +209,7 @@ struct gg_solver {
     DBuf<double> partA, partB, H, s, cs, sn, ysm;
     // persistent Arnoldi orthogonalization (kernels.hip k_arnoldi_persist)
     bool persist = false;
+    bool shared = false;                // GG_SOLVE_SHARED_DEVICE for the solve in progress
     DBuf<unsigned long long> gran;      // m * (m+2) * G hand-off granules, re-armed per cycle
     DBuf<double> hist;
     long long hist_cap = 0;
@@ -460,7 +461,8 @@ void enqueue_cycle(gg_solver *s, int m)
     const long long P = s->Ppad;
     const bool split = s->pkind == GG_PRECOND_SPLIT;
     launch_init_cycle(ds, s->r.p, s->V.p, s->s.p, s->G, P, s->st);
-    if (s->persist) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
+    const bool persist = s->persist && !s->shared;
+    if (persist) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
     for (int i = 0; i < m; i++) {
         Gate gi;
         gi.done = &ds->done;
@@ -486,7 +488,7 @@ void enqueue_cycle(gg_solver *s, int m)
             prof_end(s, mk);
         }
         mk = prof_begin(s, GG_PROF_MGS, i);
-        if (s->persist) {
+        if (persist) {
             launch_arnoldi_persist(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                    s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, s->G, P,
                                    s->err.p, s->st);
@@ -563,6 +565,16 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
     const int m = opt->restart;
     GG_REQUIRE(m >= 1 && m <= 512, GG_EINVAL, "gg_solve: restart must be in [1, 512]");
     GG_REQUIRE(opt->max_iter >= 0, GG_EINVAL, "gg_solve: negative max_iter");
+    GG_REQUIRE((opt->flags & ~GG_SOLVE_SHARED_DEVICE) == 0, GG_EINVAL, "gg_solve: unknown flags");
+    s->shared = (opt->flags & GG_SOLVE_SHARED_DEVICE) != 0;
+    if (s->shared) {
+        // only kernels whose workgroups wait on earlier-dispatched ones
+        bool ok = s->pkind == GG_PRECOND_NONE;
+        if (s->pkind != GG_PRECOND_SPLIT && s->pkind != GG_PRECOND_NONE)
+            ok = s->L.kind == DevTri::WAVE2D && s->U.kind == DevTri::WAVE2D && s->L.wl.nz == 1;
+        GG_REQUIRE(ok, GG_EINVAL, "gg_solve: GG_SOLVE_SHARED_DEVICE needs the 2D wavefront path "
+                                  "(or no preconditioner)");
+    }
     const int n = s->A.n;
     set_device(s);
     ensure_workspace(s, m);

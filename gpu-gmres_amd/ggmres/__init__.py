@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("GGMRES_LIB") or os.path.join(PKG_ROOT, "lib", "libggm
 GG_OK, GG_NOT_CONVERGED = 0, 1
 PRECOND_NONE, PRECOND_ILU0, PRECOND_ILUK, PRECOND_LU, PRECOND_SPLIT = range(5)
 APPLY_MINV, APPLY_LEFT, APPLY_RIGHT, APPLY_START = range(4)
-FLAG_NO_GRAPH, FLAG_NO_WAVEFRONT = 0x1, 0x2
+SOLVE_SHARED_DEVICE = 0x1     # gg_options.flags: other solvers share the device (ggmres.h)
 
 # every symbol include/ggmres.h declares (checked by tests/test_abi.py)
 EXPORTS = [

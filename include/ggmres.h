@@ -78,8 +78,17 @@ typedef struct gg_options {
     int restart;       /* m  (reference default 32, src/defs.h:11)                 */
     int max_iter;      /* reference semantics: in = limit                          */
     double tol;        /* relative residual target on ||M r|| / ||M b||            */
-    int flags;         /* reserved, 0                                             */
+    int flags;         /* GG_SOLVE_* bits, else 0                                 */
 } gg_options;
+
+/* gg_options.flags: other solvers run on this device at the same time (one
+ * solver object, stream and host thread per system, e.g. the many-RHS
+ * scenarios of a transient study).  The solve then launches no kernel that
+ * needs the whole device co-resident (the orthogonalization takes the
+ * per-step kernels instead of the persistent launch); it requires the 2D
+ * wavefront triangular solve or no preconditioner (else GG_EINVAL), whose
+ * workgroups only wait on workgroups dispatched before them. */
+#define GG_SOLVE_SHARED_DEVICE 0x1
 
 typedef struct gg_result {
     int status;        /* GG_OK / GG_NOT_CONVERGED / error                        */

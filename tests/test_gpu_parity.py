@@ -326,6 +326,49 @@ def test_edge_cases(solver):
         check_exact(g, ot)
 
 
+def test_concurrent_shared_solves(solver):
+    """GG_SOLVE_SHARED_DEVICE: four solvers (own streams) solving at the same
+    time from four host threads; each result bit-identical to the
+    order-matched oracle (the flag swaps the persistent orthogonalization
+    launch for the per-step kernels, same arithmetic)."""
+    import threading
+    A = M.laplacian_5pt(300, 256)
+    L, U = O.ilu0(A)
+    bs = [M.rhs_uniform(A.shape[0], seed=50 + k) for k in range(4)]
+    refs = [oracle_both(lambda b=b: O.gmres_left(A, L, U, b, m=30, max_iter=90, tol=1e-300),
+                        A.shape[0], nx=300)[1] for b in bs]
+    ss = [ggmres.Solver(0) for _ in range(4)]
+    try:
+        for s_ in ss:
+            s_.set_matrix(A)
+            s_.set_precond_ilu0()
+        out = [None] * 4
+
+        def run(k):
+            out[k] = ss[k].solve(bs[k], restart=30, max_iter=90, tol=1e-300,
+                                 flags=ggmres.SOLVE_SHARED_DEVICE)
+
+        th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for g, ot in zip(out, refs):
+            check_exact(g, ot)
+    finally:
+        for s_ in ss:
+            s_.close()
+
+
+def test_shared_flag_needs_2d_wavefront(solver):
+    solver.set_matrix(MATS["sherman1"]())
+    solver.set_precond_ilu0()
+    with pytest.raises(ggmres.GGError):
+        solver.solve(np.ones(solver.n), flags=ggmres.SOLVE_SHARED_DEVICE)
+    with pytest.raises(ggmres.GGError):
+        solver.solve(np.ones(solver.n), flags=0x100)
+
+
 def test_repeated_solves_identical(solver):
     A = M.laplacian_5pt(100)
     b = M.rhs_uniform(A.shape[0])
