@@ -11,9 +11,12 @@
 //
 // Per Arnoldi iteration: pack+all-gather of v_i's interface (SpMV), of the
 // forward solve's interface, and one 8*G-byte all-gather per MGS dot.
-// Everything is enqueued on one stream per process; RCCL collectives run on
-// that stream in between the (gated) kernels, so a whole restart cycle is
-// enqueued with one host read of the control block per cycle, as solver.hip.
+// The SpMV's exchange runs on a second stream beside the interior rows' SpMV
+// (interior rows reference only their interior and the separator replica);
+// the separator rows wait for it.  Everything else, RCCL collectives included,
+// is enqueued on the main stream between the (gated) kernels, so a whole
+// restart cycle is enqueued with one host read of the control block per
+// cycle, as solver.hip.
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -42,7 +45,7 @@ struct Shard {
     Wave2D wI, wS;
     std::vector<long long> slotI, slotS;    // region-local row -> region slot (host)
     long long PIr = 0, PSr = 0;             // region slot counts (multiples of 512)
-    DevCsr A, LSH, UIS;
+    DevCsr AI, AS, LSH, UIS;                // A's interior rows [0, S0) and separator rows [S0, H0)
     DevTri LI, LS, UI, US;
     DBuf<long long> iface_slot;             // maxI: own interface slots (-1 pad)
     DBuf<long long> slot2nat;               // H0: natural row of each slot (-1 pad)
@@ -65,7 +68,8 @@ struct gg_dd {
     int device = 0, P = 1, kind = GG_DD_LOCAL, rank = 0;
     ncclComm_t comm = nullptr;
     hipStream_t st = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t st2 = nullptr;              // the SpMV's interface exchange, beside the interior rows
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evx = nullptr, evh = nullptr;
     bool have = false;
     int n = 0, nsep = 0, maxI = 0;
     std::vector<int> pinv, q;
@@ -125,30 +129,32 @@ long long agree_max(gg_dd *d, long long v)
 }
 
 // all-gather of the slot each shard owns in buf(s) + off: slot q at off + q*cnt
-void exchange(gg_dd *d, const Get &buf, long long off, long long cnt)
+void exchange(gg_dd *d, const Get &buf, long long off, long long cnt, hipStream_t st)
 {
     if (d->P == 1 || cnt == 0) return;
     if (d->kind == GG_DD_RCCL) {
         Shard &s = *d->sh[0];
         double *b = buf(s) + off;
-        GG_NCCL(ncclAllGather(b + (long long)s.p * cnt, b, (size_t)cnt, ncclDouble, d->comm, d->st));
+        GG_NCCL(ncclAllGather(b + (long long)s.p * cnt, b, (size_t)cnt, ncclDouble, d->comm, st));
     } else {
         ShardPtrs ptr{};
         for (int q = 0; q < d->P; q++) ptr.p[q] = buf(*d->sh[q]);
-        launch_allgather_local(ptr, d->P, off, cnt, d->st);
+        launch_allgather_local(ptr, d->P, off, cnt, st);
     }
 }
+void exchange(gg_dd *d, const Get &buf, long long off, long long cnt) { exchange(d, buf, off, cnt, d->st); }
 // own interface values of vector x -> halo slot p, then the all-gather
-void halo(gg_dd *d, const Get &x)
+void halo(gg_dd *d, const Get &x, hipStream_t st)
 {
     if (d->maxI == 0 || d->P == 1) return;
     for (auto &sp : d->sh) {
         Shard &s = *sp;
         double *v = x(s);
-        launch_gather(v, s.iface_slot.p, v + d->H0 + (long long)s.p * d->maxI, d->maxI, d->st);
+        launch_gather(v, s.iface_slot.p, v + d->H0 + (long long)s.p * d->maxI, d->maxI, st);
     }
-    exchange(d, x, d->H0, d->maxI);
+    exchange(d, x, d->H0, d->maxI, st);
 }
+void halo(gg_dd *d, const Get &x) { halo(d, x, d->st); }
 
 Get vec(DBuf<double> Shard::*m) { return [m](Shard &s) { return (s.*m).p; }; }
 
@@ -179,21 +185,38 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
     }
 }
 
-void spmv(gg_dd *d, int gi, const Get &x, const Get &y)   // y = A x
+// y = A x (b = null) or y = b - A x: the interior rows reference only their
+// own interior and the separator replica, so they run on the main stream while
+// the interface exchange runs on the second; the separator rows follow it
+void spmv_rows(gg_dd *d, const Get &x, const Get &b, const Get &y, bool resid,
+               const std::function<Gate(Shard &)> &gate)
 {
-    halo(d, x);
+    const long long S0 = d->S0;
+    const bool xch = d->maxI > 0 && d->P > 1;
+    if (xch) {
+        GG_HIP(hipEventRecord(d->evx, d->st));              // x complete
+        GG_HIP(hipStreamWaitEvent(d->st2, d->evx, 0));
+        halo(d, x, d->st2);
+        GG_HIP(hipEventRecord(d->evh, d->st2));
+    }
     for (auto &sp : d->sh) {
         Shard &s = *sp;
-        launch_spmv(gate_of(s, gi, 0), s.A, x(s), nullptr, y(s), false, d->st);
+        launch_spmv(gate(s), s.AI, x(s), resid ? b(s) : nullptr, y(s), resid, d->st);
     }
+    if (xch) GG_HIP(hipStreamWaitEvent(d->st, d->evh, 0));
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        launch_spmv(gate(s), s.AS, x(s), resid ? b(s) + S0 : nullptr, y(s) + S0, resid, d->st);
+    }
+}
+void spmv(gg_dd *d, int gi, const Get &x, const Get &y)   // y = A x
+{
+    spmv_rows(d, x, Get{}, y, false, [&](Shard &s) { return gate_of(s, gi, 0); });
 }
 void resid(gg_dd *d, int mask)   // rr = b - A x
 {
-    halo(d, vec(&Shard::xv));
-    for (auto &sp : d->sh) {
-        Shard &s = *sp;
-        launch_spmv(gate_of(s, -1, mask), s.A, s.xv.p, s.bv.p, s.rr.p, true, d->st);
-    }
+    spmv_rows(d, vec(&Shard::xv), vec(&Shard::bv), vec(&Shard::rr), true,
+              [&](Shard &s) { return gate_of(s, -1, mask); });
 }
 long long dot_len(gg_dd *d, const Shard &s) { return s.p == 0 ? d->H0 : d->S0; }
 
@@ -533,7 +556,19 @@ void set_system(gg_dd *d, const Csr &A, int method)
             return H0 + (c - nI - nS);
         };
         Csr As = slot_csr(H.A, lslot, H0, lcol);
-        s.A.upload(As, d->st);
+        // split at S0: interior rows, separator rows (columns stay slot indices)
+        Csr AI, AS;
+        AI.n = (int)S0;
+        AI.rp.assign(As.rp.begin(), As.rp.begin() + S0 + 1);
+        AI.ci.assign(As.ci.begin(), As.ci.begin() + As.rp[S0]);
+        AI.v.assign(As.v.begin(), As.v.begin() + As.rp[S0]);
+        AS.n = (int)(H0 - S0);
+        AS.rp.resize(AS.n + 1);
+        for (int r = 0; r <= AS.n; r++) AS.rp[r] = As.rp[S0 + r] - As.rp[S0];
+        AS.ci.assign(As.ci.begin() + As.rp[S0], As.ci.end());
+        AS.v.assign(As.v.begin() + As.rp[S0], As.v.end());
+        s.AI.upload(AI, d->st);
+        s.AS.upload(AS, d->st);
         s.bytes_spmv = 12.0 * H.A.nnz() + 4.0 * (H0 + 1) + 16.0 * (nI + nS);
         // triangles on their regions
         build_tri(s.LI, H.LI, &s.wI, &s.slotI, s.PIr, d->st);
@@ -616,8 +651,11 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
     d->rank = comm == GG_DD_RCCL ? rank : 0;
     set_dev(d.get());
     GG_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
+    GG_HIP(hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking));
     GG_HIP(hipEventCreate(&d->ev0));
     GG_HIP(hipEventCreate(&d->ev1));
+    GG_HIP(hipEventCreateWithFlags(&d->evx, hipEventDisableTiming));
+    GG_HIP(hipEventCreateWithFlags(&d->evh, hipEventDisableTiming));
     if (comm == GG_DD_RCCL) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
@@ -639,6 +677,10 @@ int gg_dd_destroy(gg_dd *d)
     if (d->comm) (void)ncclCommDestroy(d->comm);
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
+    if (d->evx) (void)hipEventDestroy(d->evx);
+    if (d->evh) (void)hipEventDestroy(d->evh);
+    if (d->st2) (void)hipStreamSynchronize(d->st2);
+    if (d->st2) (void)hipStreamDestroy(d->st2);
     if (d->st) (void)hipStreamDestroy(d->st);
     delete d;
     return GG_OK;
