@@ -6,6 +6,7 @@ Bars (DESIGN.md "Parity"):
   * GMRES residual history and solution: within 1e-10 relative per entry
     (north_star), identical iteration counts and return codes.
 """
+import glob
 import os
 
 import numpy as np
@@ -59,6 +60,38 @@ def test_spmv_bitexact(solver, name):
     solver.set_precond_ilu0()   # wavefront layout where it applies
     assert solver.uses_wavefront == (name in WAVE)
     assert np.array_equal(solver.spmv(x), O.spmv(A, x))
+
+
+RANDOMS = sorted(os.path.basename(f) for f in glob.glob(fixture_path(os.path.join("random_10x10", "*.mtx"))))
+
+
+@pytest.mark.parametrize("name", RANDOMS)
+def test_spmv_random_fixtures(solver, name):
+    """The cusp random_10x10 fixtures (0-100 nonzeros, empty rows and an empty
+    matrix): SpMV bit-exact vs the oracle, with x random and the reference
+    driver's default y = 0.5 input (src_thermal/main.cu:128-133)."""
+    A = load(os.path.join("random_10x10", name))
+    solver.set_matrix(A)
+    solver.set_precond_none()
+    for x in (np.random.default_rng(7).standard_normal(A.shape[0]), np.full(A.shape[0], 0.5)):
+        assert np.array_equal(solver.spmv(x), O.spmv(A, x))
+
+
+@pytest.mark.parametrize("name", ["5pt_10x10", "7pt_10x10x10", "9pt_10x10", "3pt_100"])
+def test_gmres_driver_default_rhs(solver, name):
+    """The reference driver's CPU-vs-GPU GMRES check (src_thermal/main.cu:459-527)
+    on its fixtures with its default right-hand side y = 0.5: bit-identical to
+    the order-matched oracle, within 1e-10 of the serial one."""
+    A = MATS[name]()
+    b = np.full(A.shape[0], 0.5)
+    L, U = O.ilu0(A)
+    o, ot = oracle_both(lambda: O.gmres_left(A, L, U, b, m=32, max_iter=1000, tol=1e-10),
+                        A.shape[0], *(GRID[name] if name in GRID else (None, None)))
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    g = solver.solve(b, restart=32, max_iter=1000, tol=1e-10)
+    check_gmres(g, o)
+    check_exact(g, ot)
 
 
 def test_spmv_long_rows(solver):
