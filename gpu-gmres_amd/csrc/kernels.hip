@@ -59,6 +59,13 @@ __device__ __forceinline__ double2 ld2(const double *p, long long u)
 {
     return reinterpret_cast<const double2 *>(p)[u];
 }
+// streamed once: non-temporal (does not displace re-used data from the caches)
+typedef double dbl2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ld2_nt(const double *p, long long u)
+{
+    const dbl2v v = __builtin_nontemporal_load(reinterpret_cast<const dbl2v *>(p) + u);
+    return make_double2(v.x, v.y);
+}
 __device__ __forceinline__ void st2(double *p, long long u, double2 v)
 {
     reinterpret_cast<double2 *>(p)[u] = v;
@@ -1254,9 +1261,9 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
         for (int j = 0; j < kUnroll; j++) {
             const long long u = u0 + j * stride;
             if (u < units) {
-                wv[j] = ld2(w, u);
-                vv[j] = ld2(vk, u);
-                if (!NORM) nv[j] = ld2(vnext, u);
+                wv[j] = ld2(w, u);          // w: re-read every step, kept in the caches
+                vv[j] = ld2_nt(vk, u);      // the basis vectors are streamed
+                if (!NORM) nv[j] = ld2_nt(vnext, u);
             }
         }
     };
