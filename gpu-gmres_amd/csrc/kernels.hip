@@ -1430,7 +1430,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             const double *vnp = V + (long long)(k + 1) * ldv;
 #pragma unroll
             for (int j = 0; j < J; j++)
-                if (u0 + j * stride < units) vn[j] = ld2(vnp, u0 + j * stride);
+                if (u0 + j * stride < units) vn[j] = ld2_nt(vnp, u0 + j * stride);   // streamed
         }
         const double h = gather_sum(gran + (long long)k * G, G, err);
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
