@@ -210,6 +210,10 @@ struct gg_solver {
     // persistent Arnoldi orthogonalization (kernels.hip k_arnoldi_persist)
     bool persist = false;
     bool shared = false;                // GG_SOLVE_SHARED_DEVICE for the solve in progress
+    // pinned host copies of the control block and the error word (one
+    // round trip per restart cycle reads both)
+    DevState *h_state = nullptr;
+    int *h_err = nullptr;
     DBuf<unsigned long long> gran;      // m * (m+2) * G hand-off granules, re-armed per cycle
     DBuf<double> hist;
     long long hist_cap = 0;
@@ -549,6 +553,21 @@ void check_err(gg_solver *s)
     GG_REQUIRE((err & 1) == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
     if (err & 2) throw RcpFallback{};
 }
+// the control block and the error word in one round trip (after a cycle)
+DevState read_state_checked(gg_solver *s)
+{
+    if (!s->h_state) {
+        GG_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_state), sizeof(DevState), hipHostMallocDefault));
+        GG_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), sizeof(int), hipHostMallocDefault));
+    }
+    GG_HIP(hipMemcpyAsync(s->h_state, s->ds.p, sizeof(DevState), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipMemcpyAsync(s->h_err, s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
+    const int err = *s->h_err;
+    GG_REQUIRE((err & 1) == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+    if (err & 2) throw RcpFallback{};
+    return *s->h_state;
+}
 // switch every WD_RCP triangle to IEEE division for the rest of the solver's life
 void demote_rcp(gg_solver *s)
 {
@@ -620,8 +639,7 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
             restarts++;
             enqueue_cycle(s, m);
             DevState prev = h;
-            h = read_state(s);
-            check_err(s);
+            h = read_state_checked(s);
             prof_collect(s, (h.done & DONE_INNER) ? h.conv_i + 1 : h.nit);
             if (h.done & DONE_INNER) {
                 ret = 0;
@@ -747,6 +765,8 @@ int gg_destroy(gg_solver *s)
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     for (hipEvent_t e : s->prof_pool) (void)hipEventDestroy(e);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->h_state) (void)hipHostFree(s->h_state);
+    if (s->h_err) (void)hipHostFree(s->h_err);
     hipStream_t st = s->st;
     delete s;
     if (st) (void)hipStreamDestroy(st);
