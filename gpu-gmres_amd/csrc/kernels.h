@@ -38,9 +38,9 @@ int reduce_grid(long long units);  // blocks for the vector kernels (units = Ppa
 
 // ---- vector ops (lengths are Ppad, a multiple of 512) --------------------
 void launch_fill_u64(unsigned long long *p, long long n, unsigned long long v, hipStream_t st);
-// transient step: u = PULSE(it*h); w = B u + (C/h) x   (natural order, n rows)
-void launch_transient_step(int n, int nsrc, const double *pulse, int it, double h, double *u,
-                           const int *src_ptr, const int *src_idx, const double *cdiag,
+// transient step: u = sources(it*h) (DC / PULSE / PWL); w = B u + (C/h) x   (natural order, n rows)
+void launch_transient_step(int n, int nsrc, const int *kind, const int *dptr, const double *data, int it,
+                           double h, double *u, const int *src_ptr, const int *src_idx, const double *cdiag,
                            const double *x, double *w, hipStream_t st);
 void launch_gather_ports(int nport, const int *port, const double *x, double *out, hipStream_t st);
 // device ILU(0) column elimination (co-resident grid of at most ilu0_columns_max_blocks())

@@ -1144,20 +1144,49 @@ __global__ __launch_bounds__(kBlock) void k_iluk_rows(int n, const long long *__
 // ================================================== transient step (C5)
 // PULSE source values at time index it (gen_PULSEut_kernel, src/kernels.cu:223-245);
 // pulse[k] = {vlo, vhi, td, tr, tf, tw, tp}
-__global__ void k_pulse(int nsrc, const double *pulse, int it, double h, double *u)
+// Source values at time index it, t = it * h (mytime = idxt * tstep), one
+// thread per source, kind[k] / data[dptr[k] .. dptr[k+1]):
+//   GG_SRC_DC     {value}                              gen_dcVt_kernel   src/kernels.cu:73-85
+//   GG_SRC_PULSE  {vlo, vhi, td, tr, tf, tw, tp}       gen_PULSEut_kernel src/kernels.cu:223-245
+//   GG_SRC_PWL    {t0, v0, t1, v1, ...}                gen_PWLut_kernel  src/kernels.cu:146-176
+// (PWL before t0: v0; the reference reads v[-1] there)
+__device__ __forceinline__ double pulse_value(const double *q, double t)
+{
+    const double vlo = q[0], vhi = q[1], td = q[2], tr = q[3], tf = q[4], tw = q[5], tp = q[6];
+    t = t - floor(t / tp) * tp;
+    if (t < td) return vlo;
+    if (t < td + tr) return vlo + (t - td) * (vhi - vlo) / tr;
+    if (t < td + tr + tw) return vhi;
+    if (t < td + tr + tw + tf) return vhi - (t - td - tr - tw) * (vhi - vlo) / tf;
+    return vlo;
+}
+__device__ __forceinline__ double pwl_value(const double *tv, int np, double t)
+{
+    if (np <= 0) return 0.0;
+    double value = tv[1];
+    int i;
+    for (i = 0; i < np; i++) {
+        if (t < tv[2 * i]) {
+            if (i > 0)
+                value = tv[2 * i + 1] - (tv[2 * i] - t) * (tv[2 * i + 1] - tv[2 * i - 1]) /
+                                            (tv[2 * i] - tv[2 * i - 2]);
+            break;
+        }
+    }
+    if (i == np) value = tv[2 * np - 1];
+    return value;
+}
+__global__ void k_sources(int nsrc, const int *kind, const int *dptr, const double *data, int it, double h,
+                          double *u)
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nsrc) return;
-    const double *q = pulse + 7 * k;
-    const double vlo = q[0], vhi = q[1], td = q[2], tr = q[3], tf = q[4], tw = q[5], tp = q[6];
-    double t = it * h;
-    t = t - floor(t / tp) * tp;
-    double value;
-    if (t < td) value = vlo;
-    else if (t < td + tr) value = vlo + (t - td) * (vhi - vlo) / tr;
-    else if (t < td + tr + tw) value = vhi;
-    else if (t < td + tr + tw + tf) value = vhi - (t - td - tr - tw) * (vhi - vlo) / tf;
-    else value = vlo;
+    const double *q = data + dptr[k];
+    const double t = it * h;
+    double value = 0.0;
+    if (kind[k] == GG_SRC_DC) value = q[0];
+    else if (kind[k] == GG_SRC_PULSE) value = pulse_value(q, t);
+    else value = pwl_value(q, (dptr[k + 1] - dptr[k]) / 2, t);
     u[k] = value;
 }
 
@@ -1586,11 +1615,11 @@ void launch_fill_u64(unsigned long long *p, long long n, unsigned long long v, h
 {
     k_fill_u64<<<blocks_for(n, kBlock, 4096), kBlock, 0, st>>>(p, n, v);
 }
-void launch_transient_step(int n, int nsrc, const double *pulse, int it, double h, double *u,
-                           const int *src_ptr, const int *src_idx, const double *cdiag,
+void launch_transient_step(int n, int nsrc, const int *kind, const int *dptr, const double *data, int it,
+                           double h, double *u, const int *src_ptr, const int *src_idx, const double *cdiag,
                            const double *x, double *w, hipStream_t st)
 {
-    if (nsrc > 0) k_pulse<<<(nsrc + kBlock - 1) / kBlock, kBlock, 0, st>>>(nsrc, pulse, it, h, u);
+    if (nsrc > 0) k_sources<<<(nsrc + kBlock - 1) / kBlock, kBlock, 0, st>>>(nsrc, kind, dptr, data, it, h, u);
     if (n > 0)
         k_transient_rhs<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, src_ptr, src_idx, u, cdiag, x, w);
 }

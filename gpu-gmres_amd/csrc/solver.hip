@@ -1112,14 +1112,12 @@ int gg_solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_optio
     GG_API_END
 }
 
-int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc,
-                 const int *src_node, const double *pulse, int nport, const int *port,
-                 double *x, const gg_options *opt, double *port_out, int *iters_total)
+// the step loop behind gg_transient / gg_transient_src (host source tables)
+static int transient_loop(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc, const int *src_node,
+              const std::vector<int> &kind, const std::vector<int> &dptr, const std::vector<double> &data,
+              int nport, const int *port, double *x, const gg_options *opt, double *port_out,
+              int *iters_total)
 {
-    GG_API_BEGIN
-    GG_REQUIRE(s && opt && x && cdiag && iters_total, GG_EINVAL, "null argument");
-    GG_REQUIRE(nsteps >= 0 && nsrc >= 0 && nport >= 0, GG_EINVAL, "negative count");
-    GG_REQUIRE(nsrc == 0 || (src_node && pulse), GG_EINVAL, "null source arrays");
     GG_REQUIRE(nport == 0 || (port && port_out), GG_EINVAL, "null port arrays");
     GG_REQUIRE(s->have_A, GG_ESTATE, "gg_transient: no matrix");
     set_device(s);
@@ -1136,11 +1134,13 @@ int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int ns
         for (int k = 0; k < nsrc; k++) sidx[fill[src_node[k]]++] = k;
     }
     for (int j = 0; j < nport; j++) GG_REQUIRE(port[j] >= 0 && port[j] < n, GG_EINVAL, "port out of range");
-    DBuf<int> d_sptr, d_sidx, d_port;
-    DBuf<double> d_pulse, d_u, d_c, d_w, d_pv;
+    DBuf<int> d_sptr, d_sidx, d_port, d_kind, d_dptr;
+    DBuf<double> d_data, d_u, d_c, d_w, d_pv;
     d_sptr.upload(sptr, s->st);
     d_sidx.upload(sidx.data(), sidx.size(), s->st);
-    d_pulse.upload(pulse, (size_t)7 * nsrc, s->st);
+    d_kind.upload(kind.data(), kind.size(), s->st);
+    d_dptr.upload(dptr.data(), dptr.size(), s->st);
+    d_data.upload(data.data(), std::max<size_t>(data.size(), 1), s->st);
     d_u.alloc(std::max(nsrc, 1));
     d_c.upload(cdiag, n, s->st);
     d_w.alloc(std::max(n, 1));
@@ -1152,8 +1152,8 @@ int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int ns
     launch_gather_ports(nport, d_port.p, d_x, d_pv.p, s->st);
     int total = 0, status = GG_OK;
     for (int it = 1; it <= nsteps; it++) {
-        launch_transient_step(n, nsrc, d_pulse.p, it, h, d_u.p, d_sptr.p, d_sidx.p, d_c.p, d_x,
-                              d_w.p, s->st);
+        launch_transient_step(n, nsrc, d_kind.p, d_dptr.p, d_data.p, it, h, d_u.p, d_sptr.p, d_sidx.p,
+                              d_c.p, d_x, d_w.p, s->st);
         gg_result r{};
         const int rc = solve_device(s, d_w.p, d_x, opt, &r);
         if (rc != GG_OK) status = rc;
@@ -1171,6 +1171,48 @@ int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int ns
     GG_HIP(hipStreamSynchronize(s->st));
     *iters_total = total;
     return status;
+}
+
+int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc,
+                 const int *src_node, const double *pulse, int nport, const int *port,
+                 double *x, const gg_options *opt, double *port_out, int *iters_total)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && opt && x && cdiag && iters_total, GG_EINVAL, "null argument");
+    GG_REQUIRE(nsteps >= 0 && nsrc >= 0 && nport >= 0, GG_EINVAL, "negative count");
+    GG_REQUIRE(nsrc == 0 || (src_node && pulse), GG_EINVAL, "null source arrays");
+    std::vector<int> kind(std::max(nsrc, 1), GG_SRC_PULSE), dptr(nsrc + 1);
+    for (int k = 0; k <= nsrc; k++) dptr[k] = 7 * k;
+    std::vector<double> data(pulse, pulse + (size_t)7 * nsrc);
+    return transient_loop(s, nsteps, h, cdiag, nsrc, src_node, kind, dptr, data, nport, port, x, opt,
+                          port_out, iters_total);
+    GG_API_END
+}
+
+int gg_transient_src(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc,
+                     const int *src_node, const int *src_kind, const int *src_ptr, const double *src_data,
+                     int nport, const int *port, double *x, const gg_options *opt, double *port_out,
+                     int *iters_total)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && opt && x && cdiag && iters_total, GG_EINVAL, "null argument");
+    GG_REQUIRE(nsteps >= 0 && nsrc >= 0 && nport >= 0, GG_EINVAL, "negative count");
+    GG_REQUIRE(nsrc == 0 || (src_node && src_kind && src_ptr && src_data), GG_EINVAL, "null source arrays");
+    std::vector<int> kind(std::max(nsrc, 1), GG_SRC_DC), dptr(nsrc + 1, 0);
+    for (int k = 0; k < nsrc; k++) {
+        const int len = src_ptr[k + 1] - src_ptr[k];
+        GG_REQUIRE(src_ptr[k] >= 0 && len >= 0, GG_EINVAL, "gg_transient_src: bad src_ptr");
+        const int need = src_kind[k] == GG_SRC_DC ? 1 : src_kind[k] == GG_SRC_PULSE ? 7 : -1;
+        GG_REQUIRE(src_kind[k] == GG_SRC_DC || src_kind[k] == GG_SRC_PULSE || src_kind[k] == GG_SRC_PWL,
+                   GG_EINVAL, "gg_transient_src: unknown source kind");
+        GG_REQUIRE(need < 0 ? (len >= 2 && len % 2 == 0) : len == need, GG_EINVAL,
+                   "gg_transient_src: DC takes 1 value, PULSE 7, PWL (time, value) pairs");
+        kind[k] = src_kind[k];
+        dptr[k + 1] = src_ptr[k + 1] - src_ptr[0];
+    }
+    std::vector<double> data(src_data + (nsrc ? src_ptr[0] : 0), src_data + (nsrc ? src_ptr[nsrc] : 0));
+    return transient_loop(s, nsteps, h, cdiag, nsrc, src_node, kind, dptr, data, nport, port, x, opt,
+                          port_out, iters_total);
     GG_API_END
 }
 

@@ -29,7 +29,9 @@ EXPORTS = [
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
     "gg_trace_precond", "gg_bytes_trsv", "gg_transient", "gg_set_precond_ilu0_device",
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
+    "gg_transient_src",
 ]
+SRC_DC, SRC_PULSE, SRC_PWL = 0, 1, 2          # gg_src_kind
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
 PROF_NKINDS = 5
 
@@ -85,6 +87,9 @@ def lib():
         L.gg_solve_device.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options),
                                       ctypes.POINTER(Result)]
         L.gg_get_history.argtypes = [_VP, ctypes.c_void_p, ctypes.c_int]
+        L.gg_transient_src.argtypes = [_VP, ctypes.c_int, ctypes.c_double, _D, ctypes.c_int, _I, _I, _I, _D,
+                                       ctypes.c_int, _I, _D, ctypes.POINTER(Options), _D,
+                                       ctypes.POINTER(ctypes.c_int)]
         L.gg_transient.argtypes = [_VP, ctypes.c_int, ctypes.c_double, _D, ctypes.c_int, _I, _D,
                                    ctypes.c_int, _I, _D, ctypes.POINTER(Options), _D,
                                    ctypes.POINTER(ctypes.c_int)]
@@ -254,6 +259,30 @@ class Solver:
                                        pulse if pulse.size else np.zeros(7), len(ports),
                                        ports if len(ports) else np.zeros(1, np.int32), x,
                                        ctypes.byref(o), pv, ctypes.byref(tot)), allow_nc=True)
+        return dict(x=x, ports=pv[: len(ports) * (nsteps + 1)].reshape(len(ports), nsteps + 1),
+                    iters_total=tot.value, ret=rc)
+
+    def transient_src(self, nsteps, h, cdiag, src_node, sources, ports, x0, restart=32,
+                      max_iter=10000, tol=1e-7, flags=0):
+        """gg_transient_src: sources = [(kind, params), ...] (SRC_DC / SRC_PULSE /
+        SRC_PWL); returns dict(x, ports [nport, nsteps+1], iters_total, ret)."""
+        n = self.n
+        x = np.array(x0, np.float64, copy=True)
+        src_node = np.ascontiguousarray(src_node, np.int32)
+        kind = np.array([k for k, _ in sources], np.int32)
+        ptr = np.zeros(len(sources) + 1, np.int32)
+        ptr[1:] = np.cumsum([len(q) for _, q in sources])
+        data = np.concatenate([np.asarray(q, np.float64) for _, q in sources]) if sources else np.zeros(1)
+        ports = np.ascontiguousarray(ports, np.int32)
+        pv = np.zeros(max(len(ports), 1) * (nsteps + 1))
+        tot = ctypes.c_int()
+        o = Options(int(restart), int(max_iter), float(tol), int(flags))
+        one = np.zeros(1, np.int32)
+        rc = _check(lib().gg_transient_src(self.h, int(nsteps), float(h), np.ascontiguousarray(cdiag, np.float64),
+                                           len(src_node), src_node if len(src_node) else one,
+                                           kind if len(kind) else one, ptr, data, len(ports),
+                                           ports if len(ports) else one, x, ctypes.byref(o), pv,
+                                           ctypes.byref(tot)), allow_nc=True)
         return dict(x=x, ports=pv[: len(ports) * (nsteps + 1)].reshape(len(ports), nsteps + 1),
                     iters_total=tot.value, ret=rc)
 

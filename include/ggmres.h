@@ -210,6 +210,19 @@ double gg_bytes_trsv(gg_solver *s, int which);   /* 0 = L / Ml, 1 = U / Mr */
 int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc,
                  const int *src_node, const double *pulse, int nport, const int *port,
                  double *x, const gg_options *opt, double *port_out, int *iters_total);
+/* Source kinds of gg_transient_src: the waveform generators of the reference's
+ * GPU transient path (src/kernels.cu), evaluated at t = it * h for step it:
+ *   GG_SRC_DC     data {value}                          gen_dcVt_kernel   (:73-85)
+ *   GG_SRC_PULSE  data {vlo, vhi, td, tr, tf, tw, tp}   gen_PULSEut_kernel (:223-245)
+ *   GG_SRC_PWL    data {t0, v0, t1, v1, ...}            gen_PWLut_kernel  (:146-176;
+ *                 before t0 the value is v0, where the reference reads v[-1]) */
+enum gg_src_kind { GG_SRC_DC = 0, GG_SRC_PULSE = 1, GG_SRC_PWL = 2 };
+/* gg_transient with any mix of sources: source k at node src_node[k], kind
+ * src_kind[k], parameters src_data[src_ptr[k] .. src_ptr[k+1]) */
+int gg_transient_src(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc,
+                     const int *src_node, const int *src_kind, const int *src_ptr, const double *src_data,
+                     int nport, const int *port, double *x, const gg_options *opt, double *port_out,
+                     int *iters_total);
 
 /* Diagnostics: run one wavefront triangular solve (which: 0 = L / Ml, 1 = U / Mr)
  * on the current right-hand side and return, per band, the device real-time

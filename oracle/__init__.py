@@ -264,6 +264,31 @@ def pulse(q, it, h):
     return f(q.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(it), float(h))
 
 
+def pwl(tv, it, h):
+    """PWL source value at time index it (gen_PWLut_kernel, src/kernels.cu:146-176);
+    tv = [t0, v0, t1, v1, ...]; holds v0 before t0 (the reference reads v[-1])."""
+    f = lib().orc_pwl
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int, ctypes.c_double]
+    tv = np.ascontiguousarray(tv, np.float64)
+    return f(tv.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(tv) // 2, int(it), float(h))
+
+
+SRC_DC, SRC_PULSE, SRC_PWL = 0, 1, 2   # include/ggmres.h gg_src_kind
+
+
+def source_value(kind, data, it, h):
+    """One source at time index it: DC (gen_dcVt_kernel, src/kernels.cu:73-85: the
+    constant), PULSE (gen_PULSEut_kernel) or PWL (gen_PWLut_kernel)."""
+    if kind == SRC_DC:
+        return float(data[0])
+    if kind == SRC_PULSE:
+        return pulse(data, it, h)
+    if kind == SRC_PWL:
+        return pwl(data, it, h)
+    raise ValueError(kind)
+
+
 def transient_rhs(cdiag, src_node, u, x):
     """w = B u + (C/h) x as the reference step driver forms it."""
     n = len(x)
@@ -281,18 +306,20 @@ def transient_rhs(cdiag, src_node, u, x):
 
 
 def transient(A, L, U, nsteps, h, cdiag, src_node, pulses, ports, x0, m=32, max_iter=10000,
-              tol=1e-7):
+              tol=1e-7, sources=None):
     """The reference's backward-Euler step driver (src/mna_solve_gpu_gmres.cpp:564-647)
-    with GMRES_leftILU0 per step, warm start x_{t-1}; returns dict(x, ports, iters_total)."""
+    with GMRES_leftILU0 per step, warm start x_{t-1}; returns dict(x, ports, iters_total).
+    Sources: PULSE parameter rows `pulses`, or `sources` = [(kind, data), ...]."""
     x = np.array(x0, np.float64, copy=True)
-    pulses = np.asarray(pulses, np.float64).reshape(-1, 7)
+    if sources is None:
+        sources = [(SRC_PULSE, q) for q in np.asarray(pulses, np.float64).reshape(-1, 7)]
     ports = np.asarray(ports, np.int64)
     pv = np.zeros((len(ports), nsteps + 1))
     pv[:, 0] = x[ports]
     total = 0
     ret = 0
     for it in range(1, nsteps + 1):
-        u = np.array([pulse(q, it, h) for q in pulses])
+        u = np.array([source_value(k, q, it, h) for k, q in sources])
         w = transient_rhs(cdiag, src_node, u, x)
         o = gmres_left(A, L, U, w, x0=x, m=m, max_iter=max_iter, tol=tol)
         x = o["x"]

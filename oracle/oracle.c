@@ -723,6 +723,29 @@ double orc_pulse(const double *q, int it, double h)
     return vlo;
 }
 
+/* PWL source value at time index it (gen_PWLut_kernel, src/kernels.cu:146-176):
+ * tv = {t0, v0, t1, v1, ...}, np points; value = v[i] - (t[i] - t)*(v[i] - v[i-1])
+ * / (t[i] - t[i-1]) at the first i with t < t[i], v[np-1] after the last point.
+ * Deviation: for t < t[0] the reference reads v[-1], t[-1] (out of bounds);
+ * here the value is v[0] (the waveform holds its first point). */
+double orc_pwl(const double *tv, int np, int it, double h)
+{
+    const double t = it * h;                   /* mytime = idxt * tstep */
+    if (np <= 0) return 0.0;
+    double value = tv[1];
+    int i;
+    for (i = 0; i < np; i++) {
+        if (t < tv[2 * i]) {
+            if (i > 0)
+                value = tv[2 * i + 1] - (tv[2 * i] - t) * (tv[2 * i + 1] - tv[2 * i - 1]) /
+                                            (tv[2 * i] - tv[2 * i - 2]);
+            break;
+        }
+    }
+    if (i == np) value = tv[2 * np - 1];
+    return value;
+}
+
 void orc_transient_rhs(int n, int nsrc, const int *src_node, const double *u,
                        const double *cdiag, const double *x, double *w)
 {

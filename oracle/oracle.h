@@ -101,6 +101,7 @@ int orc_gmres_split(int n, const int *rp, const int *ci, const double *v,
  * source at time index it (gen_PULSEut_kernel, src/kernels.cu:223-245);
  * q = {vlo, vhi, td, tr, tf, tw, tp}. */
 double orc_pulse(const double *q, int it, double h);
+double orc_pwl(const double *tv, int np, int it, double h);
 /* w = B u + (C/h) x formed as the driver does: w = 0; w += B u (cs_dl_gaxpy,
  * B incidence: source k adds +1 * u[k] at row src_node[k], k ascending);
  * xnr = 0; xnr += diag(cdiag) x; w += xnr. */

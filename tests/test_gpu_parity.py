@@ -467,6 +467,40 @@ def test_transient_c5(solver, grid):
     assert np.max(np.abs(o["ports"])) > 0      # the sources did drive the grid
 
 
+def test_transient_mixed_sources(solver):
+    """gg_transient_src with DC, PULSE and PWL sources (gen_dcVt / gen_PULSEut /
+    gen_PWLut semantics, several sources on one node) against the restated
+    step driver: bit-identical to the order-matched oracle."""
+    nx, ny = 40, 40
+    h = 1e-2
+    A = M.transient(M.laplacian_5pt(nx, ny), c=1e-3, h=h)
+    n = A.shape[0]
+    cdiag = np.full(n, 1e-3 / h)
+    rng = np.random.default_rng(21)
+    nodes = np.sort(rng.choice(n, size=24, replace=False)).astype(np.int32)
+    nodes[5] = nodes[4]                                   # two sources on one node
+    srcs = []
+    for k in range(len(nodes)):
+        if k % 3 == 0:
+            srcs.append((O.SRC_DC, [1e-3 * (1 + k)]))
+        elif k % 3 == 1:
+            srcs.append((O.SRC_PULSE, [0.0, 2e-3, 2 * h, 3 * h, 4 * h, 5 * h, 20 * h]))
+        else:
+            srcs.append((O.SRC_PWL, [0.0, 0.0, 3 * h, 1e-3, 7.5 * h, 1e-3, 12 * h, -5e-4]))
+    ports = np.array([nodes[0], nodes[1], nodes[2], n - 1], np.int32)
+    x0 = np.zeros(n)
+    L, U = O.ilu0(A)
+    run = lambda: O.transient(A, L, U, 15, h, cdiag, nodes, None, ports, x0, m=32, max_iter=10000,
+                              tol=1e-7, sources=srcs)
+    o, ot = oracle_both(run, n, nx=nx)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    g = solver.transient_src(15, h, cdiag, nodes, srcs, ports, x0, restart=32, max_iter=10000, tol=1e-7)
+    assert g["iters_total"] == ot["iters_total"]
+    assert np.array_equal(g["ports"], ot["ports"]) and np.array_equal(g["x"], ot["x"])
+    assert rel_err(g["x"], o["x"]) <= 1e-10
+
+
 @pytest.mark.gpu
 def test_profile_kind_mask():
     """gg_profile_enable(kinds): only the selected families are bracketed."""

@@ -274,6 +274,23 @@ def test_gmres_split_warm_start():
     assert r2["ret"] == 0 and r2["iters"] <= 1
 
 
+def test_pwl_and_dc_semantics():
+    """gen_PWLut_kernel (src/kernels.cu:146-176): first point with t < t_i
+    interpolates back from it; after the last point its value holds; before t0
+    the restatement holds v0 (the reference reads v[-1]). gen_dcVt: constant."""
+    h = 1e-9
+    tv = [0.0, 0.0, 2e-9, 1.0, 5e-9, 1.0, 6e-9, 0.25]
+    assert O.pwl(tv, 0, h) == 1.0 - (2e-9 - 0.0) * (1.0 - 0.0) / (2e-9 - 0.0)       # t = t0: next segment
+    assert O.pwl(tv, 1, h) == 1.0 - (2e-9 - 1 * h) * (1.0 - 0.0) / (2e-9 - 0.0)     # rising segment
+    assert O.pwl(tv, 3, h) == 1.0 - (5e-9 - 3 * h) * (1.0 - 1.0) / (5e-9 - 2e-9)    # flat
+    t = 5 * h
+    assert O.pwl(tv, 5, h) == 0.25 - (6e-9 - t) * (0.25 - 1.0) / (6e-9 - 5e-9)       # falling
+    assert O.pwl(tv, 9, h) == 0.25                                                    # after the last
+    assert O.pwl([1e-9, 0.5, 2e-9, 1.0], 0, h) == 0.5                                 # before t0: v0
+    assert O.source_value(O.SRC_DC, [0.7], 123, h) == 0.7
+    assert O.source_value(O.SRC_PWL, tv, 1, h) == O.pwl(tv, 1, h)
+
+
 def test_pulse_semantics():
     """gen_PULSEut_kernel (src/kernels.cu:223-245): periodic trapezoid."""
     q = [0.0, 1e-3, 0.0, 0.1, 0.1, 1.0, 4.0]     # vlo vhi td tr tf tw tp
