@@ -43,6 +43,9 @@ void launch_transient_step(int n, int nsrc, const int *kind, const int *dptr, co
                            double h, double *u, const int *src_ptr, const int *src_idx, const double *cdiag,
                            const double *x, double *w, hipStream_t st);
 void launch_gather_ports(int nport, const int *port, const double *x, double *out, hipStream_t st);
+// tap statistics: mode 0 seed (max = min = sum = x[tap]), 1 update, 2 finish (sum /= npts)
+void launch_taps(int ntap, const int *tap, const double *x, double *mx, double *mn, double *sm, int mode,
+                 double npts, hipStream_t st);
 // device ILU(0) column elimination (co-resident grid of at most ilu0_columns_max_blocks())
 int ilu0_columns_max_blocks();
 void launch_ilu0_columns(int n, const int *cp, const int *ri, const double *cv0, double *cv, int *level,

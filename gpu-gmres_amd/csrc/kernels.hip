@@ -1206,6 +1206,31 @@ __global__ void k_transient_rhs(int n, const int *src_ptr, const int *src_idx, c
     w[r] = bu + xnr;
 }
 
+// tap-node voltage statistics of the transient run (the ir_info block of the
+// step driver, src/mna_solve_gpu_gmres.cpp:285-292, 633-645, 780-797): max,
+// min and the running sum, seeded with the initial state; avg = sum / time
+// points, IR = max - min at the end
+__global__ void k_taps(int ntap, const int *tap, const double *x, double *mx, double *mn, double *sm, int mode,
+                       double npts)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ntap) return;
+    if (mode == 2) {                       // finish: sum -> avg (IR = max - min on the host)
+        sm[j] = sm[j] / npts;
+        return;
+    }
+    const double v = x[tap[j]];
+    if (mode == 0) {
+        mx[j] = v;
+        mn[j] = v;
+        sm[j] = v;
+        return;
+    }
+    if (mx[j] < v) mx[j] = v;
+    if (v < mn[j]) mn[j] = v;
+    sm[j] += v;
+}
+
 __global__ void k_gather_ports(int nport, const int *port, const double *x, double *out)
 {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1624,6 +1649,11 @@ void launch_transient_step(int n, int nsrc, const int *kind, const int *dptr, co
         k_transient_rhs<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, src_ptr, src_idx, u, cdiag, x, w);
 }
 
+void launch_taps(int ntap, const int *tap, const double *x, double *mx, double *mn, double *sm, int mode,
+                 double npts, hipStream_t st)
+{
+    if (ntap > 0) k_taps<<<(ntap + kBlock - 1) / kBlock, kBlock, 0, st>>>(ntap, tap, x, mx, mn, sm, mode, npts);
+}
 void launch_gather_ports(int nport, const int *port, const double *x, double *out, hipStream_t st)
 {
     if (nport > 0) k_gather_ports<<<(nport + kBlock - 1) / kBlock, kBlock, 0, st>>>(nport, port, x, out);

@@ -214,6 +214,9 @@ struct gg_solver {
     // round trip per restart cycle reads both)
     DevState *h_state = nullptr;
     int *h_err = nullptr;
+    // transient tap-node statistics (gg_transient_set_taps / _get_taps)
+    std::vector<int> taps;
+    std::vector<double> tap_max, tap_min, tap_avg;
     DBuf<unsigned long long> gran;      // m * (m+2) * G hand-off granules, re-armed per cycle
     DBuf<double> hist;
     long long hist_cap = 0;
@@ -1150,6 +1153,17 @@ static int transient_loop(gg_solver *s, int nsteps, double h, const double *cdia
     xd.upload(x, n, s->st);
     double *d_x = xd.p;
     launch_gather_ports(nport, d_port.p, d_x, d_pv.p, s->st);
+    const int ntap = (int)s->taps.size();
+    for (int t : s->taps) GG_REQUIRE(t >= 0 && t < n, GG_EINVAL, "tap node out of range");
+    DBuf<int> d_tap;
+    DBuf<double> d_tmax, d_tmin, d_tsum;
+    if (ntap) {
+        d_tap.upload(s->taps, s->st);
+        d_tmax.alloc(ntap);
+        d_tmin.alloc(ntap);
+        d_tsum.alloc(ntap);
+        launch_taps(ntap, d_tap.p, d_x, d_tmax.p, d_tmin.p, d_tsum.p, 0, 0.0, s->st);
+    }
     int total = 0, status = GG_OK;
     for (int it = 1; it <= nsteps; it++) {
         launch_transient_step(n, nsrc, d_kind.p, d_dptr.p, d_data.p, it, h, d_u.p, d_sptr.p, d_sidx.p,
@@ -1159,6 +1173,16 @@ static int transient_loop(gg_solver *s, int nsteps, double h, const double *cdia
         if (rc != GG_OK) status = rc;
         total += r.iters;
         launch_gather_ports(nport, d_port.p, d_x, d_pv.p + (size_t)it * nport, s->st);
+        launch_taps(ntap, d_tap.p, d_x, d_tmax.p, d_tmin.p, d_tsum.p, 1, 0.0, s->st);
+    }
+    if (ntap) {   // avg over the nsteps + 1 time points (ts.size()), src/mna_solve_gpu_gmres.cpp:782
+        launch_taps(ntap, d_tap.p, d_x, d_tmax.p, d_tmin.p, d_tsum.p, 2, (double)(nsteps + 1), s->st);
+        s->tap_max.resize(ntap);
+        s->tap_min.resize(ntap);
+        s->tap_avg.resize(ntap);
+        GG_HIP(hipMemcpyAsync(s->tap_max.data(), d_tmax.p, ntap * sizeof(double), hipMemcpyDeviceToHost, s->st));
+        GG_HIP(hipMemcpyAsync(s->tap_min.data(), d_tmin.p, ntap * sizeof(double), hipMemcpyDeviceToHost, s->st));
+        GG_HIP(hipMemcpyAsync(s->tap_avg.data(), d_tsum.p, ntap * sizeof(double), hipMemcpyDeviceToHost, s->st));
     }
     if (nport) {
         std::vector<double> pv((size_t)nport * (nsteps + 1));
@@ -1186,6 +1210,34 @@ int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int ns
     std::vector<double> data(pulse, pulse + (size_t)7 * nsrc);
     return transient_loop(s, nsteps, h, cdiag, nsrc, src_node, kind, dptr, data, nport, port, x, opt,
                           port_out, iters_total);
+    GG_API_END
+}
+
+int gg_transient_set_taps(gg_solver *s, int ntap, const int *tap_node)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && ntap >= 0 && (ntap == 0 || tap_node), GG_EINVAL, "null argument");
+    s->taps.assign(tap_node, tap_node + ntap);
+    s->tap_max.clear();
+    s->tap_min.clear();
+    s->tap_avg.clear();
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_transient_get_taps(gg_solver *s, double *max_v, double *min_v, double *avg_v, double *ir)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s, GG_EINVAL, "null argument");
+    const size_t nt = s->taps.size();
+    GG_REQUIRE(s->tap_max.size() == nt && nt > 0, GG_ESTATE, "gg_transient_get_taps: no transient run with taps");
+    for (size_t j = 0; j < nt; j++) {
+        if (max_v) max_v[j] = s->tap_max[j];
+        if (min_v) min_v[j] = s->tap_min[j];
+        if (avg_v) avg_v[j] = s->tap_avg[j];
+        if (ir) ir[j] = s->tap_max[j] - s->tap_min[j];      // ir_value = max_value - min_value (:789)
+    }
+    return GG_OK;
     GG_API_END
 }
 

@@ -29,7 +29,7 @@ EXPORTS = [
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
     "gg_trace_precond", "gg_bytes_trsv", "gg_transient", "gg_set_precond_ilu0_device",
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
-    "gg_transient_src",
+    "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps",
 ]
 SRC_DC, SRC_PULSE, SRC_PWL = 0, 1, 2          # gg_src_kind
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
@@ -285,6 +285,18 @@ class Solver:
                                            ctypes.byref(tot)), allow_nc=True)
         return dict(x=x, ports=pv[: len(ports) * (nsteps + 1)].reshape(len(ports), nsteps + 1),
                     iters_total=tot.value, ret=rc)
+
+    def set_taps(self, tap_node):
+        """tap nodes whose max / min / avg / IR drop the next transient runs track"""
+        t = np.ascontiguousarray(tap_node, np.int32)
+        _check(lib().gg_transient_set_taps(self.h, len(t), t.ctypes.data_as(ctypes.c_void_p)))
+        self._ntap = len(t)
+
+    def get_taps(self):
+        """(max, min, avg, ir) of the tap nodes over the last transient run."""
+        out = [np.zeros(getattr(self, "_ntap", 0)) for _ in range(4)]
+        _check(lib().gg_transient_get_taps(self.h, *[o.ctypes.data_as(ctypes.c_void_p) for o in out]))
+        return tuple(out)
 
     def history(self):
         n = lib().gg_get_history(self.h, None, 0)

@@ -223,6 +223,14 @@ int gg_transient_src(gg_solver *s, int nsteps, double h, const double *cdiag, in
                      const int *src_node, const int *src_kind, const int *src_ptr, const double *src_data,
                      int nport, const int *port, double *x, const gg_options *opt, double *port_out,
                      int *iters_total);
+/* Tap-node statistics of the following gg_transient / gg_transient_src runs
+ * (the step driver's ir_info block, src/mna_solve_gpu_gmres.cpp:285-292,
+ * 633-645, 780-797): per tap node its maximum and minimum over the nsteps + 1
+ * time points, its average (running sum in time order / (nsteps + 1)) and the
+ * IR drop max - min.  set_taps(s, 0, NULL) turns it off; get_taps fills any
+ * non-NULL array of ntap doubles from the last run. */
+int gg_transient_set_taps(gg_solver *s, int ntap, const int *tap_node);
+int gg_transient_get_taps(gg_solver *s, double *max_v, double *min_v, double *avg_v, double *ir);
 
 /* Diagnostics: run one wavefront triangular solve (which: 0 = L / Ml, 1 = U / Mr)
  * on the current right-hand side and return, per band, the device real-time

@@ -306,7 +306,7 @@ def transient_rhs(cdiag, src_node, u, x):
 
 
 def transient(A, L, U, nsteps, h, cdiag, src_node, pulses, ports, x0, m=32, max_iter=10000,
-              tol=1e-7, sources=None):
+              tol=1e-7, sources=None, taps=None):
     """The reference's backward-Euler step driver (src/mna_solve_gpu_gmres.cpp:564-647)
     with GMRES_leftILU0 per step, warm start x_{t-1}; returns dict(x, ports, iters_total).
     Sources: PULSE parameter rows `pulses`, or `sources` = [(kind, data), ...]."""
@@ -318,6 +318,9 @@ def transient(A, L, U, nsteps, h, cdiag, src_node, pulses, ports, x0, m=32, max_
     pv[:, 0] = x[ports]
     total = 0
     ret = 0
+    if taps is not None:     # ir_info (src/mna_solve_gpu_gmres.cpp:285-292, 633-645, 780-797)
+        taps = np.asarray(taps, np.int64)
+        tmax, tmin, tsum = x[taps].copy(), x[taps].copy(), x[taps].copy()
     for it in range(1, nsteps + 1):
         u = np.array([source_value(k, q, it, h) for k, q in sources])
         w = transient_rhs(cdiag, src_node, u, x)
@@ -326,4 +329,15 @@ def transient(A, L, U, nsteps, h, cdiag, src_node, pulses, ports, x0, m=32, max_
         total += o["iters"]
         ret = ret or o["ret"]
         pv[:, it] = x[ports]
-    return dict(x=x, ports=pv, iters_total=total, ret=ret)
+        if taps is not None:
+            for j, t in enumerate(taps):
+                v = x[t]
+                if tmax[j] < v:
+                    tmax[j] = v
+                if v < tmin[j]:
+                    tmin[j] = v
+                tsum[j] += v
+    out = dict(x=x, ports=pv, iters_total=total, ret=ret)
+    if taps is not None:
+        out["taps"] = (tmax, tmin, tsum / (nsteps + 1), tmax - tmin)
+    return out

@@ -490,15 +490,22 @@ def test_transient_mixed_sources(solver):
     ports = np.array([nodes[0], nodes[1], nodes[2], n - 1], np.int32)
     x0 = np.zeros(n)
     L, U = O.ilu0(A)
+    taps = np.concatenate([nodes[:6], [0, n // 2, n - 1]]).astype(np.int32)
     run = lambda: O.transient(A, L, U, 15, h, cdiag, nodes, None, ports, x0, m=32, max_iter=10000,
-                              tol=1e-7, sources=srcs)
+                              tol=1e-7, sources=srcs, taps=taps)
     o, ot = oracle_both(run, n, nx=nx)
     solver.set_matrix(A)
     solver.set_precond_ilu0()
+    solver.set_taps(taps)
     g = solver.transient_src(15, h, cdiag, nodes, srcs, ports, x0, restart=32, max_iter=10000, tol=1e-7)
     assert g["iters_total"] == ot["iters_total"]
     assert np.array_equal(g["ports"], ot["ports"]) and np.array_equal(g["x"], ot["x"])
     assert rel_err(g["x"], o["x"]) <= 1e-10
+    # tap statistics (ir_info): bit-identical max / min / avg / IR drop
+    for a_, b_ in zip(solver.get_taps(), ot["taps"]):
+        assert np.array_equal(a_, b_)
+    assert np.max(ot["taps"][3]) > 0
+    solver.set_taps([])
 
 
 @pytest.mark.gpu
