@@ -1590,11 +1590,19 @@ __global__ __launch_bounds__(kBlock) void k_update_x(Gate g, const DevState *ds,
     for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units;
          u += (long long)gridDim.x * kBlock) {
         double2 a = ld2(acc, u);
-        for (int j = 0; j <= k; j++) {
-            const double yj = y[j];
-            double2 vv = ld2(V + j * ldv, u);
-            a.x = a.x + vv.x * yj;
-            a.y = a.y + vv.y * yj;
+        // eight basis vectors' loads in flight at a time, added in ascending j
+        for (int j0 = 0; j0 <= k; j0 += 8) {
+            double2 vv[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (j0 + q <= k) vv[q] = ld2_nt(V + (j0 + q) * ldv, u);
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (j0 + q <= k) {
+                    const double yj = y[j0 + q];
+                    a.x = a.x + vv[q].x * yj;
+                    a.y = a.y + vv[q].y * yj;
+                }
         }
         st2(acc, u, a);
     }
