@@ -529,13 +529,6 @@ void enqueue_cycle(gg_solver *s, int m)
     launch_end_cycle(s->partA.p, s->G, ds, s->hist.p, s->st);
 }
 
-DevState read_state(gg_solver *s)
-{
-    DevState h;
-    GG_HIP(hipMemcpyAsync(&h, s->ds.p, sizeof(DevState), hipMemcpyDeviceToHost, s->st));
-    GG_HIP(hipStreamSynchronize(s->st));
-    return h;
-}
 
 // re-arm a wavefront triangle's hand-off state (granules, 3D progress words)
 void reset_wave(DevTri *T, hipStream_t st)
@@ -623,26 +616,42 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
 
     GG_HIP(hipEventRecord(s->ev0, s->st));
     enqueue_init(s);
-    h = read_state(s);
+    // The first cycle goes in before the state after the initial residual is
+    // read: its kernels are gated on DONE_INIT (converged at the start), so a
+    // solve costs one host round trip less.  The state after init is j = 1,
+    // hist_len = 1 (k_init_beta).
+    bool first = opt->max_iter >= 1;
+    if (first) enqueue_cycle(s, m);
+    h = read_state_checked(s);
     int ret = 1, iters = 0, inner = 0, restarts = 0;
     long long hist_len = 1;
     double relres = h.resid;
     if (h.done & DONE_INIT) {
         ret = 0;
         iters = 0;
+        if (first) prof_collect(s, 0);
     } else {
+        DevState prev = h;
+        prev.j = 1;
+        prev.hist_len = 1;
+        if (!first) h = prev;
         while (true) {
-            if (h.j > opt->max_iter) {   // while (j <= *max_iter) exhausted
-                ret = 1;
-                relres = h.resid;
-                iters = opt->max_iter;   // the reference leaves *max_iter untouched
-                hist_len = h.hist_len;
-                break;
+            if (first) {
+                first = false;               // cycle 1: enqueued and read above
+                restarts++;
+            } else {
+                if (h.j > opt->max_iter) {   // while (j <= *max_iter) exhausted
+                    ret = 1;
+                    relres = h.resid;
+                    iters = opt->max_iter;   // the reference leaves *max_iter untouched
+                    hist_len = h.hist_len;
+                    break;
+                }
+                restarts++;
+                enqueue_cycle(s, m);
+                prev = h;
+                h = read_state_checked(s);
             }
-            restarts++;
-            enqueue_cycle(s, m);
-            DevState prev = h;
-            h = read_state_checked(s);
             prof_collect(s, (h.done & DONE_INNER) ? h.conv_i + 1 : h.nit);
             if (h.done & DONE_INNER) {
                 ret = 0;
