@@ -54,15 +54,16 @@ void DevCsr::upload(const Csr &A, hipStream_t st)
         std::vector<int> sp(nslice + 1, 0);
         long long tot = 0;
         int wmax = 0;
-        for (int s_ = 0; s_ < nslice; s_++) {
+        bool fits = true;                        // int32 entry offsets
+        for (int s_ = 0; s_ < nslice && fits; s_++) {
             int w = 0;
             for (int r = s_ * 64; r < std::min(n, s_ * 64 + 64); r++) w = std::max(w, A.rp[r + 1] - A.rp[r]);
             wmax = std::max(wmax, w);
             tot += 64LL * w;
-            GG_REQUIRE(tot < (1LL << 31), GG_EINVAL, "matrix too large for int32 entry offsets");
-            sp[s_ + 1] = (int)tot;
+            fits = tot < (1LL << 31);
+            sp[s_ + 1] = (int)std::min<long long>(tot, 1LL << 30);
         }
-        if (wmax <= 64 && tot <= (long long)(1.25 * nnz) + 64LL * wmax) {
+        if (fits && wmax <= 64 && tot <= (long long)(1.25 * nnz) + 64LL * wmax) {
             std::vector<int> c(tot, -1);
             std::vector<double> vv(tot, 0.0);
             for (int r = 0; r < n; r++) {

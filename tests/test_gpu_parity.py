@@ -111,6 +111,22 @@ def test_spmv_long_rows(solver):
     assert np.all(np.abs(y - ref) <= 1e-13 * scale)
 
 
+@pytest.mark.slow
+def test_spmv_c3_standin_full_size(solver):
+    """The C3 stand-in at circuit5M's size (5.56M rows, 59.5M nnz): its
+    sliced-ELL padding would overflow int32 offsets, so the CSR-stream kernel
+    takes it (a regression: the layout check must fall back, not fail)."""
+    A = M.power_law()
+    x = np.random.default_rng(12).standard_normal(A.shape[0])
+    solver.set_matrix(A)
+    solver.set_precond_none()
+    y, ref = solver.spmv(x), O.spmv(A, x)
+    rl = np.diff(A.indptr)
+    short = rl <= 2048
+    assert np.array_equal(y[short], ref[short])
+    assert np.all(np.abs(y - ref) <= 1e-13 * (abs(A) @ abs(x)))
+
+
 @pytest.mark.parametrize("name", sorted(MATS))
 @pytest.mark.parametrize("force_level", [False, True, "per_level"])
 def test_ilu0_apply_bitexact(solver, name, force_level, monkeypatch):
