@@ -138,6 +138,10 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U);
 // no wrap-around; nz >= 2 planes of the 2D layout
 Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U);
 
+// rows with more off-diagonal terms than this are solved by a whole wave in the
+// sync-free triangular solve (kernels.hip k_trsv_flow)
+constexpr int kFlowLong = 32;
+
 // SpMV row blocks: each block <= 256 rows and <= kSpmvCap nnz (CSR-stream)
 constexpr int kSpmvCap = 2048;
 std::vector<int> spmv_blocks(const Csr &A, std::vector<int> &long_rows);
@@ -205,6 +209,11 @@ struct DevTri {
     DBuf<double> d;
     std::vector<int> lev_ptr;    // host
     DBuf<int> lev_rows;
+    // the flow kernel's tasks over lev_rows (level order): {first, count} = up
+    // to 64 rows of at most kFlowLong terms, one per lane; count = -1: one row
+    // with more terms, taken by a whole wave
+    int ntask = 0;
+    DBuf<int2> tasks;
     // WAVE2D (layout arrays, length P)
     Wave2D wl;
     DBuf<double> c1, c2, dw, rw; // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor, rw: RN(1/dw)

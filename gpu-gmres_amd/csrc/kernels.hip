@@ -362,20 +362,74 @@ __global__ void k_fill_gated(Gate g, unsigned long long *p, long long n, unsigne
         p[i] = v;
 }
 
-__global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int n, const int *__restrict__ rows,
+__global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const int2 *__restrict__ tasks,
+                                                      const int *__restrict__ rows,
                                                       const int *__restrict__ rp, const int *__restrict__ ci,
                                                       const double *__restrict__ v,
                                                       const double *__restrict__ d,
                                                       const double *__restrict__ b, double *x, int *err)
 {
     if (gated(g)) return;
+    __shared__ double prod[kBlock];            // a long row's products, one 64-slot area per wave
     const int lane = threadIdx.x & 63;
+    double *wprod = prod + (threadIdx.x & ~63);
     const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
     const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
     unsigned long long *xu = reinterpret_cast<unsigned long long *>(x);
-    for (long long base = wid * 64; base < n; base += nw * 64) {
-        const long long idx = base + lane;
-        const int r = idx < n ? rows[idx] : -1;
+    for (long long t = wid; t < ntask; t += nw) {
+        const int2 tk = tasks[t];
+        if (tk.y < 0) {
+            // one long row, the whole wave: each round 256 of its terms (4 per
+            // lane) are loaded and polled together, their products v*x formed
+            // in parallel, then lane 0 subtracts them from acc one by one in
+            // canonical order -- the reference's serial arithmetic
+            const int r = rows[tk.x];
+            const int k0 = rp[r], k1 = rp[r + 1];
+            double acc = b[r];
+            int spins = 0;
+            for (int kc = k0; kc < k1; kc += 256) {
+                int c[4];
+                double vv[4];
+                unsigned long long u[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int k = kc + q * 64 + lane;
+                    c[q] = k < k1 ? ci[k] : -1;
+                    vv[q] = k < k1 ? v[k] : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) u[q] = c[q] >= 0 ? ld_agent(xu + c[q]) : 0ull;
+                while (true) {
+                    bool miss = false;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) miss |= c[q] >= 0 && u[q] == kSentinel;
+                    if (!__any(miss)) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > kSpinLimit) {
+                        if (lane == 0) atomicOr(err, 1);
+                        break;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        if (c[q] >= 0 && u[q] == kSentinel) u[q] = ld_agent(xu + c[q]);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    wprod[lane] = vv[q] * __longlong_as_double((long long)u[q]);
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    const int cnt = k1 - (kc + q * 64);
+                    if (lane == 0)
+                        for (int j = 0; j < 64 && j < cnt; j++) acc = acc - wprod[j];
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                }
+            }
+            if (lane == 0) st_agent(xu + r, (unsigned long long)__double_as_longlong(acc / d[r]));
+            continue;
+        }
+        // up to 64 short rows, one per lane
+        const int r = lane < tk.y ? rows[tk.x + lane] : -1;
         bool pending = r >= 0;
         int k = pending ? rp[r] : 0;
         const int k1 = pending ? rp[r + 1] : 0;
@@ -1815,14 +1869,22 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
                 (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
                 return c;
             }();
+            // one block per CU where the levels are narrow (every waiting lane
+            // polls; more pollers slow the hand-offs), up to occupancy where a
+            // level holds more tasks than 4 waves per CU can take (C3: 3,100
+            // tasks per level, 0.66 ms per solve at 8 blocks per CU vs 2.1 ms at 1)
             const char *bpc_s = getenv("GG_FLOW_BPC");
-            const int bpc = bpc_s ? std::max(1, atoi(bpc_s)) : 1;
-            const long long need = ((long long)nrows + kBlock - 1) / kBlock;
-            const int blocks = (int)std::min<long long>(std::min(flow_blocks, bpc * std::max(cus, 1)), need);
+            const long long per_level = (T.ntask + nlev - 1) / std::max(nlev, 1);
+            const long long wave_slots = 4LL * std::max(cus, 1);          // 4 waves per block, 1 block per CU
+            const int bpc = bpc_s ? std::max(1, atoi(bpc_s))
+                                  : per_level <= wave_slots ? 1
+                                  : (int)std::min<long long>(8, 2 * ((per_level + wave_slots - 1) / wave_slots));
+            const long long need = ((long long)T.ntask + kBlock / 64 - 1) / (kBlock / 64);   // a wave per task
+            const int blocks = (int)std::min<long long>(std::min<long long>(flow_blocks, (long long)bpc * std::max(cus, 1)), need);
             k_fill_gated<<<blocks_for(nrows, kBlock, 8192), kBlock, 0, st>>>(
                 g, reinterpret_cast<unsigned long long *>(x), nrows, kSentinel);
-            k_trsv_flow<<<blocks, kBlock, 0, st>>>(g, nrows, T.lev_rows.p, T.off.rp.p, T.off.ci.p, T.off.v.p,
-                                                   T.d.p, b, x, err);
+            k_trsv_flow<<<blocks, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p, T.off.ci.p,
+                                                   T.off.v.p, T.d.p, b, x, err);
             return;
         }
         for (int l = 0; l < nlev; l++) {

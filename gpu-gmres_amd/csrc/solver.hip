@@ -172,6 +172,28 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         Levels lv = level_sets(C);
         T.lev_ptr = lv.ptr;
         T.lev_rows.upload(lv.rows, st);
+        // flow tasks in level order: runs of up to 64 short rows, long rows alone
+        const char *fl = std::getenv("GG_FLOW_LONG");       // tuning: terms above which a row is long
+        const int flow_long = fl ? std::max(0, atoi(fl)) : kFlowLong;
+        std::vector<int2> tasks;
+        int run0 = 0, runn = 0;
+        auto flush = [&]() {
+            if (runn) tasks.push_back(make_int2(run0, runn));
+            runn = 0;
+        };
+        for (int q = 0; q < (int)lv.rows.size(); q++) {
+            const int r = lv.rows[q];
+            if (C.off.rp[r + 1] - C.off.rp[r] > flow_long) {
+                flush();
+                tasks.push_back(make_int2(q, -1));
+            } else {
+                if (runn == 0) run0 = q;
+                if (++runn == 64) flush();
+            }
+        }
+        flush();
+        T.ntask = (int)tasks.size();
+        T.tasks.upload(tasks, st);
         T.bytes = 12.0 * C.off.nnz() + 4.0 * (n + 1) + 24.0 * n;
     }
 }
