@@ -64,7 +64,7 @@ def parse():
                    help="dd workload on one process: shards held by this process (GG_DD_LOCAL)")
     p.add_argument("--dd-grid", choices=["c4", "c2"], default="c4",
                    help="dd workload system: c4 (216^3 7-pt) or c2 (1000^2 5-pt)")
-    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "dd"], default="c2",
+    p.add_argument("--workload", choices=["c2", "c3", "c3s", "c4", "c5", "dd"], default="c2",
                    help="c2: one C2 solve per step (the headline); c5: a backward-Euler "
                         "transient (A = G + C/h, 1%% PULSE sources) of --c5-steps time steps per step")
     p.add_argument("--c5-steps", type=int, default=100)
@@ -271,8 +271,9 @@ def main():
         return bench_dd(a, torch, dist, world, rank, local)
     c5 = a.workload == "c5"
     c4 = a.workload == "c4"
+    c3s = a.workload == "c3s"           # GMRES + ILU(0) on the C3 stand-in (general sparsity)
     h5 = 1e-2
-    A = M.grid_7pt(a.c4_grid) if c4 else M.laplacian_5pt(a.grid)
+    A = M.grid_7pt(a.c4_grid) if c4 else M.power_law() if c3s else M.laplacian_5pt(a.grid)
     if c5:
         A = M.transient(A, c=1e-3, h=h5)
     n = A.shape[0]
@@ -405,12 +406,15 @@ def main():
     roof = None
     if dom and dom in timed:
         f = timed[dom]
+        if dom == "spmv":
+            KERNEL_NAMES["spmv"] = "k_spmv_sell<false>" if s.spmv_sliced else "k_spmv_stream<false>"
         kname = KERNEL_NAMES[dom] if (s.uses_wavefront or dom == "spmv") else \
-            "k_trsv_level (one launch per dependency level; one 'launch' here = one triangle)"
+            ("k_trsv_level (one launch per dependency level; one 'launch' here = one triangle)"
+             if os.environ.get("GG_TRSV_LEVELS") == "1" else "k_trsv_flow")
         roof = {"kernel": kname, "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(KERNEL_NAMES[dom]) if (s.uses_wavefront or dom == "spmv") and not c4
+                "traffic": pmc_traffic(KERNEL_NAMES[dom]) if (s.uses_wavefront or dom == "spmv") and not c4 and not c3s
                 else None,
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
                 "launches_timed": f["launches"]}
@@ -434,7 +438,7 @@ def main():
 
     # ---- CPU baseline (rank 0, N=1): the oracle restatement -----------------------
     cpu = None
-    if rank == 0 and world == 1 and a.cpu_iters > 0 and not c5 and not c4:
+    if rank == 0 and world == 1 and a.cpu_iters > 0 and not c5 and not c4 and not c3s:
         import oracle as O
         L, U = O.ilu0(A)
         t1 = time.perf_counter()
@@ -458,6 +462,10 @@ def main():
                                 f"GMRES({a.restart}), tol {a.tol:g}, {a.c5_steps} backward-Euler "
                                 f"steps per step, warm start, {a.c5_scenarios} concurrent scenario(s) "
                                 f"per GPU") if c5 else
+                               (f"C3 stand-in: seeded power-law CSR with circuit5M's n and nnz "
+                                f"(no parity claim), ILU(0) left (C3 names ILU(1): out of reach on "
+                                f"this matrix, DESIGN.md 5.1), GMRES({a.restart}), tol {a.tol:g}, "
+                                f"b=A*1, x0=0, one solve per step") if c3s else
                                (f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU(0) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step"),
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,

@@ -1137,6 +1137,7 @@ int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const d
 
 int gg_precond_kind(gg_solver *s) { return s ? s->pkind : GG_EINVAL; }
 int gg_uses_wavefront(gg_solver *s) { return (s && s->wave) ? 1 : 0; }
+int gg_spmv_sliced(gg_solver *s) { return (s && s->dA.sell) ? 1 : 0; }
 
 int gg_solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
                     gg_result *res)

@@ -29,7 +29,7 @@ EXPORTS = [
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
     "gg_trace_precond", "gg_bytes_trsv", "gg_transient", "gg_set_precond_ilu0_device",
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
-    "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps",
+    "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced",
 ]
 SRC_DC, SRC_PULSE, SRC_PWL = 0, 1, 2          # gg_src_kind
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
@@ -73,7 +73,7 @@ def lib():
         L.gg_destroy.argtypes = [_VP]
         L.gg_set_matrix.argtypes = [_VP, ctypes.c_int, _I, _I, _D]
         for f in ("gg_set_precond_none", "gg_set_precond_ilu0", "gg_precond_kind",
-                  "gg_uses_wavefront", "gg_set_precond_ilu0_device"):
+                  "gg_uses_wavefront", "gg_spmv_sliced", "gg_set_precond_ilu0_device"):
             getattr(L, f).argtypes = [_VP]
         L.gg_set_precond_iluk.argtypes = [_VP, ctypes.c_int]
         L.gg_set_precond_iluk_device.argtypes = [_VP, ctypes.c_int]
@@ -221,6 +221,11 @@ class Solver:
     @property
     def uses_wavefront(self):
         return bool(lib().gg_uses_wavefront(self.h))
+
+    @property
+    def spmv_sliced(self):
+        """the matrix takes the sliced-ELL SpMV (else CSR-stream)"""
+        return bool(lib().gg_spmv_sliced(self.h))
 
     # ---- solve -------------------------------------------------------------
     def solve(self, b, x0=None, restart=30, max_iter=3000, tol=1e-10, flags=0):

@@ -147,6 +147,9 @@ int gg_set_precond_split(gg_solver *s,
 int gg_precond_kind(gg_solver *s);
 /* 1 if the structured-grid wavefront triangular solve is active, else 0 */
 int gg_uses_wavefront(gg_solver *s);
+/* the SpMV kernel the solver's matrix takes: 1 sliced ELL (k_spmv_sell: short,
+ * evenly filled rows), 0 CSR-stream (k_spmv_stream) */
+int gg_spmv_sliced(gg_solver *s);
 
 int gg_solve(gg_solver *s, const double *b, double *x, const gg_options *opt,
              gg_result *res);

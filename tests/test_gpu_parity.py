@@ -120,6 +120,7 @@ def test_spmv_c3_standin_full_size(solver):
     x = np.random.default_rng(12).standard_normal(A.shape[0])
     solver.set_matrix(A)
     solver.set_precond_none()
+    assert not solver.spmv_sliced
     y, ref = solver.spmv(x), O.spmv(A, x)
     rl = np.diff(A.indptr)
     short = rl <= 2048
@@ -436,7 +437,7 @@ def test_c2_full_size_properties(solver):
     L, U = O.ilu0(A)
     solver.set_matrix(A)
     solver.set_precond_ilu0()
-    assert solver.uses_wavefront
+    assert solver.uses_wavefront and solver.spmv_sliced
     # one full restart cycle against the oracle (serial order and order-matched)
     o, ot = oracle_both(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=30, tol=1e-300),
                         A.shape[0], nx=1000)
