@@ -376,6 +376,36 @@ def test_edge_cases(solver):
         check_exact(g, ot)
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 127, 513])
+def test_small_and_ragged_sizes(solver, n):
+    """Sizes around the 64-lane, 256-thread and 512-slot paddings: a seeded
+    diagonally dominant random matrix (natural layout, flow triangular solves)
+    and, where it is a grid, a 5-point n x 3 grid (wavefront layout)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(n)
+    R = sp.random(n, n, density=min(1.0, 4.0 / n), random_state=np.random.RandomState(n), format="csr")
+    R.data = -R.data
+    A = (R + sp.diags(np.asarray(abs(R).sum(axis=1)).ravel() + 1.0)).tocsr()
+    A.sort_indices()
+    cases = [(A, None)]
+    if n >= 2:
+        cases.append((M.laplacian_5pt(n, 3), n))
+    for A_, nx in cases:
+        b = rng.random(A_.shape[0])
+        L, U = O.ilu0(A_)
+        solver.set_matrix(A_)
+        solver.set_precond_ilu0()
+        wave = solver.uses_wavefront            # grids with nx >= 4 (tiny grids: level path)
+        assert wave == (nx is not None and nx >= 4) or not wave
+        o, ot = oracle_both(lambda: O.gmres_left(A_, L, U, b, m=10, max_iter=60, tol=1e-12),
+                            A_.shape[0], nx=nx if wave else None)
+        g = solver.solve(b, restart=10, max_iter=60, tol=1e-12)
+        check_gmres(g, o)
+        check_exact(g, ot)
+        x = rng.standard_normal(A_.shape[0])
+        assert np.array_equal(solver.spmv(x), O.spmv(A_, x))
+
+
 def test_concurrent_shared_solves(solver):
     """GG_SOLVE_SHARED_DEVICE: four solvers (own streams) solving at the same
     time from four host threads; each result bit-identical to the
