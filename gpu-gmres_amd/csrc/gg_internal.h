@@ -121,18 +121,25 @@ constexpr int kWaveTAlign = 32;
 struct Wave2D {
     bool ok = false;
     int nx = 0, ny = 0, nz = 1, nbands = 0, T = 0;
+    // lines lag each other by `skew` steps (1: ILU(0); k+1: ILU(k) on a 5-point
+    // grid, whose rows also reference (j-1, i+a), a <= k); 2D only.  Row (j, i)
+    // runs at step t = i + skew*l + (skew-1): the skew-1 lead-in steps fill the
+    // edge lane's history of the neighbour band's line (forward), and T keeps
+    // as many after the last row (backward)
+    int skew = 1;
     long long P2 = 0;        // one plane's layout length (nbands * T * 64)
     long long P = 0;         // padded layout length (nz * P2)
     long long ngran() const { return (long long)nz * nbands * T; }   // hand-off granules
     long long slot(long long r) const {
         const long long nxy = (long long)nx * ny;
         const long long k = r / nxy, q = r % nxy;
-        const int j = (int)(q / nx), i = (int)(q % nx), l = j & 63, t = i + l;
+        const int j = (int)(q / nx), i = (int)(q % nx), l = j & 63, t = i + skew * l + (skew - 1);
         return k * P2 + ((((long long)(j >> 6) * (T / 2) + t / 2) * 64 + l) * 2 + (t & 1));
     }
 };
-// detect: L off-diagonals only at offsets {nx (first), 1 (second)} and U only at
-// {nx (first), 1 (second)}, no wrap-around entries.  Returns ok=false otherwise.
+// detect: L off-diagonals only at offsets {nx, nx-1, .., nx-k, 1} in this order
+// and U at {nx, nx-1, .., nx-k, 1} (canonical orders; k <= 2: ILU(0..2) of a
+// 5-point grid), no wrap-around entries; skew = k + 1.  ok=false otherwise.
 Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U);
 // 3D: offsets {nx*ny, nx, 1} in this order in L and in U (canonical orders),
 // no wrap-around; nz >= 2 planes of the 2D layout
@@ -218,6 +225,7 @@ struct DevTri {
     Wave2D wl;
     DBuf<double> c1, c2, dw, rw; // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor, rw: RN(1/dw)
     DBuf<double> c0;             // 3D: |offset| = nx*ny coefficient
+    DBuf<double> ce1, ce2;       // skew 2/3 (ILU(1)/(2) fill): |offset| = nx-1, nx-2 coefficients
     DBuf<unsigned long long> prog;   // 3D: per (plane, band) batches stored (0 between launches)
     int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
     bool rcp_ok = false;         // every divisor admits WD_RCP

@@ -125,25 +125,38 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
     for (int r = 0; r < n; r++)
         for (int k = L.off.rp[r]; k < L.off.rp[r + 1]; k++) nx = std::max(nx, r - L.off.ci[k]);
     if (nx < 2 || n % nx != 0 || n / nx < 2) return w;
-    // L rows: [r-nx][r-1] in this order (either may be absent), no wrap of r-1
+    // the fill depth K: the smallest offset above 1 is nx - K
+    int K = 0;
+    for (int r = 0; r < n; r++)
+        for (int k = L.off.rp[r]; k < L.off.rp[r + 1]; k++) {
+            const int o = r - L.off.ci[k];
+            if (o > 1) K = std::max(K, nx - o);
+        }
+    if (K > 2 || nx < K + 3) return w;
+    // L rows: [r-nx][r-nx+1]..[r-nx+K][r-1] in this order (each may be absent),
+    // no wrap: (j-1, i+a) needs i + a < nx, (j, i-1) needs i > 0
     for (int r = 0; r < n; r++) {
         int lb = L.off.rp[r], ub = L.off.rp[r + 1], k = lb;
-        if (k < ub && L.off.ci[k] == r - nx) k++;
+        for (int a = 0; a <= K; a++)
+            if (k < ub && L.off.ci[k] == r - nx + a && (r % nx) + a < nx) k++;
         if (k < ub && L.off.ci[k] == r - 1 && (r % nx) != 0) k++;
         if (k != ub) return w;
     }
-    // U rows: [r+nx][r+1] in this order (LUSolve_ignoreZero walks from the row end)
+    // U rows (LUSolve_ignoreZero walks from the row end): [r+nx][r+nx-1]..[r+nx-K][r+1]
     for (int r = 0; r < n; r++) {
         int lb = U.off.rp[r], ub = U.off.rp[r + 1], k = lb;
-        if (k < ub && U.off.ci[k] == r + nx) k++;
+        for (int a = 0; a <= K; a++)
+            if (k < ub && U.off.ci[k] == r + nx - a && (r % nx) - a >= 0) k++;
         if (k < ub && U.off.ci[k] == r + 1 && (r % nx) != nx - 1) k++;
         if (k != ub) return w;
     }
     w.ok = true;
     w.nx = nx;
     w.ny = n / nx;
+    w.skew = K + 1;
     w.nbands = (w.ny + 63) / 64;
-    w.T = (nx + 63 + kWaveTAlign - 1) / kWaveTAlign * kWaveTAlign;   // the 63-step lane skew
+    // the lane skew, plus skew-1 lead-in and run-out steps (Wave2D::slot)
+    w.T = (nx + 63 * w.skew + 2 * (w.skew - 1) + kWaveTAlign - 1) / kWaveTAlign * kWaveTAlign;
     w.P2 = (long long)w.nbands * w.T * 64;
     w.P = w.P2;
     return w;

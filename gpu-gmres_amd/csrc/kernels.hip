@@ -551,11 +551,13 @@ constexpr int kWaveRing = GG_WAVE_RING;
 #endif
 constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 
-template <int DIV, bool D3 = false>
+template <int DIV, bool D3 = false, int S = 1>
 struct WaveCfg {
-    // streamed arrays: b, c1, c2 (, d (, RN(1/d))); a 3D grid adds the plane
-    // coefficient c0 and the previous plane's x
-    static constexpr int A2 = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;
+    // streamed arrays: b, c1, c2 (, d (, RN(1/d))); a skewed 2D grid (ILU(S-1))
+    // adds the fill coefficients of offsets nx-1 .. nx-S+1; a 3D grid adds the
+    // plane coefficient c0 and the previous plane's x
+    static constexpr int AE = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;    // first fill array
+    static constexpr int A2 = AE + (S - 1);
     static constexpr int A = A2 + (D3 ? 2 : 0);
     static constexpr int B16 = DIV == WD_UNIT ? GG_WAVE_BATCH_UNIT
                              : DIV == WD_HW   ? GG_WAVE_BATCH_HW
@@ -577,6 +579,7 @@ struct WaveCfg {
     static_assert(B == 8 || B == 16, "batch");
     static_assert(kWaveTAlign % (B * GG_WAVE_POLL) == 0, "batches per band must be a multiple of the poll depth");
     static_assert(!D3 || LOADERS == 1, "3D grids stream every array from one loader wave");
+    static_assert(S >= 1 && S <= 3 && (S == 1 || (!D3 && LOADERS == 1)), "skew: 2D, one loader");
     static_assert(kWaveLook >= 1 && kWaveLook <= PBN, "lookahead");
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
 };
@@ -664,14 +667,16 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
     }
 }
 
-template <bool FWD, int DIV, bool TRACE, bool D3 = false>
-__global__ __launch_bounds__((WaveCfg<DIV, D3>::THREADS)) void k_trsv_wave2d(
+template <bool FWD, int DIV, bool TRACE, bool D3 = false, int S = 1>
+__global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
     const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
     double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace,
-    int nz, long long P2, const double *__restrict__ c0, unsigned long long *prog)
+    int nz, long long P2, const double *__restrict__ c0, unsigned long long *prog,
+    const double *__restrict__ ce1, const double *__restrict__ ce2)
 {
-    using C = WaveCfg<DIV, D3>;
+    using C = WaveCfg<DIV, D3, S>;
+    static_assert(!(TRACE && S > 1), "no trace for skewed grids");
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
     static_assert(!(D3 && TRACE), "no trace for 3D grids");
     if (gated(g)) return;
@@ -710,6 +715,8 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3>::THREADS)) void k_trsv_wave2d(
                                  reinterpret_cast<const double2 *>(dv) + boff,
                                  reinterpret_cast<const double2 *>(rv) + boff,
                                  nullptr, nullptr};
+        if constexpr (S >= 2) src[C::AE] = reinterpret_cast<const double2 *>(ce1) + boff;
+        if constexpr (S >= 3) src[C::AE + 1] = reinterpret_cast<const double2 *>(ce2) + boff;
         if constexpr (D3) {
             // the plane coefficient and the previous plane's x (zeros on the
             // first plane, where c0 is 0) follow the 2D arrays
@@ -816,7 +823,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3>::THREADS)) void k_trsv_wave2d(
         const bool prog_lane = has_prev && lane == kProgLane;
         auto gaddr = [&](int bj) {
             const int t = FWD ? bj * C::B + lane : (T - 1) - (bj * C::B + lane);
-            const int gi = FWD ? t + 63 : t - 63;
+            const int gi = FWD ? t + (64 * S - 1) : t - (64 * S - 1);     // the neighbour's edge lane
             const bool need = has_src && lane < C::B && bj < nbatch && gi >= 0 && gi < T;
             return need ? src + gi : (unsigned long long *)nullptr;
         };
@@ -890,6 +897,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3>::THREADS)) void k_trsv_wave2d(
     long long ph[4] = {0, 0, 0, 0};     // TRACE: barrier wait, top->step0, step0->last, last->end
     long long t_top = 0;
     double xp = 0.0;                        // this lane's previous step value
+    double xh1 = 0.0, xh2 = 0.0;            // skew > 1: the neighbour line's values 2 and 3 steps back
     // Operands of the current batch in registers, read kWaveLook step pairs
     // ahead of their use; the boundary values are read first (LDS returns in
     // order and they are needed at the batch's first step).
@@ -966,8 +974,25 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3>::THREADS)) void k_trsv_wave2d(
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                double acc = bz - e1 * xs;      // line neighbour next (|offset| = nx)
-                acc = acc - p2;                 // then the in-line neighbour (|offset| = 1)
+                // the neighbour line's terms oldest first (|offset| = nx, nx-1, ..),
+                // then the in-line neighbour (|offset| = 1)
+                double acc;
+                if constexpr (S == 1) {
+                    acc = bz - e1 * xs;
+                } else if constexpr (S == 2) {
+                    const double f1 = sx ? rg[kk][C::AE].x : rg[kk][C::AE].y;
+                    acc = bz - e1 * xh1;
+                    acc = acc - f1 * xs;
+                } else {
+                    const double f1 = sx ? rg[kk][C::AE].x : rg[kk][C::AE].y;
+                    const double f2 = sx ? rg[kk][C::AE + 1].x : rg[kk][C::AE + 1].y;
+                    acc = bz - e1 * xh2;
+                    acc = acc - f1 * xh1;
+                    acc = acc - f2 * xs;
+                }
+                if constexpr (S >= 3) xh2 = xh1;
+                if constexpr (S >= 2) xh1 = xs;
+                acc = acc - p2;
                 if constexpr (DIV == WD_HW) {
                     acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
                 } else if constexpr (DIV == WD_RCP) {
@@ -1845,10 +1870,16 @@ int wave3d_max_blocks()
     return cached;
 }
 
-int wave_batch_steps(int div, bool d3)
+int wave_batch_steps(int div, bool d3, int skew)
 {
     if (d3) return div == WD_UNIT ? WaveCfg<WD_UNIT, true>::B : div == WD_HW ? WaveCfg<WD_HW, true>::B
                                                                               : WaveCfg<WD_RCP, true>::B;
+    if (skew == 2)
+        return div == WD_UNIT ? WaveCfg<WD_UNIT, false, 2>::B : div == WD_HW ? WaveCfg<WD_HW, false, 2>::B
+                                                                             : WaveCfg<WD_RCP, false, 2>::B;
+    if (skew == 3)
+        return div == WD_UNIT ? WaveCfg<WD_UNIT, false, 3>::B : div == WD_HW ? WaveCfg<WD_HW, false, 3>::B
+                                                                             : WaveCfg<WD_RCP, false, 3>::B;
     return div == WD_UNIT ? WaveCfg<WD_UNIT>::B : div == WD_HW ? WaveCfg<WD_HW>::B : WaveCfg<WD_RCP>::B;
 }
 
@@ -1899,16 +1930,22 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         const double *rv = T.div == WD_RCP ? T.rw.p : nullptr;
         if (w.nz == 1) {
             dim3 grid(w.nbands);
+#define GG_WAVE_LAUNCH_S(FWD, DIV, S)                                                              \
+    k_trsv_wave2d<FWD, DIV, false, false, S><<<grid, WaveCfg<DIV, false, S>::THREADS, 0, st>>>(    \
+        g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr,   \
+        nullptr, T.ce1.p, T.ce2.p)
 #define GG_WAVE_LAUNCH(FWD, DIV)                                                                   \
     do {                                                                                           \
-        if (T.trace)                                                                               \
+        if (T.trace && w.skew == 1)                                                                \
             k_trsv_wave2d<FWD, DIV, true><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                 \
                 g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, T.trace, 1, w.P2,     \
-                nullptr, nullptr);                                                                 \
+                nullptr, nullptr, nullptr, nullptr);                                               \
+        else if (w.skew == 1)                                                                      \
+            GG_WAVE_LAUNCH_S(FWD, DIV, 1);                                                         \
+        else if (w.skew == 2)                                                                      \
+            GG_WAVE_LAUNCH_S(FWD, DIV, 2);                                                         \
         else                                                                                       \
-            k_trsv_wave2d<FWD, DIV, false><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                \
-                g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2,     \
-                nullptr, nullptr);                                                                 \
+            GG_WAVE_LAUNCH_S(FWD, DIV, 3);                                                         \
     } while (0)
             if (T.lower) {
                 if (T.div == WD_UNIT) GG_WAVE_LAUNCH(true, WD_UNIT);
@@ -1920,6 +1957,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
                 else GG_WAVE_LAUNCH(false, WD_RCP);
             }
 #undef GG_WAVE_LAUNCH
+#undef GG_WAVE_LAUNCH_S
         } else {
             // 3D: persistent, every workgroup co-resident (tasks wait on tasks)
             const int ntask = w.nz * w.nbands;
@@ -1928,7 +1966,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         const int grid = std::min(ntask, wave3d_max_blocks<FWD, DIV>());                           \
         k_trsv_wave2d<FWD, DIV, false, true><<<grid, WaveCfg<DIV, true>::THREADS, 0, st>>>(        \
             g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, w.nz, w.P2,      \
-            T.c0.p, T.prog.p);                                                                     \
+            T.c0.p, T.prog.p, nullptr, nullptr);                                                   \
     } while (0)
             if (T.lower) {
                 if (T.div == WD_UNIT) GG_WAVE_LAUNCH3(true, WD_UNIT);

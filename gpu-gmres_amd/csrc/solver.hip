@@ -123,6 +123,8 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         const bool d3 = wl->nz > 1;
         std::vector<double> c1(Ppad, 0.0), c2(Ppad, 0.0), dv(Ppad, 1.0), rv(Ppad, 1.0);
         std::vector<double> c0(d3 ? Ppad : 0, 0.0);
+        const int K = wl->skew - 1;              // fill offsets nx-1 .. nx-K (2D)
+        std::vector<double> ce1(K >= 1 ? Ppad : 0, 0.0), ce2(K >= 2 ? Ppad : 0, 0.0);
         bool unit = true, rcp_ok = true;
         const int nx = wl->nx;
         const long long nxy = (long long)wl->nx * wl->ny;
@@ -131,6 +133,8 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
             for (int k = C.off.rp[r]; k < C.off.rp[r + 1]; k++) {
                 const long long off = std::abs((long long)C.off.ci[k] - r);
                 if (d3 && off == nxy) c0[p] = C.off.v[k];
+                else if (K >= 1 && off == nx - 1) ce1[p] = C.off.v[k];
+                else if (K >= 2 && off == nx - 2) ce2[p] = C.off.v[k];
                 else (off == nx ? c1 : c2)[p] = C.off.v[k];
             }
             const double d = C.d[r];
@@ -142,6 +146,8 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         }
         T.c1.upload(c1, st);
         T.c2.upload(c2, st);
+        if (K >= 1) T.ce1.upload(ce1, st);
+        if (K >= 2) T.ce2.upload(ce2, st);
         if (d3) {
             T.c0.upload(c0, st);
             T.prog.alloc((size_t)wl->nz * wl->nbands);
@@ -164,7 +170,7 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         launch_fill_u64(T.bnd.p, ngran, kSentinel, st);
         launch_fill_u64(T.bnd.p + ngran, 128, 0ull, st);
         // algorithmic bytes: b, two coefficients, (divisor (, reciprocal)), x per grid point
-        T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? 2 : 0)));
+        T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? 2 : 0) + K));
     } else {
         T.kind = DevTri::LEVEL;
         T.off.upload(C.off, st);
@@ -1469,7 +1475,8 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     GG_REQUIRE(s && out && nbands && nbatch && (which == 0 || which == 1), GG_EINVAL, "bad argument");
     GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner");
     DevTri &T = which == 0 ? s->L : s->U;
-    GG_REQUIRE(T.kind == DevTri::WAVE2D && T.wl.nz == 1, GG_ESTATE, "2D wavefront path not active");
+    GG_REQUIRE(T.kind == DevTri::WAVE2D && T.wl.nz == 1 && T.wl.skew == 1, GG_ESTATE,
+               "unskewed 2D wavefront path not active");
     set_device(s);
     ensure_workspace(s, std::max(s->m_alloc, 1));
     const int nb = T.wl.nbands, nbt = T.wl.T / wave_batch_steps(T.div);

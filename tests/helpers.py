@@ -57,13 +57,14 @@ def hist_close(h_test, h_ref, rtol):
 
 
 # ---- the device vector space (DESIGN.md "Wavefront layout", "Reduction order")
-def device_layout(n, nx=None, ny=None):
+def device_layout(n, nx=None, ny=None, skew=1):
     """(lay2nat, G) of the solver's vector space: natural order, or -- for a 2D
     grid of line length nx on the wavefront path -- band = j//64, lane l = j%64,
-    step t = i + l, slot ((band*T/2 + t//2)*64 + l)*2 + t%2 with
-    T = roundup(nx+63, 32); for a 3D grid (ny given) the planes of that layout
-    one after the other; padded to a multiple of 512 slots;
-    G = min(1024, ceil(Ppad/2 / 1024)) reduction blocks."""
+    step t = i + skew*l + skew-1, slot ((band*T/2 + t//2)*64 + l)*2 + t%2 with
+    T = roundup(nx + 63*skew + 2*(skew-1), 32) (skew = k+1 for ILU(k) factors
+    of a 5-point grid); for a 3D grid (ny given) the planes of that layout one after the
+    other; padded to a multiple of 512 slots; G = min(1024, ceil(Ppad/2 / 1024))
+    reduction blocks."""
     if nx is None:
         P = n
         slots = np.arange(n, dtype=np.int64)
@@ -71,7 +72,7 @@ def device_layout(n, nx=None, ny=None):
         nxy = n if ny is None else nx * ny
         ny = nxy // nx
         nz = n // nxy
-        T = (nx + 63 + 31) // 32 * 32
+        T = (nx + 63 * skew + 2 * (skew - 1) + 31) // 32 * 32
         nb = (ny + 63) // 64
         P2 = nb * T * 64
         P = nz * P2
@@ -79,7 +80,7 @@ def device_layout(n, nx=None, ny=None):
         k, q = r // nxy, r % nxy
         j, i = q // nx, q % nx
         lane = j % 64
-        t = i + lane
+        t = i + skew * lane + (skew - 1)
         slots = k * P2 + (((j // 64) * (T // 2) + t // 2) * 64 + lane) * 2 + t % 2
     ppad = max((max(P, 1) + 511) // 512 * 512, 512)
     lay2nat = np.full(ppad, -1, np.int64)

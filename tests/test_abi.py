@@ -167,9 +167,14 @@ def test_wavefront_detection(ggmres_lib):
         A = M.laplacian_5pt(nx, ny)
         L, U = O.ilu0(A)
         assert wave(ggmres_lib, L, U) == (1, nx, ny)
-    # 3D 7-pt, 9-pt and ILU(1) factors do not have the 2D 5-pt structure
+    # 3D 7-pt and 9-pt factors do not have the 2D 5-pt structure
     for A in (M.grid_7pt(8), load("9pt_10x10.mtx")):
         L, U = O.ilu0(A)
         assert wave(ggmres_lib, L, U)[0] == 0
-    L, U = O.iluk(M.laplacian_5pt(30), 1)
+    # ILU(1) / ILU(2) factors of a 5-point grid: the skewed wavefront (fill at
+    # offsets nx-1, nx-2); ILU(3) adds offset nx-3: beyond the kernel's skew 3
+    for k in (1, 2):
+        L, U = O.iluk(M.laplacian_5pt(30), k)
+        assert wave(ggmres_lib, L, U) == (1, 30, 30)
+    L, U = O.iluk(M.laplacian_5pt(30), 3)
     assert wave(ggmres_lib, L, U)[0] == 0

@@ -167,14 +167,34 @@ def test_wavefront_division_modes(solver, name, scale, hwdiv, monkeypatch):
         assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
 
 
-def test_lu_precond_user_factors(solver):
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_lu_precond_user_factors(solver, k):
+    """ILU(1)/ILU(2) factors of a 5-point grid: the skewed wavefront (skew k+1);
+    ILU(3) adds offset nx-3 -> the dataflow kernel"""
     A = M.laplacian_5pt(50, 70)
-    L, U = O.iluk(A, 1)   # ILU(1) factors: not grid-structured -> level path
+    L, U = O.iluk(A, k)
     solver.set_matrix(A)
     solver.set_precond_lu(L, U)
-    assert not solver.uses_wavefront
+    assert solver.uses_wavefront == (k <= 2)
     y = np.random.default_rng(4).random(A.shape[0])
     assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
+
+
+@pytest.mark.parametrize("k", [1, 2])
+@pytest.mark.parametrize("dims", [(100, 100), (37, 64), (5, 200), (300, 129)])
+@pytest.mark.parametrize("scale", [1.0, 1e250])
+def test_skewed_wavefront_apply(solver, k, dims, scale, monkeypatch):
+    """ILU(k) on 5-point grids (ragged bands, narrow lines, several bands): the
+    skewed wavefront gives the serial solve bit for bit; at 1e250 the WD_RCP
+    division leaves its safe range and the apply is redone with IEEE division"""
+    A = M.laplacian_5pt(*dims)
+    L, U = O.iluk(A, k)
+    solver.set_matrix(A)
+    solver.set_precond_iluk(k)
+    assert solver.uses_wavefront
+    y = np.random.default_rng(7).standard_normal(A.shape[0]) * scale
+    for _ in range(2):
+        assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
 
 
 def test_split_maps_bitexact(solver):
@@ -213,10 +233,10 @@ def check_exact(g, o):
     assert np.array_equal(g["x"], o["x"]), rel_err(g["x"], o["x"])
 
 
-def oracle_both(run, n, nx=None, ny=None):
+def oracle_both(run, n, nx=None, ny=None, skew=1):
     """run() under serial and under order-matched dot products."""
     o_serial = run()
-    lay, G = device_layout(n, nx, ny)
+    lay, G = device_layout(n, nx, ny, skew)
     O.set_dot_order(lay, G)
     try:
         o_tree = run()
@@ -285,6 +305,27 @@ def test_gmres_iluk_parity(solver):
     solver.set_matrix(A)
     solver.set_precond_iluk(1)
     g = solver.solve(b, restart=20, max_iter=1000, tol=1e-10)
+    check_gmres(g, o)
+    check_exact(g, ot)
+
+
+@pytest.mark.parametrize("k,dims,device", [(1, (100, 100), False), (2, (37, 64), False),
+                                           (1, (130, 70), True)])
+def test_gmres_iluk_grid_parity(solver, k, dims, device):
+    """GMRES + ILU(k) on 5-point grids through the skewed wavefront (layout
+    lane skew k+1): serial-oracle tolerance and order-matched bit-exact"""
+    A = M.laplacian_5pt(*dims)
+    b = M.rhs_uniform(A.shape[0])
+    L, U = O.iluk(A, k)
+    o, ot = oracle_both(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=2000, tol=1e-10),
+                        A.shape[0], nx=dims[0], skew=k + 1)
+    solver.set_matrix(A)
+    if device:
+        solver.set_precond_iluk_device(k)
+    else:
+        solver.set_precond_iluk(k)
+    assert solver.uses_wavefront
+    g = solver.solve(b, restart=30, max_iter=2000, tol=1e-10)
     check_gmres(g, o)
     check_exact(g, ot)
 
