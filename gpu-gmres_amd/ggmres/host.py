@@ -159,3 +159,87 @@ class DDPlan:
         out["iface"] = iface[:ni]
         out["rows"] = rows[:nI + nS]
         return out
+
+
+# ---- SPICE power-grid netlist -> MNA (gg_host_read_netlist)
+class _Netlist(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int), ("n_l", ctypes.c_int), ("n_v", ctypes.c_int),
+                ("n_i", ctypes.c_int), ("n", ctypes.c_int), ("tstep", ctypes.c_double),
+                ("tstop", ctypes.c_double),
+                ("g_row_ptr", _PI), ("g_col_idx", _PI), ("g_val", _PD),
+                ("c_row_ptr", _PI), ("c_col_idx", _PI), ("c_val", _PD),
+                ("b_row_ptr", _PI), ("b_col_idx", _PI), ("b_val", _PD),
+                ("src_kind", _PI), ("src_ptr", _PI), ("src_data", _PD),
+                ("nport", ctypes.c_int), ("port", _PI)]
+
+
+class Netlist:
+    """The MNA system of a flat SPICE power-grid netlist (parser() + stampG /
+    stampC / stampB, src/parser.cpp:69-272, 1904-2886): G, C (n x n) and B
+    (n x nsrc) as scipy CSR, sources [(kind, params)] (V first, then I),
+    tstep, tstop, ports (unknown indices, -1 = ground / unknown)."""
+
+    def __init__(self, path):
+        nl = _Netlist()
+        L = lib()
+        L.gg_host_read_netlist.argtypes = [ctypes.c_char_p, ctypes.POINTER(_Netlist)]
+        L.gg_host_free_netlist.argtypes = [ctypes.POINTER(_Netlist)]
+        L.gg_host_free_netlist.restype = None
+        _check(L.gg_host_read_netlist(str(path).encode(), ctypes.byref(nl)))
+        try:
+            n = nl.n
+            self.n, self.n_nodes, self.n_l, self.n_v, self.n_i = n, nl.n_nodes, nl.n_l, nl.n_v, nl.n_i
+            self.tstep, self.tstop = nl.tstep, nl.tstop
+            nsrc = nl.n_v + nl.n_i
+
+            def csr(rp_p, ci_p, v_p, ncols):
+                rp = np.ctypeslib.as_array(rp_p, (n + 1,)).copy()
+                nnz = int(rp[-1])
+                ci = np.ctypeslib.as_array(ci_p, (max(nnz, 1),))[:nnz].copy()
+                v = np.ctypeslib.as_array(v_p, (max(nnz, 1),))[:nnz].copy()
+                return sp.csr_matrix((v, ci, rp), shape=(n, ncols))
+
+            self.G = csr(nl.g_row_ptr, nl.g_col_idx, nl.g_val, n)
+            self.C = csr(nl.c_row_ptr, nl.c_col_idx, nl.c_val, n)
+            self.B = csr(nl.b_row_ptr, nl.b_col_idx, nl.b_val, nsrc)
+            kind = np.ctypeslib.as_array(nl.src_kind, (max(nsrc, 1),))[:nsrc].copy()
+            ptr = np.ctypeslib.as_array(nl.src_ptr, (nsrc + 1,)).copy()
+            data = np.ctypeslib.as_array(nl.src_data, (max(int(ptr[-1]), 1),))[:int(ptr[-1])].copy()
+            self.sources = [(int(kind[k]), data[ptr[k]:ptr[k + 1]].copy()) for k in range(nsrc)]
+            self.ports = np.ctypeslib.as_array(nl.port, (max(nl.nport, 1),))[:nl.nport].copy()
+        finally:
+            L.gg_host_free_netlist(ctypes.byref(nl))
+
+    def transient_inputs(self, h):
+        """(A = G + C/h, cdiag = diag(C)/h, src_node, src_kind, src_ptr, src_data)
+        for Solver.transient_src.  Needs a diagonal C and one +-1 entry per
+        source column of B; a -1 entry negates the source's values (exact)."""
+        from . import SRC_DC, SRC_PULSE
+        C = self.C.tocoo()
+        if np.any(C.row != C.col):
+            raise ValueError("C is not diagonal (capacitors between two non-ground nodes)")
+        Bc = self.B.tocsc()
+        cdiag = np.zeros(self.n)
+        cdiag[C.row] = C.data / h
+        nodes, kinds, ptr, data = [], [], [0], []
+        for k, (kind, par) in enumerate(self.sources):
+            lo, hi = Bc.indptr[k], Bc.indptr[k + 1]
+            if hi - lo != 1 or abs(Bc.data[lo]) != 1.0:
+                raise ValueError(f"source {k}: B column is not a single +-1 entry")
+            sgn = Bc.data[lo]
+            par = np.array(par, dtype=np.float64)
+            if sgn < 0:
+                if kind == SRC_DC:
+                    par = -par
+                elif kind == SRC_PULSE:
+                    par[:2] = -par[:2]
+                else:
+                    par[1::2] = -par[1::2]
+            nodes.append(int(Bc.indices[lo]))
+            kinds.append(kind)
+            data.extend(par.tolist())
+            ptr.append(len(data))
+        A = (self.G + sp.diags(cdiag)).tocsr()
+        A.sort_indices()
+        return (A, cdiag, np.array(nodes, np.int32), np.array(kinds, np.int32),
+                np.array(ptr, np.int32), np.array(data, np.float64))

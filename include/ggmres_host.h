@@ -15,6 +15,8 @@
  *   gg_host_block      dd_form block extraction  src/form_dd.cpp:32-110
  *   gg_host_read_mtx   readSparseMatrix (Matrix Market)  src_thermal/SpMV_gen.cpp:93-187
  *   gg_host_coo2csr_in coo2csrDouble_in  src/formatConvert.cpp:165-216
+ *   gg_host_read_netlist  SPICE power-grid netlist -> MNA (G, C, B, sources):
+ *                  parser() + stampG/stampC/stampB  src/parser.cpp:69-272, 1904-2886
  * Output arrays are malloc'd by the library; release them with gg_host_free.
  */
 #ifndef GGMRES_HOST_H_
@@ -73,6 +75,39 @@ int gg_host_wave3d(int n, const int *l_row_ptr, const int *l_col_idx, const doub
  * max(nz, nrows + 1) slots), entries of a row bubble-sorted by column.
  * The reference's C++ boundary-feed symbols are in include/compat/format_convert.h. */
 int gg_host_coo2csr_in(int nrows, int nz, double *val, int *row_idx, int *col_idx);
+/* Flat SPICE power-grid netlist (R, C, L, V, I element lines, '+' PWL
+ * continuation lines, .tran tstep tstop, .print/.probe ports, one .include
+ * level) -> the reference's MNA system.  Unknowns: the n_nodes non-ground
+ * nodes numbered by first appearance ("0" and "gnd" are ground), then one
+ * branch current per inductor and per voltage source, n in all.
+ *   G (n x n): R stamps 1/R; L and V branch incidences +-1
+ *   C (n x n): C stamps; L branch rows get L
+ *   B (n x (n_v + n_i)): V source k: -1 at its branch row; I source k:
+ *                        -1 at n1, +1 at n2
+ * CSR, columns ascending, duplicate stamps summed in netlist order (as the
+ * reference's matrix::pushEntry).  Source k (V first, then I, netlist order):
+ * src_kind[k] in gg_src_kind, parameters src_data[src_ptr[k] .. src_ptr[k+1]):
+ * DC {value}; PULSE {v1, v2, td, tr, tf, pw, period} from "<dc> PULSE(...)"
+ * (gen_PULSEut_kernel's parameters); PWL {t0, v0, t1, v1, ...} with a point
+ * (0, v0) in front when t0 != 0.  port[k] = unknown index of .print port k
+ * (-1: ground or unknown name).  Arrays are malloc'd; release the whole
+ * struct with gg_host_free_netlist.  GG_EINVAL if the file cannot be read. */
+typedef struct gg_netlist {
+    int n_nodes, n_l, n_v, n_i, n;
+    double tstep, tstop;
+    int *g_row_ptr, *g_col_idx;
+    double *g_val;
+    int *c_row_ptr, *c_col_idx;
+    double *c_val;
+    int *b_row_ptr, *b_col_idx;
+    double *b_val;
+    int *src_kind, *src_ptr;
+    double *src_data;
+    int nport;
+    int *port;
+} gg_netlist;
+int gg_host_read_netlist(const char *path, gg_netlist *out);
+void gg_host_free_netlist(gg_netlist *nl);
 /* Sharded-solve plan (the host half of include/ggmres_dd.h, exposed for CPU
  * checks of the decomposition): partition4 + arrow permutation B = P A P^T +
  * ILU(0) of B + per-part pieces in the part's local index space
