@@ -78,8 +78,8 @@ def parse():
 KERNEL_NAMES = {
     # sliced-ELL SpMV on short even rows (grids); GG_SPMV_CSR=1 keeps the CSR-stream kernel
     "spmv": "k_spmv_stream<false>" if os.environ.get("GG_SPMV_CSR") == "1" else "k_spmv_sell<false>",
-    "trsv_L": "k_trsv_wave2d<true, 0, false, false>",     # lower, unit diagonal (ILU(0) L), 2D grid
-    "trsv_U": "k_trsv_wave2d<false, 2, false, false>",    # upper, reciprocal division (ILU(0) U), 2D grid
+    "trsv_L": "k_trsv_wave2d<true, 0, false, false, 1>",  # lower, unit diagonal (ILU(0) L), 2D grid
+    "trsv_U": "k_trsv_wave2d<false, 2, false, false, 1>", # upper, reciprocal division (ILU(0) U), 2D grid
 }
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # bare dependent-chain latency of one wavefront step (cycles, tools/lat_probe.hip:
