@@ -447,29 +447,35 @@ def test_small_and_ragged_sizes(solver, n):
         assert np.array_equal(solver.spmv(x), O.spmv(A_, x))
 
 
-def test_concurrent_shared_solves(solver):
+@pytest.mark.parametrize("k", [0, 1])
+def test_concurrent_shared_solves(solver, k):
     """GG_SOLVE_SHARED_DEVICE: four solvers (own streams) solving at the same
     time from four host threads; each result bit-identical to the
     order-matched oracle (the flag swaps the persistent orthogonalization
-    launch for the per-step kernels, same arithmetic)."""
+    launch for the per-step kernels, same arithmetic).  k = 1: ILU(1) factors
+    on the skewed wavefront."""
     import threading
     A = M.laplacian_5pt(300, 256)
-    L, U = O.ilu0(A)
-    bs = [M.rhs_uniform(A.shape[0], seed=50 + k) for k in range(4)]
+    L, U = O.iluk(A, k) if k else O.ilu0(A)
+    bs = [M.rhs_uniform(A.shape[0], seed=50 + q) for q in range(4)]
     refs = [oracle_both(lambda b=b: O.gmres_left(A, L, U, b, m=30, max_iter=90, tol=1e-300),
-                        A.shape[0], nx=300)[1] for b in bs]
+                        A.shape[0], nx=300, skew=k + 1)[1] for b in bs]
     ss = [ggmres.Solver(0) for _ in range(4)]
     try:
         for s_ in ss:
             s_.set_matrix(A)
-            s_.set_precond_ilu0()
+            if k:
+                s_.set_precond_iluk(k)
+            else:
+                s_.set_precond_ilu0()
+            assert s_.uses_wavefront
         out = [None] * 4
 
-        def run(k):
-            out[k] = ss[k].solve(bs[k], restart=30, max_iter=90, tol=1e-300,
+        def run(q):
+            out[q] = ss[q].solve(bs[q], restart=30, max_iter=90, tol=1e-300,
                                  flags=ggmres.SOLVE_SHARED_DEVICE)
 
-        th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+        th = [threading.Thread(target=run, args=(q,)) for q in range(4)]
         for t in th:
             t.start()
         for t in th:
@@ -479,6 +485,17 @@ def test_concurrent_shared_solves(solver):
     finally:
         for s_ in ss:
             s_.close()
+
+
+def test_trace_refuses_skewed_wavefront(solver):
+    """gg_trace_precond instruments only the unskewed kernel: GG_ESTATE (-5) on ILU(1)."""
+    A = M.laplacian_5pt(64, 64)
+    solver.set_matrix(A)
+    solver.set_precond_iluk(1)
+    assert solver.uses_wavefront
+    with pytest.raises(ggmres.GGError) as e:
+        solver.trace_precond(0)
+    assert e.value.code == -5
 
 
 def test_shared_flag_needs_2d_wavefront(solver):
