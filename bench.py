@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--grid", type=int, default=1000, help="grid side (1000 = C2, 100 = C1)")
     p.add_argument("--restart", type=int, default=30)
+    p.add_argument("--ilu-level", type=int, default=0,
+                   help="c2 only: ILU(k) factors (device numeric phase); k = 1, 2 run the skewed wavefront")
     p.add_argument("--tol", type=float, default=1e-8)
     p.add_argument("--max-iter", type=int, default=20000)
     p.add_argument("--cpu-iters", type=int, default=120,
@@ -281,7 +283,13 @@ def main():
     s = ggmres.Solver(local)
     t_setup = time.perf_counter()
     s.set_matrix(A)
-    s.set_precond_ilu0()
+    kilu = a.ilu_level if a.workload == "c2" else 0
+    if kilu:
+        s.set_precond_iluk_device(kilu)
+        for dom_ in ("trsv_L", "trsv_U"):              # the skewed instantiation (skew k+1)
+            KERNEL_NAMES[dom_] = KERNEL_NAMES[dom_][:-2] + f"{kilu + 1}>"
+    else:
+        s.set_precond_ilu0()
     t_setup = time.perf_counter() - t_setup
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -415,6 +423,7 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(KERNEL_NAMES[dom]) if (s.uses_wavefront or dom == "spmv") and not c4 and not c3s
+                and not kilu
                 else None,
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
                 "launches_timed": f["launches"]}
@@ -424,7 +433,7 @@ def main():
     lat = None
     if roof and dom in ("trsv_L", "trsv_U") and s.uses_wavefront and not c4 and not c5:
         cyc = CHAIN_CYCLES["trsv_L" if dom == "trsv_L" else "trsv_U"]
-        steps = 2 * a.grid - 1
+        steps = a.grid + (kilu + 1) * (a.grid - 1)    # the DAG's longest path (ILU(k): skew k+1)
         floor_us = steps * cyc / (SHADER_GHZ * 1e3)
         lat = {"kernel": roof["kernel"], "bound": "dependency chain", "critical_steps": steps,
                "cycles_per_step": cyc, "clock_ghz": SHADER_GHZ, "floor_us": round(floor_us, 2),
@@ -466,7 +475,7 @@ def main():
                                 f"(no parity claim), ILU(0) left (C3 names ILU(1): out of reach on "
                                 f"this matrix, DESIGN.md 5.1), GMRES({a.restart}), tol {a.tol:g}, "
                                 f"b=A*1, x0=0, one solve per step") if c3s else
-                               (f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU(0) left, "
+                               (f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU({kilu}) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step"),
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
