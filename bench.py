@@ -12,8 +12,10 @@ profiled warmup step that brackets every kernel family), timed live inside the
 timed region with hipEvent pairs around its launches only, on the solver's
 stream (gg_profile_*); algorithmic bytes from SURVEY.md 8(d) (DESIGN.md
 "Kernels"); traffic: HBM bytes per launch from the committed rocprofv3 PMC
-passes (profiles/pmc_traffic.json).  cpu_baseline: the fp64 oracle restatement
-(oracle/, serial C) on a bounded sample of the same workload, rank 0 only.
+passes (profiles/pmc_traffic.json), null when those counters were taken on
+other kernel sources (src_sha).  cpu_baseline: the fp64 oracle restatement
+(oracle/, serial C, one thread pinned to one core) on a bounded sample of the
+same workload, rank 0 at N = 1 only.
 
 --workload c3: SpMV on the circuit5M stand-in (seeded power-law CSR with
 circuit5M's n = 5,558,326 and nnz ~ 59.5M; the SuiteSparse file
@@ -24,10 +26,15 @@ algorithmic SpMV bytes / time in GB/s (no parity claim on this matrix).
 PULSE sources, --c5-steps backward-Euler steps per step, warm start); value =
 GMRES iterations of all steps / time.
 
-Multi-GPU (torchrun, one rank per GPU): every rank solves its own system (C2
-replicas, or its own C5 source scenario: independent many-RHS scenarios),
-"scaling": "weak", no collective on the data path; the arrow-partitioned
-sharded solve is DESIGN.md "Multi-GPU".
+Multi-GPU: `--gpus N` (N > 1) without torchrun starts N rank processes (one
+per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, before the parent makes
+any GPU call) and exits with their status; under torchrun WORLD_SIZE must equal
+--gpus.  At N > 1 the default workload is the SHARDED solve of the C2 system
+(include/ggmres_dd.h: partition4 arrow ordering, one shard per GPU, RCCL
+all-gathers over xGMI; "scaling": "strong", parallelism "ddN"); `--workload dd`
+shards C4 (216^3 7-point) instead.  `--workload replicas` keeps the old
+independent-C2-per-rank run ("scaling": "weak", no collective on the data
+path); `--workload c5` gives each rank its own source scenario (many-RHS).
 """
 import argparse
 import json
@@ -64,11 +71,14 @@ def parse():
     p.add_argument("--c4-grid", type=int, default=216, help="C4: grid points per side (216^3 = 10.1M rows)")
     p.add_argument("--dd-parts", type=int, default=8,
                    help="dd workload on one process: shards held by this process (GG_DD_LOCAL)")
-    p.add_argument("--dd-grid", choices=["c4", "c2"], default="c4",
-                   help="dd workload system: c4 (216^3 7-pt) or c2 (1000^2 5-pt)")
-    p.add_argument("--workload", choices=["c2", "c3", "c3s", "c4", "c5", "dd"], default="c2",
-                   help="c2: one C2 solve per step (the headline); c5: a backward-Euler "
-                        "transient (A = G + C/h, 1%% PULSE sources) of --c5-steps time steps per step")
+    p.add_argument("--dd-grid", choices=["c4", "c2"], default=None,
+                   help="dd workload system: c4 (216^3 7-pt, the default of --workload dd) or c2 "
+                        "(1000^2 5-pt, the default sharded system at --gpus N > 1)")
+    p.add_argument("--workload", choices=["c2", "c3", "c3s", "c4", "c5", "dd", "replicas"], default=None,
+                   help="default: c2 at N = 1 (one C2 solve per step, the headline), the sharded C2 "
+                        "solve at N > 1; dd: the sharded solve (C4 unless --dd-grid c2); replicas: "
+                        "one independent C2 solve per rank; c5: a backward-Euler transient (A = G + C/h, "
+                        "1%% PULSE sources) of --c5-steps time steps per step")
     p.add_argument("--c5-steps", type=int, default=100)
     p.add_argument("--c5-scenarios", type=int, default=1,
                    help="c5: independent source scenarios per GPU, solved concurrently (one solver, "
@@ -101,22 +111,41 @@ def pmc_traffic(kernel, workload=None):
     try:
         with open(path) as f:
             d = json.load(f)
+        sys.path.insert(0, os.path.join(REPO, "profiles"))
+        from pmc_traffic import src_sha
+        if d.get("src_sha") != src_sha():      # counters taken on other kernel sources: stale
+            return None
         return d["kernels"][kernel]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
 
 
 def mgs_bytes(n, m, inner_list):
-    """Algorithmic MGS bytes for the inner iterations actually run:
-    iteration with cycle index i moves 40 n (i+1) (dot + AXPY per k) + 24 n (norm+scale)."""
-    tot = 0.0
+    """MGS bytes for the inner iterations actually run, as (fused, reference, iterations):
+    fused = what the one-launch orthogonalization (k_arnoldi_persist) must move at
+    cycle index i: v_0..v_i and w read once, v_{i+1} written = 8 n (i+3); reference =
+    SURVEY.md 8(d)'s count of the unfused reference operations, 40 n (i+1) (dot + AXPY
+    per k) + 24 n (norm + scale) -- a reference-equivalent figure, not HBM traffic."""
+    fused = ref = 0.0
     iters = 0
     for inner in inner_list:
         full, rem = divmod(inner, m)
         for i in list(range(m)) * full + list(range(rem)):
-            tot += 40.0 * n * (i + 1) + 24.0 * n
+            fused += 8.0 * n * (i + 3)
+            ref += 40.0 * n * (i + 1) + 24.0 * n
             iters += 1
-    return tot, iters
+    return fused, ref, iters
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def bench_c3(a, torch, dist, world, rank, local):
@@ -192,8 +221,13 @@ def bench_dd(a, torch, dist, world, rank, local):
         uid = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         d = DD(world, device=local, rank=rank, uid=uid[0])
+        ranks, myrank = d.comm_ranks()
+        if ranks != world or myrank != rank:
+            raise SystemExit(f"bench.py: RCCL communicator has {ranks} ranks (rank {myrank}), "
+                             f"expected {world} (rank {rank})")
     else:
         d = DD(a.dd_parts, device=local)
+        ranks = 1
     d.set_system(A, host.PART_BLOCKS)
     t_setup = time.perf_counter() - t_setup
     info = d.info()
@@ -237,6 +271,7 @@ def bench_dd(a, torch, dist, world, rank, local):
                    "n": n, "nnz": int(A.nnz), "parts": parts,
                    "exchange": "RCCL all-gather over xGMI" if world > 1 else
                                f"in-process ({parts} shards on one GPU)",
+                   "rccl_ranks": ranks if world > 1 else None,
                    "separator_rows": info["nsep"], "max_interface": info["max_iface"],
                    "wavefront_interior": info["wave_interior"],
                    "wavefront_separator": info["wave_separator"],
@@ -252,11 +287,64 @@ def bench_dd(a, torch, dist, world, rank, local):
         dist.destroy_process_group()
 
 
+def spawn_ranks(n, argv, visible=None):
+    """--gpus N without torchrun: start n rank processes (one per GPU, running
+    `argv` with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) and return their
+    status.  The parent makes no GPU call (torch.cuda.device_count does not
+    initialise the device on this image); a rank that fails takes the others
+    down (they would wait in a collective)."""
+    import signal
+    import socket
+    import subprocess
+    if visible is None:
+        import torch
+        visible = torch.cuda.device_count()
+    if visible < n:
+        print(f"bench.py: --gpus {n} but only {visible} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:                      # the exact children this process started
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    world = int(env_world or "1")
+    if world != max(a.gpus, 1):
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the workload: the C2 solve on one GPU, the sharded C2 solve on N > 1
+    if a.workload is None:
+        a.workload = "c2" if world == 1 else "dd"
+        a.dd_grid = a.dd_grid or "c2"
+    a.dd_grid = a.dd_grid or "c4"
+    replicas = a.workload == "replicas"
+    if replicas:
+        a.workload = "c2"
     import torch
     torch.cuda.set_device(local)
     dist = None
@@ -348,17 +436,23 @@ def main():
     def families(res, el):
         """per-family event timing of the solves in `res` (elapsed el seconds)"""
         fam = {}
-        mgs_tot, mgs_it = mgs_bytes(n, a.restart, [r["inner"] for r in res]) if not c5 else (0.0, 0)
+        mgs_f, mgs_r, mgs_it = mgs_bytes(n, a.restart, [r["inner"] for r in res]) if not c5 else (0.0, 0.0, 0)
         for name, kind, per in FAMS:
             cnt, ms = s.profile_get(kind)
             if cnt == 0:
                 continue
             avg_us = ms * 1e3 / cnt
-            byt = per() if per is not None else (mgs_tot / max(mgs_it, 1) if mgs_it else float("nan"))
+            byt = per() if per is not None else (mgs_f / mgs_it if mgs_it else float("nan"))
             fam[name] = {"launches": cnt, "avg_us": round(avg_us, 3),
                          "alg_bytes_per_launch": byt,
                          "achieved_gbs": round(byt / (avg_us * 1e-6) / 1e9, 1),
                          "share_of_step": round(ms / (el * 1e3), 4)}
+            if per is None and mgs_it:
+                # SURVEY.md 8(d)'s unfused count over the same time: what the reference's
+                # separate dot / AXPY / nrm2 launches would have had to move (not a roofline)
+                ref = mgs_r / mgs_it
+                fam[name]["reference_equiv_bytes_per_launch"] = ref
+                fam[name]["reference_equiv_gbs"] = round(ref / (avg_us * 1e-6) / 1e9, 1)
         return fam
 
     def profiled_pass():
@@ -450,13 +544,22 @@ def main():
     if rank == 0 and world == 1 and a.cpu_iters > 0 and not c5 and not c4 and not c3s:
         import oracle as O
         L, U = O.ilu0(A)
-        t1 = time.perf_counter()
-        o = O.gmres_left(A, L, U, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
-        ct = time.perf_counter() - t1
+        # one core, pinned in-process (taskset -c 0 equivalent, no re-exec)
+        aff = os.sched_getaffinity(0)
+        core = min(aff)
+        os.sched_setaffinity(0, {core})
+        try:
+            t1 = time.perf_counter()
+            o = O.gmres_left(A, L, U, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
+            ct = time.perf_counter() - t1
+        finally:
+            os.sched_setaffinity(0, aff)
         cpu = {"value": round(o["inner"] / ct, 3), "unit": "iterations/s", "cores": 1,
-               "kind": "port",
+               "kind": "port", "pinned_core": core, "nproc": os.cpu_count(),
+               "affinity_cores": len(aff), "cpu_model": cpu_model(),
                "sample": f"oracle/ fp64 serial C restatement of GMRES_leftILU0 on the same C2 "
-                         f"system, first {o['inner']} inner iterations ({ct:.1f} s)"}
+                         f"system, first {o['inner']} inner iterations ({ct:.1f} s), one thread "
+                         f"pinned to core {core}"}
 
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,

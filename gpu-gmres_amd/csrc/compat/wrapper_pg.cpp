@@ -1,0 +1,177 @@
+// wrapper_pg.cpp -- wrapperGMRESforPG (include/compat/gpuData.h), the reference's
+// legacy GPU transient entry point (src/wrapperGMRESforPG.cu:19-715), on top of
+// the C ABI: two solvers (G for the DC point, left = G + C/h for the steps),
+// the device step loop gg_transient_mna, ports written back per time point.
+//
+// Deviation, documented in the header: the reference's loop only forms the
+// right-hand sides (its csrsv solves are commented out, :422-459) and its
+// double branch exits; here every time point is solved, and x_host is filled
+// when use_cuda_double is set.
+#include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "ggmres.h"
+#include "gpuData.h"
+
+// ---- the layout is the ABI (x86-64, LP64) --------------------------------------
+static_assert(offsetof(gpuETBR, nport) == 16 && offsetof(gpuETBR, use_cuda_double) == 24 &&
+                  offsetof(gpuETBR, tstep) == 32 && offsetof(gpuETBR, ut_host) == 48 &&
+                  offsetof(gpuETBR, x_host) == 120 && offsetof(gpuETBR, x_single_host) == 184 &&
+                  offsetof(gpuETBR, ldUt) == 192 && offsetof(gpuETBR, ut_dev) == 200 &&
+                  offsetof(gpuETBR, x_single_dev) == 344 && offsetof(gpuETBR, nIS) == 352 &&
+                  offsetof(gpuETBR, dcVt_host) == 360 && offsetof(gpuETBR, PWLvolExist) == 392 &&
+                  offsetof(gpuETBR, PULSEcurExist) == 404 && offsetof(gpuETBR, PWLnumPts_host) == 408 &&
+                  offsetof(gpuETBR, PWLtime_host) == 424 && offsetof(gpuETBR, PWLval_host) == 440 &&
+                  offsetof(gpuETBR, PULSEtime_host) == 488 && offsetof(gpuETBR, PULSEval_host) == 504 &&
+                  offsetof(gpuETBR, PULSEval_single_dev) == 544 && sizeof(gpuETBR) == 552,
+              "gpuETBR layout differs from src/gpuData.h:43-116");
+static_assert(sizeof(ucr_cs_dl) == 56, "ucr_cs_dl layout differs from src/gpuData.h:146-164");
+
+namespace {
+
+constexpr int kRestart = 32;          // const int restart (src/defs.h:11)
+constexpr int kMaxIter = 10000;       // src/gmres_interface_pg.cu:66
+constexpr double kTol = 1e-7;         // gmres_tol_global (src/gmres_interface_pg.cu:7)
+
+struct HostCsr {
+    int rows = 0;
+    std::vector<int> rp, ci;
+    std::vector<double> v;
+};
+
+// CSC (cs_dl, column pointers p, row indices i) -> CSR by a stable counting
+// sort: within a row the entries keep column order, which is the order in
+// which cs_dl_gaxpy accumulates them
+HostCsr csc_to_csr(const ucr_cs_dl *M)
+{
+    HostCsr C;
+    const long m = M->m, n = M->n, nnz = n > 0 ? M->p[n] : 0;
+    C.rows = (int)m;
+    C.rp.assign(m + 1, 0);
+    C.ci.resize(nnz);
+    C.v.resize(nnz);
+    for (long k = 0; k < nnz; k++) C.rp[M->i[k] + 1]++;
+    for (long r = 0; r < m; r++) C.rp[r + 1] += C.rp[r];
+    std::vector<int> fill(C.rp.begin(), C.rp.end() - 1);
+    for (long j = 0; j < n; j++)
+        for (long k = M->p[j]; k < M->p[j + 1]; k++) {
+            const int dst = fill[M->i[k]]++;
+            C.ci[dst] = (int)j;
+            C.v[dst] = M->x[k];
+        }
+    return C;
+}
+
+bool check(int rc, const char *what)
+{
+    if (rc < 0) {
+        std::fprintf(stderr, "wrapperGMRESforPG: %s: %s (%s)\n", what, gg_strerror(rc), gg_last_error());
+        return false;
+    }
+    return true;
+}
+
+gg_solver *make_solver(const HostCsr &A)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    gg_solver *s = nullptr;
+    if (!check(gg_create(dev, &s), "gg_create")) return nullptr;
+    const int *ci = A.ci.empty() ? nullptr : A.ci.data();
+    const double *v = A.v.empty() ? nullptr : A.v.data();
+    if (!check(gg_set_matrix(s, A.rows, A.rp.data(), ci, v), "gg_set_matrix") ||
+        !check(gg_set_precond_ilu0(s), "gg_set_precond_ilu0")) {
+        gg_destroy(s);
+        return nullptr;
+    }
+    return s;
+}
+
+}  // namespace
+
+void wrapperGMRESforPG(ucr_cs_dl *left, ucr_cs_dl *right, ucr_cs_dl *G, ucr_cs_dl *B, int *invPort, int nport,
+                       gpuETBR *e)
+{
+    if (!left || !right || !G || !B || !e || (nport > 0 && !invPort)) {
+        std::fprintf(stderr, "wrapperGMRESforPG: null argument\n");
+        return;
+    }
+    const int n = (int)G->m, numPts = e->numPts, nVS = e->nVS, nIS = e->nIS, m = nVS + nIS;
+    if (numPts < 1 || left->m != n || right->m != n || B->m != n || B->n != m) {
+        std::fprintf(stderr, "wrapperGMRESforPG: inconsistent sizes (n %d, numPts %d, B %ld x %ld, m %d)\n",
+                     n, numPts, B->m, B->n, m);
+        return;
+    }
+    // sources in u order: the nVS voltage sources, then the nIS current sources
+    std::vector<int> kind(m), ptr(m + 1, 0);
+    std::vector<double> data;
+    for (int k = 0; k < nVS; k++) {
+        kind[k] = GG_SRC_DC;                                   // gen_dcVt_kernel
+        data.push_back(e->dcVt_host ? e->dcVt_host[k] : 0.0);
+        ptr[k + 1] = (int)data.size();
+    }
+    for (int k = 0; k < nIS; k++) {
+        if (e->PWLcurExist && e->PWLnumPts_host) {             // gen_PWLut_kernel
+            kind[nVS + k] = GG_SRC_PWL;
+            const int np = e->PWLnumPts_host[k];
+            for (int p = 0; p < np; p++) {
+                data.push_back(e->PWLtime_host[(size_t)k * MAX_PWL_PTS + p]);
+                data.push_back(e->PWLval_host[(size_t)k * MAX_PWL_PTS + p]);
+            }
+        } else if (e->PULSEcurExist && e->PULSEtime_host) {    // gen_PULSEut_kernel
+            kind[nVS + k] = GG_SRC_PULSE;
+            const double *t = e->PULSEtime_host + (size_t)k * 5, *v = e->PULSEval_host + (size_t)k * 2;
+            for (double q : {v[0], v[1], t[0], t[1], t[2], t[3], t[4]}) data.push_back(q);
+        } else {                                                // no waveform given: 0
+            kind[nVS + k] = GG_SRC_DC;
+            data.push_back(0.0);
+        }
+        ptr[nVS + k + 1] = (int)data.size();
+    }
+    if (data.empty()) data.push_back(0.0);
+    const HostCsr Gc = csc_to_csr(G), Ac = csc_to_csr(left), Rc = csc_to_csr(right);
+    const HostCsr Bc = csc_to_csr(B);
+    std::vector<int> one(1, 0);
+    auto ci_of = [&](const HostCsr &C) { return C.ci.empty() ? one.data() : C.ci.data(); };
+    std::vector<double> zero(1, 0.0);
+    auto v_of = [&](const HostCsr &C) { return C.v.empty() ? zero.data() : C.v.data(); };
+
+    std::vector<int> port(invPort, invPort + nport);
+    if (port.empty()) port.push_back(0);
+    std::vector<double> x(n, 0.0), pv0((size_t)std::max(nport, 1) * 2);
+    gg_options opt{kRestart, kMaxIter, kTol, 0};
+    int its = 0;
+    // DC point (i == 0): G x0 = B u(0)
+    gg_solver *sg = make_solver(Gc);
+    if (!sg) return;
+    int rc = gg_transient_mna(sg, 0, 1, e->tstep, nullptr, nullptr, nullptr, m, Bc.rp.data(), ci_of(Bc),
+                              v_of(Bc), kind.data(), ptr.data(), data.data(), nport, port.data(), x.data(), &opt,
+                              pv0.data(), &its);
+    gg_destroy(sg);
+    if (!check(rc, "DC solve")) return;
+    if (rc != GG_OK) std::printf("Failed to converge.\n");
+    // backward-Euler steps i = 1 .. numPts-1 on left = G + C/h
+    std::vector<double> pt((size_t)std::max(nport, 1) * numPts, 0.0);
+    if (numPts > 1) {
+        gg_solver *sa = make_solver(Ac);
+        if (!sa) return;
+        rc = gg_transient_mna(sa, 1, numPts - 1, e->tstep, Rc.rp.data(), ci_of(Rc), v_of(Rc), m, Bc.rp.data(),
+                              ci_of(Bc), v_of(Bc), kind.data(), ptr.data(), data.data(), nport, port.data(),
+                              x.data(), &opt, pt.data(), &its);
+        gg_destroy(sa);
+        if (!check(rc, "transient steps")) return;
+        if (rc != GG_OK) std::printf("Failed to converge.\n");
+    }
+    // port_out layouts: [j * (steps + 1) + column]; column 0 of the DC call is
+    // the zero start, column 1 the DC point == column 0 of the step call
+    for (int j = 0; j < nport; j++)
+        for (int i = 0; i < numPts; i++) {
+            const double v = (i == 0) ? pv0[(size_t)j * 2 + 1] : pt[(size_t)j * numPts + i];
+            if (e->use_cuda_single && e->x_single_host) e->x_single_host[(size_t)i * nport + j] = (float)v;
+            if (e->use_cuda_double && e->x_host) e->x_host[(size_t)i * nport + j] = v;
+        }
+}

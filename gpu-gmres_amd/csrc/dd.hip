@@ -686,6 +686,18 @@ int gg_dd_destroy(gg_dd *d)
     return GG_OK;
 }
 
+int gg_dd_comm_ranks(gg_dd *d, int *ranks, int *rank)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && ranks, GG_EINVAL, "null argument");
+    int c = 1;
+    if (d->kind == GG_DD_RCCL) GG_NCCL(ncclCommCount(d->comm, &c));
+    *ranks = c;
+    if (rank) *rank = d->rank;
+    return GG_OK;
+    GG_API_END
+}
+
 int gg_dd_set_system(gg_dd *d, int n, const int *rp, const int *ci, const double *val, int method)
 {
     GG_API_BEGIN

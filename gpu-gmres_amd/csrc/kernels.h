@@ -42,6 +42,11 @@ void launch_fill_u64(unsigned long long *p, long long n, unsigned long long v, h
 void launch_transient_step(int n, int nsrc, const int *kind, const int *dptr, const double *data, int it,
                            double h, double *u, const int *src_ptr, const int *src_idx, const double *cdiag,
                            const double *x, double *w, hipStream_t st);
+// the same with general B (n x nsrc) and R = C/h (n x n) in CSR: w = B u + R x
+void launch_transient_step_csr(int n, int nsrc, const int *kind, const int *dptr, const double *data, int it,
+                               double h, double *u, const int *bp, const int *bi, const double *bv,
+                               const int *rp, const int *ri, const double *rv, const double *x, double *w,
+                               hipStream_t st);
 void launch_gather_ports(int nport, const int *port, const double *x, double *out, hipStream_t st);
 // tap statistics: mode 0 seed (max = min = sum = x[tap]), 1 update, 2 finish (sum /= npts)
 void launch_taps(int ntap, const int *tap, const double *x, double *mx, double *mn, double *sm, int mode,

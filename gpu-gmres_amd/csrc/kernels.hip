@@ -1285,6 +1285,24 @@ __global__ void k_transient_rhs(int n, const int *src_ptr, const int *src_idx, c
     w[r] = bu + xnr;
 }
 
+// w = B u + R x_prev for a general MNA system (gg_transient_mna, the
+// wrapperGMRESforPG path): B (n x nsrc) and R = C/h (n x n, capacitor stamps
+// between nodes included) in CSR.  cs_dl_gaxpy (y += A x, column by column)
+// accumulates each row in ascending column order from 0.0, which is the CSR
+// row order here: bu = B u, xnr = R x, w = bu + xnr (the driver's w += xnr).
+__global__ void k_transient_rhs_csr(int n, const int *bp, const int *bi, const double *bv, const double *u,
+                                    const int *rp, const int *ri, const double *rv, const double *x,
+                                    double *w)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    double bu = 0.0;
+    for (int q = bp[r]; q < bp[r + 1]; q++) bu = bu + bv[q] * u[bi[q]];
+    double xnr = 0.0;
+    for (int q = rp[r]; q < rp[r + 1]; q++) xnr = xnr + rv[q] * x[ri[q]];
+    w[r] = bu + xnr;
+}
+
 // tap-node voltage statistics of the transient run (the ir_info block of the
 // step driver, src/mna_solve_gpu_gmres.cpp:285-292, 633-645, 780-797): max,
 // min and the running sum, seeded with the initial state; avg = sum / time
@@ -1734,6 +1752,15 @@ void launch_transient_step(int n, int nsrc, const int *kind, const int *dptr, co
     if (nsrc > 0) k_sources<<<(nsrc + kBlock - 1) / kBlock, kBlock, 0, st>>>(nsrc, kind, dptr, data, it, h, u);
     if (n > 0)
         k_transient_rhs<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, src_ptr, src_idx, u, cdiag, x, w);
+}
+void launch_transient_step_csr(int n, int nsrc, const int *kind, const int *dptr, const double *data, int it,
+                               double h, double *u, const int *bp, const int *bi, const double *bv,
+                               const int *rp, const int *ri, const double *rv, const double *x, double *w,
+                               hipStream_t st)
+{
+    if (nsrc > 0) k_sources<<<(nsrc + kBlock - 1) / kBlock, kBlock, 0, st>>>(nsrc, kind, dptr, data, it, h, u);
+    if (n > 0)
+        k_transient_rhs_csr<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, bp, bi, bv, u, rp, ri, rv, x, w);
 }
 
 void launch_taps(int ntap, const int *tap, const double *x, double *mx, double *mn, double *sm, int mode,

@@ -1154,37 +1154,48 @@ int gg_solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_optio
     GG_API_END
 }
 
-// the step loop behind gg_transient / gg_transient_src (host source tables)
-static int transient_loop(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc, const int *src_node,
-              const std::vector<int> &kind, const std::vector<int> &dptr, const std::vector<double> &data,
-              int nport, const int *port, double *x, const gg_options *opt, double *port_out,
-              int *iters_total)
+// the step loop behind gg_transient / gg_transient_src / gg_transient_mna (host
+// source tables).  Step j = 1..nsteps evaluates the sources at time index
+// it0 + j - 1.  The right-hand side is B u + (C/h) x with B an incidence matrix
+// (src_node) and C/h diagonal (cdiag), or -- when Rm and Bm are given -- the
+// general B u + R x of gg_transient_mna.
+static int transient_loop(gg_solver *s, int it0, int nsteps, double h, const double *cdiag, int nsrc,
+              const int *src_node, const std::vector<int> &kind, const std::vector<int> &dptr,
+              const std::vector<double> &data, int nport, const int *port, double *x, const gg_options *opt,
+              double *port_out, int *iters_total, const Csr *Rm = nullptr, const Csr *Bm = nullptr)
 {
     GG_REQUIRE(nport == 0 || (port && port_out), GG_EINVAL, "null port arrays");
     GG_REQUIRE(s->have_A, GG_ESTATE, "gg_transient: no matrix");
     set_device(s);
     const int n = s->A.n;
-    // B^T by row: the sources of each row in ascending k (cs_dl_gaxpy column order)
-    std::vector<int> sptr(n + 1, 0), sidx(nsrc);
-    for (int k = 0; k < nsrc; k++) {
-        GG_REQUIRE(src_node[k] >= 0 && src_node[k] < n, GG_EINVAL, "source node out of range");
-        sptr[src_node[k] + 1]++;
-    }
-    for (int r = 0; r < n; r++) sptr[r + 1] += sptr[r];
-    {
+    const bool general = Rm && Bm;
+    std::vector<int> sptr(n + 1, 0), sidx(general ? 0 : nsrc);
+    if (!general) {
+        // B^T by row: the sources of each row in ascending k (cs_dl_gaxpy column order)
+        for (int k = 0; k < nsrc; k++) {
+            GG_REQUIRE(src_node[k] >= 0 && src_node[k] < n, GG_EINVAL, "source node out of range");
+            sptr[src_node[k] + 1]++;
+        }
+        for (int r = 0; r < n; r++) sptr[r + 1] += sptr[r];
         std::vector<int> fill(sptr.begin(), sptr.end() - 1);
         for (int k = 0; k < nsrc; k++) sidx[fill[src_node[k]]++] = k;
     }
     for (int j = 0; j < nport; j++) GG_REQUIRE(port[j] >= 0 && port[j] < n, GG_EINVAL, "port out of range");
     DBuf<int> d_sptr, d_sidx, d_port, d_kind, d_dptr;
     DBuf<double> d_data, d_u, d_c, d_w, d_pv;
-    d_sptr.upload(sptr, s->st);
-    d_sidx.upload(sidx.data(), sidx.size(), s->st);
+    DevCsr d_R, d_B;
+    if (general) {
+        d_R.upload(*Rm, s->st);
+        d_B.upload(*Bm, s->st);
+    } else {
+        d_sptr.upload(sptr, s->st);
+        d_sidx.upload(sidx.data(), sidx.size(), s->st);
+        d_c.upload(cdiag, n, s->st);
+    }
     d_kind.upload(kind.data(), kind.size(), s->st);
     d_dptr.upload(dptr.data(), dptr.size(), s->st);
     d_data.upload(data.data(), std::max<size_t>(data.size(), 1), s->st);
     d_u.alloc(std::max(nsrc, 1));
-    d_c.upload(cdiag, n, s->st);
     d_w.alloc(std::max(n, 1));
     d_port.upload(port, nport, s->st);
     d_pv.alloc((size_t)std::max(nport, 1) * (nsteps + 1));
@@ -1205,8 +1216,13 @@ static int transient_loop(gg_solver *s, int nsteps, double h, const double *cdia
     }
     int total = 0, status = GG_OK;
     for (int it = 1; it <= nsteps; it++) {
-        launch_transient_step(n, nsrc, d_kind.p, d_dptr.p, d_data.p, it, h, d_u.p, d_sptr.p, d_sidx.p,
-                              d_c.p, d_x, d_w.p, s->st);
+        const int tidx = it0 + it - 1;              // time index of the sources
+        if (general)
+            launch_transient_step_csr(n, nsrc, d_kind.p, d_dptr.p, d_data.p, tidx, h, d_u.p, d_B.rp.p,
+                                      d_B.ci.p, d_B.v.p, d_R.rp.p, d_R.ci.p, d_R.v.p, d_x, d_w.p, s->st);
+        else
+            launch_transient_step(n, nsrc, d_kind.p, d_dptr.p, d_data.p, tidx, h, d_u.p, d_sptr.p, d_sidx.p,
+                                  d_c.p, d_x, d_w.p, s->st);
         gg_result r{};
         const int rc = solve_device(s, d_w.p, d_x, opt, &r);
         if (rc != GG_OK) status = rc;
@@ -1247,7 +1263,7 @@ int gg_transient(gg_solver *s, int nsteps, double h, const double *cdiag, int ns
     std::vector<int> kind(std::max(nsrc, 1), GG_SRC_PULSE), dptr(nsrc + 1);
     for (int k = 0; k <= nsrc; k++) dptr[k] = 7 * k;
     std::vector<double> data(pulse, pulse + (size_t)7 * nsrc);
-    return transient_loop(s, nsteps, h, cdiag, nsrc, src_node, kind, dptr, data, nport, port, x, opt,
+    return transient_loop(s, 1, nsteps, h, cdiag, nsrc, src_node, kind, dptr, data, nport, port, x, opt,
                           port_out, iters_total);
     GG_API_END
 }
@@ -1280,6 +1296,27 @@ int gg_transient_get_taps(gg_solver *s, double *max_v, double *min_v, double *av
     GG_API_END
 }
 
+// validated device tables of a gg_src_kind source list
+static void source_tables(int nsrc, const int *src_kind, const int *src_ptr, const double *src_data,
+                          std::vector<int> &kind, std::vector<int> &dptr, std::vector<double> &data)
+{
+    GG_REQUIRE(nsrc == 0 || (src_kind && src_ptr && src_data), GG_EINVAL, "null source arrays");
+    kind.assign(std::max(nsrc, 1), GG_SRC_DC);
+    dptr.assign(nsrc + 1, 0);
+    for (int k = 0; k < nsrc; k++) {
+        const int len = src_ptr[k + 1] - src_ptr[k];
+        GG_REQUIRE(src_ptr[k] >= 0 && len >= 0, GG_EINVAL, "transient: bad src_ptr");
+        const int need = src_kind[k] == GG_SRC_DC ? 1 : src_kind[k] == GG_SRC_PULSE ? 7 : -1;
+        GG_REQUIRE(src_kind[k] == GG_SRC_DC || src_kind[k] == GG_SRC_PULSE || src_kind[k] == GG_SRC_PWL,
+                   GG_EINVAL, "transient: unknown source kind");
+        GG_REQUIRE(need < 0 ? (len >= 2 && len % 2 == 0) : len == need, GG_EINVAL,
+                   "transient: DC takes 1 value, PULSE 7, PWL (time, value) pairs");
+        kind[k] = src_kind[k];
+        dptr[k + 1] = src_ptr[k + 1] - src_ptr[0];
+    }
+    data.assign(src_data + (nsrc ? src_ptr[0] : 0), src_data + (nsrc ? src_ptr[nsrc] : 0));
+}
+
 int gg_transient_src(gg_solver *s, int nsteps, double h, const double *cdiag, int nsrc,
                      const int *src_node, const int *src_kind, const int *src_ptr, const double *src_data,
                      int nport, const int *port, double *x, const gg_options *opt, double *port_out,
@@ -1288,22 +1325,49 @@ int gg_transient_src(gg_solver *s, int nsteps, double h, const double *cdiag, in
     GG_API_BEGIN
     GG_REQUIRE(s && opt && x && cdiag && iters_total, GG_EINVAL, "null argument");
     GG_REQUIRE(nsteps >= 0 && nsrc >= 0 && nport >= 0, GG_EINVAL, "negative count");
-    GG_REQUIRE(nsrc == 0 || (src_node && src_kind && src_ptr && src_data), GG_EINVAL, "null source arrays");
-    std::vector<int> kind(std::max(nsrc, 1), GG_SRC_DC), dptr(nsrc + 1, 0);
-    for (int k = 0; k < nsrc; k++) {
-        const int len = src_ptr[k + 1] - src_ptr[k];
-        GG_REQUIRE(src_ptr[k] >= 0 && len >= 0, GG_EINVAL, "gg_transient_src: bad src_ptr");
-        const int need = src_kind[k] == GG_SRC_DC ? 1 : src_kind[k] == GG_SRC_PULSE ? 7 : -1;
-        GG_REQUIRE(src_kind[k] == GG_SRC_DC || src_kind[k] == GG_SRC_PULSE || src_kind[k] == GG_SRC_PWL,
-                   GG_EINVAL, "gg_transient_src: unknown source kind");
-        GG_REQUIRE(need < 0 ? (len >= 2 && len % 2 == 0) : len == need, GG_EINVAL,
-                   "gg_transient_src: DC takes 1 value, PULSE 7, PWL (time, value) pairs");
-        kind[k] = src_kind[k];
-        dptr[k + 1] = src_ptr[k + 1] - src_ptr[0];
-    }
-    std::vector<double> data(src_data + (nsrc ? src_ptr[0] : 0), src_data + (nsrc ? src_ptr[nsrc] : 0));
-    return transient_loop(s, nsteps, h, cdiag, nsrc, src_node, kind, dptr, data, nport, port, x, opt,
+    GG_REQUIRE(nsrc == 0 || src_node, GG_EINVAL, "null source arrays");
+    std::vector<int> kind, dptr;
+    std::vector<double> data;
+    source_tables(nsrc, src_kind, src_ptr, src_data, kind, dptr, data);
+    return transient_loop(s, 1, nsteps, h, cdiag, nsrc, src_node, kind, dptr, data, nport, port, x, opt,
                           port_out, iters_total);
+    GG_API_END
+}
+
+int gg_transient_mna(gg_solver *s, int it0, int nsteps, double h, const int *r_row_ptr, const int *r_col_idx,
+                     const double *r_val, int nsrc, const int *b_row_ptr, const int *b_col_idx,
+                     const double *b_val, const int *src_kind, const int *src_ptr, const double *src_data,
+                     int nport, const int *port, double *x, const gg_options *opt, double *port_out,
+                     int *iters_total)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && opt && x && iters_total, GG_EINVAL, "null argument");
+    GG_REQUIRE(s->have_A, GG_ESTATE, "gg_transient_mna: no matrix");
+    GG_REQUIRE(it0 >= 0 && nsteps >= 0 && nsrc >= 0 && nport >= 0, GG_EINVAL, "negative count");
+    const int n = s->A.n;
+    Csr R, Bm;
+    R.n = Bm.n = n;
+    if (r_row_ptr) {
+        check_csr(n, r_row_ptr, r_col_idx, r_val, "gg_transient_mna R");
+        R = make_csr(n, r_row_ptr, r_col_idx, r_val);
+    } else {
+        R.rp.assign(n + 1, 0);                // R = 0 (a DC operating point)
+    }
+    GG_REQUIRE(b_row_ptr && b_row_ptr[0] == 0, GG_EINVAL, "gg_transient_mna: bad B row_ptr");
+    for (int r = 0; r < n; r++) {
+        GG_REQUIRE(b_row_ptr[r + 1] >= b_row_ptr[r], GG_EINVAL, "gg_transient_mna: B row_ptr not monotone");
+        for (int k = b_row_ptr[r]; k < b_row_ptr[r + 1]; k++)
+            GG_REQUIRE(b_col_idx && b_val && b_col_idx[k] >= 0 && b_col_idx[k] < nsrc, GG_EINVAL,
+                       "gg_transient_mna: B column (source) index out of range");
+    }
+    Bm.rp.assign(b_row_ptr, b_row_ptr + n + 1);
+    Bm.ci.assign(b_col_idx, b_col_idx + b_row_ptr[n]);
+    Bm.v.assign(b_val, b_val + b_row_ptr[n]);
+    std::vector<int> kind, dptr;
+    std::vector<double> data;
+    source_tables(nsrc, src_kind, src_ptr, src_data, kind, dptr, data);
+    return transient_loop(s, it0, nsteps, h, nullptr, nsrc, nullptr, kind, dptr, data, nport, port, x, opt,
+                          port_out, iters_total, &R, &Bm);
     GG_API_END
 }
 

@@ -30,6 +30,7 @@ EXPORTS = [
     "gg_trace_precond", "gg_bytes_trsv", "gg_transient", "gg_set_precond_ilu0_device",
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
     "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced",
+    "gg_transient_mna",
 ]
 SRC_DC, SRC_PULSE, SRC_PWL = 0, 1, 2          # gg_src_kind
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
@@ -93,6 +94,9 @@ def lib():
         L.gg_transient.argtypes = [_VP, ctypes.c_int, ctypes.c_double, _D, ctypes.c_int, _I, _D,
                                    ctypes.c_int, _I, _D, ctypes.POINTER(Options), _D,
                                    ctypes.POINTER(ctypes.c_int)]
+        L.gg_transient_mna.argtypes = [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_double, _VP, _VP, _VP,
+                                       ctypes.c_int, _I, _I, _D, _I, _I, _D, ctypes.c_int, _I, _D,
+                                       ctypes.POINTER(Options), _D, ctypes.POINTER(ctypes.c_int)]
         L.gg_spmv.argtypes = [_VP, _D, _D]
         L.gg_precond_apply.argtypes = [_VP, ctypes.c_int, _D, _D]
         L.gg_time_spmv.argtypes = [_VP, ctypes.c_int, ctypes.c_int,
@@ -288,6 +292,46 @@ class Solver:
                                            kind if len(kind) else one, ptr, data, len(ports),
                                            ports if len(ports) else one, x, ctypes.byref(o), pv,
                                            ctypes.byref(tot)), allow_nc=True)
+        return dict(x=x, ports=pv[: len(ports) * (nsteps + 1)].reshape(len(ports), nsteps + 1),
+                    iters_total=tot.value, ret=rc)
+
+    def transient_mna(self, it0, nsteps, h, R, B, sources, ports, x0, restart=32, max_iter=10000,
+                      tol=1e-7, flags=0):
+        """gg_transient_mna: w = B u(it h) + R x per step, it = it0 .. it0+nsteps-1;
+        R (n x n) and B (n x nsrc) scipy sparse (R None = 0); sources as
+        transient_src.  Returns dict(x, ports [nport, nsteps+1], iters_total, ret)."""
+        import scipy.sparse as sp
+        x = np.array(x0, np.float64, copy=True)
+        n = len(x)
+        Bc = sp.csr_matrix(B)
+        Bc.sort_indices()
+        keep = []
+        if R is not None:
+            Rc = sp.csr_matrix(R)
+            Rc.sort_indices()
+            rp = np.ascontiguousarray(Rc.indptr, np.int32)
+            ri = np.ascontiguousarray(Rc.indices, np.int32) if Rc.nnz else np.zeros(1, np.int32)
+            rv = np.ascontiguousarray(Rc.data, np.float64) if Rc.nnz else np.zeros(1)
+            keep = [rp, ri, rv]
+            rargs = [rp.ctypes.data, ri.ctypes.data, rv.ctypes.data]
+        else:
+            rargs = [None, None, None]
+        bp = np.ascontiguousarray(Bc.indptr, np.int32)
+        bi = np.ascontiguousarray(Bc.indices, np.int32) if Bc.nnz else np.zeros(1, np.int32)
+        bv = np.ascontiguousarray(Bc.data, np.float64) if Bc.nnz else np.zeros(1)
+        kind = np.array([k for k, _ in sources] or [0], np.int32)
+        ptr = np.zeros(len(sources) + 1, np.int32)
+        ptr[1:] = np.cumsum([len(q) for _, q in sources])
+        data = np.concatenate([np.asarray(q, np.float64) for _, q in sources]) if sources else np.zeros(1)
+        ports = np.ascontiguousarray(ports, np.int32)
+        pv = np.zeros(max(len(ports), 1) * (nsteps + 1))
+        tot = ctypes.c_int()
+        o = Options(int(restart), int(max_iter), float(tol), int(flags))
+        rc = _check(lib().gg_transient_mna(self.h, int(it0), int(nsteps), float(h), *rargs, len(sources),
+                                           bp, bi, bv, kind, ptr, data, len(ports),
+                                           ports if len(ports) else np.zeros(1, np.int32), x,
+                                           ctypes.byref(o), pv, ctypes.byref(tot)), allow_nc=True)
+        del keep
         return dict(x=x, ports=pv[: len(ports) * (nsteps + 1)].reshape(len(ports), nsteps + 1),
                     iters_total=tot.value, ret=rc)
 

@@ -17,7 +17,8 @@ _I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
 _D = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
 _done = False
 
-EXPORTS = ["gg_dd_unique_id", "gg_dd_create", "gg_dd_destroy", "gg_dd_set_system", "gg_dd_info",
+EXPORTS = ["gg_dd_unique_id", "gg_dd_create", "gg_dd_destroy", "gg_dd_comm_ranks",
+           "gg_dd_set_system", "gg_dd_info",
            "gg_dd_perm", "gg_dd_dot_layout", "gg_dd_solve", "gg_dd_solve_device",
            "gg_dd_get_history", "gg_dd_spmv", "gg_dd_precond_apply"]
 
@@ -30,6 +31,7 @@ def _lib():
         L.gg_dd_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_char_p, ctypes.POINTER(_VP)]
         L.gg_dd_destroy.argtypes = [_VP]
+        L.gg_dd_comm_ranks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.gg_dd_set_system.argtypes = [_VP, ctypes.c_int, _I, _I, _D, ctypes.c_int]
         L.gg_dd_info.argtypes = [_VP, _I]
         L.gg_dd_perm.argtypes = [_VP, _I, _I]
@@ -70,6 +72,12 @@ class DD:
             self.close()
         except Exception:
             pass
+
+    def comm_ranks(self):
+        """(ranks in the exchange, this process's rank): RCCL ncclCommCount, LOCAL (1, 0)"""
+        c, r = ctypes.c_int(), ctypes.c_int()
+        _check(_lib().gg_dd_comm_ranks(self.h, ctypes.byref(c), ctypes.byref(r)))
+        return c.value, r.value
 
     def set_system(self, A, method=1):
         n, rp, ci, v = _csr_arrays(A)

@@ -226,6 +226,23 @@ int gg_transient_src(gg_solver *s, int nsteps, double h, const double *cdiag, in
                      const int *src_node, const int *src_kind, const int *src_ptr, const double *src_data,
                      int nport, const int *port, double *x, const gg_options *opt, double *port_out,
                      int *iters_total);
+/* The step loop for a general MNA system (the wrapperGMRESforPG path,
+ * src/wrapperGMRESforPG.cu:411-459, and the step driver's cs_dl_gaxpy forms,
+ * src/mna_solve_gpu_gmres.cpp:585-591): the matrix set by gg_set_matrix is A
+ * (G + C/h for the transient, G for a DC point); B is n x nsrc and R (= C/h,
+ * capacitor stamps between nodes included) n x n, both CSR.  For step
+ * j = 1..nsteps, with time index it = it0 + j - 1:
+ *   u = sources(it * h)  (src_kind / src_ptr / src_data as gg_transient_src)
+ *   w = B u + R x        (each row in ascending column order from 0.0; R may
+ *                         be NULL: R = 0, a DC operating point)
+ *   x = GMRES(A, w; warm start x)
+ *   port_out[jp * (nsteps + 1) + j] = x[port[jp]]   (column 0 = the initial x)
+ * Taps (gg_transient_set_taps) are tracked as in gg_transient. */
+int gg_transient_mna(gg_solver *s, int it0, int nsteps, double h, const int *r_row_ptr, const int *r_col_idx,
+                     const double *r_val, int nsrc, const int *b_row_ptr, const int *b_col_idx,
+                     const double *b_val, const int *src_kind, const int *src_ptr, const double *src_data,
+                     int nport, const int *port, double *x, const gg_options *opt, double *port_out,
+                     int *iters_total);
 /* Tap-node statistics of the following gg_transient / gg_transient_src runs
  * (the step driver's ir_info block, src/mna_solve_gpu_gmres.cpp:285-292,
  * 633-645, 780-797): per tap node its maximum and minimum over the nsteps + 1

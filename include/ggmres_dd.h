@@ -53,6 +53,9 @@ typedef struct gg_dd gg_dd;
 int gg_dd_unique_id(unsigned char *id);
 int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char *id, gg_dd **out);
 int gg_dd_destroy(gg_dd *d);
+/* processes in the exchange: GG_DD_RCCL the communicator's rank count
+ * (ncclCommCount), GG_DD_LOCAL 1; *rank = this process's rank */
+int gg_dd_comm_ranks(gg_dd *d, int *ranks, int *rank);
 
 /* the global system (identical on every rank): partition (gg_part_method of
  * ggmres_host.h), arrow permutation, ILU(0) of the permuted matrix, shards */

@@ -341,3 +341,46 @@ def transient(A, L, U, nsteps, h, cdiag, src_node, pulses, ports, x0, m=32, max_
     if taps is not None:
         out["taps"] = (tmax, tmin, tsum / (nsteps + 1), tmax - tmin)
     return out
+
+
+def gaxpy_csc(A, x, y):
+    """cs_dl_gaxpy restated: y += A x, A (scipy) in compressed columns, column by column."""
+    import scipy.sparse as sp
+    A = sp.csc_matrix(A)
+    p = np.ascontiguousarray(A.indptr, np.int64)
+    i = np.ascontiguousarray(A.indices, np.int64)
+    v = np.ascontiguousarray(A.data, np.float64)
+    f = lib().orc_gaxpy_csc
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p]
+    xx = np.ascontiguousarray(x, np.float64)
+    assert y.dtype == np.float64 and y.flags.c_contiguous
+    f(A.shape[1], p.ctypes.data, i.ctypes.data, v.ctypes.data, xx.ctypes.data, y.ctypes.data)
+    return y
+
+
+def transient_mna(A, L, U, it0, nsteps, h, R, B, sources, ports, x0, m=32, max_iter=10000, tol=1e-7):
+    """The step driver with a general MNA right-hand side (src/mna_solve_gpu_gmres.cpp:585-591:
+    w = 0; cs_dl_gaxpy(B, u, w); xnr = 0; cs_dl_gaxpy(right, xn, xnr); w += xnr), sources at
+    time index it0 + j - 1 for step j; R None = 0 (a DC point).  GMRES_leftILU0 per step,
+    warm start.  Returns dict(x, ports [nport, nsteps+1], iters_total, ret)."""
+    x = np.array(x0, np.float64, copy=True)
+    n = len(x)
+    ports = np.asarray(ports, np.int64)
+    pv = np.zeros((len(ports), nsteps + 1))
+    pv[:, 0] = x[ports]
+    total, ret = 0, 0
+    for j in range(1, nsteps + 1):
+        it = it0 + j - 1
+        u = np.array([source_value(k, q, it, h) for k, q in sources])
+        w = gaxpy_csc(B, u, np.zeros(n))
+        xnr = np.zeros(n)
+        if R is not None:
+            gaxpy_csc(R, x, xnr)
+        w += xnr
+        o = gmres_left(A, L, U, w, x0=x, m=m, max_iter=max_iter, tol=tol)
+        x = o["x"]
+        total += o["iters"]
+        ret = ret or o["ret"]
+        pv[:, j] = x[ports]
+    return dict(x=x, ports=pv, iters_total=total, ret=ret)

@@ -758,6 +758,15 @@ void orc_transient_rhs(int n, int nsrc, const int *src_node, const double *u,
     }
 }
 
+/* cs_dl_gaxpy (CXSparse, called by the step driver at
+ * src/mna_solve_gpu_gmres.cpp:585-591): y += A x for A in compressed columns,
+ * column by column -- each y[i] accumulates its terms in column order */
+void orc_gaxpy_csc(int ncol, const long *p, const long *i, const double *ax, const double *x, double *y)
+{
+    for (int j = 0; j < ncol; j++)
+        for (long k = p[j]; k < p[j + 1]; k++) y[i[k]] += ax[k] * x[j];
+}
+
 /* ------------------------------------------------ sharded solve (oracle/dd.py)
  * One row of a triangular solve in the reference's arithmetic
  * (LUSolve_ignoreZero, src/SpMV_compute.cpp:92-136): x[r] = b[r], then

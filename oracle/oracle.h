@@ -105,6 +105,7 @@ double orc_pwl(const double *tv, int np, int it, double h);
 /* w = B u + (C/h) x formed as the driver does: w = 0; w += B u (cs_dl_gaxpy,
  * B incidence: source k adds +1 * u[k] at row src_node[k], k ascending);
  * xnr = 0; xnr += diag(cdiag) x; w += xnr. */
+void orc_gaxpy_csc(int ncol, const long *p, const long *i, const double *ax, const double *x, double *y);
 void orc_transient_rhs(int n, int nsrc, const int *src_node, const double *u,
                        const double *cdiag, const double *x, double *w);
 

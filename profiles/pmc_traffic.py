@@ -13,10 +13,24 @@ are counted by these memory-side counters, not excluded.
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import re
 import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL_SOURCES = ["gpu-gmres_amd/csrc/kernels.hip", "gpu-gmres_amd/csrc/solver.hip",
+                  "gpu-gmres_amd/csrc/kernels.h", "gpu-gmres_amd/csrc/gg_internal.h"]
+
+
+def src_sha():
+    """sha256 (16 hex digits) over the kernel sources, in a fixed order"""
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(REPO, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def short(name):
@@ -62,6 +76,9 @@ def main():
                   "hbm_bytes_per_launch": rd + wr, "dispatches": [fn, wn]}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (separate passes)",
            "correction": "read = 2 x FETCH_SIZE KiB (gfx950 16-B/lane streaming reads); write = WRITE_SIZE KiB",
+           # the kernel sources these counters were taken on: bench.py drops the
+           # traffic figure when the sources have changed since (stale counters)
+           "src_sha": src_sha(),
            "kernels": res}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)

@@ -52,8 +52,28 @@ def test_reference_boundary_classes_exported(ggmres_lib):
                 "gmresInterfacePGfloat::~gmresInterfacePGfloat()",
                 "gmresInterfacePG::setPrecondPG(MySpMatrix*, MySpMatrixDouble*, MySpMatrixDouble*, "
                 "MySpMatrix*, MySpMatrix*, MySpMatrix*, MySpMatrixDouble*, MySpMatrixDouble*)",
-                "gmresInterfacePG::GMRES_host_PG()", "gmresInterfacePG::~gmresInterfacePG()"]:
+                "gmresInterfacePG::GMRES_host_PG()", "gmresInterfacePG::~gmresInterfacePG()",
+                "wrapperGMRESforPG(ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, int*, int, gpuETBR*)"]:
         assert sig in out, sig
+
+
+@pytest.mark.parametrize("prog, sym", [
+    ("pg_driver", "gmresInterfacePGfloat::GMRES_dev_PG()"),
+    ("wrapper_driver", "wrapperGMRESforPG(ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, int*, int, gpuETBR*)"),
+])
+def test_reference_callers_link_unchanged(ggmres_lib, prog, sym):
+    """The g++-built stand-ins for the reference's callers (tests/boundary/) take
+    their boundary symbols from libggmres.so: undefined in the program, defined
+    (same mangled name) in the library, resolved by the dynamic loader."""
+    exe = os.path.join(REPO, "tests", "boundary", prog)
+    subprocess.check_call(["make", "-s", "-C", os.path.dirname(exe)])
+    und = subprocess.check_output(f"nm -u {exe} | c++filt", shell=True, text=True)
+    assert sym in und
+    ldd = subprocess.check_output(["ldd", exe], text=True)
+    lib_line = [ln for ln in ldd.splitlines() if "libggmres.so" in ln]
+    assert lib_line and "not found" not in lib_line[0]
+    assert os.path.realpath(lib_line[0].split("=>")[1].split("(")[0].strip()) == \
+        os.path.realpath(os.path.join(PKG, "lib", "libggmres.so"))
 
 
 def test_headers_compile_as_c_and_cpp(tmp_path):
@@ -62,9 +82,10 @@ def test_headers_compile_as_c_and_cpp(tmp_path):
     subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only",
                            f"-I{REPO}/include", str(c)])
     cc = tmp_path / "t.cpp"
-    cc.write_text('#include "gmres_interface_pg.h"\n#include <cstddef>\n'
+    cc.write_text('#include "gmres_interface_pg.h"\n#include "gpuData.h"\n#include <cstddef>\n'
                   'static_assert(sizeof(gmresInterfacePGfloat) == 120, "layout");\n'
                   'static_assert(offsetof(gmresInterfacePGfloat, rhs_h) == 80, "layout");\n'
+                  'static_assert(sizeof(gpuETBR) == 552 && offsetof(gpuETBR, x_single_host) == 184, "layout");\n'
                   'int main(){return 0;}\n')
     subprocess.check_call(["g++", "-std=c++11", "-Wall", "-fsyntax-only",
                            f"-I{REPO}/include/compat", f"-I{REPO}/include", str(cc)])
