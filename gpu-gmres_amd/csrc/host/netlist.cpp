@@ -21,6 +21,7 @@
 #include <string>
 #include <vector>
 
+#include "gg_internal.h"
 #include "ggmres.h"
 #include "ggmres_host.h"
 
@@ -142,10 +143,33 @@ void pwl_points(const std::string &line, Src &s)
     }
 }
 
-std::string strip(std::string s, char c)
+// PULSE(v1, v2, td, tr, tf, pw, period): the numbers between the '(' after the
+// keyword and the next ')', separated by blanks and/or commas.  On the
+// reference's own spelling ("PULSE(v1, v2, ..., period)") this reads the same
+// values as its fixed-offset sscanf (src/parser.cpp:2655-2686); a blank
+// before '(' or after it is accepted too.  Fewer than 7 numbers: empty.
+std::vector<double> pulse_args(const std::string &line, size_t kw)
 {
-    if (!s.empty() && s.back() == c) s.pop_back();
-    return s;
+    const size_t a = line.find('(', kw);
+    if (a == std::string::npos) return {};
+    const size_t b = line.find(')', a);
+    std::string body = line.substr(a + 1, (b == std::string::npos ? line.size() : b) - a - 1);
+    for (char &ch : body)
+        if (ch == ',') ch = ' ';
+    std::vector<std::string> t = tokens(body);
+    if (t.size() < 7) return {};
+    std::vector<double> v;
+    for (int k = 0; k < 7; k++) v.push_back(str_to_num(t[k]));
+    return v;
+}
+
+// an element line R/C/L/V/I needs its name, two nodes and a value: both
+// passes apply the same rule, and a shorter line rejects the netlist (naming
+// it) instead of reserving an unknown it never stamps
+void check_element(const std::vector<std::string> &t, const std::string &l)
+{
+    if (t.size() < 4)
+        throw gg::Error{GG_EINVAL, "netlist: element line needs a name, two nodes and a value: '" + l + "'"};
 }
 
 }  // namespace
@@ -173,14 +197,13 @@ extern "C" int gg_host_read_netlist(const char *path, gg_netlist *out)
             if (l.empty()) continue;
             const char c = (char)std::toupper((unsigned char)l[0]);
             if (c == 'R' || c == 'C' || c == 'L' || c == 'V' || c == 'I') {
+                std::vector<std::string> t = tokens(l);
+                check_element(t, l);
                 if (c == 'L') nl++;
                 if (c == 'V') nv++;
                 if (c == 'I') ni++;
-                std::vector<std::string> t = tokens(l);
-                if (t.size() >= 3) {
-                    node(t[1]);
-                    node(t[2]);
-                }
+                node(t[1]);
+                node(t[2]);
             } else if (c == '.' && l.size() > 1) {
                 if (l[1] == 't') {
                     std::vector<std::string> t = tokens(l);
@@ -225,9 +248,9 @@ extern "C" int gg_host_read_netlist(const char *path, gg_netlist *out)
                 continue;
             }
             if (!(c == 'R' || c == 'C' || c == 'L' || c == 'V' || c == 'I')) continue;
+            check_element(t, l);
             if (c == 'V') iv++;
             if (c == 'I') ii++;
-            if (t.size() < 4) continue;
             const int n1 = row.at(t[1]), n2 = row.at(t[2]);
             if (c == 'R' || c == 'C') {
                 const double v = c == 'R' ? 1.0 / str_to_num(t[3]) : str_to_num(t[3]);
@@ -279,16 +302,8 @@ extern "C" int gg_host_read_netlist(const char *path, gg_netlist *out)
                     // "<dc> PULSE(v1, v2, td, tr, tf, pw, period)": the GPU path's
                     // gen_PULSEut_kernel parameters (the CPU path expands them to PWL)
                     s.kind = GG_SRC_PULSE;
-                    if (t.size() >= 11) {
-                        const double v1 = str_to_num(strip(t[4], ',').substr(6));
-                        const double v2 = str_to_num(strip(t[5], ','));
-                        const double td = str_to_num(strip(t[6], ','));
-                        const double tr = str_to_num(strip(t[7], ','));
-                        const double tf = str_to_num(strip(t[8], ','));
-                        const double pwd = str_to_num(strip(t[9], ','));
-                        const double per = str_to_num(strip(t[10], ')'));
-                        s.data = {v1, v2, td, tr, tf, pwd, per};
-                    } else {
+                    s.data = pulse_args(l, l.find(t[4]));
+                    if (s.data.empty()) {
                         s.kind = GG_SRC_DC;          // malformed: no waveform (value 0)
                         s.data = {0.0};
                     }
@@ -325,6 +340,10 @@ extern "C" int gg_host_read_netlist(const char *path, gg_netlist *out)
             auto it = row.find(ports[k]);
             out->port[k] = it == row.end() ? -1 : it->second;
         }
+    } catch (const gg::Error &e) {
+        gg_host_free_netlist(out);
+        gg::set_error(e.msg);
+        return e.code;
     } catch (...) {
         gg_host_free_netlist(out);
         return GG_EINVAL;

@@ -61,6 +61,24 @@ def _lines(path, depth=0):
     return out
 
 
+def _check_element(t, l):
+    # both passes: an element line needs a name, two nodes and a value
+    if len(t) < 4:
+        raise ValueError(f"netlist: element line needs a name, two nodes and a value: {l!r}")
+
+
+def _pulse_args(l, kw):
+    # the numbers between the '(' after the PULSE keyword and the next ')',
+    # blank- and/or comma-separated (the reference's spelling reads the same
+    # values as its sscanf, src/parser.cpp:2655-2686); fewer than 7: None
+    a = l.find("(", kw)
+    if a < 0:
+        return None
+    b = l.find(")", a)
+    body = l[a + 1:(b if b >= 0 else len(l))].replace(",", " ").split()
+    return [str_to_num(x) for x in body[:7]] if len(body) >= 7 else None
+
+
 def read_netlist(path):
     """dict: n, n_nodes, n_l, n_v, n_i, tstep, tstop, G, C, B as
     {(i, j): value} accumulated in push order, sources [(kind, [params])],
@@ -85,13 +103,13 @@ def read_netlist(path):
             continue
         c = l[0].upper()
         if c in "RCLVI":
+            t = l.split()
+            _check_element(t, l)
             nl += c == "L"
             nv += c == "V"
             ni += c == "I"
-            t = l.split()
-            if len(t) >= 3:
-                node(t[1])
-                node(t[2])
+            node(t[1])
+            node(t[2])
         elif c == "." and len(l) > 1:
             if l[1] == "t":
                 t = l.split()
@@ -123,10 +141,9 @@ def read_netlist(path):
             continue
         if c not in "RCLVI":
             continue
+        _check_element(t, l)
         iv += c == "V"
         ii += c == "I"
-        if len(t) < 4:
-            continue
         n1, n2 = rows[t[1]], rows[t[2]]
         if c in "RC":
             v = 1.0 / str_to_num(t[3]) if c == "R" else str_to_num(t[3])
@@ -177,11 +194,8 @@ def read_netlist(path):
                         s[1] += [0.0, v]
                     s[1] += [tm, v]
             elif len(t) >= 5 and t[4][:2].upper() == "PU":
-                if len(t) >= 11:
-                    f = [x.rstrip(",") for x in t[4:10]] + [t[10].rstrip(")")]
-                    s = [SRC_PULSE, [str_to_num(f[0][6:])] + [str_to_num(x) for x in f[1:]]]
-                else:
-                    s = [SRC_DC, [0.0]]
+                q = _pulse_args(l, l.find(t[4]))
+                s = [SRC_PULSE, q] if q is not None else [SRC_DC, [0.0]]
             else:
                 s = [SRC_DC, [str_to_num(w)]]
             src[j] = s

@@ -118,6 +118,55 @@ def test_netlist_missing_file(tmp_path):
         H.Netlist(str(tmp_path / "none.sp"))
 
 
+@pytest.mark.parametrize("bad", ["L1 b c", "V1 c 0", "I1 a", "R1 a b", "C1 a"])
+def test_netlist_short_element_line_rejected(tmp_path, bad):
+    """An element line without two nodes and a value is rejected, naming the
+    line, in both passes alike (no reserved branch row left unstamped)."""
+    from ggmres import GGError
+    p = str(tmp_path / "short.sp")
+    with open(p, "w") as f:
+        f.write(f"* x\nR0 a b 1k\nL0 b 0 1n\n{bad}\nV0 a 0 1\n.end\n")
+    with pytest.raises(GGError) as ei:
+        H.Netlist(p)
+    assert bad in str(ei.value)
+    with pytest.raises(ValueError):
+        ON.read_netlist(p)
+
+
+@pytest.mark.parametrize("spelling", ["PULSE(0, 10m, 0.2n, 0.1n, 0.1n, 0.5n, 1n)",
+                                      "PULSE (0, 10m, 0.2n, 0.1n, 0.1n, 0.5n, 1n)",
+                                      "pulse( 0 10m 0.2n 0.1n 0.1n 0.5n 1n )",
+                                      "PULSE(0,10m,0.2n,0.1n,0.1n,0.5n,1n)"])
+def test_netlist_pulse_spellings(tmp_path, spelling):
+    """PULSE arguments are read between the parentheses, blank- or
+    comma-separated: every spelling gives the reference spelling's values."""
+    p = str(tmp_path / "pulse.sp")
+    with open(p, "w") as f:
+        f.write(f"* x\nR0 a 0 1k\nC0 a 0 1p\nI1 a 0 0 {spelling}\n.end\n")
+    nl = H.Netlist(p)
+    o = ON.read_netlist(p)
+    want = [0.0, 10e-3, 0.2e-9, 0.1e-9, 0.1e-9, 0.5e-9, 1e-9]
+    k, par = nl.sources[0]
+    assert k == 1 and np.allclose(par, want, rtol=0, atol=1e-25)
+    assert o["sources"][0][0] == 1 and np.array_equal(np.array(o["sources"][0][1]), par)
+    ref = H.Netlist(_write(tmp_path / "ref.sp", "* x\nR0 a 0 1k\nC0 a 0 1p\n"
+                           "I1 a 0 0 PULSE(0, 10m, 0.2n, 0.1n, 0.1n, 0.5n, 1n)\n.end\n"))
+    assert np.array_equal(ref.sources[0][1], par)
+
+
+def test_netlist_pulse_malformed_is_dc_zero(tmp_path):
+    p = _write(tmp_path / "m.sp", "* x\nR0 a 0 1k\nI1 a 0 0 PULSE(1, 2, 3)\n.end\n")
+    nl = H.Netlist(p)
+    assert nl.sources[0][0] == 0 and np.array_equal(nl.sources[0][1], [0.0])
+    assert ON.read_netlist(p)["sources"][0] == (0, [0.0])
+
+
+def _write(path, text):
+    with open(str(path), "w") as f:
+        f.write(text)
+    return str(path)
+
+
 @pytest.mark.gpu
 def test_netlist_transient_on_device(tmp_path):
     """RC grid netlist (C to ground, R mesh, current sources) -> A = G + C/h,
