@@ -70,6 +70,12 @@ int iluk_itsol(const Csr &A, int lof, Csr &L, Csr &U);        // lofC + ilukC, 0
 // insertion order) and the emission of ilukC's factors in the solver's forms
 void iluk_symbolic(const Csr &A, int lof, std::vector<std::vector<int>> &Lja,
                    std::vector<std::vector<int>> &Uja);
+// ILU(k) pattern as flat ascending rows (L part, diagonal, U part); k = 1
+// row-parallel over host threads (factor.cpp)
+void iluk_pattern(const Csr &A, int lof, int threads, std::vector<long long> &prow, std::vector<int> &nl,
+                  std::vector<int> &pcol);
+void iluk_emit_flat(int n, const std::vector<long long> &prow, const std::vector<int> &nl,
+                    const std::vector<int> &pcol, const std::vector<double> &val, Csr &L, Csr &U);
 void iluk_emit(const std::vector<std::vector<int>> &Lja, const std::vector<std::vector<int>> &Uja,
                const std::vector<std::vector<double>> &Lma, const std::vector<std::vector<double>> &Uma,
                const std::vector<double> &Draw, Csr &L, Csr &U);

@@ -8,8 +8,10 @@
 //                                       splitLU_csr :481-541)
 //   iluk_itsol  lofC + ilukC            src/iluk.cpp:56-334
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <numeric>
+#include <thread>
 
 #include "../gg_internal.h"
 
@@ -183,6 +185,124 @@ void iluk_symbolic(const Csr &A, int lof, std::vector<std::vector<int>> &Lja,
         Lja[i].assign(jbuf.begin(), jbuf.begin() + incl);
         Uja[i].assign(jbuf.begin() + i, jbuf.begin() + incu);
         ulvl[i].assign(levls.begin() + i, levls.begin() + incu);
+    }
+}
+
+// The ILU(k) pattern as flat rows (each row ascending: L part, the diagonal,
+// U part) -- the order-free content of lofC's output (src/iluk.cpp:193-334:
+// its L part is built in leftmost-pivot = ascending order, its U part is
+// sorted by the emission; ilukC's arithmetic per entry only depends on the
+// ascending pivot order, not on where an entry is stored).
+//   k = 1: a fill entry has level 1 exactly when it comes from an ORIGINAL L
+//     entry (i, k) of row i and an ORIGINAL U entry (k, c) of row k (every other
+//     path has level >= 2), so row i's pattern is A(i) united with U_A(k) over
+//     k in L_A(i): independent of every other row's fill, built row-parallel
+//     over `threads` host threads (dynamic blocks of 1024 rows);
+//   k >= 2: lofC itself (serial: a row's fill depends on earlier rows' fill
+//     levels), flattened.
+void iluk_pattern(const Csr &A, int lof, int threads, std::vector<long long> &prow, std::vector<int> &nl,
+                  std::vector<int> &pcol)
+{
+    const int n = A.n;
+    prow.assign((size_t)n + 1, 0);
+    nl.assign(n, 0);
+    if (lof != 1) {
+        std::vector<std::vector<int>> Lja, Uja;
+        iluk_symbolic(A, lof, Lja, Uja);
+        for (int i = 0; i < n; i++) {
+            nl[i] = (int)Lja[i].size();
+            prow[i + 1] = prow[i] + nl[i] + 1 + (long long)Uja[i].size();
+        }
+        pcol.resize((size_t)prow[n]);
+        for (int i = 0; i < n; i++) {
+            int *o = pcol.data() + prow[i];
+            std::copy(Lja[i].begin(), Lja[i].end(), o);        // ascending (leftmost pivot first)
+            o[nl[i]] = i;
+            std::vector<int> u = Uja[i];
+            std::sort(u.begin(), u.end());
+            std::copy(u.begin(), u.end(), o + nl[i] + 1);
+        }
+        return;
+    }
+    constexpr int kRows = 1024;
+    const int nblk = (n + kRows - 1) / kRows;
+    std::vector<std::vector<int>> bcols(nblk), blen(nblk);
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        std::vector<int> mark(n, -1), row;
+        for (int b; (b = next.fetch_add(1)) < nblk;) {
+            const int r0 = b * kRows, r1 = std::min(n, r0 + kRows);
+            std::vector<int> &cols = bcols[b], &len = blen[b];
+            len.resize(r1 - r0);
+            for (int i = r0; i < r1; i++) {
+                row.clear();
+                mark[i] = i;
+                row.push_back(i);
+                for (int e = A.rp[i]; e < A.rp[i + 1]; e++) {
+                    const int c = A.ci[e];
+                    if (mark[c] != i) { mark[c] = i; row.push_back(c); }
+                }
+                for (int e = A.rp[i]; e < A.rp[i + 1]; e++) {
+                    const int k = A.ci[e];
+                    if (k >= i) continue;
+                    for (int f = A.rp[k]; f < A.rp[k + 1]; f++) {
+                        const int c = A.ci[f];
+                        if (c > k && mark[c] != i) { mark[c] = i; row.push_back(c); }
+                    }
+                }
+                std::sort(row.begin(), row.end());
+                len[i - r0] = (int)row.size();
+                cols.insert(cols.end(), row.begin(), row.end());
+            }
+        }
+    };
+    const int nt = std::max(1, std::min(threads, nblk));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work);
+    work();
+    for (std::thread &t : pool) t.join();
+    for (int b = 0; b < nblk; b++)
+        for (size_t q = 0; q < blen[b].size(); q++) {
+            const int i = b * kRows + (int)q;
+            prow[i + 1] = prow[i] + blen[b][q];
+        }
+    pcol.resize((size_t)prow[n]);
+    for (int b = 0; b < nblk; b++) {
+        std::copy(bcols[b].begin(), bcols[b].end(), pcol.data() + prow[(size_t)b * kRows]);
+        std::vector<int>().swap(bcols[b]);
+    }
+    for (int i = 0; i < n; i++) {
+        const int *r = pcol.data() + prow[i];
+        nl[i] = (int)(std::lower_bound(r, r + (prow[i + 1] - prow[i]), i) - r);
+    }
+}
+
+// ilukC's factors from the flat pattern (iluk_pattern) and the factored
+// values (the diagonal position holds the un-inverted pivot): L strict
+// ascending + unit diagonal last, U diagonal first + strict ascending --
+// iluk_emit's forms
+void iluk_emit_flat(int n, const std::vector<long long> &prow, const std::vector<int> &nl,
+                    const std::vector<int> &pcol, const std::vector<double> &val, Csr &L, Csr &U)
+{
+    L.n = U.n = n;
+    L.rp.assign((size_t)n + 1, 0);
+    U.rp.assign((size_t)n + 1, 0);
+    for (int i = 0; i < n; i++) {
+        L.rp[i + 1] = L.rp[i] + nl[i] + 1;
+        U.rp[i + 1] = U.rp[i] + (int)(prow[i + 1] - prow[i] - nl[i]);
+    }
+    L.ci.resize(L.rp[n]);
+    L.v.resize(L.rp[n]);
+    U.ci.resize(U.rp[n]);
+    U.v.resize(U.rp[n]);
+    for (int i = 0; i < n; i++) {
+        const long long p0 = prow[i], d0 = p0 + nl[i];
+        std::copy(pcol.begin() + p0, pcol.begin() + d0, L.ci.begin() + L.rp[i]);
+        std::copy(val.begin() + p0, val.begin() + d0, L.v.begin() + L.rp[i]);
+        L.ci[L.rp[i + 1] - 1] = i;
+        L.v[L.rp[i + 1] - 1] = 1.0;
+        std::copy(pcol.begin() + d0, pcol.begin() + prow[i + 1], U.ci.begin() + U.rp[i]);
+        std::copy(val.begin() + d0, val.begin() + prow[i + 1], U.v.begin() + U.rp[i]);
     }
 }
 

@@ -55,11 +55,14 @@ void launch_taps(int ntap, const int *tap, const double *x, double *mx, double *
 int ilu0_columns_max_blocks();
 void launch_ilu0_columns(int n, const int *cp, const int *ri, const double *cv0, double *cv, int *level,
                          int *done, int *err, int blocks, hipStream_t st);
-// device ILU(k) numeric factorization on lofC's pattern (k_iluk_rows; co-resident grid)
-int iluk_rows_max_blocks();
-void launch_iluk_rows(int n, const long long *prow, const int *nl, const int *pcol, const long long *uptr,
-                      const long long *usrc, const long long *udst, double *val, double *dinv, double *draw,
-                      int *done, int *err, int blocks, hipStream_t st);
+// device ILU(k) numeric factorization on the flat ILU(k) pattern (k_iluk_wave; co-resident grid)
+int iluk_wave_max_blocks();   // co-resident blocks of k_iluk_wave
+int iluk_wave_cap();          // row length above which k_iluk_wave takes the long-row path
+void launch_iluk_scatter(int n, const int *arp, const int *aci, const double *av, const long long *prow,
+                         const int *pcol, double *val, hipStream_t st);
+void launch_iluk_wave(int n, const long long *prow, const int *nl, const int *pcol, double *val, double *dinv,
+                      int *done, const int *rows_short, int nshort, const int *rows_long, int nlong,
+                      int long_blocks, int *scratch, int *err, int blocks, hipStream_t st);
 void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st);  // out[i] = idx[i]<0 ? 0 : in[idx[i]]
 void launch_copy(const double *in, double *out, long long n, hipStream_t st);
 void launch_dot(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, hipStream_t st);

@@ -1156,66 +1156,136 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_columns(int n, const int *__res
 }
 
 // ILU(k) numeric factorization (ilukC, src/iluk.cpp:108-188) on lofC's pattern
-// (built on the host, src/iluk.cpp:193-334).  Row i's entries: its L part in
-// lofC's order, the diagonal, its U part (prow[i] .. prow[i+1]; nl[i] L
-// entries; pcol = column).  For L entry t (column jrow) the host lists, in the
-// reference's loop order, the (source U entry of row jrow, destination entry of
-// row i) pairs whose column is in row i's pattern (jw[col] != -1).  Lane = row;
-// a row is ready when every row of its L part is done; then, per L entry in
-// order: l = val[t] * Dinv[jrow]; val[dst] = val[dst] - l * val[src] for its
-// pairs; then Draw[i] = val[diag], Dinv[i] = 1 / Draw[i] (err bit 2 on a zero
-// pivot, src/iluk.cpp:175-185), every store drained, done[i] published.  Same
-// wave-uniform retry loop and co-resident grid as k_ilu0_columns.
-__global__ __launch_bounds__(kBlock) void k_iluk_rows(int n, const long long *__restrict__ prow,
-                                                      const int *__restrict__ nl,
-                                                      const int *__restrict__ pcol,
-                                                      const long long *__restrict__ uptr,
-                                                      const long long *__restrict__ usrc,
-                                                      const long long *__restrict__ udst, double *val,
-                                                      double *dinv, double *draw, int *done, int *err)
+// (host, iluk_pattern): row i = prow[i] .. prow[i+1], every row ascending (its
+// nl[i] L entries, the diagonal, its U part).  One WAVE per row; a row's pivots
+// (its L entries) are taken one after the other in ascending column order --
+// the order ilukC applies them, so every entry sees the same updates in the
+// same order and the factors are bit-identical:
+//   wait done[k]; l = val[t] * Dinv[k]; for the U entries (k, c) of row k, in
+//   parallel over the lanes: if c is in row i's pattern, val[i, c] -= l * u
+// then Dinv[i] = 1 / val[diag] (err bit 2 on a zero pivot, src/iluk.cpp:175-185),
+// the row's values stored write-through, drained, done[i] published.
+// Ordinary rows (<= kIlukCap entries) are staged in the wave's LDS (columns
+// and values; a column is found by binary search above the pivot's position);
+// longer rows (the hub rows of circuit matrices) keep their values in HBM and
+// find columns through a dense column -> position map of their own (scratch,
+// n ints per long-row wave, -1 outside the row).  Rows are split into the two
+// lists (ascending); the first `long_blocks` blocks take the long list, the
+// rest the short one, each wave its list's rows in ascending order: with every
+// block co-resident the smallest unfinished row always progresses.  Spins are
+// bounded (err bit 0).
+constexpr int kIlukCap = 3200;
+__device__ __forceinline__ int lds_bsearch(const int *a, int lo, int hi, int c)
 {
-    const int lane = threadIdx.x & 63;
-    const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
-    const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
-    for (long long base = wid * 64; base < n; base += nw * 64) {
-        const int i = (int)(base + lane);
-        bool fin = i >= n;
-        int spins = 0;
-        const long long p0 = fin ? 0 : prow[i];
-        const int nli = fin ? 0 : nl[i];
-        while (__any(!fin)) {
-            bool moved = false;
-            if (!fin) {
-                bool ready = true;
-                for (int t = 0; t < nli; t++)
-                    if (ld_agent_i(done + pcol[p0 + t]) == 0) { ready = false; break; }
-                if (ready) {
-                    for (int t = 0; t < nli; t++) {
-                        const long long e = p0 + t;
-                        const double l = ld_agent_d(val + e) * ld_agent_d(dinv + pcol[e]);
-                        st_agent_d(val + e, l);
-                        for (long long q = uptr[e]; q < uptr[e + 1]; q++) {
-                            const long long d = udst[q];
-                            st_agent_d(val + d, ld_agent_d(val + d) - l * ld_agent_d(val + usrc[q]));
-                        }
-                    }
-                    const double dg = ld_agent_d(val + p0 + nli);
-                    if (dg == 0.0) atomicOr(err, 2);
-                    st_agent_d(draw + i, dg);
-                    st_agent_d(dinv + i, 1.0 / dg);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // values out before the flag
-                    st_agent_i(done + i, 1);
-                    fin = true;
-                    moved = true;
-                }
+    const int end = hi;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < c) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < end && a[lo] == c) ? lo : -1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_iluk_wave(int n, const long long *__restrict__ prow,
+                                                      const int *__restrict__ nl,
+                                                      const int *__restrict__ pcol, double *val,
+                                                      double *dinv, int *done,
+                                                      const int *__restrict__ rows_short, int nshort,
+                                                      const int *__restrict__ rows_long, int nlong,
+                                                      int long_blocks, int *scratch, int *err)
+{
+    __shared__ int scol[kBlock / 64][kIlukCap];
+    __shared__ double sval[kBlock / 64][kIlukCap];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool lng = (int)blockIdx.x < long_blocks;
+    const int gw = (lng ? (int)blockIdx.x : (int)blockIdx.x - long_blocks) * (kBlock / 64) + w;
+    const int nw = (lng ? long_blocks : (int)gridDim.x - long_blocks) * (kBlock / 64);
+    const int cnt = lng ? nlong : nshort;
+    const int *rows = lng ? rows_long : rows_short;
+    int *jw = lng ? scratch + (long long)gw * n : nullptr;
+    int *sc = scol[w];
+    double *sv = sval[w];
+    bool dead = false;
+    for (int q = gw; q < cnt && !dead; q += nw) {
+        const int i = rows[q];
+        const long long p0 = prow[i];
+        const int len = (int)(prow[i + 1] - p0), nli = nl[i];
+        if (!lng) {
+            for (int t = lane; t < len; t += 64) {
+                sc[t] = pcol[p0 + t];
+                sv[t] = val[p0 + t];
             }
-            if (!moved && !fin) {
+        } else {
+            for (int t = lane; t < len; t += 64) __hip_atomic_store(jw + pcol[p0 + t], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        for (int j = 0; j < nli && !dead; j++) {
+            const int k = lng ? pcol[p0 + j] : sc[j];
+            int spins = 0;
+            while (__builtin_amdgcn_readfirstlane(ld_agent_i(done + k)) == 0) {
                 __builtin_amdgcn_s_sleep(2);
                 if (++spins > kSpinLimit) {
-                    atomicOr(err, 1);
-                    fin = true;
+                    if (lane == 0) atomicOr(err, 1);
+                    dead = true;
+                    break;
                 }
             }
+            const double l = (lng ? ld_agent_d(val + p0 + j) : sv[j]) * ld_agent_d(dinv + k);
+            if (lane == 0) {
+                if (lng) st_agent_d(val + p0 + j, l);
+                else sv[j] = l;
+            }
+            const long long u0 = prow[k] + nl[k] + 1, u1 = prow[k + 1];
+            for (long long e = u0 + lane; e < u1; e += 64) {
+                const int c = pcol[e];
+                const double u = ld_agent_d(val + e);
+                if (lng) {
+                    const int pos = __hip_atomic_load(jw + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (pos >= 0) st_agent_d(val + p0 + pos, ld_agent_d(val + p0 + pos) - l * u);
+                } else {
+                    const int pos = lds_bsearch(sc, j + 1, len, c);
+                    if (pos >= 0) sv[pos] = sv[pos] - l * u;
+                }
+            }
+            if (lng) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const double dg = lng ? ld_agent_d(val + p0 + nli) : sv[nli];
+        if (!lng)
+            for (int t = lane; t < len; t += 64) st_agent_d(val + p0 + t, sv[t]);
+        if (lane == 0) {
+            if (dg == 0.0) atomicOr(err, 2);
+            st_agent_d(dinv + i, 1.0 / dg);
+        }
+        if (lng)
+            for (int t = lane; t < len; t += 64) __hip_atomic_store(jw + pcol[p0 + t], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the row's values out before the flag
+        if (lane == 0) st_agent_i(done + i, 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // LDS reads done before the next row's staging
+    }
+}
+
+// A's values into the ILU(k) pattern (val pre-zeroed), ilukC's initial
+// scatter (src/iluk.cpp:120-133): one thread per row, entries in CSR order (a
+// repeated column keeps its last value, as the reference's assignment does),
+// each position found by binary search in the row's ascending columns
+__global__ __launch_bounds__(kBlock) void k_iluk_scatter(int n, const int *__restrict__ arp,
+                                                         const int *__restrict__ aci,
+                                                         const double *__restrict__ av,
+                                                         const long long *__restrict__ prow,
+                                                         const int *__restrict__ pcol, double *val)
+{
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const long long p0 = prow[i], p1 = prow[i + 1];
+        for (int e = arp[i]; e < arp[i + 1]; e++) {
+            const int c = aci[e];
+            long long lo = p0, hi = p1;
+            while (lo < hi) {
+                const long long mid = (lo + hi) >> 1;
+                if (pcol[mid] < c) lo = mid + 1;
+                else hi = mid;
+            }
+            val[lo] = av[e];                     // every entry of A is in its row's pattern
         }
     }
 }
@@ -1794,19 +1864,26 @@ void launch_ilu0_columns(int n, const int *cp, const int *ri, const double *cv0,
 {
     k_ilu0_columns<<<blocks, kBlock, 0, st>>>(n, cp, ri, cv0, cv, level, done, err);
 }
-int iluk_rows_max_blocks()
+int iluk_wave_max_blocks()
 {
     int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_iluk_rows, kBlock, 0) != hipSuccess) return 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_iluk_wave, kBlock, 0) != hipSuccess) return 0;
     return cus * per;
 }
-void launch_iluk_rows(int n, const long long *prow, const int *nl, const int *pcol, const long long *uptr,
-                      const long long *usrc, const long long *udst, double *val, double *dinv, double *draw,
-                      int *done, int *err, int blocks, hipStream_t st)
+int iluk_wave_cap() { return kIlukCap; }
+void launch_iluk_scatter(int n, const int *arp, const int *aci, const double *av, const long long *prow,
+                         const int *pcol, double *val, hipStream_t st)
 {
-    k_iluk_rows<<<blocks, kBlock, 0, st>>>(n, prow, nl, pcol, uptr, usrc, udst, val, dinv, draw, done, err);
+    k_iluk_scatter<<<blocks_for(n, kBlock, 8192), kBlock, 0, st>>>(n, arp, aci, av, prow, pcol, val);
+}
+void launch_iluk_wave(int n, const long long *prow, const int *nl, const int *pcol, double *val, double *dinv,
+                      int *done, const int *rows_short, int nshort, const int *rows_long, int nlong,
+                      int long_blocks, int *scratch, int *err, int blocks, hipStream_t st)
+{
+    k_iluk_wave<<<blocks, kBlock, 0, st>>>(n, prow, nl, pcol, val, dinv, done, rows_short, nshort, rows_long,
+                                           nlong, long_blocks, scratch, err);
 }
 void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st)
 {

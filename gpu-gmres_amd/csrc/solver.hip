@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <thread>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -950,80 +951,74 @@ int gg_set_precond_ilu0_device(gg_solver *s)
     GG_API_END
 }
 
-// ILU(k) with the numeric phase on the device (k_iluk_rows): lofC's pattern
-// and the per-row update lists built on the host (the reference runs lofC on
-// the host too), A's values gathered into the pattern and factored on the
-// device, the factors emitted as iluk_itsol does; bit-identical to iluk_itsol.
+// ILU(k) with the numeric phase on the device (k_iluk_wave): the pattern on
+// the host (iluk_pattern: row-parallel for k = 1, lofC for k >= 2; the
+// reference runs lofC on the host too), A's values scattered into it and the
+// rows factored on the device, the factors emitted in iluk_itsol's forms;
+// bit-identical to iluk_itsol.  Host threads: GG_HOST_THREADS (default: the
+// hardware threads, at most 16).
 void iluk_device_factor(gg_solver *s, int level, Csr &L, Csr &U, double *ms)
 {
     const Csr &A = s->A;
     const int n = A.n;
-    std::vector<std::vector<int>> Lja, Uja;
-    iluk_symbolic(A, level, Lja, Uja);
-    std::vector<long long> prow(n + 1, 0);
-    std::vector<int> nl(n);
-    for (int i = 0; i < n; i++) {
-        nl[i] = (int)Lja[i].size();
-        prow[i + 1] = prow[i] + nl[i] + 1 + (long long)Uja[i].size();
-    }
+    static const int threads = [] {
+        const char *e = std::getenv("GG_HOST_THREADS");
+        const int hw = (int)std::thread::hardware_concurrency();
+        return e ? std::max(1, atoi(e)) : std::max(1, std::min(hw, 16));
+    }();
+    std::vector<long long> prow;
+    std::vector<int> nl, pcol;
+    iluk_pattern(A, level, threads, prow, nl, pcol);
     const long long np = prow[n];
-    std::vector<int> pcol(np);
-    std::vector<long long> p2a(np, -1), uptr(np + 1, 0), usrc, udst;
-    std::vector<int> jw(n, -1);
-    for (int i = 0; i < n; i++) {
-        const long long p0 = prow[i], d0 = p0 + nl[i];
-        for (int j = 0; j < nl[i]; j++) { pcol[p0 + j] = Lja[i][j]; jw[Lja[i][j]] = (int)(p0 + j - p0); }
-        pcol[d0] = i;
-        jw[i] = nl[i];
-        for (size_t j = 0; j < Uja[i].size(); j++) { pcol[d0 + 1 + j] = Uja[i][j]; jw[Uja[i][j]] = nl[i] + 1 + (int)j; }
-        for (int k = A.rp[i]; k < A.rp[i + 1]; k++) p2a[p0 + jw[A.ci[k]]] = k;   // A's entries are in lofC's pattern
-        for (int j = 0; j < nl[i]; j++) {
-            const int jrow = Lja[i][j];
-            const long long s0 = prow[jrow] + nl[jrow] + 1;
-            for (size_t k = 0; k < Uja[jrow].size(); k++) {
-                const int jp = jw[Uja[jrow][k]];
-                if (jp < 0) continue;
-                usrc.push_back(s0 + (long long)k);
-                udst.push_back(p0 + jp);
-            }
-            uptr[p0 + j + 1] = (long long)usrc.size();
-        }
-        for (long long e = p0 + nl[i]; e < prow[i + 1]; e++) uptr[e + 1] = (long long)usrc.size();
-        for (int j = 0; j < nl[i]; j++) jw[Lja[i][j]] = -1;
-        jw[i] = -1;
-        for (int c : Uja[i]) jw[c] = -1;
+    // rows of more than the kernel's LDS capacity take the long-row path
+    // (GG_ILUK_LONG: a lower threshold, to exercise that path on small systems)
+    const char *lg = std::getenv("GG_ILUK_LONG");
+    const int cap = lg ? std::max(0, std::min(iluk_wave_cap(), atoi(lg))) : iluk_wave_cap();
+    std::vector<int> rshort, rlong;
+    for (int i = 0; i < n; i++) (prow[i + 1] - prow[i] > cap ? rlong : rshort).push_back(i);
+    const int maxb = iluk_wave_max_blocks();
+    GG_REQUIRE(maxb > 1, GG_EHIP, "ILU(k) device: occupancy query failed");
+    const int wpb = kBlock / 64;
+    int long_blocks = 0;
+    if (!rlong.empty()) {
+        // long-row waves: the long rows' share of the entries, at most half
+        // the grid and 16 GiB of position maps (n ints per wave)
+        long long long_nnz = 0;
+        for (int i : rlong) long_nnz += prow[i + 1] - prow[i];
+        const long long want = std::max<long long>(1, (long long)((double)maxb * long_nnz / std::max<long long>(np, 1)));
+        const long long by_mem = std::max<long long>(1, (16LL << 30) / ((long long)wpb * n * (long long)sizeof(int)));
+        long_blocks = (int)std::min<long long>({want, std::max(1, maxb / 2), by_mem,
+                                                (long long)(rlong.size() + wpb - 1) / wpb});
     }
-    DBuf<long long> dprow, dp2a, duptr, dusrc, dudst;
-    DBuf<int> dnl, dpcol, ddone;
-    DBuf<double> dav, dval, ddinv, ddraw;
+    const int short_blocks = (int)std::min<long long>(maxb - long_blocks, std::max<long long>(1, ((long long)rshort.size() + wpb - 1) / wpb));
+    const int blocks = long_blocks + (rshort.empty() ? 0 : short_blocks);
+    DBuf<long long> dprow;
+    DBuf<int> dnl, dpcol, ddone, drs, drl, darp, daci, dscr;
+    DBuf<double> dav, dval, ddinv;
     dprow.upload(prow, s->st);
-    dp2a.upload(p2a, s->st);
-    duptr.upload(uptr, s->st);
-    if (usrc.empty()) { usrc.push_back(0); udst.push_back(0); }   // no updates (diagonal L parts)
-    dusrc.upload(usrc, s->st);
-    dudst.upload(udst, s->st);
     dnl.upload(nl, s->st);
     dpcol.upload(pcol, s->st);
+    darp.upload(A.rp, s->st);
+    daci.upload(A.ci, s->st);
     dav.upload(A.v, s->st);
+    drs.upload(rshort, s->st);
+    drl.upload(rlong, s->st);
     dval.alloc(np);
     ddinv.alloc(n);
-    ddraw.alloc(n);
     ddone.alloc(n);
+    dscr.alloc((size_t)std::max(long_blocks, 1) * wpb * (rlong.empty() ? 1 : (size_t)n));
     if (!s->err.p) s->err.alloc(1);
+    GG_HIP(hipMemsetAsync(dval.p, 0, (size_t)np * sizeof(double), s->st));
     GG_HIP(hipMemsetAsync(ddone.p, 0, (size_t)n * sizeof(int), s->st));
+    GG_HIP(hipMemsetAsync(dscr.p, 0xFF, dscr.n * sizeof(int), s->st));
     GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
-    const int maxb = iluk_rows_max_blocks();
-    GG_REQUIRE(maxb > 0, GG_EHIP, "ILU(k) device: occupancy query failed");
-    const long long need = ((long long)n + kBlock - 1) / kBlock;
-    const int blocks = (int)std::max<long long>(1, std::min<long long>(maxb, need));
     GG_HIP(hipEventRecord(s->ev0, s->st));
-    launch_gather(dav.p, dp2a.p, dval.p, np, s->st);                    // A into the pattern, fill = 0
-    launch_iluk_rows(n, dprow.p, dnl.p, dpcol.p, duptr.p, dusrc.p, dudst.p, dval.p, ddinv.p, ddraw.p,
-                     ddone.p, s->err.p, blocks, s->st);
+    launch_iluk_scatter(n, darp.p, daci.p, dav.p, dprow.p, dpcol.p, dval.p, s->st);   // fill = 0
+    launch_iluk_wave(n, dprow.p, dnl.p, dpcol.p, dval.p, ddinv.p, ddone.p, drs.p, (int)rshort.size(), drl.p,
+                     (int)rlong.size(), long_blocks, dscr.p, s->err.p, blocks, s->st);
     GG_HIP(hipEventRecord(s->ev1, s->st));
-    std::vector<double> val(np), draw(n);
+    std::vector<double> val(np);
     GG_HIP(hipMemcpyAsync(val.data(), dval.p, (size_t)np * sizeof(double), hipMemcpyDeviceToHost, s->st));
-    GG_HIP(hipMemcpyAsync(draw.data(), ddraw.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s->st));
     int err = 0;
     GG_HIP(hipMemcpyAsync(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
     GG_HIP(hipStreamSynchronize(s->st));
@@ -1032,13 +1027,7 @@ void iluk_device_factor(gg_solver *s, int level, Csr &L, Csr &U, double *ms)
     float t = 0.f;
     GG_HIP(hipEventElapsedTime(&t, s->ev0, s->ev1));
     if (ms) *ms = t;
-    std::vector<std::vector<double>> Lma(n), Uma(n);
-    for (int i = 0; i < n; i++) {
-        const long long p0 = prow[i];
-        Lma[i].assign(val.begin() + p0, val.begin() + p0 + nl[i]);
-        Uma[i].assign(val.begin() + p0 + nl[i] + 1, val.begin() + prow[i + 1]);
-    }
-    iluk_emit(Lja, Uja, Lma, Uma, draw, L, U);
+    iluk_emit_flat(n, prow, nl, pcol, val, L, U);
 }
 
 int gg_set_precond_iluk_device(gg_solver *s, int level)

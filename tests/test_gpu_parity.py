@@ -330,12 +330,19 @@ def test_gmres_iluk_grid_parity(solver, k, dims, device):
     check_exact(g, ot)
 
 
-@pytest.mark.parametrize("name,k", [("5pt_10x10", 1), ("7pt_10x10x10", 1), ("9pt_10x10", 2),
-                                    ("sherman1", 1), ("c1_5pt_100x100", 0), ("c1_5pt_100x100", 2),
-                                    ("thermal_7pt_12", 1), ("powerlaw_3000", 1)])
-def test_iluk_device_factors_bitexact(solver, name, k):
+@pytest.mark.parametrize("name,k,long_rows", [("5pt_10x10", 1, None), ("7pt_10x10x10", 1, None),
+                                              ("9pt_10x10", 2, None), ("sherman1", 1, None),
+                                              ("c1_5pt_100x100", 0, None), ("c1_5pt_100x100", 2, None),
+                                              ("thermal_7pt_12", 1, None), ("powerlaw_3000", 1, None),
+                                              ("powerlaw_3000", 1, 12), ("sherman1", 1, 6),
+                                              ("9pt_10x10", 2, 0), ("thermal_7pt_12", 1, 9)])
+def test_iluk_device_factors_bitexact(solver, name, k, long_rows, monkeypatch):
     """ILU(k) with ilukC's numeric phase on the GPU: the same factors, bit for bit,
-    as the oracle's lofC + ilukC restatement (and hence as the host path)."""
+    as the oracle's lofC + ilukC restatement (and hence as the host path).
+    long_rows: rows longer than this take the kernel's long-row path (HBM values,
+    dense position map) instead of the LDS path (GG_ILUK_LONG)."""
+    if long_rows is not None:
+        monkeypatch.setenv("GG_ILUK_LONG", str(long_rows))
     A = MATS[name]()
     solver.set_matrix(A)
     try:
