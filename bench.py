@@ -371,11 +371,12 @@ def main():
     s = ggmres.Solver(local)
     t_setup = time.perf_counter()
     s.set_matrix(A)
-    kilu = a.ilu_level if a.workload == "c2" else 0
+    kilu = a.ilu_level if a.workload in ("c2", "c3s") else 0
     if kilu:
         s.set_precond_iluk_device(kilu)
-        for dom_ in ("trsv_L", "trsv_U"):              # the skewed instantiation (skew k+1)
-            KERNEL_NAMES[dom_] = KERNEL_NAMES[dom_][:-2] + f"{kilu + 1}>"
+        if not c3s:
+            for dom_ in ("trsv_L", "trsv_U"):              # the skewed instantiation (skew k+1)
+                KERNEL_NAMES[dom_] = KERNEL_NAMES[dom_][:-2] + f"{kilu + 1}>"
     else:
         s.set_precond_ilu0()
     t_setup = time.perf_counter() - t_setup
@@ -575,8 +576,8 @@ def main():
                                 f"steps per step, warm start, {a.c5_scenarios} concurrent scenario(s) "
                                 f"per GPU") if c5 else
                                (f"C3 stand-in: seeded power-law CSR with circuit5M's n and nnz "
-                                f"(no parity claim), ILU(0) left (C3 names ILU(1): out of reach on "
-                                f"this matrix, DESIGN.md 5.1), GMRES({a.restart}), tol {a.tol:g}, "
+                                f"(no parity claim at this size), ILU({kilu}) left (device-factored; "
+                                f"C3 names ILU(1)), GMRES({a.restart}), tol {a.tol:g}, "
                                 f"b=A*1, x0=0, one solve per step") if c3s else
                                (f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU({kilu}) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step"),

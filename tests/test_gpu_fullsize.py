@@ -155,3 +155,54 @@ def test_c5_transient_1000_steps_c2_grid():
     # the source nodes respond within the first pulse (td 0, rise 10 h)
     assert np.all(np.abs(P[:2, 20]) > 0)
     s.close()
+
+
+# --------------------------------------------------------------- C3, ILU(k=1)
+C3_ILU1_PATTERN = 234_215_488
+
+
+def test_c3_standin_iluk1_full_size():
+    """C3 -- the circuit5M stand-in (seeded power-law CSR with circuit5M's n and
+    nnz, uniform columns: 5,558,326 rows, 59.5M entries; the SuiteSparse file
+    is not available offline) with the ILU(1) preconditioner C3 names, at full
+    size.  The factors: the level-1 pattern (234,215,488 entries with the
+    diagonal: A's pattern united with U_A(k) over k in L_A(i), counted with
+    scipy outside the product), unit lower L, nonzero pivots on U's diagonal,
+    L*U reproducing A on A's pattern (ILU's defining property) on a sample of
+    rows.  The solve: GMRES(30) to 1e-10, history monotone inside the first
+    cycle, true residual ||b - A x|| / ||b|| < 1e-8.  Bit-exactness of the device factors against the oracle is pinned
+    at covered sizes (test_gpu_parity.py::test_iluk_device_factors_bitexact,
+    incl. the hub-row path)."""
+    import scipy.sparse as sp
+    A = M.power_law()
+    n = A.shape[0]
+    solver = ggmres.Solver(0)
+    solver.set_matrix(A)
+    (lrp, lci, lv), (urp, uci, uv), ms = solver.iluk_device_factors(1)
+    assert ms > 0
+    L = sp.csr_matrix((lv, lci, lrp), shape=(n, n))
+    U = sp.csr_matrix((uv, uci, urp), shape=(n, n))
+    # the level-1 pattern (diagonal included): 234,215,488 entries, counted
+    # independently with scipy (pattern of tril(A,-1) @ triu(A,1) united with A's)
+    assert L.nnz + U.nnz - n == C3_ILU1_PATTERN
+    assert sp.tril(L, -1).nnz + sp.triu(U, 1).nnz + n == C3_ILU1_PATTERN
+    assert np.array_equal(L.diagonal(), np.ones(n))
+    assert np.all(U.diagonal() != 0)
+    # ILU(1): (L U)_ij = a_ij on A's pattern up to rounding (a sample of rows)
+    rows = np.random.default_rng(3).choice(n, 2000, replace=False)
+    LU = (L[rows] @ U).tocsr()
+    Ar = A[rows].tocsr()
+    d = np.asarray(abs(LU - Ar).multiply(Ar != 0).max(axis=1).todense()).ravel()
+    scale = np.asarray(abs(Ar).max(axis=1).todense()).ravel()
+    assert np.all(d <= 1e-11 * scale)
+    # GMRES(30) + ILU(1) to 1e-10
+    solver.set_precond_iluk_device(1)
+    b = M.rhs_ones(A)
+    g = solver.solve(b, restart=30, max_iter=300, tol=1e-10)
+    assert g["ret"] == 0 and g["relres"] < 1e-10
+    h = g["hist"]
+    assert np.all(np.isfinite(h)) and h[0] == pytest.approx(1.0, rel=1e-12)
+    assert np.all(np.diff(h[: min(30, len(h))]) <= 1e-12)        # monotone inside the first cycle
+    solver.close()
+    r = b - A @ g["x"]
+    assert np.linalg.norm(r) / np.linalg.norm(b) < 1e-8
