@@ -124,6 +124,9 @@ Levels level_sets(const CanonTri &T);
 // steps per band are padded to a multiple of this (whole batches, an even
 // number of them for the two-deep boundary polls; kernels.hip checks it)
 constexpr int kWaveTAlign = 32;
+// 3D tiles: steps per tile padded to whole pairs of 8-step batches (k_trsv_tile3d)
+constexpr int kTileTAlign = 16;
+constexpr int kTileDummyBlocks = 2048;   // workgroups with their own dummy granules (grid cap)
 struct Wave2D {
     bool ok = false;
     int nx = 0, ny = 0, nz = 1, nbands = 0, T = 0;
@@ -135,10 +138,27 @@ struct Wave2D {
     int skew = 1;
     long long P2 = 0;        // one plane's layout length (nbands * T * 64)
     long long P = 0;         // padded layout length (nz * P2)
-    long long ngran() const { return (long long)nz * nbands * T; }   // hand-off granules
+    // 3D tile layout (tile = true; kernels.hip k_trsv_tile3d): a wave owns a
+    // tile of 16 lines x 4 planes, lane l = a + 16*row(c) for line j = 16J + a,
+    // plane k = 4K + c, row(c) = 0, 1, 3, 2 for c = 0..3 (so every plane's
+    // predecessor is one permlane swap away); point (i, j, k) at step
+    // t = i + a + 2c of its tile (a plane lags its predecessor by 2 steps, so
+    // the cross-row move is off the recurrence); tiles K-major (band = K*NJ +
+    // J), each stored as
+    // a 2D band of T steps (nbands = NJ * NK; nz stays the grid's plane count).
+    bool tile = false;
+    int NJ = 0, NK = 0;           // tiles along the line / plane directions
+    static constexpr int kTileGran = 20;   // hand-off values per step: 16 plane-edge + 4 line-edge
+    long long ngran() const { return tile ? (long long)nbands * T * kTileGran : (long long)nz * nbands * T; }
     long long slot(long long r) const {
         const long long nxy = (long long)nx * ny;
         const long long k = r / nxy, q = r % nxy;
+        if (tile) {
+            const int j = (int)(q / nx), i = (int)(q % nx), a = j & 15, c = (int)(k & 3);
+            const int l = a + 16 * (c < 2 ? c : 5 - c), t = i + a + 2 * c;
+            const long long band = (k >> 2) * NJ + (j >> 4);
+            return ((band * (T / 2) + t / 2) * 64 + l) * 2 + (t & 1);
+        }
         const int j = (int)(q / nx), i = (int)(q % nx), l = j & 63, t = i + skew * l + (skew - 1);
         return k * P2 + ((((long long)(j >> 6) * (T / 2) + t / 2) * 64 + l) * 2 + (t & 1));
     }
@@ -233,6 +253,7 @@ struct DevTri {
     DBuf<double> c0;             // 3D: |offset| = nx*ny coefficient
     DBuf<double> ce1, ce2;       // skew 2/3 (ILU(1)/(2) fill): |offset| = nx-1, nx-2 coefficients
     DBuf<unsigned long long> prog;   // 3D: per (plane, band) batches stored (0 between launches)
+    DBuf<int> order;             // 3D tiles: forward dependency order (the backward solve reverses it)
     int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
     bool rcp_ok = false;         // every divisor admits WD_RCP
     DBuf<unsigned long long> bnd;  // nbands * T hand-off granules (sentinel = not ready) + 128 dummies

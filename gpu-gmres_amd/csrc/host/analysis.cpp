@@ -9,6 +9,7 @@
 //  * level sets (replaces cusparse*csrsv_analysis, src/preconditioner.cu:1313-1316)
 //  * 2D structured-grid detection for the wavefront solve
 //  * CSR-stream row blocks for SpMV
+#include <cstdlib>
 #include <algorithm>
 #include <cmath>
 
@@ -199,6 +200,18 @@ Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U)
     w.nx = (int)nx;
     w.ny = (int)(nxy / nx);
     w.nz = (int)(n / nxy);
+    const char *pl = std::getenv("GG_WAVE3D_PLANES");     // the (plane, band) pipeline instead
+    if (!(pl && pl[0] == '1')) {
+        // 16-line x 4-plane tiles (Wave2D::slot); the lane skew is a + 2c <= 21 steps
+        w.tile = true;
+        w.NJ = (w.ny + 15) / 16;
+        w.NK = (w.nz + 3) / 4;
+        w.nbands = w.NJ * w.NK;
+        w.T = (w.nx + 21 + kTileTAlign - 1) / kTileTAlign * kTileTAlign;
+        w.P2 = (long long)w.nbands * w.T * 64;
+        w.P = w.P2;
+        return w;
+    }
     w.nbands = (w.ny + 63) / 64;
     w.T = (w.nx + 63 + kWaveTAlign - 1) / kWaveTAlign * kWaveTAlign;
     w.P2 = (long long)w.nbands * w.T * 64;

@@ -92,6 +92,7 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
 // ---- triangular solves ---------------------------------------------------------
 void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st);
 int wave_batch_steps(int div, bool d3 = false, int skew = 1);   // steps per batch of the wavefront kernel
+int tile_batch_steps();                                          // steps per batch of the 3D tile kernel
 
 // ---- GMRES scalar / MGS kernels ----------------------------------------------
 void launch_set_normb(const double *part, int G, DevState *ds, hipStream_t st);

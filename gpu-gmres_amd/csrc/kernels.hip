@@ -629,7 +629,8 @@ __device__ __forceinline__ bool rcp_safe(double v)
 
 // loader wave: batch j -> ring slot j % R; batch j landed by barrier j
 template <bool FWD, int R, int SLOT, int NA, int PBN, int SC1 = -1>
-__device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *lds, int np, int nbatch)
+__device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *lds, int np, int nbatch,
+                                            long long *tr = nullptr)
 {
     // array SC1 (a 3D grid's previous-plane x, written by another workgroup in
     // this launch) is read write-through coherent (sc1: cache policy 16)
@@ -662,6 +663,7 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
         // batch j must have landed; the ones after it may stay in flight
         const int issued = j + R - 1 < nbatch ? j + R - 1 : nbatch;
         vm_wait_batches<R - 2, NA * PBN>(issued - (j + 1));
+        if (tr && (threadIdx.x & 63) == 0) tr[j] = (long long)__builtin_amdgcn_s_memrealtime();   // diagnostics
         raw_barrier();                          // slot (j-1) % R is free from here on
         if (j + R - 1 < nbatch) issue(j + R - 1);
     }
@@ -1036,6 +1038,440 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 #pragma unroll
         for (int k = 0; k < 4; k++) tr[nbatch + 1 + k] = ph[k];
     }
+    }   // task loop
+}
+
+// ================================================ 3D 7-point grids: tile wavefront
+// Layout (gg_internal.h Wave2D, tile = true): one wave owns a tile of 16 lines
+// x 4 planes, lane l = a + 16 row(c) with row(c) = 0, 1, 3, 2 for planes
+// c = 0..3, and runs point (i, j, k) at step t = i + a + 2c.  Every term of a
+// row is then a recent value of a neighbouring lane: the in-line term the
+// lane's own previous step, the line term the previous step one lane down the
+// 16-lane row (DPP row_shr:1, backward row_shl:1; the row's edge lane takes
+// the neighbouring tile's value as the DPP `old`), the plane term the value of
+// TWO steps back in the predecessor plane's row -- rows 0 -> 1 and 3 -> 2 are
+// one v_permlane16_swap, 1 -> 3 one v_permlane32_swap (backward the reverse
+// moves), the first plane's row takes the neighbouring tile's value -- so the
+// swaps and selects (~90 cycles) run a step ahead, off the recurrence, whose
+// chain is the 2D one: DPP, multiply, two subtractions (and the division).  The dependency chain (nx + ny + nz - 2
+// steps) crosses a workgroup boundary every 16 lines and every 4 planes: 13 +
+// 53 hand-offs at 216^3 instead of 216 plane hand-offs through HBM, and no
+// previous-plane x is streamed.
+// Hand-off granules (8 B, value = flag, kSentinel = not ready, re-armed by the
+// consumer): per tile and step 20 words, [0, 16) the last plane's row for tile
+// (J, K +- 1), [16, 20) the four rows' edge lanes for tile (J +- 1, K).  The
+// consumer's step t needs the plane granules of step t +- 6 and the line
+// granules of step t +- 15 (same point i, skew a + 2c).
+// Roles as k_trsv_wave2d: wave 0 computes, 1 polls the granules, 2 stores x
+// and publishes, 3 streams b, c1, c2 (, d (, RN(1/d))), c0 into the LDS ring.
+// Persistent grid, every workgroup co-resident, tiles taken in dependency
+// order (host tile_order; the backward solve walks it from the end).
+#ifndef GG_TILE_BATCH
+#define GG_TILE_BATCH 8
+#endif
+template <int DIV>
+struct TileCfg {
+    static constexpr int A = DIV == WD_UNIT ? 4 : DIV == WD_HW ? 5 : 6;
+    static constexpr int AC0 = A - 1;                   // the plane coefficient streams last
+    static constexpr int B = GG_TILE_BATCH;
+    static constexpr int PBN = B / 2;
+    static constexpr int SLOT = A * PBN * 64;           // double2 per ring slot
+    static constexpr int NPER = A * PBN;                // DMA instructions per batch
+    static constexpr int NG = Wave2D::kTileGran;
+    static constexpr int GL = (B * NG + 63) / 64;       // granule loads (stores) per lane per batch
+    static constexpr int BND = 2 * PBN * 32;            // boundary values: double2 [2][PBN][32]
+    static constexpr int XST = 2 * PBN * 64;            // x staging: double2 [2][PBN][64]
+    static constexpr int RFIT = (150 * 1024 / 16 - BND - XST) / SLOT;
+    static constexpr int RVM = 2 + 63 / NPER;
+    static constexpr int R = kWaveRing < RFIT ? (kWaveRing < RVM ? kWaveRing : RVM) : (RFIT < RVM ? RFIT : RVM);
+    static constexpr int LDS2 = R * SLOT + BND + XST;
+    static constexpr int THREADS = 256;
+    static_assert(R >= 3 && (R - 2) * NPER <= 63, "ring depth vs vmcnt range");
+    static_assert(kTileTAlign % (B * GG_WAVE_POLL) == 0, "steps per tile: whole poll groups of batches");
+    static_assert(2 * GL * (GG_WAVE_POLL - 1) <= 63, "boundary wave vmcnt");
+    static_assert(kWaveLook >= 1 && kWaveLook <= PBN, "lookahead");
+    static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
+};
+
+// the plane predecessor's previous-step value (rows as in the layout comment);
+// the first plane's row takes kb.  Branch-free: per-lane masks of the rows
+// (precomputed) select with v_bfi_b32.
+__device__ __forceinline__ unsigned bfi(unsigned m, unsigned a, unsigned b) { return (a & m) | (b & ~m); }
+struct RowMasks {
+    unsigned m0, m1, m3, mhi;   // lane is in row 0 / 1 / 3 / in rows 2-3
+};
+template <bool FWD>
+__device__ __forceinline__ double plane_shift(double x, double kb, const RowMasks &rm)
+{
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const unsigned klo = (unsigned)__double2loint(kb), khi = (unsigned)__double2hiint(kb);
+    // (vdst, src) = p16(x, x): rows (x0, x0, x2, x2), (x1, x1, x3, x3)
+    // (vdst, src) = p32(x, x): rows (x0, x1, x0, x1), (x2, x3, x2, x3)
+    const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const auto l32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    unsigned rlo, rhi;
+    if constexpr (FWD) {    // row 0 <- kb, row 1 <- row 0, row 2 <- row 3, row 3 <- row 1
+        rlo = bfi(rm.mhi, bfi(rm.m3, l32[0], l16[1]), bfi(rm.m1, l16[0], klo));
+        rhi = bfi(rm.mhi, bfi(rm.m3, h32[0], h16[1]), bfi(rm.m1, h16[0], khi));
+    } else {                // row 0 <- row 1, row 1 <- row 3, row 2 <- kb, row 3 <- row 2
+        rlo = bfi(rm.mhi, bfi(rm.m3, l16[0], klo), bfi(rm.m0, l16[1], l32[1]));
+        rhi = bfi(rm.mhi, bfi(rm.m3, h16[0], khi), bfi(rm.m0, h16[1], h32[1]));
+    }
+    return __hiloint2double((int)rhi, (int)rlo);
+}
+
+// TRACE (diagnostics, gg_trace_precond): per tile 8 + 5 nbatch words -- compute
+// wave's start (barrier 0) and end (realtime, 10 ns), workgroup, boundary-wave
+// poll retries and cycles spent retrying, realtime after batch 0 and at the
+// loader's first issue; then per batch the compute wave's start, the writer's
+// publication, the boundary wave's "all values seen", the loader's "landed"
+// and the compute wave's end.
+// the same move through the LDS crossbar (ds_bpermute; GG_TILE_PLANE=2, a
+// measured alternative) -- GG_TILE_PLANE=1 skips the move (timing only, wrong
+// results)
+#ifndef GG_TILE_PLANE
+#define GG_TILE_PLANE 0
+#endif
+// boundary wave: barrier right after the values are in LDS (1), or after the
+// re-arm stores and the next polls are issued (0)
+#ifndef GG_TILE_EARLYBAR
+#define GG_TILE_EARLYBAR 1
+#endif
+// the first plane's row takes kb (after plane_move with any kb)
+template <bool FWD>
+__device__ __forceinline__ double plane_fix(double p, double kb, const RowMasks &rm)
+{
+    const unsigned m = FWD ? rm.m0 : (rm.mhi & ~rm.m3);
+    return __hiloint2double((int)bfi(m, (unsigned)__double2hiint(kb), (unsigned)__double2hiint(p)),
+                            (int)bfi(m, (unsigned)__double2loint(kb), (unsigned)__double2loint(p)));
+}
+template <bool FWD>
+__device__ __forceinline__ double plane_move(double x, double kb, const RowMasks &rm, int baddr)
+{
+    if constexpr (GG_TILE_PLANE == 0) {
+        return plane_shift<FWD>(x, kb, rm);
+    } else if constexpr (GG_TILE_PLANE == 1) {
+        return x + kb;
+    } else {
+        const int lo = __builtin_amdgcn_ds_bpermute(baddr, __double2loint(x));
+        const int hi = __builtin_amdgcn_ds_bpermute(baddr, __double2hiint(x));
+        const unsigned m = FWD ? rm.m0 : (rm.mhi & ~rm.m3);      // the first plane's row takes kb
+        return __hiloint2double((int)bfi(m, (unsigned)__double2hiint(kb), (unsigned)hi),
+                                (int)bfi(m, (unsigned)__double2loint(kb), (unsigned)lo));
+    }
+}
+
+template <bool FWD, int DIV, bool TRACE = false>
+__global__ __launch_bounds__(256) void k_trsv_tile3d(
+    Gate g, int T, int NJ, int NK, const int *__restrict__ order, const double *__restrict__ b,
+    const double *__restrict__ c1, const double *__restrict__ c2, const double *__restrict__ dv,
+    const double *__restrict__ rv, const double *__restrict__ c0, double *__restrict__ x,
+    unsigned long long *gran, int *err, long long *trace)
+{
+    using C = TileCfg<DIV>;
+    constexpr int PB = C::PBN * 64;             // double2 per array per slot
+    constexpr int NG = C::NG;
+    constexpr int GL = C::GL;
+    if (gated(g)) return;
+    __shared__ double2 lds[C::LDS2];
+    __shared__ int xdone;                       // batches the compute wave has staged (this workgroup)
+    double2 *bring = lds + C::R * C::SLOT;      // [2][PBN][32]: [0, 16) plane values, [16, 20) line values
+    double2 *xbuf = bring + C::BND;             // [2][PBN][64]
+    if (threadIdx.x == 0) xdone = 0;            // read only after the first barrier
+    int seq = 0;                                // batches this workgroup has run (uniform)
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int np = T / 2;
+    const int nbatch = T / C::B;                // T is a multiple of kTileTAlign
+    const long long TS = 8 + 5LL * nbatch;      // TRACE words per tile
+    const int ntask = NJ * NK;
+    const long long tgran = (long long)T * NG;  // granules per tile
+    // dummy granules of this workgroup (64 zeros to read, 64 write-only words):
+    // a line every boundary wave of the chip polled and re-armed would be a
+    // hot spot on one memory channel
+    unsigned long long *dummy_ld = gran + (long long)ntask * tgran + (long long)blockIdx.x * 128 + lane;
+    unsigned long long *dummy_st = dummy_ld + 64;
+    for (int task = blockIdx.x; task < ntask; task += gridDim.x) {
+    const int band = order[FWD ? task : ntask - 1 - task];
+    const int J = band % NJ, K = band / NJ;
+    const long long boff = (long long)band * np * 64 + lane;     // double2 units
+    if (wave == 3) {
+        // ------------------------------------------------ loader wave
+        const double2 *src[6] = {reinterpret_cast<const double2 *>(b) + boff,
+                                 reinterpret_cast<const double2 *>(c1) + boff,
+                                 reinterpret_cast<const double2 *>(c2) + boff,
+                                 reinterpret_cast<const double2 *>(dv) + boff,
+                                 reinterpret_cast<const double2 *>(rv) + boff, nullptr};
+        src[C::AC0] = reinterpret_cast<const double2 *>(c0) + boff;
+        if (TRACE && lane == 0) trace[(long long)band * TS + 6] = (long long)__builtin_amdgcn_s_memrealtime();
+        wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN>(src, lds, np, nbatch,
+                                                      TRACE ? trace + (long long)band * TS + 8 + 3 * nbatch : nullptr);
+        raw_barrier();                          // final barrier (the writer drains the last batch)
+        continue;
+    }
+    if (wave == 2) {
+        // ------------------------------------------------ writer wave
+        // Batch bi's edge values as granules, then x, as soon as the compute
+        // wave has staged the batch (LDS counter xdone), not at barrier bi+1:
+        // that barrier also waits for batch bi+1's boundary values, and a tile's
+        // sources must not hold back what it publishes.
+        double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
+        unsigned long long *gmine = gran + (long long)band * tgran;
+        const bool pub_k = FWD ? (K < NK - 1) : (K > 0);
+        const bool pub_j = FWD ? (J < NJ - 1) : (J > 0);
+        [[maybe_unused]] bool bad = false;
+        raw_barrier();                          // barrier 0
+        for (int pb = 0; pb < nbatch; pb++) {
+            // wait for the compute wave's counter (its x staging precedes it)
+            while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&xdone, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_WORKGROUP)) <= seq + pb)
+                __builtin_amdgcn_s_sleep(1);
+            const double2 *xb = xbuf + (pb & 1) * PB;
+#pragma unroll
+            for (int m = 0; m < GL; m++) {
+                const int e = lane + 64 * m;
+                const int tt = e / NG, idx = e - tt * NG;
+                if (e < C::B * NG && (idx < 16 ? pub_k : pub_j)) {
+                    // the last plane's row (forward: plane 3 = row 2; backward:
+                    // plane 0 = row 0), or a row's edge lane (a = 15 / a = 0)
+                    const int sl = idx < 16 ? (FWD ? 32 + idx : idx) : (FWD ? 15 : 0) + 16 * (idx - 16);
+                    const double v = reinterpret_cast<const double *>(xb + (tt >> 1) * 64 + sl)
+                        [FWD ? (tt & 1) : 1 - (tt & 1)];
+                    const int t = FWD ? pb * C::B + tt : (T - 1) - (pb * C::B + tt);
+                    st_agent(gmine + (long long)t * NG + idx, (unsigned long long)__double_as_longlong(v));
+                }
+            }
+            if (TRACE && lane == 0) trace[(long long)band * TS + 8 + nbatch + pb] = (long long)__builtin_amdgcn_s_memrealtime();
+            double2 v[C::PBN];
+#pragma unroll
+            for (int kk = 0; kk < C::PBN; kk++) v[kk] = xb[kk * 64 + lane];
+#pragma unroll
+            for (int kk = 0; kk < C::PBN; kk++) {
+                const int p = pb * C::PBN + kk;
+                X2[(long long)(FWD ? p : np - 1 - p) * 64] = v[kk];
+                if constexpr (DIV == WD_RCP) bad |= !rcp_safe(v[kk].x) || !rcp_safe(v[kk].y);
+            }
+            raw_barrier();                      // barrier pb+1 (the last one: the task's final barrier)
+        }
+        seq += nbatch;
+        if constexpr (DIV == WD_RCP) {
+            if (__any(bad) && lane == 0) atomicOr(err, 2);
+        }
+        continue;
+    }
+    if (wave == 1) {
+        // ------------------------------------------------ boundary wave
+        // Before barrier bi it places batch bi's boundary values in bring[bi & 1]:
+        // entry e = lane + 64 m of the batch is (step tt = e / NG, index e % NG).
+        // Polls run kPoll batches deep (GL loads per batch); every lane issues
+        // every load and store (unused ones on the dummy granules), which keeps
+        // the vmcnt arithmetic exact.
+        constexpr int kPoll = GG_WAVE_POLL;
+        const bool has_k = FWD ? (K > 0) : (K < NK - 1);
+        const bool has_j = FWD ? (J > 0) : (J < NJ - 1);
+        unsigned long long *gk = has_k ? gran + (long long)(FWD ? band - NJ : band + NJ) * tgran : gran;
+        unsigned long long *gj = has_j ? gran + (long long)(FWD ? band - 1 : band + 1) * tgran : gran;
+        auto gaddr = [&](int bj, int m) -> unsigned long long * {
+            const int e = lane + 64 * m;
+            const int tt = e / NG, idx = e - tt * NG;
+            if (e >= C::B * NG || bj >= nbatch) return nullptr;
+            const int t = FWD ? bj * C::B + tt : (T - 1) - (bj * C::B + tt);
+            const bool pl = idx < 16;
+            const int tp = pl ? (FWD ? t + 6 : t - 6) : (FWD ? t + 15 : t - 15);
+            if (!(pl ? has_k : has_j) || tp < 0 || tp >= T) return nullptr;
+            return (pl ? gk : gj) + (long long)tp * NG + idx;
+        };
+        auto paddr = [&](int bj, int m) {
+            unsigned long long *a = gaddr(bj, m);
+            return a ? a : dummy_ld;
+        };
+        unsigned long long v[kPoll][GL];
+#pragma unroll
+        for (int u = 0; u < kPoll; u++) {
+            if (u > 0) {
+#pragma unroll
+                for (int m = 0; m < GL; m++) st_agent(dummy_st, kSentinel);
+            }
+#pragma unroll
+            for (int m = 0; m < GL; m++) v[u][m] = ld_agent(paddr(u, m));
+        }
+        bool dead = false;
+        long long bw_spins = 0, bw_cyc = 0;     // TRACE
+        for (int bi0 = 0; bi0 < nbatch; bi0 += kPoll) {     // nbatch is a multiple of kPoll
+#pragma unroll
+            for (int u = 0; u < kPoll; u++) {
+                const int bi = bi0 + u;
+                // this batch's polls done: after them come kPoll-1 batches of
+                // GL re-arm stores and GL loads
+                __builtin_amdgcn_s_waitcnt(vm_wait(2 * GL * (kPoll - 1)));
+                int spins = 0;
+                const long long tw = TRACE ? (long long)__builtin_amdgcn_s_memtime() : 0;
+                auto ready = [&]() {
+                    bool r = true;
+#pragma unroll
+                    for (int m = 0; m < GL; m++) r = r && v[u][m] != kSentinel;
+                    return r;
+                };
+                while (!dead && !__all(ready())) {
+                    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                    for (int m = 0; m < GL; m++) v[u][m] = ld_agent(paddr(bi, m));
+                    if (++spins > kSpinLimit) {
+                        dead = true;
+                        if (lane == 0) atomicOr(err, 1);
+                    }
+                    __builtin_amdgcn_s_waitcnt(vm_wait(0));
+                }
+                if constexpr (TRACE) {
+                    bw_spins += spins;
+                    if (spins) bw_cyc += (long long)__builtin_amdgcn_s_memtime() - tw;
+                    if (lane == 0) trace[(long long)band * TS + 8 + 2 * nbatch + bi] = (long long)__builtin_amdgcn_s_memrealtime();
+                }
+                double *bd = reinterpret_cast<double *>(bring + (bi & 1) * (C::PBN * 32));
+#pragma unroll
+                for (int m = 0; m < GL; m++) {
+                    const int e = lane + 64 * m;
+                    const int tt = e / NG, idx = e - tt * NG;
+                    if (e < C::B * NG) bd[((tt >> 1) * 32 + idx) * 2 + (tt & 1)] = __longlong_as_double((long long)v[u][m]);
+                }
+                if constexpr (GG_TILE_EARLYBAR) {
+                    // hand the values over first, then re-arm and poll ahead
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    raw_barrier();
+                }
+#pragma unroll
+                for (int m = 0; m < GL; m++) {
+                    unsigned long long *ga = gaddr(bi, m);
+                    st_agent(ga ? ga : dummy_st, kSentinel);     // re-arm for the next launch
+                }
+#pragma unroll
+                for (int m = 0; m < GL; m++) v[u][m] = ld_agent(paddr(bi + kPoll, m));
+                if constexpr (!GG_TILE_EARLYBAR) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    raw_barrier();
+                }
+            }
+        }
+        raw_barrier();                      // final barrier (the writer drains the last batch)
+        if (TRACE && lane == 0) {
+            trace[(long long)band * TS + 3] = bw_spins;
+            trace[(long long)band * TS + 4] = bw_cyc;
+        }
+        continue;
+    }
+
+    // ---------------------------------------------------- compute wave
+    constexpr int ctrl = FWD ? 0x111 : 0x101;   // row_shr:1 / row_shl:1
+    const int row = lane >> 4;
+    const RowMasks rm{row == 0 ? ~0u : 0u, row == 1 ? ~0u : 0u, row == 3 ? ~0u : 0u, row >= 2 ? ~0u : 0u};
+    // ds_bpermute source lane: the predecessor plane's row (forward 0 -> 1 -> 3 -> 2)
+    const int prow = FWD ? (row == 1 ? 0 : row == 3 ? 1 : row == 2 ? 3 : 0) : (row == 0 ? 1 : row == 1 ? 3 : row == 3 ? 2 : 0);
+    const int baddr = ((lane & 15) + 16 * prow) * 4;
+    double xp = 0.0, xq = 0.0;              // this lane's values of the previous two steps
+    double2 rg[C::PBN][C::A];
+    raw_barrier();                          // barrier 0: batch 0 is in LDS
+    if (TRACE && lane == 0) {
+        trace[(long long)band * TS + 0] = (long long)__builtin_amdgcn_s_memrealtime();
+        trace[(long long)band * TS + 2] = blockIdx.x;
+    }
+    for (int bi = 0; bi < nbatch; bi++) {
+        // the first step's plane neighbour (two steps back) is moved before the
+        // barrier; only the first plane's row waits for the boundary value
+        const double xzp = plane_move<FWD>(xq, 0.0, rm, baddr);
+        if (bi > 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // x staging of batch bi-1 written
+            raw_barrier();                  // batch bi's data and boundary values
+            if (TRACE && bi == 1 && lane == 0) trace[(long long)band * TS + 5] = (long long)__builtin_amdgcn_s_memrealtime();
+        }
+        if (TRACE && lane == 0) trace[(long long)band * TS + 8 + bi] = (long long)__builtin_amdgcn_s_memrealtime();
+        const double2 *br = bring + (bi & 1) * (C::PBN * 32);
+        const double2 *sc = lds + (bi % C::R) * C::SLOT + lane;
+        double2 bk[C::PBN], bj[C::PBN];     // plane / line boundary values of each step pair
+        bk[0] = br[lane & 15];
+        bj[0] = br[16 + row];
+#pragma unroll
+        for (int a = 0; a < C::A; a++) rg[0][a] = sc[a * PB];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 1; kk < kWaveLook; kk++)
+#pragma unroll
+            for (int a = 0; a < C::A; a++) rg[kk][a] = sc[a * PB + kk * 64];
+#pragma unroll
+        for (int kk = 1; kk < C::PBN; kk++) {
+            bk[kk] = br[kk * 32 + (lane & 15)];
+            bj[kk] = br[kk * 32 + 16 + row];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        double xv[C::B];
+        // the plane neighbour's value for the batch's first step (two steps back)
+        double xzn = plane_fix<FWD>(xzp, bk[0].x, rm);
+#pragma unroll
+        for (int kk = 0; kk < C::PBN; kk++) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int tt = 2 * kk + h;
+                const bool sx = FWD ? (h == 0) : (h == 1);     // even storage step <-> .x
+                const double bb = sx ? rg[kk][0].x : rg[kk][0].y;
+                const double e1 = sx ? rg[kk][1].x : rg[kk][1].y;
+                const double e2 = sx ? rg[kk][2].x : rg[kk][2].y;
+                const double e0 = sx ? rg[kk][C::AC0].x : rg[kk][C::AC0].y;
+                const double oj = h ? bj[kk].y : bj[kk].x;      // boundary entries by sweep step
+                const double xz = xzn;
+                const double p2 = e2 * xp;
+                const double xs = dpp_shift_old<ctrl>(xp, oj);
+                // the next step's plane neighbour: this lane's row predecessor's
+                // value of the previous step (xp), moved while the chain runs
+                if (tt + 1 < C::B) xzn = plane_move<FWD>(xp, h ? bk[kk + 1].x : bk[kk].y, rm, baddr);
+                if constexpr (kWaveShadow) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (h == 0 && kk + kWaveLook < C::PBN) {
+#pragma unroll
+                        for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
+                    }
+                    if (h == 1 && kk > 0) {
+                        xbuf[(bi & 1) * PB + (kk - 1) * 64 + lane] =
+                            FWD ? make_double2(xv[2 * kk - 2], xv[2 * kk - 1])
+                                : make_double2(xv[2 * kk - 1], xv[2 * kk - 2]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                // canonical order: plane term, line term, in-line term
+                double acc = bb - e0 * xz;
+                acc = acc - e1 * xs;
+                acc = acc - p2;
+                if constexpr (DIV == WD_HW) {
+                    acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
+                } else if constexpr (DIV == WD_RCP) {
+                    const double d = sx ? rg[kk][3].x : rg[kk][3].y;
+                    const double y = sx ? rg[kk][4].x : rg[kk][4].y;
+                    const double q0 = acc * y;
+                    const double q1 = __builtin_fma(-__builtin_fma(q0, d, -acc), y, q0);
+                    acc = __builtin_fma(-__builtin_fma(q1, d, -acc), y, q1);
+                }
+                xq = xp;
+                xp = acc;
+                xv[tt] = acc;
+            }
+            if (!kWaveShadow || kk == C::PBN - 1)
+                xbuf[(bi & 1) * PB + kk * 64 + lane] =
+                    FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
+            if (!kWaveShadow && kk + kWaveLook < C::PBN) {
+#pragma unroll
+                for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // the batch's x staging, then the writer's counter
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (TRACE && lane == 0) trace[(long long)band * TS + 8 + 4 * nbatch + bi] = (long long)__builtin_amdgcn_s_memrealtime();
+        if (lane == 0) __hip_atomic_store(&xdone, seq + bi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    seq += nbatch;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();                          // final barrier: the writer drains the last batch
+    if (TRACE && lane == 0) trace[(long long)band * TS + 1] = (long long)__builtin_amdgcn_s_memrealtime();
     }   // task loop
 }
 
@@ -1974,6 +2410,24 @@ int wave3d_max_blocks()
     return cached;
 }
 
+template <bool FWD, int DIV>
+int tile3d_max_blocks()
+{
+    static int cached = -1;
+    if (cached < 0) {
+        int dev = 0, per = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_trsv_tile3d<FWD, DIV>, TileCfg<DIV>::THREADS, 0) !=
+            hipSuccess)
+            per = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        cached = std::max(1, per * cus);
+    }
+    return cached;
+}
+
+int tile_batch_steps() { return GG_TILE_BATCH; }
+
 int wave_batch_steps(int div, bool d3, int skew)
 {
     if (d3) return div == WD_UNIT ? WaveCfg<WD_UNIT, true>::B : div == WD_HW ? WaveCfg<WD_HW, true>::B
@@ -2032,7 +2486,32 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         const Wave2D &w = T.wl;
         const double *dv = T.div == WD_UNIT ? nullptr : T.dw.p;
         const double *rv = T.div == WD_RCP ? T.rw.p : nullptr;
-        if (w.nz == 1) {
+        if (w.tile) {
+            // 3D tiles: persistent, every workgroup co-resident (tiles wait on tiles)
+            const int ntask = w.nbands;
+#define GG_TILE_LAUNCH(FWD, DIV)                                                                   \
+    do {                                                                                           \
+        const int grid = std::min(std::min(ntask, tile3d_max_blocks<FWD, DIV>()), kTileDummyBlocks);  \
+        if (T.trace)                                                                               \
+            k_trsv_tile3d<FWD, DIV, true><<<grid, TileCfg<DIV>::THREADS, 0, st>>>(                 \
+                g, w.T, w.NJ, w.NK, T.order.p, b, T.c1.p, T.c2.p, dv, rv, T.c0.p, x, T.bnd.p, err,  \
+                T.trace);                                                                          \
+        else                                                                                       \
+            k_trsv_tile3d<FWD, DIV><<<grid, TileCfg<DIV>::THREADS, 0, st>>>(                       \
+                g, w.T, w.NJ, w.NK, T.order.p, b, T.c1.p, T.c2.p, dv, rv, T.c0.p, x, T.bnd.p, err,  \
+                nullptr);                                                                          \
+    } while (0)
+            if (T.lower) {
+                if (T.div == WD_UNIT) GG_TILE_LAUNCH(true, WD_UNIT);
+                else if (T.div == WD_HW) GG_TILE_LAUNCH(true, WD_HW);
+                else GG_TILE_LAUNCH(true, WD_RCP);
+            } else {
+                if (T.div == WD_UNIT) GG_TILE_LAUNCH(false, WD_UNIT);
+                else if (T.div == WD_HW) GG_TILE_LAUNCH(false, WD_HW);
+                else GG_TILE_LAUNCH(false, WD_RCP);
+            }
+#undef GG_TILE_LAUNCH
+        } else if (w.nz == 1) {
             dim3 grid(w.nbands);
 #define GG_WAVE_LAUNCH_S(FWD, DIV, S)                                                              \
     k_trsv_wave2d<FWD, DIV, false, false, S><<<grid, WaveCfg<DIV, false, S>::THREADS, 0, st>>>(    \

@@ -110,6 +110,23 @@ void DevCsr::copy_from(const DevCsr &o, hipStream_t st)
 
 long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
 
+// Tiles of a 3D layout in a forward dependency order: tile (J, K) waits on
+// (J-1, K) and (J, K-1), whose hand-offs lag it by about 3 and 2 batches
+// (k_trsv_tile3d), so tiles are taken by that expected start, 3J + 2K, then J.
+// Any order that lists a tile after both its sources keeps the persistent grid
+// deadlock-free (every workgroup takes its tiles in list order).
+std::vector<int> tile_order(const Wave2D &w)
+{
+    std::vector<int> ord(w.nbands);
+    for (int q = 0; q < w.nbands; q++) ord[q] = q;
+    auto key = [&](int q) { return 3LL * (q % w.NJ) + 2LL * (q / w.NJ); };
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+        const long long ka = key(a), kb = key(b);
+        return ka != kb ? ka < kb : (a % w.NJ) < (b % w.NJ);
+    });
+    return ord;
+}
+
 // Build a device triangular solve from a canonical triangle.  WAVE2D when a
 // grid layout is active, else LEVEL (one launch per dependency level).
 void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector<long long> *nat2lay,
@@ -149,11 +166,12 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         T.c2.upload(c2, st);
         if (K >= 1) T.ce1.upload(ce1, st);
         if (K >= 2) T.ce2.upload(ce2, st);
-        if (d3) {
-            T.c0.upload(c0, st);
+        if (d3) T.c0.upload(c0, st);
+        if (d3 && !wl->tile) {
             T.prog.alloc((size_t)wl->nz * wl->nbands);
             GG_HIP(hipMemsetAsync(T.prog.p, 0, T.prog.n * sizeof(unsigned long long), st));
         }
+        if (wl->tile) T.order.upload(tile_order(*wl), st);
         T.rcp_ok = false;
         if (unit) {
             T.div = WD_UNIT;
@@ -166,12 +184,14 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         }
         // one hand-off granule per band and step, then 64 zero granules (dummy
         // reads) and 64 write-only ones (dummy re-arms); kernels.hip k_trsv_wave2d
+        // (3D tiles: 128 dummy words per workgroup, kTileDummyBlocks of them)
         const long long ngran = wl->ngran();
-        T.bnd.alloc((size_t)ngran + 128);
+        const long long ndummy = wl->tile ? 128LL * kTileDummyBlocks : 128;
+        T.bnd.alloc((size_t)(ngran + ndummy));
         launch_fill_u64(T.bnd.p, ngran, kSentinel, st);
-        launch_fill_u64(T.bnd.p + ngran, 128, 0ull, st);
+        launch_fill_u64(T.bnd.p + ngran, ndummy, 0ull, st);
         // algorithmic bytes: b, two coefficients, (divisor (, reciprocal)), x per grid point
-        T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? 2 : 0) + K));
+        T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
     } else {
         T.kind = DevTri::LEVEL;
         T.off.upload(C.off, st);
@@ -1528,12 +1548,13 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     GG_REQUIRE(s && out && nbands && nbatch && (which == 0 || which == 1), GG_EINVAL, "bad argument");
     GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner");
     DevTri &T = which == 0 ? s->L : s->U;
-    GG_REQUIRE(T.kind == DevTri::WAVE2D && T.wl.nz == 1 && T.wl.skew == 1, GG_ESTATE,
-               "unskewed 2D wavefront path not active");
+    GG_REQUIRE(T.kind == DevTri::WAVE2D && ((T.wl.nz == 1 && T.wl.skew == 1) || T.wl.tile), GG_ESTATE,
+               "unskewed 2D or 3D tile wavefront path not active");
     set_device(s);
     ensure_workspace(s, std::max(s->m_alloc, 1));
-    const int nb = T.wl.nbands, nbt = T.wl.T / wave_batch_steps(T.div);
-    const long long need = (long long)nb * (3 * nbt + 8);
+    // per band (2D) 3 nbatch + 8 words, per tile (3D tiles, k_trsv_tile3d) 5 nbatch + 8
+    const int nb = T.wl.nbands, nbt = T.wl.tile ? T.wl.T / tile_batch_steps() : T.wl.T / wave_batch_steps(T.div);
+    const long long need = (long long)nb * ((T.wl.tile ? 5 : 3) * nbt + 8);
     GG_REQUIRE(cap >= need, GG_EINVAL, "trace buffer too small");
     DBuf<long long> buf;
     buf.alloc((size_t)need);

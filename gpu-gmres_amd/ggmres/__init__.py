@@ -380,6 +380,21 @@ class Solver:
         a = np.ctypeslib.as_array(buf)[: nb.value * (3 * nbt.value + 8)].copy()
         return a.reshape(nb.value, 3 * nbt.value + 8)
 
+    def trace_tiles(self, which=0):
+        """3D tile wavefront (k_trsv_tile3d) diagnostics of one triangular solve:
+        array [tiles, 8 + 5 nbatch] per tile (band = K*NJ + J): compute start /
+        end (100 MHz realtime), workgroup, boundary poll retries, retry cycles,
+        realtime after batch 0, loader start; per batch: compute start, writer
+        publication, boundary values seen, loader landed, compute end."""
+        import numpy as np
+        cap = 1 << 22
+        buf = (ctypes.c_longlong * cap)()
+        nb, nbt = ctypes.c_int(), ctypes.c_int()
+        _check(lib().gg_trace_precond(self.h, int(which), buf, cap, ctypes.byref(nb),
+                                      ctypes.byref(nbt)))
+        w = 8 + 5 * nbt.value
+        return np.ctypeslib.as_array(buf)[: nb.value * w].copy().reshape(nb.value, w)
+
     def time_precond(self, reps=20):
         ms = ctypes.c_double()
         _check(lib().gg_time_precond(self.h, int(reps), ctypes.byref(ms)))
