@@ -819,7 +819,8 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
         // it (up to bi + R - 1); its word is never re-armed here, but reset to
         // 0 when this task is done (the producer has finished by then).
         unsigned long long *src = bnd + ((long long)kp * nbands + (FWD ? band - 1 : band + 1)) * T;
-        unsigned long long *dummy_ld = bnd + (long long)nz * nbands * T + lane;
+        // this workgroup's dummy granules (64 zeros to read, 64 write-only words)
+        unsigned long long *dummy_ld = bnd + (long long)nz * nbands * T + (long long)blockIdx.x * 128 + lane;
         unsigned long long *dummy_st = dummy_ld + 64;
         constexpr int kProgLane = 32;
         const bool prog_lane = has_prev && lane == kProgLane;
@@ -2546,7 +2547,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
             const int ntask = w.nz * w.nbands;
 #define GG_WAVE_LAUNCH3(FWD, DIV)                                                                  \
     do {                                                                                           \
-        const int grid = std::min(ntask, wave3d_max_blocks<FWD, DIV>());                           \
+        const int grid = std::min(std::min(ntask, wave3d_max_blocks<FWD, DIV>()), kTileDummyBlocks); \
         k_trsv_wave2d<FWD, DIV, false, true><<<grid, WaveCfg<DIV, true>::THREADS, 0, st>>>(        \
             g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, w.nz, w.P2,      \
             T.c0.p, T.prog.p, nullptr, nullptr);                                                   \

@@ -182,11 +182,12 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
             if (T.rcp_ok) T.rw.upload(rv, st);
             T.div = T.rcp_ok ? WD_RCP : WD_HW;
         }
-        // one hand-off granule per band and step, then 64 zero granules (dummy
-        // reads) and 64 write-only ones (dummy re-arms); kernels.hip k_trsv_wave2d
-        // (3D tiles: 128 dummy words per workgroup, kTileDummyBlocks of them)
+        // one hand-off granule per band (tile) and step, then per workgroup 64
+        // zero granules (dummy reads) and 64 write-only ones (dummy re-arms),
+        // for up to kTileDummyBlocks workgroups: one line that every boundary
+        // wave polled and re-armed would be a hot spot on one memory channel
         const long long ngran = wl->ngran();
-        const long long ndummy = wl->tile ? 128LL * kTileDummyBlocks : 128;
+        const long long ndummy = 128LL * kTileDummyBlocks;
         T.bnd.alloc((size_t)(ngran + ndummy));
         launch_fill_u64(T.bnd.p, ngran, kSentinel, st);
         launch_fill_u64(T.bnd.p + ngran, ndummy, 0ull, st);
