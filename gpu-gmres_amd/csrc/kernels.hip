@@ -550,6 +550,18 @@ constexpr int kWaveRing = GG_WAVE_RING;
 #define GG_WAVE_LOADERS 1
 #endif
 constexpr int kWaveLoaders = GG_WAVE_LOADERS;
+// the writer publishes a batch when the compute wave has staged it (1) or after
+// the next batch's barrier (0); the boundary wave passes the barrier before (1)
+// or after (0) its re-arm store and look-ahead poll.  Measured on C2 (U solve):
+// 0/0 120.4 us, early barrier 123.8, decoupled 191-194 (the writer's LDS polls
+// slow the compute wave's LDS traffic) -- so 0/0 for the 2D kernel, while the
+// 3D tile kernel, whose bands wait on two sources, gains from both.
+#ifndef GG_WAVE_DECOUPLE
+#define GG_WAVE_DECOUPLE 0
+#endif
+#ifndef GG_WAVE_EARLYBAR
+#define GG_WAVE_EARLYBAR 0
+#endif
 
 template <int DIV, bool D3 = false, int S = 1>
 struct WaveCfg {
@@ -685,8 +697,11 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     // one LDS object: data ring [R][A][C::PBN][64] double2, 2 x 64 boundary values
     // (lanes 0..C::B-1 of each half are used), x staging [2][C::PBN][64]
     __shared__ double2 lds[C::LDS2];
+    __shared__ int xdone;                       // batches the compute wave has staged (GG_WAVE_DECOUPLE)
     double *bring = reinterpret_cast<double *>(lds + C::R * C::SLOT);
     double2 *xbuf = lds + C::R * C::SLOT + 64;
+    if (threadIdx.x == 0) xdone = 0;            // read only after the first barrier
+    int seq = 0;                                // batches this workgroup has run (uniform)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int np = T / 2;                       // step pairs per band
@@ -757,12 +772,21 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
         // 3D: x is stored write-through (sc1) and, once a batch's stores have
         // drained (checked one batch later, off the critical path), counted in
         // prog_mine for the next plane.
+        // GG_WAVE_DECOUPLE: batch bi is published as soon as the compute wave
+        // has staged it (LDS counter xdone), not after barrier bi+1, which
+        // also waits for this band's boundary values of batch bi+1: a band's
+        // upstream must not hold back what it hands downstream.
         double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
         [[maybe_unused]] bool bad = false;  // WD_RCP range guard (see rcp_safe)
         for (int bi = 0; bi <= nbatch; bi++) {
-            raw_barrier();
+            if (!GG_WAVE_DECOUPLE || bi == 0) raw_barrier();
             if (bi == 0) continue;
             const int pb = bi - 1;
+            if constexpr (GG_WAVE_DECOUPLE) {
+                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&xdone, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) <= seq + pb)
+                    __builtin_amdgcn_s_sleep(1);
+            }
             if constexpr (D3) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // batches < pb stored
                 if (lane == 0 && pb > 0) st_agent(prog_mine, (unsigned long long)pb);
@@ -793,7 +817,9 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
             if (TRACE && lane == 0)
                 trace[(long long)band * (3 * nbatch + 8) + nbatch + 8 + pb] =
                     (long long)__builtin_amdgcn_s_memrealtime();
+            if constexpr (GG_WAVE_DECOUPLE) raw_barrier();     // barrier bi (the last: the final one)
         }
+        seq += nbatch;
         if constexpr (D3) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) st_agent(prog_mine, (unsigned long long)nbatch);
@@ -875,10 +901,17 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                             (long long)__builtin_amdgcn_s_memrealtime();
                 }
                 bring[(bi & 1) * 64 + lane] = __longlong_as_double((long long)v[u]);
+                if constexpr (GG_WAVE_EARLYBAR) {
+                    // hand the values over first, then re-arm and poll ahead
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    raw_barrier();
+                }
                 st_agent(ga ? ga : dummy_st, kSentinel);       // re-arm for the next launch
                 v[u] = ld_agent(poll_addr(bi + kPoll));
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                raw_barrier();
+                if constexpr (!GG_WAVE_EARLYBAR) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    raw_barrier();
+                }
             }
         }
         raw_barrier();                      // final barrier (the writer drains the last batch)
@@ -1031,7 +1064,12 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (GG_WAVE_DECOUPLE) {       // the batch's x staging, then the writer's counter
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(&xdone, seq + bi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
+    seq += nbatch;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();                          // final barrier: the writer drains the last batch
     if (TRACE && lane == 0) {
@@ -1140,6 +1178,14 @@ __device__ __forceinline__ double plane_shift(double x, double kb, const RowMask
 #ifndef GG_TILE_EARLYBAR
 #define GG_TILE_EARLYBAR 1
 #endif
+// writer: publish when the compute wave has staged the batch (1) or at the next
+// barrier (0); GG_TILE_WSLEEP: s_sleep between its LDS counter polls
+#ifndef GG_TILE_DECOUPLE
+#define GG_TILE_DECOUPLE 1
+#endif
+#ifndef GG_TILE_WSLEEP
+#define GG_TILE_WSLEEP 1
+#endif
 // the first plane's row takes kb (after plane_move with any kb)
 template <bool FWD>
 __device__ __forceinline__ double plane_fix(double p, double kb, const RowMasks &rm)
@@ -1225,10 +1271,14 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
         [[maybe_unused]] bool bad = false;
         raw_barrier();                          // barrier 0
         for (int pb = 0; pb < nbatch; pb++) {
-            // wait for the compute wave's counter (its x staging precedes it)
-            while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&xdone, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_WORKGROUP)) <= seq + pb)
-                __builtin_amdgcn_s_sleep(1);
+            if constexpr (GG_TILE_DECOUPLE) {
+                // wait for the compute wave's counter (its x staging precedes it)
+                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&xdone, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) <= seq + pb)
+                    __builtin_amdgcn_s_sleep(GG_TILE_WSLEEP);
+            } else {
+                raw_barrier();                  // barrier pb+1
+            }
             const double2 *xb = xbuf + (pb & 1) * PB;
 #pragma unroll
             for (int m = 0; m < GL; m++) {
@@ -1254,7 +1304,7 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                 X2[(long long)(FWD ? p : np - 1 - p) * 64] = v[kk];
                 if constexpr (DIV == WD_RCP) bad |= !rcp_safe(v[kk].x) || !rcp_safe(v[kk].y);
             }
-            raw_barrier();                      // barrier pb+1 (the last one: the task's final barrier)
+            if constexpr (GG_TILE_DECOUPLE) raw_barrier();   // barrier pb+1 (the last: the task's final one)
         }
         seq += nbatch;
         if constexpr (DIV == WD_RCP) {
@@ -1467,7 +1517,8 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
         // the batch's x staging, then the writer's counter
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (TRACE && lane == 0) trace[(long long)band * TS + 8 + 4 * nbatch + bi] = (long long)__builtin_amdgcn_s_memrealtime();
-        if (lane == 0) __hip_atomic_store(&xdone, seq + bi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (GG_TILE_DECOUPLE && lane == 0)
+            __hip_atomic_store(&xdone, seq + bi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     seq += nbatch;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
