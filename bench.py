@@ -379,6 +379,10 @@ def main():
                 KERNEL_NAMES[dom_] = KERNEL_NAMES[dom_][:-2] + f"{kilu + 1}>"
     else:
         s.set_precond_ilu0()
+        if c4 and os.environ.get("GG_WAVE3D_PLANES") != "1" and s.uses_wavefront:
+            # 3D 7-point: the 16-line x 4-plane tile wavefront (kernels.hip k_trsv_tile3d)
+            KERNEL_NAMES["trsv_L"] = "k_trsv_tile3d<true, 0, false>"
+            KERNEL_NAMES["trsv_U"] = "k_trsv_tile3d<false, 2, false>"
     t_setup = time.perf_counter() - t_setup
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -517,18 +521,19 @@ def main():
         roof = {"kernel": kname, "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(KERNEL_NAMES[dom]) if (s.uses_wavefront or dom == "spmv") and not c4 and not c3s
-                and not kilu
-                else None,
+                "traffic": (pmc_traffic(KERNEL_NAMES[dom], "c4") if c4 else pmc_traffic(KERNEL_NAMES[dom]))
+                if (s.uses_wavefront or dom == "spmv") and not c3s and not kilu else None,
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
                 "launches_timed": f["launches"]}
     # the triangular solves are latency-bound: their other roofline is the
     # dependency chain, nx + ny - 1 wavefront steps at the bare per-step chain
     # latency (tools/lat_probe.hip on MI355X, profiles/r01_lat_probe.txt)
     lat = None
-    if roof and dom in ("trsv_L", "trsv_U") and s.uses_wavefront and not c4 and not c5:
+    if roof and dom in ("trsv_L", "trsv_U") and s.uses_wavefront and not c5:
         cyc = CHAIN_CYCLES["trsv_L" if dom == "trsv_L" else "trsv_U"]
-        steps = a.grid + (kilu + 1) * (a.grid - 1)    # the DAG's longest path (ILU(k): skew k+1)
+        # the DAG's longest path (ILU(k): skew k+1; 3D: nx + ny + nz - 2, whose
+        # per-step chain is the 2D one: the tile kernel's plane term is off it)
+        steps = 3 * a.c4_grid - 2 if c4 else a.grid + (kilu + 1) * (a.grid - 1)
         floor_us = steps * cyc / (SHADER_GHZ * 1e3)
         lat = {"kernel": roof["kernel"], "bound": "dependency chain", "critical_steps": steps,
                "cycles_per_step": cyc, "clock_ghz": SHADER_GHZ, "floor_us": round(floor_us, 2),
