@@ -121,6 +121,12 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             long long ldv, double *H, double *cs, double *sn, double *s,
                             double *hist, unsigned long long *gran, int G, long long Ppad, int *err,
                             hipStream_t st);
+// the same for long vectors (w on chip, the basis streamed): kWideG blocks
+constexpr int kWideG = 512;
+bool arnoldi_wide_ok(int G, long long Ppad);
+void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, double *V, long long ldv,
+                         double *H, double *cs, double *sn, double *s, double *hist,
+                         unsigned long long *gran, int G, long long Ppad, int *err, hipStream_t st);
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
                    const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st);
 void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st);

@@ -2192,6 +2192,132 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     }
 }
 
+// k_arnoldi_wide -- the same inner iteration for vectors too long for
+// k_arnoldi_persist's registers (C4: 11.6M slots): only w stays on chip (kWideJR
+// units per thread in registers, kWideJL in LDS), v_k and v_{k+1} are streamed
+// (non-temporal) at every step, kWideD units ahead of their use -- 16 B per
+// slot and step against the per-step kernels' 32 (w read and written).  Same
+// reduction tree as k_dot / k_mgs_step (G blocks of 256 threads, grid-stride
+// units, per thread ascending j, block_sum, G partials summed in sum_partials
+// order), so it is bit-identical to the per-step path.  Needs every block
+// co-resident (host: kWideG blocks, two per CU).
+constexpr int kWideJR = 40, kWideJL = 5, kWideD = 8;
+__global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m, DevState *ds,
+                                                            const double *__restrict__ w_in,
+                                                            double *__restrict__ V, long long ldv,
+                                                            double *H, double *cs, double *sn,
+                                                            double *s, double *hist,
+                                                            unsigned long long *gran, long long units,
+                                                            int *err)
+{
+    constexpr int J = kWideJR + kWideJL;
+    if (gated(g)) return;
+    __shared__ double2 wl[kWideJL * kBlock];
+    const int G = gridDim.x;
+    const int stride = G * kBlock;                      // units (vectors < 2^31 units: host check)
+    const int u0 = blockIdx.x * kBlock + threadIdx.x;
+    // this thread's units u0 + j stride, j < nval
+    const int nval = units > u0 ? (int)((units - u0 + stride - 1) / stride) : 0;
+    double2 wr[kWideJR];
+    auto wget = [&](int j) -> double2 { return j < kWideJR ? wr[j] : wl[(j - kWideJR) * kBlock + threadIdx.x]; };
+    auto wset = [&](int j, double2 v) {
+        if (j < kWideJR) wr[j] = v;
+        else wl[(j - kWideJR) * kBlock + threadIdx.x] = v;
+    };
+    auto publish = [&](int k, double acc) {
+        acc = block_sum(acc);
+        if (threadIdx.x == 0) st_agent(gran + (long long)k * G + blockIdx.x, (unsigned long long)__double_as_longlong(acc));
+    };
+    // streaming ring: slot j % kWideD holds unit j's v_k (and v_{k+1}).  The
+    // unit offsets are recomputed in every step from a laundered base (not
+    // hoisted: 45 live offsets would not fit beside w)
+    double2 pk[kWideD], pn[kWideD];
+    auto fetch = [&](int j, int ub, const double2 *vkp, const double2 *vnp) {
+        if (j < J && j < nval) {
+            pk[j % kWideD] = vkp[ub + j * stride];
+            if (vnp) pn[j % kWideD] = vnp[ub + j * stride];
+        }
+    };
+    auto vec = [&](const double *p) { return reinterpret_cast<const double2 *>(p); };
+    double acc = 0.0;
+    {
+        int ub = u0;
+        asm volatile("" : "+v"(ub));
+#pragma unroll
+        for (int j = 0; j < kWideD; j++) fetch(j, ub, vec(V), nullptr);
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (j < nval) {
+                const double2 wv = vec(w_in)[ub + j * stride];
+                wset(j, wv);
+                const double2 v0 = pk[j % kWideD];
+                acc += wv.x * v0.x;
+                acc += wv.y * v0.y;
+            }
+            fetch(j + kWideD, ub, vec(V), nullptr);
+        }
+    }
+    publish(0, acc);                                          // <w, v_0>
+    for (int k = 0; k <= i; k++) {
+        const double2 *vkp = vec(V + (long long)k * ldv);
+        const double2 *vnp = (k < i) ? vec(V + (long long)(k + 1) * ldv) : nullptr;
+        int ub = u0;
+        asm volatile("" : "+v"(ub));
+#pragma unroll
+        for (int j = 0; j < kWideD; j++) fetch(j, ub, vkp, vnp);    // in flight during the sum
+        const double h = gather_sum(gran + (long long)k * G, G, err);
+        if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
+        const double a = -h;
+        acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (j < nval) {
+                double2 wv = wget(j);
+                const double2 vk = pk[j % kWideD];
+                wv.x = a * vk.x + wv.x;
+                wv.y = a * vk.y + wv.y;
+                wset(j, wv);
+                const double2 o = vnp ? pn[j % kWideD] : wv;    // next dot: v_{k+1}, or the norm
+                acc += wv.x * o.x;
+                acc += wv.y * o.y;
+            }
+            fetch(j + kWideD, ub, vkp, vnp);
+        }
+        publish(k + 1, acc);
+    }
+    const double hn = sqrt(gather_sum(gran + (long long)(i + 1) * G, G, err));
+    if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
+        const int ld = m + 1;
+        double *Hc = H + i * ld;
+        Hc[i + 1] = hn;
+        for (int k = 0; k < i; k++) apply_rot(Hc[k], Hc[k + 1], cs[k], sn[k]);
+        double c, sv;
+        gen_rot(Hc[i], Hc[i + 1], c, sv);
+        cs[i] = c;
+        sn[i] = sv;
+        apply_rot(Hc[i], Hc[i + 1], c, sv);
+        apply_rot(s[i], s[i + 1], c, sv);
+        const double resid = fabs(s[i + 1]) / ds->normb;
+        hist[ds->hist_len + i] = resid;
+        ds->resid = resid;
+        if (resid < ds->tol) {
+            ds->conv_i = i;
+            ds->done = DONE_INNER;
+        }
+    }
+    const double inv = (hn != 0.0) ? 1.0 / hn : 0.0;
+    double2 *vout = reinterpret_cast<double2 *>(V + (long long)(i + 1) * ldv);
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        if (j < nval) {
+            double2 a = wget(j);
+            a.x = inv * a.x;
+            a.y = inv * a.y;
+            vout[u0 + j * stride] = a;
+        }
+    }
+}
+
 // y = H(0:k,0:k)^-1 s(0:k)  (Update, src/gmres.cu:93-116); k = conv_i or nit-1.
 // One wave: lane j keeps y[j] and row j of H in registers; for i = k..0 lane i
 // divides, the value is broadcast, lanes j < i subtract -- per element the same
@@ -2293,6 +2419,10 @@ inline int blocks_for(long long n, int bs = kBlock, int cap = 65535)
 // ======================================================= host launchers
 int reduce_grid(long long units)
 {
+    // vectors too long for k_arnoldi_persist's registers at 1024 blocks (more
+    // than 8 units per thread) reduce over kWideG blocks, two per CU, so that
+    // k_arnoldi_wide can keep w on chip with the same tree
+    if (units > (long long)1024 * kBlock * 8) return kWideG;
     long long g = (units + kBlock * 4 - 1) / (kBlock * 4);   // >= 8 elements / thread
     if (g < 1) g = 1;
     if (g > 1024) g = 1024;
@@ -2675,6 +2805,30 @@ int arnoldi_persist_max_blocks()
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_arnoldi_persist<8>, kBlock, 0) != hipSuccess)
         return 0;
     return cus * per;
+}
+
+// k_arnoldi_wide: usable when G = kWideG blocks of kWideJR + kWideJL units per
+// thread cover the vectors and every block is co-resident
+bool arnoldi_wide_ok(int G, long long Ppad)
+{
+    static int maxb = -1;
+    if (maxb < 0) {
+        int dev = 0, cus = 0, per = 0;
+        maxb = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_arnoldi_wide, kBlock, 0) == hipSuccess)
+            maxb = cus * per;
+    }
+    const long long units = Ppad / 2;
+    return G == kWideG && G <= maxb && units <= (long long)G * kBlock * (kWideJR + kWideJL) && units < (1LL << 31);
+}
+
+void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, double *V, long long ldv,
+                         double *H, double *cs, double *sn, double *s, double *hist,
+                         unsigned long long *gran, int G, long long Ppad, int *err, hipStream_t st)
+{
+    k_arnoldi_wide<<<G, kBlock, 0, st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, Ppad / 2, err);
 }
 
 void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,

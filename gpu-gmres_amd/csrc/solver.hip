@@ -260,6 +260,7 @@ struct gg_solver {
     DBuf<double> partA, partB, H, s, cs, sn, ysm;
     // persistent Arnoldi orthogonalization (kernels.hip k_arnoldi_persist)
     bool persist = false;
+    bool wide = false;                  // k_arnoldi_wide (vectors beyond persist's registers)
     bool shared = false;                // GG_SOLVE_SHARED_DEVICE for the solve in progress
     // pinned host copies of the control block and the error word (one
     // round trip per restart cycle reads both)
@@ -393,9 +394,10 @@ void ensure_workspace(gg_solver *s, int m)
     s->partB.alloc(1024);
     {
         const char *e = std::getenv("GG_NO_PERSIST");
-        s->persist = !(e && e[0] == '1') && arnoldi_persist_units(s->G, s->Ppad) != 0 &&
-                     s->G <= arnoldi_persist_max_blocks();
-        if (s->persist) s->gran.alloc((size_t)m * (m + 2) * s->G);
+        const bool off = e && e[0] == '1';
+        s->persist = !off && arnoldi_persist_units(s->G, s->Ppad) != 0 && s->G <= arnoldi_persist_max_blocks();
+        s->wide = !off && !s->persist && arnoldi_wide_ok(s->G, s->Ppad);   // long vectors: w on chip
+        if (s->persist || s->wide) s->gran.alloc((size_t)m * (m + 2) * s->G);
     }
     s->H.alloc((size_t)(m + 1) * m);
     GG_HIP(hipMemsetAsync(s->H.p, 0, (size_t)(m + 1) * m * sizeof(double), s->st));
@@ -520,7 +522,8 @@ void enqueue_cycle(gg_solver *s, int m)
     const bool split = s->pkind == GG_PRECOND_SPLIT;
     launch_init_cycle(ds, s->r.p, s->V.p, s->s.p, s->G, P, s->st);
     const bool persist = s->persist && !s->shared;
-    if (persist) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
+    const bool wide = s->wide && !s->shared;
+    if (persist || wide) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
     for (int i = 0; i < m; i++) {
         Gate gi;
         gi.done = &ds->done;
@@ -550,6 +553,10 @@ void enqueue_cycle(gg_solver *s, int m)
             launch_arnoldi_persist(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                    s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, s->G, P,
                                    s->err.p, s->st);
+        } else if (wide) {
+            launch_arnoldi_wide(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
+                                s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, s->G, P, s->err.p,
+                                s->st);
         } else {
             double *pin = s->partA.p, *pout = s->partB.p;
             launch_dot(gi, s->w.p, s->V.p, pin, s->G, P, s->st);               // <w, v_0>

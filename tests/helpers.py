@@ -62,7 +62,7 @@ def device_layout(n, nx=None, ny=None, skew=1):
     grid of line length nx on the wavefront path -- band = j//64, lane l = j%64,
     step t = i + skew*l + skew-1, slot ((band*T/2 + t//2)*64 + l)*2 + t%2 with
     T = roundup(nx + 63*skew + 2*(skew-1), 32) (skew = k+1 for ILU(k) factors
-    of a 5-point grid); for a 3D grid (ny given) 16-line x 4-plane tiles; padded to a multiple of 512 slots; G = min(1024, ceil(Ppad/2 / 1024))
+    of a 5-point grid); for a 3D grid (ny given) 16-line x 4-plane tiles; padded to a multiple of 512 slots; G = min(1024, ceil(Ppad/2 / 1024)), or 512 beyond 2M units
     reduction blocks."""
     if nx is None:
         P = n
@@ -102,5 +102,6 @@ def device_layout(n, nx=None, ny=None, skew=1):
     lay2nat = np.full(ppad, -1, np.int64)
     lay2nat[slots] = np.arange(n, dtype=np.int64)
     units = ppad // 2
-    G = min(1024, max(1, (units + 1023) // 1024))
+    # kernels.hip reduce_grid: beyond 8 units per thread at 1024 blocks, kWideG = 512
+    G = 512 if units > 1024 * 256 * 8 else min(1024, max(1, (units + 1023) // 1024))
     return lay2nat, G
