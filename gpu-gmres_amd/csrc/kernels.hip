@@ -1128,7 +1128,7 @@ struct TileCfg {
     static_assert(R >= 3 && (R - 2) * NPER <= 63, "ring depth vs vmcnt range");
     static_assert(kTileTAlign % (B * GG_WAVE_POLL) == 0, "steps per tile: whole poll groups of batches");
     static_assert(2 * GL * (GG_WAVE_POLL - 1) <= 63, "boundary wave vmcnt");
-    static_assert(kWaveLook >= 1 && kWaveLook <= PBN, "lookahead");
+    static constexpr int LOOK = kWaveLook < PBN ? kWaveLook : PBN;   // look-ahead pairs
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
 };
 
@@ -1446,7 +1446,7 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
         for (int a = 0; a < C::A; a++) rg[0][a] = sc[a * PB];
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kk = 1; kk < kWaveLook; kk++)
+        for (int kk = 1; kk < C::LOOK; kk++)
 #pragma unroll
             for (int a = 0; a < C::A; a++) rg[kk][a] = sc[a * PB + kk * 64];
 #pragma unroll
@@ -1477,9 +1477,9 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                 if (tt + 1 < C::B) xzn = plane_move<FWD>(xp, h ? bk[kk + 1].x : bk[kk].y, rm, baddr);
                 if constexpr (kWaveShadow) {
                     __builtin_amdgcn_sched_barrier(0);
-                    if (h == 0 && kk + kWaveLook < C::PBN) {
+                    if (h == 0 && kk + C::LOOK < C::PBN) {
 #pragma unroll
-                        for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
+                        for (int a = 0; a < C::A; a++) rg[kk + C::LOOK][a] = sc[a * PB + (kk + C::LOOK) * 64];
                     }
                     if (h == 1 && kk > 0) {
                         xbuf[(bi & 1) * PB + (kk - 1) * 64 + lane] =
@@ -1508,9 +1508,9 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
             if (!kWaveShadow || kk == C::PBN - 1)
                 xbuf[(bi & 1) * PB + kk * 64 + lane] =
                     FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
-            if (!kWaveShadow && kk + kWaveLook < C::PBN) {
+            if (!kWaveShadow && kk + C::LOOK < C::PBN) {
 #pragma unroll
-                for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
+                for (int a = 0; a < C::A; a++) rg[kk + C::LOOK][a] = sc[a * PB + (kk + C::LOOK) * 64];
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -2202,6 +2202,9 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
 // order), so it is bit-identical to the per-step path.  Needs every block
 // co-resident (host: kWideG blocks, two per CU).
 constexpr int kWideJR = 40, kWideJL = 5, kWideD = 8;
+#ifndef GG_WIDE_NEXT_NT
+#define GG_WIDE_NEXT_NT 0
+#endif
 __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m, DevState *ds,
                                                             const double *__restrict__ w_in,
                                                             double *__restrict__ V, long long ldv,
@@ -2232,10 +2235,21 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
     // unit offsets are recomputed in every step from a laundered base (not
     // hoisted: 45 live offsets would not fit beside w)
     double2 pk[kWideD], pn[kWideD];
+    // v_{k+1} is read again as v_k in the next step: GG_WIDE_NEXT_NT=0 reads it
+    // with the default policy (it may stay in the Infinity Cache for that
+    // second read), 1 streams it non-temporally like v_k's last read
     auto fetch = [&](int j, int ub, const double2 *vkp, const double2 *vnp) {
         if (j < J && j < nval) {
-            pk[j % kWideD] = vkp[ub + j * stride];
-            if (vnp) pn[j % kWideD] = vnp[ub + j * stride];
+            const dbl2v a = __builtin_nontemporal_load(reinterpret_cast<const dbl2v *>(vkp) + ub + j * stride);
+            pk[j % kWideD] = make_double2(a.x, a.y);
+            if (vnp) {
+                if constexpr (GG_WIDE_NEXT_NT) {
+                    const dbl2v c = __builtin_nontemporal_load(reinterpret_cast<const dbl2v *>(vnp) + ub + j * stride);
+                    pn[j % kWideD] = make_double2(c.x, c.y);
+                } else {
+                    pn[j % kWideD] = vnp[ub + j * stride];
+                }
+            }
         }
     };
     auto vec = [&](const double *p) { return reinterpret_cast<const double2 *>(p); };
