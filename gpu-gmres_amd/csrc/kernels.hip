@@ -1167,11 +1167,12 @@ __device__ __forceinline__ double plane_shift(double x, double kb, const RowMask
 // loader's first issue; then per batch the compute wave's start, the writer's
 // publication, the boundary wave's "all values seen", the loader's "landed"
 // and the compute wave's end.
-// the same move through the LDS crossbar (ds_bpermute; GG_TILE_PLANE=2, a
-// measured alternative) -- GG_TILE_PLANE=1 skips the move (timing only, wrong
+// the plane move: 3 = self-swaps (default; per batch compute L 1.00 -> 0.68 us
+// traced, C4 L 270 -> 266 us), 0 = two-register swaps, 2 = through the LDS
+// crossbar (ds_bpermute, same time as 0), 1 = skipped (timing only, wrong
 // results)
 #ifndef GG_TILE_PLANE
-#define GG_TILE_PLANE 0
+#define GG_TILE_PLANE 3
 #endif
 // boundary wave: barrier right after the values are in LDS (1), or after the
 // re-arm stores and the next polls are issued (0)
@@ -1194,11 +1195,40 @@ __device__ __forceinline__ double plane_fix(double p, double kb, const RowMasks 
     return __hiloint2double((int)bfi(m, (unsigned)__double2hiint(kb), (unsigned)__double2hiint(p)),
                             (int)bfi(m, (unsigned)__double2loint(kb), (unsigned)__double2loint(p)));
 }
+// one register as both swap operands exchanges rows in place (checked on the
+// GPU, tools/permlane_probe.hip): p16 -> rows (x1, x0, x3, x2), p32 -> (x2, x3,
+// x0, x1) -- half the copies of the two-register form.  The asm carries the
+// VALU-write -> permlane-read wait states itself.
+__device__ __forceinline__ unsigned p16_self(unsigned v)
+{
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %0" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ unsigned p32_self(unsigned v)
+{
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %0" : "+v"(v));
+    return v;
+}
+template <bool FWD>
+__device__ __forceinline__ double plane_shift_self(double x, double kb, const RowMasks &rm)
+{
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const unsigned klo = (unsigned)__double2loint(kb), khi = (unsigned)__double2hiint(kb);
+    const unsigned l16 = p16_self(lo), h16 = p16_self(hi), l32 = p32_self(lo), h32 = p32_self(hi);
+    // forward: row 0 <- kb, rows 1, 2 <- p16, row 3 <- p32
+    // backward: row 2 <- kb, rows 0, 3 <- p16, row 1 <- p32
+    const unsigned mk = FWD ? rm.m0 : (rm.mhi & ~rm.m3);
+    const unsigned m32 = FWD ? rm.m3 : rm.m1;
+    const unsigned rlo = bfi(mk, klo, bfi(m32, l32, l16)), rhi = bfi(mk, khi, bfi(m32, h32, h16));
+    return __hiloint2double((int)rhi, (int)rlo);
+}
 template <bool FWD>
 __device__ __forceinline__ double plane_move(double x, double kb, const RowMasks &rm, int baddr)
 {
     if constexpr (GG_TILE_PLANE == 0) {
         return plane_shift<FWD>(x, kb, rm);
+    } else if constexpr (GG_TILE_PLANE == 3) {
+        return plane_shift_self<FWD>(x, kb, rm);
     } else if constexpr (GG_TILE_PLANE == 1) {
         return x + kb;
     } else {

@@ -14,16 +14,22 @@ __global__ void k(unsigned *out)
     out[64 + l] = p16[1];
     out[128 + l] = p32[0];
     out[192 + l] = p32[1];
+    // one register as both operands (a row-pair / half swap in place?)
+    unsigned c = 3000 + l, d = 4000 + l;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %0" : "+v"(c));
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %0" : "+v"(d));
+    out[256 + l] = c;
+    out[320 + l] = d;
 }
 
 int main()
 {
-    unsigned *d, h[256];
+    unsigned *d, h[384];
     if (hipMalloc(&d, sizeof(h)) != hipSuccess) return 1;
     k<<<1, 64>>>(d);
     if (hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return 1;
-    const char *nm[4] = {"p16.vdst", "p16.src", "p32.vdst", "p32.src"};
-    for (int q = 0; q < 4; q++) {
+    const char *nm[6] = {"p16.vdst", "p16.src", "p32.vdst", "p32.src", "p16 self", "p32 self"};
+    for (int q = 0; q < 6; q++) {
         printf("%s:", nm[q]);
         for (int l = 0; l < 64; l += 8) printf(" [%d]=%u", l, h[q * 64 + l]);
         printf("\n");
