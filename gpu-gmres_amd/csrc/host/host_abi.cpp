@@ -97,6 +97,36 @@ int gg_host_wave3d(int n, const int *l_rp, const int *l_ci, const double *l_v, c
     }
 }
 
+int gg_host_wave_layout(int n, const int *l_rp, const int *l_ci, const double *l_v, const int *u_rp,
+                        const int *u_ci, const double *u_v, long long *slot, int *info)
+{
+    if (n < 0 || !info) return GG_EINVAL;
+    try {
+        const CanonTri cl = canon_lower_unit(wrap(n, l_rp, l_ci, l_v));
+        const CanonTri cu = canon_upper_ignorezero(wrap(n, u_rp, u_ci, u_v));
+        // the solver's choice (solver.hip setup_left): 2D band layout, else 3D
+        Wave2D w = detect_wave2d(cl, cu);
+        if (w.ok && w.nbands > 512) w.ok = false;
+        if (!w.ok) w = detect_wave3d(cl, cu);
+        for (int k = 0; k < 9; k++) info[k] = 0;
+        if (!w.ok) return 0;
+        info[0] = w.tile ? 3 : (w.nz > 1 ? 4 : 2);
+        info[1] = w.nx;
+        info[2] = w.ny;
+        info[3] = w.nz;
+        info[4] = w.nbands;
+        info[5] = w.T;
+        info[6] = w.NJ;
+        info[7] = w.NK;
+        info[8] = w.skew;
+        if (slot)
+            for (int r = 0; r < n; r++) slot[r] = w.slot(r);
+        return 1;
+    } catch (...) {
+        return GG_EINVAL;
+    }
+}
+
 int gg_host_partition(int n, const int *rp, const int *ci, int nparts, int method, int *node_part,
                       int *part_size, int *pinv, int *q)
 {

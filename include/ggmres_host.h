@@ -70,6 +70,16 @@ int gg_host_read_mtx(const char *path, int expand_symmetric, int *nrows, int *nc
 int gg_host_wave3d(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,
                    const int *u_row_ptr, const int *u_col_idx, const double *u_val,
                    int *nx, int *ny, int *nz);
+/* The wavefront vector layout the solver would use for these factors (no
+ * device needed): returns 1 and fills slot[r] (natural row -> layout slot,
+ * n entries, may be NULL) and info[9] = {kind (2: 2D bands, 3: 3D tiles,
+ * 4: 3D planes), nx, ny, nz, bands or tiles, steps per band T, tiles along
+ * the lines NJ / planes NK, lane skew}; 0 when the layout is natural.
+ * Replaces the level analysis cusparseScsrsv_analysis (src/gmres.cu:1516-1517)
+ * for grid-shaped triangles (kernels.hip k_trsv_wave2d / k_trsv_tile3d). */
+int gg_host_wave_layout(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,
+                        const int *u_row_ptr, const int *u_col_idx, const double *u_val,
+                        long long *slot, int *info);
 /* coo2csrDouble_in (src/formatConvert.cpp:165-216): COO -> CSR in place;
  * on return row_idx[0..nrows] holds the row pointers (row_idx needs
  * max(nz, nrows + 1) slots), entries of a row bubble-sorted by column.

@@ -199,3 +199,35 @@ def test_wavefront_detection(ggmres_lib):
         assert wave(ggmres_lib, L, U) == (1, 30, 30)
     L, U = O.iluk(M.laplacian_5pt(30), 3)
     assert wave(ggmres_lib, L, U)[0] == 0
+
+
+def layout(lib, L, U):
+    n = L.n
+    slot = np.zeros(max(n, 1), np.int64)
+    info = np.zeros(9, np.int32)
+    ok = lib.gg_host_wave_layout(ctypes.c_int(n), L.rp.ctypes.data_as(PI), L.ci.ctypes.data_as(PI),
+                                 L.v.ctypes.data_as(PD), U.rp.ctypes.data_as(PI), U.ci.ctypes.data_as(PI),
+                                 U.v.ctypes.data_as(PD), slot.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)),
+                                 info.ctypes.data_as(PI))
+    return ok, slot[:n], info
+
+
+@pytest.mark.parametrize("dims", [(20, 30, 7), (16, 70, 5), (8, 8, 300), (130, 3, 4), (100, 100, 1), (37, 64, 1)])
+def test_wave_layout_matches_restatement(ggmres_lib, dims):
+    """The solver's wavefront vector layout (gg_host_wave_layout: 2D bands, 3D
+    16-line x 4-plane tiles) equals the restatement the order-matched oracle
+    uses (tests/helpers.py device_layout), and is one-to-one."""
+    from helpers import device_layout
+    nx, ny, nz = dims
+    A = M.grid_7pt(nx, ny, nz, upwind=0.1) if nz > 1 else M.laplacian_5pt(nx, ny)
+    n = A.shape[0]
+    L, U = O.ilu0(A)
+    ok, slot, info = layout(ggmres_lib, L, U)
+    assert ok == 1
+    assert info[0] == (3 if nz > 1 else 2) and tuple(info[1:4]) == (nx, ny, nz)
+    if nz > 1:
+        assert info[6] == (ny + 15) // 16 and info[7] == (nz + 3) // 4 and info[4] == info[6] * info[7]
+        assert info[5] == (nx + 21 + 15) // 16 * 16
+    assert len(np.unique(slot)) == n
+    lay2nat, _ = device_layout(n, nx, ny if nz > 1 else None)
+    assert np.array_equal(lay2nat[slot], np.arange(n))
