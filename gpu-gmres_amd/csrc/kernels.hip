@@ -362,6 +362,11 @@ __global__ void k_fill_gated(Gate g, unsigned long long *p, long long n, unsigne
         p[i] = v;
 }
 
+// long rows: issue the next round's loads before this round's serial sum (1;
+// 92 VGPRs, 5 waves per SIMD) or after it (0; 62 VGPRs, 8 waves per SIMD)
+#ifndef GG_FLOW_PREFETCH
+#define GG_FLOW_PREFETCH 1
+#endif
 __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const int2 *__restrict__ tasks,
                                                       const int *__restrict__ rows,
                                                       const int *__restrict__ rp, const int *__restrict__ ci,
@@ -387,18 +392,24 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
             const int k0 = rp[r], k1 = rp[r + 1];
             double acc = b[r];
             int spins = 0;
-            for (int kc = k0; kc < k1; kc += 256) {
-                int c[4];
-                double vv[4];
-                unsigned long long u[4];
+            // round kc's columns, coefficients and x polls; the next round's
+            // are issued before this round's serial sum (their latency hidden)
+            int c[4];
+            double vv[4];
+            unsigned long long u[4];
+            auto fetch = [&](int kc, int *cc, double *vc, unsigned long long *uc) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int k = kc + q * 64 + lane;
-                    c[q] = k < k1 ? ci[k] : -1;
-                    vv[q] = k < k1 ? v[k] : 0.0;
+                    cc[q] = k < k1 ? ci[k] : -1;
+                    vc[q] = k < k1 ? v[k] : 0.0;
                 }
 #pragma unroll
-                for (int q = 0; q < 4; q++) u[q] = c[q] >= 0 ? ld_agent(xu + c[q]) : 0ull;
+                for (int q = 0; q < 4; q++) uc[q] = cc[q] >= 0 ? ld_agent(xu + cc[q]) : 0ull;
+            };
+            fetch(k0, c, vv, u);
+            for (int kc = k0; kc < k1; kc += 256) {
+                if (!GG_FLOW_PREFETCH && kc > k0) fetch(kc, c, vv, u);
                 while (true) {
                     bool miss = false;
 #pragma unroll
@@ -413,14 +424,40 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                     for (int q = 0; q < 4; q++)
                         if (c[q] >= 0 && u[q] == kSentinel) u[q] = ld_agent(xu + c[q]);
                 }
+                double pq[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) pq[q] = vv[q] * __longlong_as_double((long long)u[q]);
+                if (GG_FLOW_PREFETCH && kc + 256 < k1) fetch(kc + 256, c, vv, u);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    wprod[lane] = vv[q] * __longlong_as_double((long long)u[q]);
+                    wprod[lane] = pq[q];
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     const int cnt = k1 - (kc + q * 64);
-                    if (lane == 0)
-                        for (int j = 0; j < 64 && j < cnt; j++) acc = acc - wprod[j];
+                    if (lane == 0) {
+                        // the 64 products in canonical order, read 8 at a time one
+                        // chunk ahead (a read-then-subtract loop waits an LDS round
+                        // trip per term)
+                        const double2 *wp2 = reinterpret_cast<const double2 *>(wprod);
+                        double2 cur[4], nxt[4];
+#pragma unroll
+                        for (int e = 0; e < 4; e++) cur[e] = wp2[e];
+#pragma unroll
+                        for (int c8 = 0; c8 < 8; c8++) {
+                            if (c8 + 1 < 8) {
+#pragma unroll
+                                for (int e = 0; e < 4; e++) nxt[e] = wp2[(c8 + 1) * 4 + e];
+                            }
+#pragma unroll
+                            for (int e = 0; e < 4; e++) {
+                                const int j = c8 * 8 + 2 * e;
+                                if (j < cnt) acc = acc - cur[e].x;
+                                if (j + 1 < cnt) acc = acc - cur[e].y;
+                            }
+#pragma unroll
+                            for (int e = 0; e < 4; e++) cur[e] = nxt[e];
+                        }
+                    }
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 }
