@@ -279,9 +279,19 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
     }
     __syncthreads();
     if (tid < nr) {
+        // the row's products in CSR order; eight LDS reads in flight per
+        // group (a read-then-add loop waits an LDS round trip per term)
         double acc = 0.0;
         const int a = srp[tid] - e0, z = srp[tid + 1] - e0;
-        for (int e = a; e < z; e++) acc += prod[e];
+        int e = a;
+        for (; e + 8 <= z; e += 8) {
+            double t[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) t[q] = prod[e + q];
+#pragma unroll
+            for (int q = 0; q < 8; q++) acc += t[q];
+        }
+        for (; e < z; e++) acc += prod[e];
         const int r = r0 + tid;
         y[r] = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
     }
