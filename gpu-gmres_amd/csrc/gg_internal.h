@@ -139,24 +139,25 @@ struct Wave2D {
     long long P2 = 0;        // one plane's layout length (nbands * T * 64)
     long long P = 0;         // padded layout length (nz * P2)
     // 3D tile layout (tile = true; kernels.hip k_trsv_tile3d): a wave owns a
-    // tile of 16 lines x 4 planes, lane l = a + 16*row(c) for line j = 16J + a,
-    // plane k = 4K + c, row(c) = 0, 1, 3, 2 for c = 0..3 (so every plane's
-    // predecessor is one permlane swap away); point (i, j, k) at step
-    // t = i + a + 2c of its tile (a plane lags its predecessor by 2 steps, so
-    // the cross-row move is off the recurrence); tiles K-major (band = K*NJ +
-    // J), each stored as
-    // a 2D band of T steps (nbands = NJ * NK; nz stays the grid's plane count).
+    // tile of 8 lines x 8 planes, lane l = a + 8*g(c) for line j = 8J + a,
+    // plane k = 8K + c, with the Gray code g(c) = c ^ (c >> 1): consecutive
+    // planes sit in half-rows that differ in one bit, i.e. one DPP row_ror:8,
+    // v_permlane16_swap or v_permlane32_swap apart.  Point (i, j, k) runs at
+    // step t = i + a + 2c of its tile (a plane lags its predecessor by 2 steps,
+    // so the cross-lane move is off the recurrence); tiles K-major (band =
+    // K*NJ + J), each stored as a 2D band of T steps (nbands = NJ * NK; nz
+    // stays the grid's plane count).
     bool tile = false;
     int NJ = 0, NK = 0;           // tiles along the line / plane directions
-    static constexpr int kTileGran = 20;   // hand-off values per step: 16 plane-edge + 4 line-edge
+    static constexpr int kTileGran = 16;   // hand-off values per step: 8 plane-edge + 8 line-edge
     long long ngran() const { return tile ? (long long)nbands * T * kTileGran : (long long)nz * nbands * T; }
     long long slot(long long r) const {
         const long long nxy = (long long)nx * ny;
         const long long k = r / nxy, q = r % nxy;
         if (tile) {
-            const int j = (int)(q / nx), i = (int)(q % nx), a = j & 15, c = (int)(k & 3);
-            const int l = a + 16 * (c < 2 ? c : 5 - c), t = i + a + 2 * c;
-            const long long band = (k >> 2) * NJ + (j >> 4);
+            const int j = (int)(q / nx), i = (int)(q % nx), a = j & 7, c = (int)(k & 7);
+            const int l = a + 8 * (c ^ (c >> 1)), t = i + a + 2 * c;
+            const long long band = (k >> 3) * NJ + (j >> 3);
             return ((band * (T / 2) + t / 2) * 64 + l) * 2 + (t & 1);
         }
         const int j = (int)(q / nx), i = (int)(q % nx), l = j & 63, t = i + skew * l + (skew - 1);

@@ -202,10 +202,10 @@ Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U)
     w.nz = (int)(n / nxy);
     const char *pl = std::getenv("GG_WAVE3D_PLANES");     // the (plane, band) pipeline instead
     if (!(pl && pl[0] == '1')) {
-        // 16-line x 4-plane tiles (Wave2D::slot); the lane skew is a + 2c <= 21 steps
+        // 8-line x 8-plane tiles (Wave2D::slot); the lane skew is a + 2c <= 21 steps
         w.tile = true;
-        w.NJ = (w.ny + 15) / 16;
-        w.NK = (w.nz + 3) / 4;
+        w.NJ = (w.ny + 7) / 8;
+        w.NK = (w.nz + 7) / 8;
         w.nbands = w.NJ * w.NK;
         w.T = (w.nx + 21 + kTileTAlign - 1) / kTileTAlign * kTileTAlign;
         w.P2 = (long long)w.nbands * w.T * 64;

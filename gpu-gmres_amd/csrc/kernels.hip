@@ -1128,26 +1128,26 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 }
 
 // ================================================ 3D 7-point grids: tile wavefront
-// Layout (gg_internal.h Wave2D, tile = true): one wave owns a tile of 16 lines
-// x 4 planes, lane l = a + 16 row(c) with row(c) = 0, 1, 3, 2 for planes
-// c = 0..3, and runs point (i, j, k) at step t = i + a + 2c.  Every term of a
-// row is then a recent value of a neighbouring lane: the in-line term the
-// lane's own previous step, the line term the previous step one lane down the
-// 16-lane row (DPP row_shr:1, backward row_shl:1; the row's edge lane takes
-// the neighbouring tile's value as the DPP `old`), the plane term the value of
-// TWO steps back in the predecessor plane's row -- rows 0 -> 1 and 3 -> 2 are
-// one v_permlane16_swap, 1 -> 3 one v_permlane32_swap (backward the reverse
-// moves), the first plane's row takes the neighbouring tile's value -- so the
-// swaps and selects (~90 cycles) run a step ahead, off the recurrence, whose
-// chain is the 2D one: DPP, multiply, two subtractions (and the division).  The dependency chain (nx + ny + nz - 2
-// steps) crosses a workgroup boundary every 16 lines and every 4 planes: 13 +
-// 53 hand-offs at 216^3 instead of 216 plane hand-offs through HBM, and no
-// previous-plane x is streamed.
+// Layout (gg_internal.h Wave2D, tile = true): one wave owns a tile of 8 lines
+// x 8 planes, lane l = a + 8 g(c) with the Gray code g(c) = c ^ (c >> 1) for
+// plane c = 0..7, and runs point (i, j, k) at step t = i + a + 2c.  Every term
+// of a row is then a recent value of a neighbouring lane: the in-line term the
+// lane's own previous step; the line term the previous step one lane down its
+// 8-lane half-row (DPP row_shr:1, backward row_shl:1; the half-row's edge lane
+// takes the neighbouring tile's value -- as the DPP `old` in half-row 0 of a
+// row, by a select in half-row 1); the plane term the value of TWO steps back
+// in the predecessor plane's half-row, which differs in one bit of g: one DPP
+// row_ror:8 (bit 0), in-place v_permlane16_swap (bit 1) or v_permlane32_swap
+// (bit 2) plus selects, computed a step ahead, off the recurrence, whose chain
+// is the 2D one (DPP, multiply, two subtractions, the division).  The first
+// plane's half-row takes the neighbouring tile's value.  The dependency chain
+// (nx + ny + nz - 2 steps) crosses a workgroup boundary every 8 lines and every
+// 8 planes: 26 + 26 hand-offs at 216^3 (round 1: 216 plane hops through HBM).
 // Hand-off granules (8 B, value = flag, kSentinel = not ready, re-armed by the
-// consumer): per tile and step 20 words, [0, 16) the last plane's row for tile
-// (J, K +- 1), [16, 20) the four rows' edge lanes for tile (J +- 1, K).  The
-// consumer's step t needs the plane granules of step t +- 6 and the line
-// granules of step t +- 15 (same point i, skew a + 2c).
+// consumer): per tile and step 16 words, [0, 8) the last plane's half-row for
+// tile (J, K +- 1), [8, 16) the eight planes' edge lanes for tile (J +- 1, K).
+// The consumer's step t needs the plane granules of step t +- 14 and the line
+// granules of step t +- 7 (same point i, skew a + 2c).
 // Roles as k_trsv_wave2d: wave 0 computes, 1 polls the granules, 2 stores x
 // and publishes, 3 streams b, c1, c2 (, d (, RN(1/d))), c0 into the LDS ring.
 // Persistent grid, every workgroup co-resident, tiles taken in dependency
@@ -1165,7 +1165,7 @@ struct TileCfg {
     static constexpr int NPER = A * PBN;                // DMA instructions per batch
     static constexpr int NG = Wave2D::kTileGran;
     static constexpr int GL = (B * NG + 63) / 64;       // granule loads (stores) per lane per batch
-    static constexpr int BND = 2 * PBN * 32;            // boundary values: double2 [2][PBN][32]
+    static constexpr int BND = 2 * PBN * NG;            // boundary values: double2 [2][PBN][NG]
     static constexpr int XST = 2 * PBN * 64;            // x staging: double2 [2][PBN][64]
     static constexpr int RFIT = (150 * 1024 / 16 - BND - XST) / SLOT;
     static constexpr int RVM = 2 + 63 / NPER;
@@ -1179,33 +1179,42 @@ struct TileCfg {
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
 };
 
-// the plane predecessor's previous-step value (rows as in the layout comment);
-// the first plane's row takes kb.  Branch-free: per-lane masks of the rows
-// (precomputed) select with v_bfi_b32.
 __device__ __forceinline__ unsigned bfi(unsigned m, unsigned a, unsigned b) { return (a & m) | (b & ~m); }
-struct RowMasks {
-    unsigned m0, m1, m3, mhi;   // lane is in row 0 / 1 / 3 / in rows 2-3
+__device__ __forceinline__ double bfi64(unsigned m, double a, double b)
+{
+    return __hiloint2double((int)bfi(m, (unsigned)__double2hiint(a), (unsigned)__double2hiint(b)),
+                            (int)bfi(m, (unsigned)__double2loint(a), (unsigned)__double2loint(b)));
+}
+// per-lane masks of the tile layout (all ones / zero)
+struct TileMasks {
+    unsigned kb;     // the first plane's half-row: plane term from the neighbouring tile
+    unsigned r8;     // plane predecessor one row_ror:8 away (Gray bit 0)
+    unsigned p16;    // one v_permlane16_swap away (bit 1); else v_permlane32_swap (bit 2)
+    unsigned lfix;   // half-row edge lanes whose line term the DPP shift cannot give
 };
-template <bool FWD>
-__device__ __forceinline__ double plane_shift(double x, double kb, const RowMasks &rm)
+// one register as both swap operands exchanges rows in place (checked on the
+// GPU, tools/permlane_probe.hip): p16 -> rows (x1, x0, x3, x2), p32 -> (x2, x3,
+// x0, x1).  The asm carries the VALU-write -> permlane-read wait states itself.
+__device__ __forceinline__ unsigned p16_self(unsigned v)
+{
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %0" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ unsigned p32_self(unsigned v)
+{
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %0" : "+v"(v));
+    return v;
+}
+// the plane predecessor's value of x (any lane of the first plane: kb)
+__device__ __forceinline__ double plane_move(double x, double kb, const TileMasks &tm)
 {
     const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const unsigned klo = (unsigned)__double2loint(kb), khi = (unsigned)__double2hiint(kb);
-    // (vdst, src) = p16(x, x): rows (x0, x0, x2, x2), (x1, x1, x3, x3)
-    // (vdst, src) = p32(x, x): rows (x0, x1, x0, x1), (x2, x3, x2, x3)
-    const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    const auto l32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    unsigned rlo, rhi;
-    if constexpr (FWD) {    // row 0 <- kb, row 1 <- row 0, row 2 <- row 3, row 3 <- row 1
-        rlo = bfi(rm.mhi, bfi(rm.m3, l32[0], l16[1]), bfi(rm.m1, l16[0], klo));
-        rhi = bfi(rm.mhi, bfi(rm.m3, h32[0], h16[1]), bfi(rm.m1, h16[0], khi));
-    } else {                // row 0 <- row 1, row 1 <- row 3, row 2 <- kb, row 3 <- row 2
-        rlo = bfi(rm.mhi, bfi(rm.m3, l16[0], klo), bfi(rm.m0, l16[1], l32[1]));
-        rhi = bfi(rm.mhi, bfi(rm.m3, h16[0], khi), bfi(rm.m0, h16[1], h32[1]));
-    }
-    return __hiloint2double((int)rhi, (int)rlo);
+    const unsigned r8l = (unsigned)__builtin_amdgcn_mov_dpp((int)lo, 0x128, 0xf, 0xf, false);   // row_ror:8
+    const unsigned r8h = (unsigned)__builtin_amdgcn_mov_dpp((int)hi, 0x128, 0xf, 0xf, false);
+    const unsigned l16 = p16_self(lo), h16 = p16_self(hi), l32 = p32_self(lo), h32 = p32_self(hi);
+    const unsigned rlo = bfi(tm.r8, r8l, bfi(tm.p16, l16, l32));
+    const unsigned rhi = bfi(tm.r8, r8h, bfi(tm.p16, h16, h32));
+    return bfi64(tm.kb, kb, __hiloint2double((int)rhi, (int)rlo));
 }
 
 // TRACE (diagnostics, gg_trace_precond): per tile 8 + 5 nbatch words -- compute
@@ -1214,13 +1223,6 @@ __device__ __forceinline__ double plane_shift(double x, double kb, const RowMask
 // loader's first issue; then per batch the compute wave's start, the writer's
 // publication, the boundary wave's "all values seen", the loader's "landed"
 // and the compute wave's end.
-// the plane move: 3 = self-swaps (default; per batch compute L 1.00 -> 0.68 us
-// traced, C4 L 270 -> 266 us), 0 = two-register swaps, 2 = through the LDS
-// crossbar (ds_bpermute, same time as 0), 1 = skipped (timing only, wrong
-// results)
-#ifndef GG_TILE_PLANE
-#define GG_TILE_PLANE 3
-#endif
 // boundary wave: barrier right after the values are in LDS (1), or after the
 // re-arm stores and the next polls are issued (0)
 #ifndef GG_TILE_EARLYBAR
@@ -1234,58 +1236,6 @@ __device__ __forceinline__ double plane_shift(double x, double kb, const RowMask
 #ifndef GG_TILE_WSLEEP
 #define GG_TILE_WSLEEP 1
 #endif
-// the first plane's row takes kb (after plane_move with any kb)
-template <bool FWD>
-__device__ __forceinline__ double plane_fix(double p, double kb, const RowMasks &rm)
-{
-    const unsigned m = FWD ? rm.m0 : (rm.mhi & ~rm.m3);
-    return __hiloint2double((int)bfi(m, (unsigned)__double2hiint(kb), (unsigned)__double2hiint(p)),
-                            (int)bfi(m, (unsigned)__double2loint(kb), (unsigned)__double2loint(p)));
-}
-// one register as both swap operands exchanges rows in place (checked on the
-// GPU, tools/permlane_probe.hip): p16 -> rows (x1, x0, x3, x2), p32 -> (x2, x3,
-// x0, x1) -- half the copies of the two-register form.  The asm carries the
-// VALU-write -> permlane-read wait states itself.
-__device__ __forceinline__ unsigned p16_self(unsigned v)
-{
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %0" : "+v"(v));
-    return v;
-}
-__device__ __forceinline__ unsigned p32_self(unsigned v)
-{
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %0" : "+v"(v));
-    return v;
-}
-template <bool FWD>
-__device__ __forceinline__ double plane_shift_self(double x, double kb, const RowMasks &rm)
-{
-    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const unsigned klo = (unsigned)__double2loint(kb), khi = (unsigned)__double2hiint(kb);
-    const unsigned l16 = p16_self(lo), h16 = p16_self(hi), l32 = p32_self(lo), h32 = p32_self(hi);
-    // forward: row 0 <- kb, rows 1, 2 <- p16, row 3 <- p32
-    // backward: row 2 <- kb, rows 0, 3 <- p16, row 1 <- p32
-    const unsigned mk = FWD ? rm.m0 : (rm.mhi & ~rm.m3);
-    const unsigned m32 = FWD ? rm.m3 : rm.m1;
-    const unsigned rlo = bfi(mk, klo, bfi(m32, l32, l16)), rhi = bfi(mk, khi, bfi(m32, h32, h16));
-    return __hiloint2double((int)rhi, (int)rlo);
-}
-template <bool FWD>
-__device__ __forceinline__ double plane_move(double x, double kb, const RowMasks &rm, int baddr)
-{
-    if constexpr (GG_TILE_PLANE == 0) {
-        return plane_shift<FWD>(x, kb, rm);
-    } else if constexpr (GG_TILE_PLANE == 3) {
-        return plane_shift_self<FWD>(x, kb, rm);
-    } else if constexpr (GG_TILE_PLANE == 1) {
-        return x + kb;
-    } else {
-        const int lo = __builtin_amdgcn_ds_bpermute(baddr, __double2loint(x));
-        const int hi = __builtin_amdgcn_ds_bpermute(baddr, __double2hiint(x));
-        const unsigned m = FWD ? rm.m0 : (rm.mhi & ~rm.m3);      // the first plane's row takes kb
-        return __hiloint2double((int)bfi(m, (unsigned)__double2hiint(kb), (unsigned)hi),
-                                (int)bfi(m, (unsigned)__double2loint(kb), (unsigned)lo));
-    }
-}
 
 template <bool FWD, int DIV, bool TRACE = false>
 __global__ __launch_bounds__(256) void k_trsv_tile3d(
@@ -1361,10 +1311,11 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
             for (int m = 0; m < GL; m++) {
                 const int e = lane + 64 * m;
                 const int tt = e / NG, idx = e - tt * NG;
-                if (e < C::B * NG && (idx < 16 ? pub_k : pub_j)) {
-                    // the last plane's row (forward: plane 3 = row 2; backward:
-                    // plane 0 = row 0), or a row's edge lane (a = 15 / a = 0)
-                    const int sl = idx < 16 ? (FWD ? 32 + idx : idx) : (FWD ? 15 : 0) + 16 * (idx - 16);
+                if (e < C::B * NG && (idx < 8 ? pub_k : pub_j)) {
+                    // the last plane's half-row (forward: plane 7, g = 4; backward:
+                    // plane 0, g = 0), or plane c's edge lane (a = 7 / a = 0)
+                    const int cq = idx - 8;
+                    const int sl = idx < 8 ? (FWD ? 32 + idx : idx) : (FWD ? 7 : 0) + 8 * (cq ^ (cq >> 1));
                     const double v = reinterpret_cast<const double *>(xb + (tt >> 1) * 64 + sl)
                         [FWD ? (tt & 1) : 1 - (tt & 1)];
                     const int t = FWD ? pb * C::B + tt : (T - 1) - (pb * C::B + tt);
@@ -1406,8 +1357,8 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
             const int tt = e / NG, idx = e - tt * NG;
             if (e >= C::B * NG || bj >= nbatch) return nullptr;
             const int t = FWD ? bj * C::B + tt : (T - 1) - (bj * C::B + tt);
-            const bool pl = idx < 16;
-            const int tp = pl ? (FWD ? t + 6 : t - 6) : (FWD ? t + 15 : t - 15);
+            const bool pl = idx < 8;
+            const int tp = pl ? (FWD ? t + 14 : t - 14) : (FWD ? t + 7 : t - 7);
             if (!(pl ? has_k : has_j) || tp < 0 || tp >= T) return nullptr;
             return (pl ? gk : gj) + (long long)tp * NG + idx;
         };
@@ -1457,12 +1408,12 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                     if (spins) bw_cyc += (long long)__builtin_amdgcn_s_memtime() - tw;
                     if (lane == 0) trace[(long long)band * TS + 8 + 2 * nbatch + bi] = (long long)__builtin_amdgcn_s_memrealtime();
                 }
-                double *bd = reinterpret_cast<double *>(bring + (bi & 1) * (C::PBN * 32));
+                double *bd = reinterpret_cast<double *>(bring + (bi & 1) * (C::PBN * NG));
 #pragma unroll
                 for (int m = 0; m < GL; m++) {
                     const int e = lane + 64 * m;
                     const int tt = e / NG, idx = e - tt * NG;
-                    if (e < C::B * NG) bd[((tt >> 1) * 32 + idx) * 2 + (tt & 1)] = __longlong_as_double((long long)v[u][m]);
+                    if (e < C::B * NG) bd[((tt >> 1) * NG + idx) * 2 + (tt & 1)] = __longlong_as_double((long long)v[u][m]);
                 }
                 if constexpr (GG_TILE_EARLYBAR) {
                     // hand the values over first, then re-arm and poll ahead
@@ -1492,11 +1443,11 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
 
     // ---------------------------------------------------- compute wave
     constexpr int ctrl = FWD ? 0x111 : 0x101;   // row_shr:1 / row_shl:1
-    const int row = lane >> 4;
-    const RowMasks rm{row == 0 ? ~0u : 0u, row == 1 ? ~0u : 0u, row == 3 ? ~0u : 0u, row >= 2 ? ~0u : 0u};
-    // ds_bpermute source lane: the predecessor plane's row (forward 0 -> 1 -> 3 -> 2)
-    const int prow = FWD ? (row == 1 ? 0 : row == 3 ? 1 : row == 2 ? 3 : 0) : (row == 0 ? 1 : row == 1 ? 3 : row == 3 ? 2 : 0);
-    const int baddr = ((lane & 15) + 16 * prow) * 4;
+    const int la = lane & 7, hr = lane >> 3;
+    const int cp = hr ^ (hr >> 1) ^ (hr >> 2);  // this lane's plane (inverse Gray code)
+    const int cs = FWD ? cp : cp + 1;           // the plane whose predecessor move applies
+    const TileMasks tm{(FWD ? cp == 0 : cp == 7) ? ~0u : 0u, (cs & 1) ? ~0u : 0u, (cs & 3) == 2 ? ~0u : 0u,
+                       (lane & 15) == (FWD ? 8 : 7) ? ~0u : 0u};
     double xp = 0.0, xq = 0.0;              // this lane's values of the previous two steps
     double2 rg[C::PBN][C::A];
     raw_barrier();                          // barrier 0: batch 0 is in LDS
@@ -1507,18 +1458,18 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     for (int bi = 0; bi < nbatch; bi++) {
         // the first step's plane neighbour (two steps back) is moved before the
         // barrier; only the first plane's row waits for the boundary value
-        const double xzp = plane_move<FWD>(xq, 0.0, rm, baddr);
+        const double xzp = plane_move(xq, 0.0, tm);
         if (bi > 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // x staging of batch bi-1 written
             raw_barrier();                  // batch bi's data and boundary values
             if (TRACE && bi == 1 && lane == 0) trace[(long long)band * TS + 5] = (long long)__builtin_amdgcn_s_memrealtime();
         }
         if (TRACE && lane == 0) trace[(long long)band * TS + 8 + bi] = (long long)__builtin_amdgcn_s_memrealtime();
-        const double2 *br = bring + (bi & 1) * (C::PBN * 32);
+        const double2 *br = bring + (bi & 1) * (C::PBN * NG);
         const double2 *sc = lds + (bi % C::R) * C::SLOT + lane;
         double2 bk[C::PBN], bj[C::PBN];     // plane / line boundary values of each step pair
-        bk[0] = br[lane & 15];
-        bj[0] = br[16 + row];
+        bk[0] = br[la];
+        bj[0] = br[8 + cp];
 #pragma unroll
         for (int a = 0; a < C::A; a++) rg[0][a] = sc[a * PB];
         __builtin_amdgcn_sched_barrier(0);
@@ -1528,13 +1479,13 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
             for (int a = 0; a < C::A; a++) rg[kk][a] = sc[a * PB + kk * 64];
 #pragma unroll
         for (int kk = 1; kk < C::PBN; kk++) {
-            bk[kk] = br[kk * 32 + (lane & 15)];
-            bj[kk] = br[kk * 32 + 16 + row];
+            bk[kk] = br[kk * NG + la];
+            bj[kk] = br[kk * NG + 8 + cp];
         }
         __builtin_amdgcn_sched_barrier(0);
         double xv[C::B];
         // the plane neighbour's value for the batch's first step (two steps back)
-        double xzn = plane_fix<FWD>(xzp, bk[0].x, rm);
+        double xzn = bfi64(tm.kb, bk[0].x, xzp);
 #pragma unroll
         for (int kk = 0; kk < C::PBN; kk++) {
 #pragma unroll
@@ -1548,10 +1499,10 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                 const double oj = h ? bj[kk].y : bj[kk].x;      // boundary entries by sweep step
                 const double xz = xzn;
                 const double p2 = e2 * xp;
-                const double xs = dpp_shift_old<ctrl>(xp, oj);
+                const double xs = bfi64(tm.lfix, oj, dpp_shift_old<ctrl>(xp, oj));
                 // the next step's plane neighbour: this lane's row predecessor's
                 // value of the previous step (xp), moved while the chain runs
-                if (tt + 1 < C::B) xzn = plane_move<FWD>(xp, h ? bk[kk + 1].x : bk[kk].y, rm, baddr);
+                if (tt + 1 < C::B) xzn = plane_move(xp, h ? bk[kk + 1].x : bk[kk].y, tm);
                 if constexpr (kWaveShadow) {
                     __builtin_amdgcn_sched_barrier(0);
                     if (h == 0 && kk + C::LOOK < C::PBN) {

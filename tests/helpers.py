@@ -62,27 +62,27 @@ def device_layout(n, nx=None, ny=None, skew=1):
     grid of line length nx on the wavefront path -- band = j//64, lane l = j%64,
     step t = i + skew*l + skew-1, slot ((band*T/2 + t//2)*64 + l)*2 + t%2 with
     T = roundup(nx + 63*skew + 2*(skew-1), 32) (skew = k+1 for ILU(k) factors
-    of a 5-point grid); for a 3D grid (ny given) 16-line x 4-plane tiles; padded to a multiple of 512 slots; G = min(1024, ceil(Ppad/2 / 1024)), or 512 beyond 2M units
+    of a 5-point grid); for a 3D grid (ny given) 8-line x 8-plane tiles; padded to a multiple of 512 slots; G = min(1024, ceil(Ppad/2 / 1024)), or 512 beyond 2M units
     reduction blocks."""
     if nx is None:
         P = n
         slots = np.arange(n, dtype=np.int64)
     elif ny is not None and n // (nx * ny) >= 2:
-        # 3D: 16-line x 4-plane tiles (gg_internal.h Wave2D::slot, tile = true):
-        # lane a + 16*row(c), row(c) = 0, 1, 3, 2; step t = i + a + 2c;
+        # 3D: 8-line x 8-plane tiles (gg_internal.h Wave2D::slot, tile = true):
+        # lane a + 8*g(c), g(c) = c ^ (c >> 1); step t = i + a + 2c;
         # T = roundup(nx + 21, 16); tiles K-major
         nxy = nx * ny
         nz = n // nxy
-        NJ, NK = (ny + 15) // 16, (nz + 3) // 4
+        NJ, NK = (ny + 7) // 8, (nz + 7) // 8
         T = (nx + 21 + 15) // 16 * 16
         P = NJ * NK * T * 64
         r = np.arange(n, dtype=np.int64)
         k, q = r // nxy, r % nxy
         j, i = q // nx, q % nx
-        a, c = j % 16, k % 4
-        lane = a + 16 * np.where(c < 2, c, 5 - c)
+        a, c = j % 8, k % 8
+        lane = a + 8 * (c ^ (c >> 1))
         t = i + a + 2 * c
-        band = (k // 4) * NJ + j // 16
+        band = (k // 8) * NJ + j // 8
         slots = ((band * (T // 2) + t // 2) * 64 + lane) * 2 + t % 2
     else:
         nxy = n if ny is None else nx * ny

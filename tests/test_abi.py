@@ -215,7 +215,7 @@ def layout(lib, L, U):
 @pytest.mark.parametrize("dims", [(20, 30, 7), (16, 70, 5), (8, 8, 300), (130, 3, 4), (100, 100, 1), (37, 64, 1)])
 def test_wave_layout_matches_restatement(ggmres_lib, dims):
     """The solver's wavefront vector layout (gg_host_wave_layout: 2D bands, 3D
-    16-line x 4-plane tiles) equals the restatement the order-matched oracle
+    8-line x 8-plane tiles) equals the restatement the order-matched oracle
     uses (tests/helpers.py device_layout), and is one-to-one."""
     from helpers import device_layout
     nx, ny, nz = dims
@@ -226,7 +226,7 @@ def test_wave_layout_matches_restatement(ggmres_lib, dims):
     assert ok == 1
     assert info[0] == (3 if nz > 1 else 2) and tuple(info[1:4]) == (nx, ny, nz)
     if nz > 1:
-        assert info[6] == (ny + 15) // 16 and info[7] == (nz + 3) // 4 and info[4] == info[6] * info[7]
+        assert info[6] == (ny + 7) // 8 and info[7] == (nz + 7) // 8 and info[4] == info[6] * info[7]
         assert info[5] == (nx + 21 + 15) // 16 * 16
     assert len(np.unique(slot)) == n
     lay2nat, _ = device_layout(n, nx, ny if nz > 1 else None)

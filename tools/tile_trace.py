@@ -25,7 +25,7 @@ s.set_precond_ilu0()
 b = np.ones(A.shape[0])
 s.precond_apply(0, b)
 print("precond apply avg ms", s.time_precond(10))
-NJ, NK = (n1 + 15) // 16, (n1 + 3) // 4
+NJ, NK = (n1 + 7) // 8, (n1 + 7) // 8
 raws = {}
 for which in (0, 1):
     for rep in range(2):
@@ -71,11 +71,11 @@ for which in (0, 1):
         for bi in range(1, nbt - 3):
             need = []
             if 0 <= sk < NK:
-                kb = (KB * bi + KB - 1 + 3) // KB
+                kb = (KB * bi + KB - 1 + 14) // KB
                 if kb < nbt:
                     need.append(pub[sk * NJ + J, kb])
             if 0 <= sj < NJ:
-                jb = (KB * bi + KB - 1 + 15) // KB
+                jb = (KB * bi + KB - 1 + 7) // KB
                 if jb < nbt:
                     need.append(pub[K * NJ + sj, jb])
             if len(need) == 2:
