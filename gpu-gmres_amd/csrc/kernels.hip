@@ -1155,6 +1155,9 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 #ifndef GG_TILE_BATCH
 #define GG_TILE_BATCH 8
 #endif
+#ifndef GG_TILE_RING
+#define GG_TILE_RING GG_WAVE_RING
+#endif
 template <int DIV>
 struct TileCfg {
     static constexpr int A = DIV == WD_UNIT ? 4 : DIV == WD_HW ? 5 : 6;
@@ -1169,7 +1172,8 @@ struct TileCfg {
     static constexpr int XST = 2 * PBN * 64;            // x staging: double2 [2][PBN][64]
     static constexpr int RFIT = (150 * 1024 / 16 - BND - XST) / SLOT;
     static constexpr int RVM = 2 + 63 / NPER;
-    static constexpr int R = kWaveRing < RFIT ? (kWaveRing < RVM ? kWaveRing : RVM) : (RFIT < RVM ? RFIT : RVM);
+    static constexpr int RING = GG_TILE_RING;
+    static constexpr int R = RING < RFIT ? (RING < RVM ? RING : RVM) : (RFIT < RVM ? RFIT : RVM);
     static constexpr int LDS2 = R * SLOT + BND + XST;
     static constexpr int THREADS = 256;
     static_assert(R >= 3 && (R - 2) * NPER <= 63, "ring depth vs vmcnt range");
