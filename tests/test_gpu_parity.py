@@ -670,6 +670,26 @@ def test_ilu0_device_factor_bitexact(solver, name):
     assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
 
 
+@pytest.mark.parametrize("dims", [(9, 5, 3), (17, 9, 8), (33, 16, 17), (2, 40, 40)])
+def test_tile3d_edges_and_ranges(solver, dims):
+    """3D tile wavefront at its edges: tiles cut by the grid in both directions
+    (9 x 5 x 3: one partial tile; 17 x 9 x 8 and 33 x 16 x 17: whole and
+    partial tiles), the shortest lines (nx = 2), and right-hand sides at
+    1e-250 / 1e250 (WD_RCP's range guard repeating the U solve with IEEE
+    division): every apply bit-exact vs the oracle."""
+    nx, ny, nz = dims
+    A = M.grid_7pt(nx, ny, nz, upwind=0.2)
+    n = A.shape[0]
+    L, U = O.ilu0(A)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert solver.uses_wavefront
+    rng = np.random.default_rng(11)
+    for scale in (1.0, 1e-250, 1e250):
+        y = rng.standard_normal(n) * scale
+        assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y)), scale
+
+
 @pytest.mark.parametrize("dims", [(20, 30, 7), (16, 70, 5), (8, 8, 300), (130, 3, 4)])
 def test_wave3d_apply_and_gmres(solver, dims):
     """3D 7-point grids on the pipelined (plane, band) wavefront kernel: several
