@@ -1158,6 +1158,13 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 #ifndef GG_TILE_RING
 #define GG_TILE_RING GG_WAVE_RING
 #endif
+// boundary wave retries: 0 = one poll at a time, n > 0 = two generations in
+// flight, the second issued s_sleep(n) after the first (measured at C4: L/U
+// 260-263 / 286-287 us against 246 / 269 -- the extra polls cost more than
+// the earlier sight gains)
+#ifndef GG_TILE_POLL2
+#define GG_TILE_POLL2 0
+#endif
 template <int DIV>
 struct TileCfg {
     static constexpr int A = DIV == WD_UNIT ? 4 : DIV == WD_HW ? 5 : 6;
@@ -1397,15 +1404,60 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                     for (int m = 0; m < GL; m++) r = r && v[u][m] != kSentinel;
                     return r;
                 };
-                while (!dead && !__all(ready())) {
-                    __builtin_amdgcn_s_sleep(1);
+                if constexpr (GG_TILE_POLL2) {
+                    // not ready: two poll generations in flight, staggered, so a
+                    // value that lands is seen within about half a round trip
+                    // (every load completes in order: vm_wait(GL) = the older
+                    // generation is back)
+                    if (!__all(ready())) {
+                        unsigned long long pa[GL], pb2[GL];
 #pragma unroll
-                    for (int m = 0; m < GL; m++) v[u][m] = ld_agent(paddr(bi, m));
-                    if (++spins > kSpinLimit) {
-                        dead = true;
-                        if (lane == 0) atomicOr(err, 1);
+                        for (int m = 0; m < GL; m++) pa[m] = ld_agent(paddr(bi, m));
+                        __builtin_amdgcn_s_sleep(GG_TILE_POLL2);
+#pragma unroll
+                        for (int m = 0; m < GL; m++) pb2[m] = ld_agent(paddr(bi, m));
+                        auto rdy = [&](const unsigned long long *q) {
+                            bool r = true;
+#pragma unroll
+                            for (int m = 0; m < GL; m++) r = r && q[m] != kSentinel;
+                            return r;
+                        };
+                        while (true) {
+                            __builtin_amdgcn_s_waitcnt(vm_wait(GL));
+                            if (dead || __all(rdy(pa))) {
+#pragma unroll
+                                for (int m = 0; m < GL; m++) v[u][m] = pa[m];
+                                break;
+                            }
+#pragma unroll
+                            for (int m = 0; m < GL; m++) pa[m] = ld_agent(paddr(bi, m));
+                            __builtin_amdgcn_s_waitcnt(vm_wait(GL));
+                            if (__all(rdy(pb2))) {
+#pragma unroll
+                                for (int m = 0; m < GL; m++) v[u][m] = pb2[m];
+                                break;
+                            }
+#pragma unroll
+                            for (int m = 0; m < GL; m++) pb2[m] = ld_agent(paddr(bi, m));
+                            spins += 2;
+                            if (spins > kSpinLimit) {
+                                dead = true;
+                                if (lane == 0) atomicOr(err, 1);
+                            }
+                        }
+                        __builtin_amdgcn_s_waitcnt(vm_wait(0));   // the other generation
                     }
-                    __builtin_amdgcn_s_waitcnt(vm_wait(0));
+                } else {
+                    while (!dead && !__all(ready())) {
+                        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                        for (int m = 0; m < GL; m++) v[u][m] = ld_agent(paddr(bi, m));
+                        if (++spins > kSpinLimit) {
+                            dead = true;
+                            if (lane == 0) atomicOr(err, 1);
+                        }
+                        __builtin_amdgcn_s_waitcnt(vm_wait(0));
+                    }
                 }
                 if constexpr (TRACE) {
                     bw_spins += spins;
