@@ -350,6 +350,8 @@ void setup_space(gg_solver *s, const Wave2D *wl)
     s->lay2nat.upload(l2n, s->st);
     s->nat2lay.upload(s->nat2lay_h, s->st);
     s->G = reduce_grid(s->Ppad / 2);
+    const char *wf = std::getenv("GG_WIDE_FORCE");     // tests: k_arnoldi_wide at any size
+    if (wf && wf[0] == '1') s->G = kWideG;
     // A in layout space: row p = A row nat(p), columns remapped, entry order kept
     if (!s->wave) {
         Csr Ap = s->A;
@@ -395,7 +397,10 @@ void ensure_workspace(gg_solver *s, int m)
     {
         const char *e = std::getenv("GG_NO_PERSIST");
         const bool off = e && e[0] == '1';
-        s->persist = !off && arnoldi_persist_units(s->G, s->Ppad) != 0 && s->G <= arnoldi_persist_max_blocks();
+        const char *wf = std::getenv("GG_WIDE_FORCE");
+        const bool force_wide = wf && wf[0] == '1';
+        s->persist = !off && !force_wide && arnoldi_persist_units(s->G, s->Ppad) != 0 &&
+                     s->G <= arnoldi_persist_max_blocks();
         s->wide = !off && !s->persist && arnoldi_wide_ok(s->G, s->Ppad);   // long vectors: w on chip
         if (s->persist || s->wide) s->gran.alloc((size_t)m * (m + 2) * s->G);
     }

@@ -266,6 +266,34 @@ def test_gmres_left_c1_parity(solver, m, rhs, persist, monkeypatch):
     check_exact(g, ot)
 
 
+@pytest.mark.parametrize("case", ["c1", "grid3d"])
+def test_gmres_wide_orthogonalization_parity(solver, case, monkeypatch):
+    """k_arnoldi_wide (w on chip, basis streamed; the path of vectors beyond
+    the persistent kernel's registers, C4 / C3) forced onto small systems
+    (GG_WIDE_FORCE=1: its 512-block tree at any size, most threads with 0-1
+    units): history, iterations and solution bit-identical to the oracle in
+    that reduction order."""
+    monkeypatch.setenv("GG_WIDE_FORCE", "1")
+    if case == "c1":
+        A, nx, ny = M.laplacian_5pt(100), 100, None
+    else:
+        A, nx, ny = M.grid_7pt(20, 30, 7, upwind=0.1), 20, 30
+    n = A.shape[0]
+    b = M.rhs_uniform(n)
+    L, U = O.ilu0(A)
+    lay, _ = device_layout(n, nx, ny)
+    O.set_dot_order(lay, 512)
+    try:
+        ot = O.gmres_left(A, L, U, b, m=30, max_iter=200, tol=1e-10)
+    finally:
+        O.set_dot_order(None)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert solver.uses_wavefront
+    g = solver.solve(b, restart=30, max_iter=200, tol=1e-10)
+    check_exact(g, ot)
+
+
 def test_gmres_left_fixed_iterations(solver):
     # fixed-length run (tol unreachable): exhaustion semantics + full history
     A = M.laplacian_5pt(100)
