@@ -79,6 +79,9 @@ def parse():
                         "solve at N > 1; dd: the sharded solve (C4 unless --dd-grid c2); replicas: "
                         "one independent C2 solve per rank; c5: a backward-Euler transient (A = G + C/h, "
                         "1%% PULSE sources) of --c5-steps time steps per step")
+    p.add_argument("--dd-sep", choices=["color", "natural"], default="color",
+                   help="dd: separator order -- a greedy colouring of its graph (GG_PART_COLOR_SEP, "
+                        "default: a few-level separator solve) or partition4's ascending index")
     p.add_argument("--c5-steps", type=int, default=100)
     p.add_argument("--c5-scenarios", type=int, default=1,
                    help="c5: independent source scenarios per GPU, solved concurrently (one solver, "
@@ -228,7 +231,7 @@ def bench_dd(a, torch, dist, world, rank, local):
     else:
         d = DD(a.dd_parts, device=local)
         ranks = 1
-    d.set_system(A, host.PART_BLOCKS)
+    d.set_system(A, host.PART_BLOCKS | (host.PART_COLOR_SEP if a.dd_sep == "color" else 0))
     t_setup = time.perf_counter() - t_setup
     info = d.info()
     db = torch.from_numpy(b).cuda()
@@ -265,7 +268,8 @@ def bench_dd(a, torch, dist, world, rank, local):
         "ms_per_step": round(el_max * 1e3 / a.steps, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": (f"sharded solve: {'C4 %d^3 7-pt' % a.c4_grid if a.dd_grid == 'c4' else 'C2 %dx%d 5-pt' % (a.grid, a.grid)}"
-                                f", {parts}-way partition4 (contiguous slabs) arrow ordering, ILU(0) of "
+                                f", {parts}-way partition4 (contiguous slabs) arrow ordering"
+                                f"{', separator by colour' if a.dd_sep == 'color' else ''}, ILU(0) of "
                                 f"the permuted matrix, GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, "
                                 f"one solve per step"),
                    "n": n, "nnz": int(A.nnz), "parts": parts,

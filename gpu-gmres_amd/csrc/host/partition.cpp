@@ -113,7 +113,7 @@ void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &nod
     std::vector<int> xadj, adj;
     node_graph(A, xadj, adj);
     node_part.assign(n, 0);
-    if (method == GG_PART_BLOCKS) {
+    if ((method & 3) == GG_PART_BLOCKS) {
         // contiguous index ranges: strips / slabs of a natural-order grid
         for (int j = 0; j < n; j++) node_part[j] = (int)((long long)j * nparts / n);
     } else {
@@ -146,6 +146,28 @@ void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &nod
         pinv[j] = begin[p] + cur[p];
         q[begin[p] + cur[p]] = j;
         cur[p]++;
+    }
+    if (method & GG_PART_COLOR_SEP) {
+        // extension: the separator ordered by a greedy colouring of its own
+        // graph (first fit, ascending index), then by index -- the separator's
+        // triangles become a few levels instead of chains as long as its lines
+        const int s0 = begin[nparts];
+        std::vector<int> color(n, -1);
+        int ncol = 0;
+        for (int i = s0; i < n; i++) {
+            const int v = q[i];
+            std::vector<char> used(ncol + 1, 0);
+            for (int p = xadj[v]; p < xadj[v + 1]; p++) {
+                const int w = adj[p];
+                if (node_part[w] == nparts && color[w] >= 0) used[color[w]] = 1;
+            }
+            int c = 0;
+            while (used[c]) c++;
+            color[v] = c;
+            ncol = std::max(ncol, c + 1);
+        }
+        std::stable_sort(q.begin() + s0, q.end(), [&](int a, int b) { return color[a] < color[b]; });
+        for (int i = s0; i < n; i++) pinv[q[i]] = i;
     }
 }
 

@@ -39,7 +39,9 @@ int gg_host_wave2d(int n, const int *l_row_ptr, const int *l_col_idx, const doub
                    int *nx, int *ny);
 enum gg_part_method {
     GG_PART_BISECT = 0,    /* recursive BFS bisection of the node graph (METIS stand-in) */
-    GG_PART_BLOCKS = 1     /* contiguous index ranges (strips / slabs of a natural-order grid) */
+    GG_PART_BLOCKS = 1,    /* contiguous index ranges (strips / slabs of a natural-order grid) */
+    GG_PART_COLOR_SEP = 4  /* flag (extension): separator ordered by a greedy colouring of its
+                              graph, then by index, instead of by index alone */
 };
 /* nparts interiors + the separator part `nparts` (every endpoint of a cut edge
  * of the symmetrized pattern).  node_part[n]; part_size[nparts + 1];

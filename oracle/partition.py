@@ -51,6 +51,29 @@ def partition4_adjust(rp, ci, n, nparts, base):
     return node_part, part_size, pinv, q
 
 
+def color_separator(rp, ci, n, nparts, node_part, pinv, q):
+    """GG_PART_COLOR_SEP (an extension of partition4, not in the reference):
+    the separator part re-ordered by a greedy colouring of its own graph --
+    first fit over the separator's nodes in their partition4 order (ascending
+    index) -- then by index.  Returns the new pinv, q."""
+    nb = node_graph(rp, ci, n)
+    pinv, q = np.array(pinv), np.array(q)
+    s0 = int(np.sum(np.asarray(node_part) < nparts))
+    color = {}
+    for i in range(s0, n):
+        v = int(q[i])
+        used = {color[w] for w in nb[v] if node_part[w] == nparts and w in color}
+        c = 0
+        while c in used:
+            c += 1
+        color[v] = c
+    seg = sorted(range(s0, n), key=lambda i: (color[int(q[i])], i))
+    q[s0:] = [q[i] for i in seg]
+    for i in range(s0, n):
+        pinv[q[i]] = i
+    return pinv, q
+
+
 def blocks_base(n, nparts):
     """contiguous index ranges (GG_PART_BLOCKS)"""
     return [j * nparts // n for j in range(n)]

@@ -29,6 +29,11 @@ CASES = {
     "7pt_16_P4_bisect": (lambda: M.grid_7pt(16), 4, host.PART_BISECT, None, None),
     "sherman1_P4": (lambda: M.read_rua(fixture_path("sherman1.rua")), 4, host.PART_BISECT, None, None),
     "5pt_60x60_P1": (lambda: M.laplacian_5pt(60, 60), 1, host.PART_BLOCKS, 2, 0),
+    # the separator ordered by a greedy colouring (GG_PART_COLOR_SEP): a
+    # few-level separator solve on the dataflow kernel
+    "5pt_200x160_P4_color": (lambda: M.laplacian_5pt(200, 160), 4, host.PART_BLOCKS | host.PART_COLOR_SEP, 2, 0),
+    "7pt_16x16x32_P8_upwind_color": (lambda: M.grid_7pt(16, 16, 32, upwind=0.1), 8,
+                                     host.PART_BLOCKS | host.PART_COLOR_SEP, 3, 0),
 }
 
 _cache = {}

@@ -31,7 +31,38 @@ def test_partition4_blocks_exact(name, nparts):
 
 
 @pytest.mark.parametrize("name", sorted(GRIDS))
-@pytest.mark.parametrize("method", [H.PART_BLOCKS, H.PART_BISECT])
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+def test_partition4_color_separator_exact(name, nparts):
+    """GG_PART_COLOR_SEP: partition4, then the separator ordered by a greedy
+    colouring of its graph; exact vs the restatement, and each colour class of
+    the separator is an independent set in A's graph"""
+    A = GRIDS[name]()
+    n = A.shape[0]
+    got = H.partition(A, nparts, H.PART_BLOCKS | H.PART_COLOR_SEP)
+    node_part, part_size, pinv, q = OP.partition4_adjust(A.indptr, A.indices, n, nparts,
+                                                         OP.blocks_base(n, nparts))
+    pinv, q = OP.color_separator(A.indptr, A.indices, n, nparts, node_part, pinv, q)
+    assert np.array_equal(got["node_part"], node_part) and np.array_equal(got["part_size"], part_size)
+    assert np.array_equal(got["pinv"], pinv) and np.array_equal(got["q"], q)
+    # the separator's lower triangle is as deep as the colouring (greedy: at
+    # most max degree + 1 classes; well separated 5-point slabs' ladders take 2)
+    s0 = n - part_size[nparts]
+    nb = OP.node_graph(A.indptr, A.indices, n)
+    pos = {int(v): i for i, v in enumerate(q)}
+    lev, deg = {}, 0
+    for i in range(s0, n):
+        v = int(q[i])
+        sn = [w for w in nb[v] if node_part[w] == nparts]
+        deg = max(deg, len(sn))
+        lev[v] = 1 + max([lev[w] for w in sn if pos[w] < i], default=-1)
+    if n > s0:
+        assert max(lev.values()) + 1 <= deg + 1
+        if name == "5pt_40x30" and nparts <= 3:
+            assert max(lev.values()) + 1 <= 2
+
+
+@pytest.mark.parametrize("name", sorted(GRIDS))
+@pytest.mark.parametrize("method", [H.PART_BLOCKS, H.PART_BISECT, H.PART_BLOCKS | H.PART_COLOR_SEP])
 @pytest.mark.parametrize("nparts", [2, 4, 8])
 def test_arrow_structure(name, method, nparts):
     """interiors are mutually uncoupled; the separator is last; dd_form's blocks
