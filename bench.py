@@ -82,7 +82,11 @@ def parse():
     p.add_argument("--dd-sep", choices=["color", "natural"], default="color",
                    help="dd: separator order -- a greedy colouring of its graph (GG_PART_COLOR_SEP, "
                         "default: a few-level separator solve) or partition4's ascending index")
-    p.add_argument("--c5-steps", type=int, default=100)
+    p.add_argument("--division", choices=["rcp", "exact"], default="rcp",
+                   help="non-unit triangular solves: rcp = x = acc * RN(1/d) on the wavefront solves "
+                        "(gg_set_division GG_DIV_RCP, tolerance parity 1e-10, tests/test_gpu_fastdiv.py), "
+                        "exact = RN(acc / d), the reference's division bit for bit")
+    p.add_argument("--c5-steps", type=int, default=1000)
     p.add_argument("--c5-scenarios", type=int, default=1,
                    help="c5: independent source scenarios per GPU, solved concurrently (one solver, "
                         "stream and host thread each; GG_SOLVE_SHARED_DEVICE)")
@@ -100,7 +104,7 @@ PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # bare dependent-chain latency of one wavefront step (cycles, tools/lat_probe.hip:
 # "step(dpp)" = unit L, "U step (WD_RCP)" = U with the reciprocal-FMA division)
 # and the shader clock it ran at (profiles/r01_lat_probe.txt)
-CHAIN_CYCLES = {"trsv_L": 39.2, "trsv_U": 63.4}
+CHAIN_CYCLES = {"trsv_L": 39.2, "trsv_U": 63.4, "trsv_U_mul": 47.3}
 SHADER_GHZ = 2.396
 
 
@@ -383,10 +387,13 @@ def main():
                 KERNEL_NAMES[dom_] = KERNEL_NAMES[dom_][:-2] + f"{kilu + 1}>"
     else:
         s.set_precond_ilu0()
-        if c4 and os.environ.get("GG_WAVE3D_PLANES") != "1" and s.uses_wavefront:
-            # 3D 7-point: the 16-line x 4-plane tile wavefront (kernels.hip k_trsv_tile3d)
-            KERNEL_NAMES["trsv_L"] = "k_trsv_tile3d<true, 0, false>"
-            KERNEL_NAMES["trsv_U"] = "k_trsv_tile3d<false, 2, false>"
+    s.set_division(ggmres.DIV_RCP if a.division == "rcp" else ggmres.DIV_EXACT)
+    if s.uses_wavefront:
+        # the kernels the solver launches for L and U (2D band / 3D tile
+        # wavefront, skew, division mode), as rocprofv3 names them
+        KERNEL_NAMES["trsv_L"] = s.trsv_kernel(0)
+        KERNEL_NAMES["trsv_U"] = s.trsv_kernel(1)
+    u_mul = s.division_active(1) == ggmres.DIV_RCP
     t_setup = time.perf_counter() - t_setup
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -402,6 +409,7 @@ def main():
             s2 = ggmres.Solver(local)
             s2.set_matrix(A)
             s2.set_precond_ilu0()
+            s2.set_division(ggmres.DIV_RCP if a.division == "rcp" else ggmres.DIV_EXACT)
             solvers.append(s2)
         flags = ggmres.SOLVE_SHARED_DEVICE if S > 1 else 0
 
@@ -491,6 +499,11 @@ def main():
         if not fam:
             dom = "trsv_U"
         else:
+            # single-kernel families: SpMV, each triangular solve, and the
+            # orthogonalization when one launch per inner iteration does it
+            # (k_arnoldi_persist / k_arnoldi_wide)
+            if not c5 and s.mgs_kernel():
+                KERNEL_NAMES["mgs_givens"] = s.mgs_kernel()
             single = {k: v for k, v in fam.items() if k in KERNEL_NAMES}
             dom = max(single, key=lambda k: single[k]["share_of_step"]) if single else None
         if dom:
@@ -519,22 +532,27 @@ def main():
         f = timed[dom]
         if dom == "spmv":
             KERNEL_NAMES["spmv"] = "k_spmv_sell<false>" if s.spmv_sliced else "k_spmv_stream<false>"
-        kname = KERNEL_NAMES[dom] if (s.uses_wavefront or dom == "spmv") else \
-            ("k_trsv_level (one launch per dependency level; one 'launch' here = one triangle)"
-             if os.environ.get("GG_TRSV_LEVELS") == "1" else "k_trsv_flow")
+        if dom in ("trsv_L", "trsv_U") and not s.uses_wavefront:
+            kname = ("k_trsv_level (one launch per dependency level; one 'launch' here = one triangle)"
+                     if os.environ.get("GG_TRSV_LEVELS") == "1" else "k_trsv_flow")
+        else:
+            kname = KERNEL_NAMES[dom]
+        pmc_wl = "c4" if c4 else "c3s" if c3s else None
         roof = {"kernel": kname, "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": (pmc_traffic(KERNEL_NAMES[dom], "c4") if c4 else pmc_traffic(KERNEL_NAMES[dom]))
-                if (s.uses_wavefront or dom == "spmv") and not c3s and not kilu else None,
+                "traffic": pmc_traffic(kname, pmc_wl) if not kilu else None,
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
                 "launches_timed": f["launches"]}
+        if dom == "mgs_givens":
+            roof["alg_bytes_note"] = ("v_0..v_i and w read once, v_{i+1} written: 8 n (i+3) bytes at "
+                                      "cycle index i, averaged over the launches timed")
     # the triangular solves are latency-bound: their other roofline is the
     # dependency chain, nx + ny - 1 wavefront steps at the bare per-step chain
     # latency (tools/lat_probe.hip on MI355X, profiles/r01_lat_probe.txt)
     lat = None
     if roof and dom in ("trsv_L", "trsv_U") and s.uses_wavefront and not c5:
-        cyc = CHAIN_CYCLES["trsv_L" if dom == "trsv_L" else "trsv_U"]
+        cyc = CHAIN_CYCLES["trsv_L" if dom == "trsv_L" else "trsv_U_mul" if u_mul else "trsv_U"]
         # the DAG's longest path (ILU(k): skew k+1; 3D: nx + ny + nz - 2, whose
         # per-step chain is the 2D one: the tile kernel's plane term is off it)
         steps = 3 * a.c4_grid - 2 if c4 else a.grid + (kilu + 1) * (a.grid - 1)
@@ -593,6 +611,9 @@ def main():
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
                    "wavefront_sptrsv": s.uses_wavefront,
+                   "division": ("x = acc * RN(1/d) on the wavefront U solve (GG_DIV_RCP; tolerance "
+                                "parity 1e-10 vs the reference's division)") if u_mul else
+                               "x = RN(acc / d) (the reference's division, bit-exact)",
                    "parallelism": "single" if world == 1 else f"replicas{world}",
                    "setup_s": round(t_setup, 3)},
         "roofline": roof, "latency_roofline": lat,

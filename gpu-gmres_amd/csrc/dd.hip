@@ -53,6 +53,7 @@ struct Shard {
     long long nown = 0;
     // workspace
     DBuf<double> V, w, ww, r, rr, bb, t1, t2, xv, bv, partA, partB, H, s, cs, sn, ysm, hist;
+    DBuf<double> partC, hcgs;               // CGS2: P x (m+1) x G dot partials, the m+1 coefficients
     long long hist_cap = 0;
     DBuf<DevState> ds;
     DBuf<int> err;                          // P words (slot p is this shard's)
@@ -67,6 +68,16 @@ using Get = std::function<double *(Shard &)>;
 struct gg_dd {
     int device = 0, P = 1, kind = GG_DD_LOCAL, rank = 0;
     ncclComm_t comm = nullptr;
+    // GG_DD_IPC: this rank's exchange area (uncached device memory), every
+    // rank's area as mapped here (hipIpcOpenMemHandle; own = ipc_area), the
+    // per-exchange sequence number (identical on every rank: every rank
+    // enqueues the same exchanges in the same order) and the error word
+    void *ipc_area = nullptr;
+    long long ipc_capd = 0;
+    IpcPeers ipc{};
+    bool ipc_connected = false;
+    unsigned long long ipc_seq = 0;
+    DBuf<int> xerr;
     hipStream_t st = nullptr;
     hipStream_t st2 = nullptr;              // the SpMV's interface exchange, beside the interior rows
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evx = nullptr, evh = nullptr;
@@ -77,6 +88,7 @@ struct gg_dd {
     int G = 1;
     std::vector<std::unique_ptr<Shard>> sh;
     int m_alloc = -1;
+    bool cgs2 = false;                      // GG_SOLVE_CGS2 for the solve in progress
     std::vector<double> last_hist;
     DBuf<double> nat_a, nat_b;
     DBuf<long long> dtmp;
@@ -115,9 +127,43 @@ Gate gate_mask(Shard &s, int mask)
     return g;
 }
 
+// GG_DD_IPC: enqueue one all-gather of cnt doubles (slot q at buf + q*cnt)
+void ipc_allgather(gg_dd *d, double *buf, long long cnt, hipStream_t st)
+{
+    GG_REQUIRE(d->ipc_connected, GG_ESTATE, "dd: IPC exchange used before gg_dd_ipc_connect");
+    GG_REQUIRE(cnt <= d->ipc_capd, GG_EINVAL,
+               "dd: IPC exchange of " + std::to_string(cnt) + " doubles exceeds the area's " +
+                   std::to_string(d->ipc_capd) + " per rank (GG_DD_IPC_CAP)");
+    launch_ipc_allgather(d->ipc, d->rank, d->P, buf, cnt, ++d->ipc_seq, d->ipc_capd, d->xerr.p, st);
+}
+void ipc_check(gg_dd *d)
+{
+    int e = 0;
+    GG_HIP(hipMemcpyAsync(&e, d->xerr.p, sizeof(int), hipMemcpyDeviceToHost, d->st));
+    GG_HIP(hipStreamSynchronize(d->st));
+    GG_REQUIRE((e & 4) == 0, GG_ETIMEOUT, "dd: IPC exchange: a peer did not arrive within 30 s");
+}
+// GG_DD_IPC, host-synchronous (setup, error checks): every rank's value
+std::vector<long long> ipc_allgather_host(gg_dd *d, long long v)
+{
+    DBuf<double> b;
+    b.alloc(d->P);
+    GG_HIP(hipMemsetAsync(b.p, 0, d->P * sizeof(double), d->st));
+    GG_HIP(hipMemcpyAsync(b.p + d->rank, &v, sizeof(v), hipMemcpyHostToDevice, d->st));
+    ipc_allgather(d, b.p, 1, d->st);
+    std::vector<long long> out(d->P);
+    GG_HIP(hipMemcpyAsync(out.data(), b.p, d->P * sizeof(long long), hipMemcpyDeviceToHost, d->st));
+    ipc_check(d);
+    return out;
+}
+
 // max over all shards of all processes (setup only: host-synchronous)
 long long agree_max(gg_dd *d, long long v)
 {
+    if (d->kind == GG_DD_IPC && d->P > 1) {
+        for (long long w : ipc_allgather_host(d, v)) v = std::max(v, w);
+        return v;
+    }
     if (d->kind != GG_DD_RCCL || d->P == 1) return v;
     DBuf<long long> b;
     b.alloc(1);
@@ -136,6 +182,8 @@ void exchange(gg_dd *d, const Get &buf, long long off, long long cnt, hipStream_
         Shard &s = *d->sh[0];
         double *b = buf(s) + off;
         GG_NCCL(ncclAllGather(b + (long long)s.p * cnt, b, (size_t)cnt, ncclDouble, d->comm, st));
+    } else if (d->kind == GG_DD_IPC) {
+        ipc_allgather(d, buf(*d->sh[0]) + off, cnt, st);
     } else {
         ShardPtrs ptr{};
         for (int q = 0; q < d->P; q++) ptr.p[q] = buf(*d->sh[q]);
@@ -248,6 +296,9 @@ void ensure_workspace(gg_dd *d, int m)
         }
         s.H.alloc((size_t)(m + 1) * m);
         GG_HIP(hipMemsetAsync(s.H.p, 0, (size_t)(m + 1) * m * sizeof(double), d->st));
+        s.partC.alloc((size_t)d->P * (m + 1) * d->G);
+        GG_HIP(hipMemsetAsync(s.partC.p, 0, (size_t)d->P * (m + 1) * d->G * sizeof(double), d->st));
+        s.hcgs.alloc(m + 1);
         s.s.alloc(m + 1);
         s.cs.alloc(m + 1);
         s.sn.alloc(m + 1);
@@ -278,6 +329,34 @@ void enqueue_cycle(gg_dd *d, int m)
         const Get vi = [i, Pl](Shard &s) { return s.V.p + (long long)i * Pl; };
         spmv(d, i, vi, vec(&Shard::ww));                                        // ww = A v_i
         apply_minv(d, i, 0, vec(&Shard::ww), vec(&Shard::w));                   // w = M^-1 ww
+        if (d->cgs2) {
+            // CGS2: h = V^T w, w -= V h, h2 = V^T w, w -= V h2 (+ the norm's
+            // partials), H[:, i] = h + h2 -- three all-gathers
+            const long long cnt = (long long)(i + 1) * d->G;
+            for (int pass = 0; pass < 2; pass++) {
+                for (auto &sp : d->sh) {
+                    Shard &s = *sp;
+                    launch_multidot(gate_i(s, i), s.w.p, s.V.p, Pl, i + 1, s.partC.p + (long long)s.p * cnt, d->G,
+                                    dot_len(d, s), d->st);
+                }
+                exchange(d, vec(&Shard::partC), 0, cnt);
+                for (auto &sp : d->sh) {
+                    Shard &s = *sp;
+                    launch_cgs_reduce(gate_i(s, i), s.partC.p, d->P, d->G, cnt, i + 1, s.hcgs.p, s.H.p, i, m,
+                                      pass == 1, d->st);
+                    launch_cgs_update(gate_i(s, i), s.w.p, s.V.p, Pl, s.hcgs.p, i + 1, d->G, H0, dot_len(d, s),
+                                      pass == 1 ? s.partA.p + (long long)s.p * d->G : nullptr, d->st);
+                }
+            }
+            exchange(d, vec(&Shard::partA), 0, d->G);
+            for (auto &sp : d->sh) {
+                Shard &s = *sp;
+                launch_arnoldi_finalize_r(gate_i(s, i), i, m, s.ds.p, s.partA.p, NP, d->G, s.w.p,
+                                          s.V.p + (long long)(i + 1) * Pl, s.H.p, s.cs.p, s.sn.p, s.s.p,
+                                          s.hist.p, H0, d->st);
+            }
+            continue;
+        }
         dot(d, i, 0, vec(&Shard::w), [](Shard &s) { return s.V.p; }, &Shard::partA);
         DBuf<double> Shard::*pin = &Shard::partA, Shard::*pout = &Shard::partB;
         for (int k = 0; k <= i; k++) {
@@ -326,11 +405,22 @@ DevState read_state(gg_dd *d)
 struct RcpFallback {};
 void check_err(gg_dd *d)
 {
+    int any = 0;
     if (d->kind == GG_DD_RCCL && d->P > 1) {
         Shard &s = *d->sh[0];
         GG_NCCL(ncclAllGather(s.err.p + s.p, s.err.p, 1, ncclInt32, d->comm, d->st));
     }
-    int any = 0;
+    if (d->kind == GG_DD_IPC) {
+        ipc_check(d);
+        if (d->P > 1) {
+            // the shards' error words (this rank's own slot), OR-ed over the ranks
+            Shard &s = *d->sh[0];
+            int mine = 0;
+            GG_HIP(hipMemcpyAsync(&mine, s.err.p + s.p, sizeof(int), hipMemcpyDeviceToHost, d->st));
+            GG_HIP(hipStreamSynchronize(d->st));
+            for (long long w : ipc_allgather_host(d, mine)) any |= (int)w;
+        }
+    }
     for (auto &sp : d->sh) {
         std::vector<int> e(d->P, 0);
         GG_HIP(hipMemcpyAsync(e.data(), sp->err.p, d->P * sizeof(int), hipMemcpyDeviceToHost, d->st));
@@ -375,6 +465,8 @@ int solve_once(gg_dd *d, const double *d_b, double *d_x, const gg_options *opt, 
     const int m = opt->restart;
     GG_REQUIRE(m >= 1 && m <= 512, GG_EINVAL, "gg_dd_solve: restart must be in [1, 512]");
     GG_REQUIRE(opt->max_iter >= 0, GG_EINVAL, "gg_dd_solve: negative max_iter");
+    GG_REQUIRE((opt->flags & ~GG_SOLVE_CGS2) == 0, GG_EINVAL, "gg_dd_solve: unknown flags");
+    d->cgs2 = (opt->flags & GG_SOLVE_CGS2) != 0;
     set_dev(d);
     ensure_workspace(d, m);
     const long long need = (long long)opt->max_iter + opt->max_iter / m + 4;
@@ -512,7 +604,7 @@ void set_system(gg_dd *d, const Csr &A, int method)
     d->q = plan.q;
     // pass 1: host pieces and region layouts of this process's shards
     std::vector<int> mine;
-    if (d->kind == GG_DD_RCCL) mine.push_back(d->rank);
+    if (d->kind != GG_DD_LOCAL) mine.push_back(d->rank);
     else for (int p = 0; p < d->P; p++) mine.push_back(p);
     std::vector<DDShardHost> hs;
     d->sh.clear();
@@ -594,7 +686,7 @@ void set_system(gg_dd *d, const Csr &A, int method)
             s.slot2perm[lslot[r]] = H.rows[r];
         }
         s.slot2nat.upload(s2n, d->st);
-        const bool own_sep = d->kind == GG_DD_RCCL || s.p == 0;
+        const bool own_sep = d->kind != GG_DD_LOCAL || s.p == 0;
         for (int r = 0; r < nI + (own_sep ? nS : 0); r++) {
             os.push_back(lslot[r]);
             on.push_back(plan.q[H.rows[r]]);
@@ -641,14 +733,17 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
     GG_API_BEGIN
     GG_REQUIRE(out, GG_EINVAL, "null out");
     GG_REQUIRE(nparts >= 1 && nparts <= kMaxShards, GG_EINVAL, "dd: nparts must be in [1, 16]");
-    GG_REQUIRE(comm == GG_DD_LOCAL || comm == GG_DD_RCCL, GG_EINVAL, "dd: unknown communicator");
-    GG_REQUIRE(comm == GG_DD_LOCAL || (id && rank >= 0 && rank < nparts), GG_EINVAL,
+    GG_REQUIRE(comm == GG_DD_LOCAL || comm == GG_DD_RCCL || comm == GG_DD_IPC, GG_EINVAL,
+               "dd: unknown communicator");
+    GG_REQUIRE(comm != GG_DD_RCCL || (id && rank >= 0 && rank < nparts), GG_EINVAL,
                "dd: RCCL needs an id and 0 <= rank < nparts");
+    GG_REQUIRE(comm != GG_DD_IPC || (rank >= 0 && rank < nparts), GG_EINVAL,
+               "dd: IPC needs 0 <= rank < nparts");
     auto d = std::make_unique<gg_dd>();
     d->device = device;
     d->P = nparts;
     d->kind = comm;
-    d->rank = comm == GG_DD_RCCL ? rank : 0;
+    d->rank = comm == GG_DD_LOCAL ? 0 : rank;
     set_dev(d.get());
     GG_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
     GG_HIP(hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking));
@@ -660,6 +755,21 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
         GG_NCCL(ncclCommInitRank(&d->comm, nparts, u, rank));
+    }
+    if (comm == GG_DD_IPC) {
+        // [flags kMaxShards x kIpcXB u64 (zero: sequence numbers start at 1)]
+        // [data 2 x nparts x capd doubles], uncached so that peers' stores and
+        // this rank's polls meet in memory
+        const char *cap = std::getenv("GG_DD_IPC_CAP");
+        d->ipc_capd = cap ? std::max(1LL, atoll(cap)) : (1LL << 20);
+        const size_t bytes = sizeof(double) * ((size_t)kMaxShards * kIpcXB + 2ull * nparts * d->ipc_capd);
+        GG_HIP(hipExtMallocWithFlags(&d->ipc_area, bytes, hipDeviceMallocUncached));
+        GG_HIP(hipMemset(d->ipc_area, 0, bytes));
+        GG_HIP(hipDeviceSynchronize());
+        d->xerr.alloc(1);
+        GG_HIP(hipMemset(d->xerr.p, 0, sizeof(int)));
+        d->ipc.base[rank] = d->ipc_area;
+        d->ipc_connected = nparts == 1;
     }
     *out = d.release();
     return GG_OK;
@@ -675,6 +785,13 @@ int gg_dd_destroy(gg_dd *d)
     d->nat_a.release();
     d->nat_b.release();
     if (d->comm) (void)ncclCommDestroy(d->comm);
+    if (d->ipc_area) {
+        (void)hipDeviceSynchronize();
+        for (int q = 0; q < d->P; q++)
+            if (q != d->rank && d->ipc.base[q]) (void)hipIpcCloseMemHandle(d->ipc.base[q]);
+        (void)hipFree(d->ipc_area);
+    }
+    d->xerr.release();
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
     if (d->evx) (void)hipEventDestroy(d->evx);
@@ -686,12 +803,58 @@ int gg_dd_destroy(gg_dd *d)
     return GG_OK;
 }
 
+int gg_dd_ipc_handle(gg_dd *d, unsigned char *handle)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && handle, GG_EINVAL, "null argument");
+    GG_REQUIRE(d->kind == GG_DD_IPC, GG_ESTATE, "dd: not an IPC communicator");
+    static_assert(sizeof(hipIpcMemHandle_t) <= GG_DD_IPC_HANDLE_BYTES, "hipIpcMemHandle_t size");
+    set_dev(d);
+    hipIpcMemHandle_t h;
+    GG_HIP(hipIpcGetMemHandle(&h, d->ipc_area));
+    std::memset(handle, 0, GG_DD_IPC_HANDLE_BYTES);
+    std::memcpy(handle, &h, sizeof(h));
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_ipc_connect(gg_dd *d, const unsigned char *handles)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && handles, GG_EINVAL, "null argument");
+    GG_REQUIRE(d->kind == GG_DD_IPC, GG_ESTATE, "dd: not an IPC communicator");
+    GG_REQUIRE(!d->ipc_connected || d->P == 1, GG_ESTATE, "dd: IPC areas already connected");
+    set_dev(d);
+    for (int q = 0; q < d->P; q++) {
+        if (q == d->rank) continue;
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)q * GG_DD_IPC_HANDLE_BYTES, sizeof(h));
+        void *p = nullptr;
+        GG_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        d->ipc.base[q] = p;
+    }
+    d->ipc_connected = true;
+    // a first exchange: every rank has mapped every area before anyone moves on
+    (void)ipc_allgather_host(d, d->rank);
+    return GG_OK;
+    GG_API_END
+}
+
 int gg_dd_comm_ranks(gg_dd *d, int *ranks, int *rank)
 {
     GG_API_BEGIN
     GG_REQUIRE(d && ranks, GG_EINVAL, "null argument");
     int c = 1;
     if (d->kind == GG_DD_RCCL) GG_NCCL(ncclCommCount(d->comm, &c));
+    if (d->kind == GG_DD_IPC) {
+        c = 0;
+        for (int q = 0; q < d->P; q++) c += d->ipc.base[q] != nullptr;
+        if (d->P > 1) {
+            // every rank reports its own rank: the ranks are distinct and complete
+            const std::vector<long long> r = ipc_allgather_host(d, d->rank);
+            for (int q = 0; q < d->P; q++) GG_REQUIRE(r[q] == q, GG_ECOMM, "dd: IPC rank mismatch");
+        }
+    }
     *ranks = c;
     if (rank) *rank = d->rank;
     return GG_OK;

@@ -230,8 +230,10 @@ struct DevCsr {
     void copy_from(const DevCsr &o, hipStream_t st);   // device-side duplicate
 };
 
-// wavefront division modes: unit diagonal, IEEE division, reciprocal + FMA corrections
-enum WaveDiv { WD_UNIT = 0, WD_HW = 1, WD_RCP = 2 };
+// wavefront division modes: unit diagonal, IEEE division, reciprocal + FMA
+// corrections (both RN(acc/d)), multiply by the reciprocal (gg_set_division
+// GG_DIV_RCP: RN(acc * RN(1/d)), tolerance parity)
+enum WaveDiv { WD_UNIT = 0, WD_HW = 1, WD_RCP = 2, WD_MUL = 3 };
 
 // device triangular solve
 struct DevTri {
@@ -257,9 +259,14 @@ struct DevTri {
     DBuf<int> order;             // 3D tiles: forward dependency order (the backward solve reverses it)
     int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
     bool rcp_ok = false;         // every divisor admits WD_RCP
+    bool mul_ok = false;         // every 1/d is finite and normal (WD_MUL admissible; rw uploaded)
+    bool fast = false;           // the owner asked for WD_MUL (gg_set_division)
+    int eff_div() const { return (fast && mul_ok && div != WD_UNIT) ? (int)WD_MUL : div; }
     DBuf<unsigned long long> bnd;  // nbands * T hand-off granules (sentinel = not ready) + 128 dummies
     long long *trace = nullptr;  // diagnostics: per band, nbatch+1 timestamps (gg_trace_precond)
     double bytes = 0;            // algorithmic bytes per solve
+    double bytes_mul = 0;        // the same with WD_MUL (y streamed in place of d (, y))
+    double alg_bytes() const { return eff_div() == WD_MUL ? bytes_mul : bytes; }
 };
 
 // device triangle from a canonical one: WAVE2D when `wl` is an active grid

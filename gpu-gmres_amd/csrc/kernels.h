@@ -76,6 +76,13 @@ struct ShardPtrs { double *p[kMaxShards]; };
 void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long cnt, hipStream_t st);
 void launch_scatter_idx(const double *in, const long long *src, const long long *dst, double *out,
                         long long n, hipStream_t st);   // out[dst[i]] = in[src[i]]
+// GG_DD_IPC: the exchange areas of all ranks as mapped in this process
+constexpr int kIpcXB = 64;             // blocks (flag words per source rank) of one exchange
+struct IpcPeers { void *base[kMaxShards]; };
+// all-gather of cnt doubles per rank: slot q at buf + q*cnt (this rank's slot
+// me already in place); err |= 4 when a peer did not arrive in time
+void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long long cnt,
+                          unsigned long long seq, long long capd, int *err, hipStream_t st);
 
 // ---- split (PG) elementwise maps -------------------------------------------
 void launch_mul(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in*s
@@ -107,6 +114,16 @@ void launch_mgs_step(Gate g, int i, int k, int m, double *w, const double *vk, c
 void launch_mgs_step_r(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
                        const double *part_in, int nparts_in, double *part_out, double *H, int G,
                        long long Ppad, long long Pdot, hipStream_t st);
+// CGS2 (sharded solve, GG_SOLVE_CGS2): block partials of <w, v_k>, k < nk, at
+// part[k*G + b]; every shard's partials of dot k summed into h[k] (shard q's
+// slot at part + q*cnt) and into H[k, i] (add: +=); w -= sum_k h[k] v_k with
+// the norm's block partials when part_norm is given
+void launch_multidot(Gate g, const double *w, const double *V, long long ldv, int nk, double *part, int G,
+                     long long Pdot, hipStream_t st);
+void launch_cgs_reduce(Gate g, const double *part, int P, int G, long long cnt, int nk, double *h, double *H,
+                       int i, int m, bool add, hipStream_t st);
+void launch_cgs_update(Gate g, double *w, const double *V, long long ldv, const double *h, int nk, int G,
+                       long long Ppad, long long Pdot, double *part_norm, hipStream_t st);
 void launch_arnoldi_finalize_r(Gate g, int i, int m, DevState *ds, const double *part, int nparts_in,
                                int G, const double *w, double *vnext, double *H, double *cs,
                                double *sn, double *s, double *hist, long long Ppad, hipStream_t st);

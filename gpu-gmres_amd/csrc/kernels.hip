@@ -169,6 +169,60 @@ __global__ void k_allgather_local(ShardPtrs b, int P, long long off, long long c
             if (q != src) b.p[q][off + e] = v;
     }
 }
+// GG_DD_IPC all-gather: one process per shard, every shard's exchange area
+// mapped into every process (hipIpc; xGMI between GPUs).  Area of rank q:
+// [flags: kMaxShards x kIpcXB u64][data: 2 parities x P slots x capd doubles].
+// Block b owns chunk b of the cnt exchanged doubles: it stores the chunk of
+// this rank's slot (buf + me*cnt) into every peer's data[seq & 1][me], releases
+// flag[me][b] = seq at system scope in every peer's area, then waits (acquire,
+// time-bounded) until every peer's flag[q][b] in this rank's area reached seq
+// and copies those chunks to buf + q*cnt.  Sequence numbers only grow, so the
+// flags are never re-armed; two parities suffice because a rank enters
+// exchange k+1 only after every peer has entered exchange k, i.e. after it has
+// finished copying out exchange k-1.  The area is uncached device memory
+// (hipDeviceMallocUncached): remote stores and local polls need no cache
+// maintenance beyond the system-scope release / acquire.
+__global__ __launch_bounds__(kBlock) void k_ipc_allgather(IpcPeers pp, int me, int P, double *buf,
+                                                          long long cnt, unsigned long long seq,
+                                                          long long capd, int *err)
+{
+    const int nb = gridDim.x, b = blockIdx.x, t = threadIdx.x;
+    const long long chunk = (cnt + nb - 1) / nb;
+    const long long lo = (long long)b * chunk, hi = lo + chunk < cnt ? lo + chunk : cnt;
+    const int par = (int)(seq & 1);
+    constexpr long long kFlagWords = (long long)kMaxShards * kIpcXB;
+    const double *src = buf + (long long)me * cnt;
+    for (int q = 0; q < P; q++) {
+        if (q == me) continue;
+        double *dst = reinterpret_cast<double *>(pp.base[q]) + kFlagWords + ((long long)par * P + me) * capd;
+        for (long long e = lo + t; e < hi; e += kBlock) dst[e] = src[e];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (t < P && t != me) {
+        unsigned long long *f = reinterpret_cast<unsigned long long *>(pp.base[t]) + (long long)me * kIpcXB + b;
+        __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // wait for peer t's chunk b in this rank's area (bounded: ~30 s of the 100 MHz clock)
+        const unsigned long long *w = reinterpret_cast<const unsigned long long *>(pp.base[me]) +
+                                      (long long)t * kIpcXB + b;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+                atomicOr(err, 4);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    for (int q = 0; q < P; q++) {
+        if (q == me) continue;
+        const double *rcv = reinterpret_cast<const double *>(pp.base[me]) + kFlagWords + ((long long)par * P + q) * capd;
+        double *dst = buf + (long long)q * cnt;
+        for (long long e = lo + t; e < hi; e += kBlock) dst[e] = rcv[e];
+    }
+}
+
 // out[dst[i]] = in[src[i]]
 __global__ void k_scatter_idx(const double *in, const long long *src, const long long *dst,
                               double *out, long long n)
@@ -557,6 +611,11 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
 // needs every intermediate in the normal range: the host admits WD_RCP only for
 // 2^-100 <= |d| <= 2^100, and the writer wave flags results outside rcp_safe
 // (err bit 2), on which the caller repeats the work with WD_HW.
+// WD_MUL (gg_set_division(GG_DIV_RCP), tolerance parity): x = RN(acc * y) with
+// the streamed y = RN(1/d) in place of d -- within about one ulp of RN(acc/d)
+// per row, one dependent multiply instead of five operations, four streamed
+// arrays instead of five.  The oracle restates it (orc_set_div_mode) for the
+// order-matched checks; the host admits it when every 1/d is finite and normal.
 // Steps per batch: one barrier, one boundary hand-over and one LDS-latency
 // exposure per batch, so longer is cheaper per step, as far as the LDS budget
 // lets the ring hold kWaveRing of them (GG_WAVE_BATCH_UNIT for the unit
@@ -618,12 +677,12 @@ struct WaveCfg {
     // streamed arrays: b, c1, c2 (, d (, RN(1/d))); a skewed 2D grid (ILU(S-1))
     // adds the fill coefficients of offsets nx-1 .. nx-S+1; a 3D grid adds the
     // plane coefficient c0 and the previous plane's x
-    static constexpr int AE = DIV == WD_UNIT ? 3 : DIV == WD_HW ? 4 : 5;    // first fill array
+    static constexpr int AE = DIV == WD_UNIT ? 3 : DIV == WD_RCP ? 5 : 4;   // first fill array (WD_MUL streams y as d)
     static constexpr int A2 = AE + (S - 1);
     static constexpr int A = A2 + (D3 ? 2 : 0);
     static constexpr int B16 = DIV == WD_UNIT ? GG_WAVE_BATCH_UNIT
-                             : DIV == WD_HW   ? GG_WAVE_BATCH_HW
-                                              : GG_WAVE_BATCH_RCP;
+                             : DIV == WD_RCP  ? GG_WAVE_BATCH_RCP
+                                              : GG_WAVE_BATCH_HW;
     // steps per batch: 8 where 16-step slots of A arrays would not leave room for 3 slots
     static constexpr int B = (B16 == 16 && 3 * A * 8 * 64 + 64 + 2 * 8 * 64 > 150 * 1024 / 16) ? 8 : B16;
     static constexpr int PBN = B / 2;                                     // step pairs per batch
@@ -1090,6 +1149,8 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 acc = acc - p2;
                 if constexpr (DIV == WD_HW) {
                     acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
+                } else if constexpr (DIV == WD_MUL) {
+                    acc = acc * (sx ? rg[kk][3].x : rg[kk][3].y);
                 } else if constexpr (DIV == WD_RCP) {
                     const double d = sx ? rg[kk][3].x : rg[kk][3].y;
                     const double y = sx ? rg[kk][4].x : rg[kk][4].y;
@@ -1179,7 +1240,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 #endif
 template <int DIV>
 struct TileCfg {
-    static constexpr int A = DIV == WD_UNIT ? 4 : DIV == WD_HW ? 5 : 6;
+    static constexpr int A = DIV == WD_UNIT ? 4 : DIV == WD_RCP ? 6 : 5;   // WD_MUL streams y as d
     static constexpr int AC0 = A - 1;                   // the plane coefficient streams last
     static constexpr int B = GG_TILE_BATCH;
     static constexpr int PBN = B / 2;
@@ -1590,6 +1651,8 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                 acc = acc - p2;
                 if constexpr (DIV == WD_HW) {
                     acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
+                } else if constexpr (DIV == WD_MUL) {
+                    acc = acc * (sx ? rg[kk][3].x : rg[kk][3].y);
                 } else if constexpr (DIV == WD_RCP) {
                     const double d = sx ? rg[kk][3].x : rg[kk][3].y;
                     const double y = sx ? rg[kk][4].x : rg[kk][4].y;
@@ -2096,6 +2159,89 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
     }
     acc = block_sum(acc);
     if (threadIdx.x == 0) part_out[blockIdx.x] = acc;
+}
+
+// ---- CGS2 (the sharded solve's GG_SOLVE_CGS2): classical Gram-Schmidt with
+// one re-orthogonalization, h = V^T w; w -= V h; h2 = V^T w; w -= V h2;
+// H[:, i] = h + h2 -- three all-gathers per inner iteration (h, h2, ||w||)
+// instead of MGS's i + 2.  Every dot keeps k_dot's tree (thread t of block b:
+// units b*256 + t + j*G*256 ascending, block_sum), so the oracle restates it
+// bit for bit (orc_set_orth).
+constexpr int kCgsKC = 8;                  // dots per block of k_multidot
+__global__ __launch_bounds__(kBlock) void k_multidot(Gate g, const double *__restrict__ w,
+                                                     const double *__restrict__ V, long long ldv, int nk,
+                                                     double *part, int G, long long dunits)
+{
+    // part[k*G + blockIdx.x] = block partial of <w, v_k>, k = blockIdx.y*kCgsKC + kk < nk
+    if (gated(g)) return;
+    const int k0 = blockIdx.y * kCgsKC;
+    const int kc = nk - k0 < kCgsKC ? nk - k0 : kCgsKC;
+    double acc[kCgsKC];
+#pragma unroll
+    for (int kk = 0; kk < kCgsKC; kk++) acc[kk] = 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < dunits; u += stride) {
+        const double2 a = ld2(w, u);
+#pragma unroll
+        for (int kk = 0; kk < kCgsKC; kk++) {
+            if (kk < kc) {
+                const double2 b = ld2_nt(V + (long long)(k0 + kk) * ldv, u);
+                acc[kk] += a.x * b.x;
+                acc[kk] += a.y * b.y;
+            }
+        }
+    }
+    for (int kk = 0; kk < kc; kk++) {
+        const double r = block_sum(acc[kk]);
+        if (threadIdx.x == 0) part[(long long)(k0 + kk) * G + blockIdx.x] = r;
+    }
+}
+// h[k] = sum of every shard's partials of dot k (shard q's at part + q*cnt + k*G,
+// summed in sum_partials' order over the P*G partials, shard-major);
+// add = 0: H[k, i] = h[k]; add = 1: H[k, i] += h[k].  One block per k.
+__global__ __launch_bounds__(kBlock) void k_cgs_reduce(Gate g, const double *part, int P, int G, long long cnt,
+                                                       double *h, double *H, int i, int m, int add)
+{
+    if (gated(g)) return;
+    const int k = blockIdx.x;
+    double v = 0.0;
+    for (int e = threadIdx.x; e < P * G; e += kBlock) v += part[(long long)(e / G) * cnt + (long long)k * G + e % G];
+    v = block_sum(v);
+    if (threadIdx.x == 0) {
+        h[k] = v;
+        double *hk = H + k + (long long)i * (m + 1);
+        *hk = add ? *hk + v : v;
+    }
+}
+// w = w - sum_k h[k] v_k (per element, k ascending: w = (-h_k) v_k + w as the
+// MGS AXPY); norm: block partials of <w, w> over [0, dunits) into part_norm
+template <bool NORM>
+__global__ __launch_bounds__(kBlock) void k_cgs_update(Gate g, double *__restrict__ w,
+                                                       const double *__restrict__ V, long long ldv,
+                                                       const double *h, int nk, long long units,
+                                                       long long dunits, double *part_norm)
+{
+    if (gated(g)) return;
+    double acc = 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units; u += stride) {
+        double2 a = ld2(w, u);
+        for (int k = 0; k < nk; k++) {
+            const double2 b = ld2_nt(V + (long long)k * ldv, u);
+            const double c = -h[k];
+            a.x = c * b.x + a.x;
+            a.y = c * b.y + a.y;
+        }
+        st2(w, u, a);
+        if (NORM && u < dunits) {
+            acc += a.x * a.x;
+            acc += a.y * a.y;
+        }
+    }
+    if (NORM) {
+        acc = block_sum(acc);
+        if (threadIdx.x == 0) part_norm[blockIdx.x] = acc;
+    }
 }
 
 __device__ __forceinline__ void apply_rot(double &dx, double &dy, double cs, double sn)
@@ -2637,6 +2783,13 @@ void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long 
     if (P <= 1 || cnt == 0) return;
     k_allgather_local<<<blocks_for(P * cnt, kBlock, 8192), kBlock, 0, st>>>(b, P, off, cnt);
 }
+void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long long cnt,
+                          unsigned long long seq, long long capd, int *err, hipStream_t st)
+{
+    // every rank must pick the same block count for the same cnt
+    const int nb = (int)std::min<long long>(kIpcXB, std::max<long long>(1, (cnt + 2047) / 2048));
+    k_ipc_allgather<<<nb, kBlock, 0, st>>>(pp, me, P, buf, cnt, seq, capd, err);
+}
 void launch_scatter_idx(const double *in, const long long *src, const long long *dst, double *out,
                         long long n, hipStream_t st)
 {
@@ -2722,15 +2875,17 @@ int tile_batch_steps() { return GG_TILE_BATCH; }
 
 int wave_batch_steps(int div, bool d3, int skew)
 {
-    if (d3) return div == WD_UNIT ? WaveCfg<WD_UNIT, true>::B : div == WD_HW ? WaveCfg<WD_HW, true>::B
-                                                                              : WaveCfg<WD_RCP, true>::B;
+    // WD_MUL streams as many arrays as WD_HW (y in d's place): the same batches
+    const bool hw = div == WD_HW || div == WD_MUL;
+    if (d3) return div == WD_UNIT ? WaveCfg<WD_UNIT, true>::B : hw ? WaveCfg<WD_HW, true>::B
+                                                                   : WaveCfg<WD_RCP, true>::B;
     if (skew == 2)
-        return div == WD_UNIT ? WaveCfg<WD_UNIT, false, 2>::B : div == WD_HW ? WaveCfg<WD_HW, false, 2>::B
-                                                                             : WaveCfg<WD_RCP, false, 2>::B;
+        return div == WD_UNIT ? WaveCfg<WD_UNIT, false, 2>::B : hw ? WaveCfg<WD_HW, false, 2>::B
+                                                                   : WaveCfg<WD_RCP, false, 2>::B;
     if (skew == 3)
-        return div == WD_UNIT ? WaveCfg<WD_UNIT, false, 3>::B : div == WD_HW ? WaveCfg<WD_HW, false, 3>::B
-                                                                             : WaveCfg<WD_RCP, false, 3>::B;
-    return div == WD_UNIT ? WaveCfg<WD_UNIT>::B : div == WD_HW ? WaveCfg<WD_HW>::B : WaveCfg<WD_RCP>::B;
+        return div == WD_UNIT ? WaveCfg<WD_UNIT, false, 3>::B : hw ? WaveCfg<WD_HW, false, 3>::B
+                                                                   : WaveCfg<WD_RCP, false, 3>::B;
+    return div == WD_UNIT ? WaveCfg<WD_UNIT>::B : hw ? WaveCfg<WD_HW>::B : WaveCfg<WD_RCP>::B;
 }
 
 void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st)
@@ -2776,8 +2931,10 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         }
     } else if (T.kind == DevTri::WAVE2D) {
         const Wave2D &w = T.wl;
-        const double *dv = T.div == WD_UNIT ? nullptr : T.dw.p;
-        const double *rv = T.div == WD_RCP ? T.rw.p : nullptr;
+        const int div = T.eff_div();
+        // WD_MUL streams y = RN(1/d) in d's place
+        const double *dv = div == WD_UNIT ? nullptr : div == WD_MUL ? T.rw.p : T.dw.p;
+        const double *rv = div == WD_RCP ? T.rw.p : nullptr;
         if (w.tile) {
             // 3D tiles: persistent, every workgroup co-resident (tiles wait on tiles)
             const int ntask = w.nbands;
@@ -2794,12 +2951,14 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
                 nullptr);                                                                          \
     } while (0)
             if (T.lower) {
-                if (T.div == WD_UNIT) GG_TILE_LAUNCH(true, WD_UNIT);
-                else if (T.div == WD_HW) GG_TILE_LAUNCH(true, WD_HW);
+                if (div == WD_UNIT) GG_TILE_LAUNCH(true, WD_UNIT);
+                else if (div == WD_HW) GG_TILE_LAUNCH(true, WD_HW);
+                else if (div == WD_MUL) GG_TILE_LAUNCH(true, WD_MUL);
                 else GG_TILE_LAUNCH(true, WD_RCP);
             } else {
-                if (T.div == WD_UNIT) GG_TILE_LAUNCH(false, WD_UNIT);
-                else if (T.div == WD_HW) GG_TILE_LAUNCH(false, WD_HW);
+                if (div == WD_UNIT) GG_TILE_LAUNCH(false, WD_UNIT);
+                else if (div == WD_HW) GG_TILE_LAUNCH(false, WD_HW);
+                else if (div == WD_MUL) GG_TILE_LAUNCH(false, WD_MUL);
                 else GG_TILE_LAUNCH(false, WD_RCP);
             }
 #undef GG_TILE_LAUNCH
@@ -2823,12 +2982,14 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
             GG_WAVE_LAUNCH_S(FWD, DIV, 3);                                                         \
     } while (0)
             if (T.lower) {
-                if (T.div == WD_UNIT) GG_WAVE_LAUNCH(true, WD_UNIT);
-                else if (T.div == WD_HW) GG_WAVE_LAUNCH(true, WD_HW);
+                if (div == WD_UNIT) GG_WAVE_LAUNCH(true, WD_UNIT);
+                else if (div == WD_HW) GG_WAVE_LAUNCH(true, WD_HW);
+                else if (div == WD_MUL) GG_WAVE_LAUNCH(true, WD_MUL);
                 else GG_WAVE_LAUNCH(true, WD_RCP);
             } else {
-                if (T.div == WD_UNIT) GG_WAVE_LAUNCH(false, WD_UNIT);
-                else if (T.div == WD_HW) GG_WAVE_LAUNCH(false, WD_HW);
+                if (div == WD_UNIT) GG_WAVE_LAUNCH(false, WD_UNIT);
+                else if (div == WD_HW) GG_WAVE_LAUNCH(false, WD_HW);
+                else if (div == WD_MUL) GG_WAVE_LAUNCH(false, WD_MUL);
                 else GG_WAVE_LAUNCH(false, WD_RCP);
             }
 #undef GG_WAVE_LAUNCH
@@ -2844,12 +3005,14 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
             T.c0.p, T.prog.p, nullptr, nullptr);                                                   \
     } while (0)
             if (T.lower) {
-                if (T.div == WD_UNIT) GG_WAVE_LAUNCH3(true, WD_UNIT);
-                else if (T.div == WD_HW) GG_WAVE_LAUNCH3(true, WD_HW);
+                if (div == WD_UNIT) GG_WAVE_LAUNCH3(true, WD_UNIT);
+                else if (div == WD_HW) GG_WAVE_LAUNCH3(true, WD_HW);
+                else if (div == WD_MUL) GG_WAVE_LAUNCH3(true, WD_MUL);
                 else GG_WAVE_LAUNCH3(true, WD_RCP);
             } else {
-                if (T.div == WD_UNIT) GG_WAVE_LAUNCH3(false, WD_UNIT);
-                else if (T.div == WD_HW) GG_WAVE_LAUNCH3(false, WD_HW);
+                if (div == WD_UNIT) GG_WAVE_LAUNCH3(false, WD_UNIT);
+                else if (div == WD_HW) GG_WAVE_LAUNCH3(false, WD_HW);
+                else if (div == WD_MUL) GG_WAVE_LAUNCH3(false, WD_MUL);
                 else GG_WAVE_LAUNCH3(false, WD_RCP);
             }
 #undef GG_WAVE_LAUNCH3
@@ -2886,6 +3049,25 @@ void launch_mgs_step_r(Gate g, int i, int k, int m, double *w, const double *vk,
     else
         k_mgs_step<false><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, vnext, part_in, part_out, H,
                                                  nparts_in, Ppad / 2, Pdot / 2);
+}
+void launch_multidot(Gate g, const double *w, const double *V, long long ldv, int nk, double *part, int G,
+                     long long Pdot, hipStream_t st)
+{
+    dim3 grid(G, (nk + kCgsKC - 1) / kCgsKC);
+    k_multidot<<<grid, kBlock, 0, st>>>(g, w, V, ldv, nk, part, G, Pdot / 2);
+}
+void launch_cgs_reduce(Gate g, const double *part, int P, int G, long long cnt, int nk, double *h, double *H,
+                       int i, int m, bool add, hipStream_t st)
+{
+    k_cgs_reduce<<<nk, kBlock, 0, st>>>(g, part, P, G, cnt, h, H, i, m, add ? 1 : 0);
+}
+void launch_cgs_update(Gate g, double *w, const double *V, long long ldv, const double *h, int nk, int G,
+                       long long Ppad, long long Pdot, double *part_norm, hipStream_t st)
+{
+    if (part_norm)
+        k_cgs_update<true><<<G, kBlock, 0, st>>>(g, w, V, ldv, h, nk, Ppad / 2, Pdot / 2, part_norm);
+    else
+        k_cgs_update<false><<<G, kBlock, 0, st>>>(g, w, V, ldv, h, nk, Ppad / 2, Pdot / 2, nullptr);
 }
 void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *part, int G,
                              const double *w, double *vnext, double *H, double *cs, double *sn,

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <thread>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -143,7 +144,7 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         std::vector<double> c0(d3 ? Ppad : 0, 0.0);
         const int K = wl->skew - 1;              // fill offsets nx-1 .. nx-K (2D)
         std::vector<double> ce1(K >= 1 ? Ppad : 0, 0.0), ce2(K >= 2 ? Ppad : 0, 0.0);
-        bool unit = true, rcp_ok = true;
+        bool unit = true, rcp_ok = true, mul_ok = true;
         const int nx = wl->nx;
         const long long nxy = (long long)wl->nx * wl->ny;
         for (int r = 0; r < n; r++) {
@@ -161,6 +162,8 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
             if (d != 1.0) unit = false;
             // WD_RCP keeps every intermediate normal for 2^-100 <= |d| <= 2^100
             if (!(std::fabs(d) >= 0x1p-100 && std::fabs(d) <= 0x1p100)) rcp_ok = false;
+            // WD_MUL: 1/d finite and normal
+            if (!(std::fabs(d) >= 0x1p-1020 && std::fabs(d) <= 0x1p1020)) mul_ok = false;
         }
         T.c1.upload(c1, st);
         T.c2.upload(c2, st);
@@ -173,13 +176,15 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         }
         if (wl->tile) T.order.upload(tile_order(*wl), st);
         T.rcp_ok = false;
+        T.mul_ok = false;
         if (unit) {
             T.div = WD_UNIT;
         } else {
             T.dw.upload(dv, st);
             const char *hw = std::getenv("GG_WAVE_HWDIV");
             T.rcp_ok = rcp_ok && !(hw && hw[0] == '1');
-            if (T.rcp_ok) T.rw.upload(rv, st);
+            T.mul_ok = mul_ok;
+            if (T.rcp_ok || T.mul_ok) T.rw.upload(rv, st);
             T.div = T.rcp_ok ? WD_RCP : WD_HW;
         }
         // one hand-off granule per band (tile) and step, then per workgroup 64
@@ -193,6 +198,7 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         launch_fill_u64(T.bnd.p + ngran, ndummy, 0ull, st);
         // algorithmic bytes: b, two coefficients, (divisor (, reciprocal)), x per grid point
         T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
+        T.bytes_mul = (double)n * (8.0 * ((unit ? 4 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
     } else {
         T.kind = DevTri::LEVEL;
         T.off.upload(C.off, st);
@@ -262,6 +268,7 @@ struct gg_solver {
     bool persist = false;
     bool wide = false;                  // k_arnoldi_wide (vectors beyond persist's registers)
     bool shared = false;                // GG_SOLVE_SHARED_DEVICE for the solve in progress
+    int div_mode = GG_DIV_EXACT;        // gg_set_division: the wavefront solves' division
     // pinned host copies of the control block and the error word (one
     // round trip per restart cycle reads both)
     DevState *h_state = nullptr;
@@ -422,6 +429,7 @@ void prof_end(gg_solver *s, int mark);
 void trsv(gg_solver *s, Gate g, DevTri &T, int kind, int i, const double *in, double *out)
 {
     const int mk = i >= 0 ? prof_begin(s, kind, i) : -1;
+    T.fast = s->div_mode == GG_DIV_RCP;
     launch_trsv(g, T, in, out, s->err.p, s->st);
     prof_end(s, mk);
 }
@@ -643,7 +651,9 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
     const int m = opt->restart;
     GG_REQUIRE(m >= 1 && m <= 512, GG_EINVAL, "gg_solve: restart must be in [1, 512]");
     GG_REQUIRE(opt->max_iter >= 0, GG_EINVAL, "gg_solve: negative max_iter");
-    GG_REQUIRE((opt->flags & ~GG_SOLVE_SHARED_DEVICE) == 0, GG_EINVAL, "gg_solve: unknown flags");
+    GG_REQUIRE((opt->flags & ~GG_SOLVE_SHARED_DEVICE) == 0, GG_EINVAL,
+               (opt->flags & GG_SOLVE_CGS2) ? "gg_solve: GG_SOLVE_CGS2 is a sharded-solve (gg_dd_solve) mode"
+                                            : "gg_solve: unknown flags");
     s->shared = (opt->flags & GG_SOLVE_SHARED_DEVICE) != 0;
     if (s->shared) {
         // only kernels whose workgroups wait on earlier-dispatched ones
@@ -1165,6 +1175,55 @@ int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const d
 
 int gg_precond_kind(gg_solver *s) { return s ? s->pkind : GG_EINVAL; }
 int gg_uses_wavefront(gg_solver *s) { return (s && s->wave) ? 1 : 0; }
+int gg_set_division(gg_solver *s, int mode)
+{
+    if (!s) return GG_EINVAL;
+    if (mode != GG_DIV_EXACT && mode != GG_DIV_RCP) {
+        set_error("gg_set_division: mode must be GG_DIV_EXACT or GG_DIV_RCP");
+        return GG_EINVAL;
+    }
+    s->div_mode = mode;
+    return GG_OK;
+}
+int gg_mgs_kernel(gg_solver *s, char *name, int cap)
+{
+    if (!s || !name || cap <= 0) return GG_EINVAL;
+    std::string k;
+    if (s->m_alloc > 0 && !s->shared) {
+        if (s->persist) k = "k_arnoldi_persist<" + std::to_string(arnoldi_persist_units(s->G, s->Ppad)) + ">";
+        else if (s->wide) k = "k_arnoldi_wide";
+    }
+    std::snprintf(name, (size_t)cap, "%s", k.c_str());
+    return (int)k.size();
+}
+int gg_trsv_kernel(gg_solver *s, int which, char *name, int cap)
+{
+    if (!s || (which != 0 && which != 1) || !name || cap <= 0) return GG_EINVAL;
+    DevTri &T = which == 0 ? s->L : s->U;
+    T.fast = s->div_mode == GG_DIV_RCP;
+    std::string k;
+    if (T.kind == DevTri::WAVE2D) {
+        const char *fwd = T.lower ? "true" : "false";
+        const int div = T.eff_div();
+        if (T.wl.tile)
+            k = std::string("k_trsv_tile3d<") + fwd + ", " + std::to_string(div) + ", false>";
+        else
+            k = std::string("k_trsv_wave2d<") + fwd + ", " + std::to_string(div) + ", false, " +
+                (T.wl.nz > 1 ? "true" : "false") + ", " + std::to_string(T.wl.nz > 1 ? 1 : T.wl.skew) + ">";
+    } else if (T.kind == DevTri::LEVEL) {
+        const char *lv = std::getenv("GG_TRSV_LEVELS");
+        k = (lv && atoi(lv) != 0) ? "k_trsv_level" : "k_trsv_flow";
+    }
+    std::snprintf(name, (size_t)cap, "%s", k.c_str());
+    return (int)k.size();
+}
+int gg_division_active(gg_solver *s, int which)
+{
+    if (!s || (which != 0 && which != 1)) return GG_EINVAL;
+    DevTri &T = which == 0 ? s->L : s->U;
+    T.fast = s->div_mode == GG_DIV_RCP;
+    return (T.kind == DevTri::WAVE2D && T.eff_div() == WD_MUL) ? GG_DIV_RCP : GG_DIV_EXACT;
+}
 int gg_spmv_sliced(gg_solver *s) { return (s && s->dA.sell) ? 1 : 0; }
 
 int gg_solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
@@ -1566,7 +1625,7 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     set_device(s);
     ensure_workspace(s, std::max(s->m_alloc, 1));
     // per band (2D) 3 nbatch + 8 words, per tile (3D tiles, k_trsv_tile3d) 5 nbatch + 8
-    const int nb = T.wl.nbands, nbt = T.wl.tile ? T.wl.T / tile_batch_steps() : T.wl.T / wave_batch_steps(T.div);
+    const int nb = T.wl.nbands, nbt = T.wl.tile ? T.wl.T / tile_batch_steps() : T.wl.T / wave_batch_steps(T.eff_div());
     const long long need = (long long)nb * ((T.wl.tile ? 5 : 3) * nbt + 8);
     GG_REQUIRE(cap >= need, GG_EINVAL, "trace buffer too small");
     DBuf<long long> buf;
@@ -1574,6 +1633,7 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
     T.trace = buf.p;
     Gate none;
+    T.fast = s->div_mode == GG_DIV_RCP;
     launch_trsv(none, T, s->bv.p, s->t1.p, s->err.p, s->st);
     T.trace = nullptr;
     GG_HIP(hipMemcpyAsync(out, buf.p, need * sizeof(long long), hipMemcpyDeviceToHost, s->st));
@@ -1619,13 +1679,15 @@ double gg_bytes_spmv(gg_solver *s)
 double gg_bytes_precond(gg_solver *s)
 {
     if (!s || s->pkind < 0) return 0.0;
-    return s->L.bytes + s->U.bytes;
+    s->L.fast = s->U.fast = s->div_mode == GG_DIV_RCP;
+    return s->L.alg_bytes() + s->U.alg_bytes();
 }
 
 double gg_bytes_trsv(gg_solver *s, int which)
 {
     if (!s || s->pkind < 0 || (which != 0 && which != 1)) return 0.0;
-    return which == 0 ? s->L.bytes : s->U.bytes;
+    s->L.fast = s->U.fast = s->div_mode == GG_DIV_RCP;
+    return which == 0 ? s->L.alg_bytes() : s->U.alg_bytes();
 }
 
 }  // extern "C"

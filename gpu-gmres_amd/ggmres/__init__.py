@@ -18,6 +18,7 @@ GG_OK, GG_NOT_CONVERGED = 0, 1
 PRECOND_NONE, PRECOND_ILU0, PRECOND_ILUK, PRECOND_LU, PRECOND_SPLIT = range(5)
 APPLY_MINV, APPLY_LEFT, APPLY_RIGHT, APPLY_START = range(4)
 SOLVE_SHARED_DEVICE = 0x1     # gg_options.flags: other solvers share the device (ggmres.h)
+SOLVE_CGS2 = 0x2              # gg_options.flags: CGS2 orthogonalization (sharded solve only)
 
 # every symbol include/ggmres.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -30,8 +31,10 @@ EXPORTS = [
     "gg_trace_precond", "gg_bytes_trsv", "gg_transient", "gg_set_precond_ilu0_device",
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
     "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced",
-    "gg_transient_mna",
+    "gg_transient_mna", "gg_set_division", "gg_division_active",
+    "gg_trsv_kernel", "gg_mgs_kernel",
 ]
+DIV_EXACT, DIV_RCP = 0, 1     # gg_div_mode
 SRC_DC, SRC_PULSE, SRC_PWL = 0, 1, 2          # gg_src_kind
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
 PROF_NKINDS = 5
@@ -77,6 +80,10 @@ def lib():
                   "gg_uses_wavefront", "gg_spmv_sliced", "gg_set_precond_ilu0_device"):
             getattr(L, f).argtypes = [_VP]
         L.gg_set_precond_iluk.argtypes = [_VP, ctypes.c_int]
+        L.gg_set_division.argtypes = [_VP, ctypes.c_int]
+        L.gg_division_active.argtypes = [_VP, ctypes.c_int]
+        L.gg_trsv_kernel.argtypes = [_VP, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.gg_mgs_kernel.argtypes = [_VP, ctypes.c_char_p, ctypes.c_int]
         L.gg_set_precond_iluk_device.argtypes = [_VP, ctypes.c_int]
         _PI, _PD = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)
         L.gg_iluk_device_factors.argtypes = [_VP, ctypes.c_int, _I, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
@@ -221,6 +228,28 @@ class Solver:
         i = lambda a: np.ascontiguousarray(a, np.int32)
         _check(lib().gg_set_precond_split(self.h, lrp, lci, lv, urp, uci, uv, f(middle),
                                           i(perm_row), i(perm_col), f(lscale), f(rscale)))
+
+    def set_division(self, mode):
+        """DIV_EXACT (x = RN(acc/d), the default) or DIV_RCP (x = RN(acc * RN(1/d))
+        on the wavefront triangular solves, tolerance parity) -- ggmres.h"""
+        _check(lib().gg_set_division(self.h, int(mode)))
+
+    def division_active(self, which):
+        """the division triangle `which` (0 = L / Ml, 1 = U / Mr) runs with"""
+        return _check(lib().gg_division_active(self.h, int(which)))
+
+    def trsv_kernel(self, which):
+        """rocprofv3 name of the kernel running triangle `which` (0 = L, 1 = U)"""
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().gg_trsv_kernel(self.h, int(which), buf, 256))
+        return buf.value.decode()
+
+    def mgs_kernel(self):
+        """rocprofv3 name of the last solve's one-launch orthogonalization kernel
+        ('' = the per-step kernels)"""
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().gg_mgs_kernel(self.h, buf, 256))
+        return buf.value.decode()
 
     @property
     def uses_wavefront(self):

@@ -3,6 +3,10 @@
 DD(nparts, device=0)                    all shards in this process on one GPU
 DD(nparts, rank=r, uid=bytes, device=d) one shard per process (RCCL); uid from
                                         unique_id() on rank 0, broadcast by the caller
+DD(nparts, rank=r, comm="ipc", device=d) one shard per process, device-initiated
+                                        exchanges through hipIpc-mapped areas; then
+                                        d.connect_ipc(allgather) with any host
+                                        all-gather of bytes (e.g. torch.distributed)
 """
 import ctypes
 
@@ -10,14 +14,16 @@ import numpy as np
 
 from . import Options, Result, _check, _csr_arrays, lib
 
-LOCAL, RCCL = 0, 1
+LOCAL, RCCL, IPC = 0, 1, 2
 ID_BYTES = 128
+IPC_HANDLE_BYTES = 64
 _VP = ctypes.c_void_p
 _I = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
 _D = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
 _done = False
 
 EXPORTS = ["gg_dd_unique_id", "gg_dd_create", "gg_dd_destroy", "gg_dd_comm_ranks",
+           "gg_dd_ipc_handle", "gg_dd_ipc_connect",
            "gg_dd_set_system", "gg_dd_info",
            "gg_dd_perm", "gg_dd_dot_layout", "gg_dd_solve", "gg_dd_solve_device",
            "gg_dd_get_history", "gg_dd_spmv", "gg_dd_precond_apply"]
@@ -31,6 +37,8 @@ def _lib():
         L.gg_dd_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_char_p, ctypes.POINTER(_VP)]
         L.gg_dd_destroy.argtypes = [_VP]
+        L.gg_dd_ipc_handle.argtypes = [_VP, ctypes.c_char_p]
+        L.gg_dd_ipc_connect.argtypes = [_VP, ctypes.c_char_p]
         L.gg_dd_comm_ranks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.gg_dd_set_system.argtypes = [_VP, ctypes.c_int, _I, _I, _D, ctypes.c_int]
         L.gg_dd_info.argtypes = [_VP, _I]
@@ -54,13 +62,31 @@ def unique_id():
 
 
 class DD:
-    def __init__(self, nparts, device=0, rank=None, uid=None):
+    def __init__(self, nparts, device=0, rank=None, uid=None, comm=None):
         h = _VP()
-        kind = LOCAL if rank is None else RCCL
+        kind = IPC if comm == "ipc" else LOCAL if rank is None else RCCL
+        if kind == IPC and rank is None:
+            raise ValueError("dd: comm='ipc' needs a rank")
         _check(_lib().gg_dd_create(int(device), int(nparts), kind, int(rank or 0),
                                    uid if uid is not None else None, ctypes.byref(h)))
         self.h, self.P, self.kind, self.rank = h, nparts, kind, rank
         self.n = 0
+
+    def ipc_handle(self):
+        """this rank's exchange-area handle (GG_DD_IPC)"""
+        buf = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+        _check(_lib().gg_dd_ipc_handle(self.h, buf))
+        return buf.raw
+
+    def ipc_connect(self, handles):
+        """every rank's handle, rank order: maps the peers' areas (collective)"""
+        if len(handles) != self.P or any(len(x) != IPC_HANDLE_BYTES for x in handles):
+            raise ValueError("dd: need nparts handles of IPC_HANDLE_BYTES")
+        _check(_lib().gg_dd_ipc_connect(self.h, b"".join(handles)))
+
+    def connect_ipc(self, allgather):
+        """allgather(bytes) -> list of every rank's bytes (rank order)"""
+        self.ipc_connect(list(allgather(self.ipc_handle())))
 
     def close(self):
         if self.h:
@@ -74,7 +100,8 @@ class DD:
             pass
 
     def comm_ranks(self):
-        """(ranks in the exchange, this process's rank): RCCL ncclCommCount, LOCAL (1, 0)"""
+        """(ranks in the exchange, this process's rank): RCCL ncclCommCount, IPC the
+        mapped areas (collective: every rank must call it), LOCAL (1, 0)"""
         c, r = ctypes.c_int(), ctypes.c_int()
         _check(_lib().gg_dd_comm_ranks(self.h, ctypes.byref(c), ctypes.byref(r)))
         return c.value, r.value
@@ -104,17 +131,18 @@ class DD:
         _lib().gg_dd_dot_layout(self.h, int(part), out.ctypes.data, ln, ctypes.byref(G))
         return out[:ln], G.value
 
-    def solve(self, b, x0=None, restart=30, max_iter=3000, tol=1e-10):
+    def solve(self, b, x0=None, restart=30, max_iter=3000, tol=1e-10, flags=0):
+        """flags: ggmres.SOLVE_CGS2 for the three-all-gather orthogonalization"""
         b = np.ascontiguousarray(b, np.float64)
         x = np.zeros(self.n) if x0 is None else np.array(x0, np.float64, copy=True)
-        o = Options(int(restart), int(max_iter), float(tol), 0)
+        o = Options(int(restart), int(max_iter), float(tol), int(flags))
         r = Result()
         rc = _check(_lib().gg_dd_solve(self.h, b, x, ctypes.byref(o), ctypes.byref(r)), allow_nc=True)
         return dict(ret=rc, x=x, iters=r.iters, inner=r.inner_iters, restarts=r.restarts,
                     relres=r.relres, solve_ms=r.solve_ms, hist=self.history())
 
-    def solve_device(self, b_ptr, x_ptr, restart=30, max_iter=3000, tol=1e-10):
-        o = Options(int(restart), int(max_iter), float(tol), 0)
+    def solve_device(self, b_ptr, x_ptr, restart=30, max_iter=3000, tol=1e-10, flags=0):
+        o = Options(int(restart), int(max_iter), float(tol), int(flags))
         r = Result()
         rc = _check(_lib().gg_dd_solve_device(self.h, _VP(b_ptr), _VP(x_ptr), ctypes.byref(o),
                                               ctypes.byref(r)), allow_nc=True)

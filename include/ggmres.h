@@ -89,6 +89,14 @@ typedef struct gg_options {
  * wavefront triangular solve or no preconditioner (else GG_EINVAL), whose
  * workgroups only wait on workgroups dispatched before them. */
 #define GG_SOLVE_SHARED_DEVICE 0x1
+/* gg_options.flags, the sharded solve (ggmres_dd.h) only: orthogonalize each
+ * Arnoldi vector by classical Gram-Schmidt with one re-orthogonalization
+ * (CGS2: h = V^T w, w -= V h, h2 = V^T w, w -= V h2, H[:, i] = h + h2) instead
+ * of the reference's modified Gram-Schmidt (src/gmres.cu:2356-2359): three
+ * all-gathers per inner iteration (h, h2, the norm) instead of i + 2.  A
+ * different rounding (north_star's 1e-10 history tolerance); the default
+ * stays MGS.  gg_solve refuses it (GG_EINVAL). */
+#define GG_SOLVE_CGS2 0x2
 
 typedef struct gg_result {
     int status;        /* GG_OK / GG_NOT_CONVERGED / error                        */
@@ -145,6 +153,32 @@ int gg_set_precond_split(gg_solver *s,
                          const double *middle, const int *perm_row, const int *perm_col,
                          const double *lscale, const double *rscale);
 int gg_precond_kind(gg_solver *s);
+/* Division in the non-unit triangular solves (the reference divides,
+ * LUSolve_ignoreZero src/SpMV_compute.cpp:118-133, HostPrecond_left/right
+ * src/preconditioner.cu:1094-1137):
+ *   GG_DIV_EXACT (default)  x = RN(acc / d), bit-identical to the reference's
+ *                           per-row arithmetic;
+ *   GG_DIV_RCP              x = RN(acc * RN(1/d)) on the wavefront solves
+ *                           (2D band / 3D tile): within about one ulp per row,
+ *                           one multiply on the dependency chain instead of a
+ *                           five-operation correctly rounded quotient, and one
+ *                           streamed array fewer.  Tolerance parity (north_star
+ *                           1e-10 on the residual history); the dataflow solve
+ *                           of other sparsity keeps dividing.
+ * Applies to every later solve / apply of this solver. */
+enum gg_div_mode { GG_DIV_EXACT = 0, GG_DIV_RCP = 1 };
+int gg_set_division(gg_solver *s, int mode);
+/* the division the last-set mode gives triangle `which` (0 = L / Ml, 1 = U /
+ * Mr): GG_DIV_RCP only on a non-unit wavefront triangle whose 1/d are normal */
+int gg_division_active(gg_solver *s, int which);
+/* the kernel (rocprofv3 name) that runs triangle `which` (0 = L / Ml, 1 = U /
+ * Mr) under the current division mode, into name[cap]; returns its length
+ * ("" when the preconditioner has no triangles) */
+int gg_trsv_kernel(gg_solver *s, int which, char *name, int cap);
+/* the one-launch orthogonalization kernel of the last solve's inner
+ * iterations (k_arnoldi_persist<J> / k_arnoldi_wide), "" when the per-step
+ * kernels ran (or before the first solve); returns its length */
+int gg_mgs_kernel(gg_solver *s, char *name, int cap);
 /* 1 if the structured-grid wavefront triangular solve is active, else 0 */
 int gg_uses_wavefront(gg_solver *s);
 /* the SpMV kernel the solver's matrix takes: 1 sliced ELL (k_spmv_sell: short,

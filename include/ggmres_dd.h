@@ -18,18 +18,29 @@
  *     reference's order (LUSolve_ignoreZero, src/SpMV_compute.cpp:92-136):
  *     the operators are bit-identical to the single-GPU solve of B.
  *
- * Two communicators:
+ * Three communicators:
  *   GG_DD_RCCL   one process per GPU (torchrun), shard = rank, RCCL collectives
  *                on the solver's stream; the 128-byte id comes from
  *                gg_dd_unique_id on rank 0 and is broadcast by the caller.
+ *   GG_DD_IPC    one process per shard, device-initiated exchanges: every
+ *                rank's exchange area (uncached device memory) is mapped into
+ *                every process (hipIpc; over xGMI between GPUs) and each
+ *                all-gather is ONE small kernel that stores this rank's slot
+ *                into every peer's area and waits on the peers' sequence-
+ *                numbered flags -- no collective library.  Several ranks may
+ *                share a GPU (the one-GPU test of the multi-process path).
+ *                Bootstrap: gg_dd_create, gg_dd_ipc_handle, the caller
+ *                all-gathers the nparts handles (any host channel), then
+ *                gg_dd_ipc_connect before gg_dd_set_system.
  *   GG_DD_LOCAL  all nparts shards in this process on one device (the same
  *                kernels, the exchanges done by a copy kernel): tests and
  *                single-GPU studies of the decomposition.
  *
  * Vectors are global, natural (unpermuted) order, length n, identical on every
  * rank on input.  On output a process writes the rows it holds (GG_DD_LOCAL:
- * all rows; GG_DD_RCCL: interior p and the separator); other entries are left
- * untouched.  Status codes as ggmres.h; GG_ECOMM for RCCL failures.
+ * all rows; GG_DD_RCCL / GG_DD_IPC: interior p and the separator); other
+ * entries are left untouched.  Status codes as ggmres.h; GG_ECOMM for RCCL
+ * failures, GG_ETIMEOUT when an IPC peer does not arrive within 30 s.
  */
 #ifndef GGMRES_DD_H_
 #define GGMRES_DD_H_
@@ -42,9 +53,12 @@ extern "C" {
 
 #define GG_DD_ID_BYTES 128
 
+#define GG_DD_IPC_HANDLE_BYTES 64
+
 enum gg_dd_comm {
     GG_DD_LOCAL = 0,
-    GG_DD_RCCL = 1
+    GG_DD_RCCL = 1,
+    GG_DD_IPC = 2
 };
 
 typedef struct gg_dd gg_dd;
@@ -53,8 +67,14 @@ typedef struct gg_dd gg_dd;
 int gg_dd_unique_id(unsigned char *id);
 int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char *id, gg_dd **out);
 int gg_dd_destroy(gg_dd *d);
+/* GG_DD_IPC: this rank's exchange-area handle (GG_DD_IPC_HANDLE_BYTES) ... */
+int gg_dd_ipc_handle(gg_dd *d, unsigned char *handle);
+/* ... and every rank's, rank-major (nparts * GG_DD_IPC_HANDLE_BYTES): maps the
+ * peers' areas; returns once every rank has connected */
+int gg_dd_ipc_connect(gg_dd *d, const unsigned char *handles);
 /* processes in the exchange: GG_DD_RCCL the communicator's rank count
- * (ncclCommCount), GG_DD_LOCAL 1; *rank = this process's rank */
+ * (ncclCommCount), GG_DD_IPC the mapped areas (checked: every rank reports
+ * its own rank), GG_DD_LOCAL 1; *rank = this process's rank */
 int gg_dd_comm_ranks(gg_dd *d, int *ranks, int *rank);
 
 /* the global system (identical on every rank): partition (gg_part_method of

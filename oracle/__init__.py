@@ -68,6 +68,8 @@ def lib():
                                      _f64p, _f64p]
         L.orc_sub_seq.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
         L.orc_gen_rot.argtypes = [ctypes.c_double, ctypes.c_double, _PD, _PD]
+        L.orc_set_div_mode.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_set_orth.argtypes = [ctypes.c_int]
         L.orc_apply_rot.argtypes = [_PD, _PD, ctypes.c_double, ctypes.c_double]
         common = [_f64p, _f64p, ctypes.c_int, _PI, _PD, _f64p, ctypes.c_int, _PI, _PI]
         L.orc_gmres_left.argtypes = ([ctypes.c_int, _i32p, _i32p, _f64p,
@@ -213,6 +215,19 @@ def set_dot_order_shards(segments, G):
     cat = np.ascontiguousarray(np.concatenate(segments), np.int64)
     _dot_keep = (seglen, cat)
     lib().orc_set_dot_order_shards(len(segments), seglen.ctypes.data, int(G), cat.ctypes.data)
+
+
+def set_div_mode(mul_l=False, mul_u=False):
+    """Division of the non-unit triangles: False = x / d (the reference), True =
+    x * (1.0 / d) (the device's GG_DIV_RCP on a wavefront triangle); for
+    order-matched checks only -- reset with set_div_mode()."""
+    lib().orc_set_div_mode(int(bool(mul_l)), int(bool(mul_u)))
+
+
+def set_orth(cgs2=False):
+    """False: modified Gram-Schmidt (the reference); True: CGS2, the sharded
+    solve's GG_SOLVE_CGS2 restated (reset with set_orth())."""
+    lib().orc_set_orth(int(bool(cgs2)))
 
 
 def gen_rot(dx, dy):

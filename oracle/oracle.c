@@ -326,6 +326,18 @@ int orc_iluk(int lofM, int n, const int *rp, const int *ci, const double *v,
 }
 
 /* ------------------------------------------------------- triangular solve */
+/* Division mode of the non-unit triangles (the device's gg_set_division):
+ * 0 = x / d as the reference; 1 = x * (1.0 / d), the device's WD_MUL
+ * (x = RN(acc * RN(1/d))), per triangle (L = the lower / Ml one, U = the upper
+ * / Mr one).  Only for order-matched checks of GG_DIV_RCP solves. */
+static int g_mul_l = 0, g_mul_u = 0;
+void orc_set_div_mode(int mul_l, int mul_u)
+{
+    g_mul_l = mul_l != 0;
+    g_mul_u = mul_u != 0;
+}
+static double divide(double a, double d, int mul) { return mul ? a * (1.0 / d) : a / d; }
+
 void orc_lusolve(int n, const int *l_rp, const int *l_ci, const double *l_v,
                  const int *u_rp, const int *u_ci, const double *u_v,
                  const double *y, double *x)
@@ -347,7 +359,7 @@ void orc_lusolve(int n, const int *l_rp, const int *l_ci, const double *l_v,
             if (u_ci[j] <= i) break;
             x[i] -= u_v[j] * x[u_ci[j]];
         }
-        if (j >= lb && u_ci[j] == i && !is_zero(u_v[j])) x[i] /= u_v[j];
+        if (j >= lb && u_ci[j] == i && !is_zero(u_v[j])) x[i] = divide(x[i], u_v[j], g_mul_u);
     }
     free(w);
 }
@@ -363,7 +375,7 @@ void orc_split_left(const orc_split_t *p, const double *in, double *out)
     for (int i = 0; i < n; i++) {
         int lb = p->l_rp[i], ub = p->l_rp[i + 1];
         for (int j = lb; j < ub - 1; j++) out[i] -= p->l_v[j] * out[p->l_ci[j]];
-        out[i] /= p->l_v[ub - 1];
+        out[i] = divide(out[i], p->l_v[ub - 1], g_mul_l);
     }
     free(t);
 }
@@ -377,7 +389,7 @@ void orc_split_right(const orc_split_t *p, const double *in, double *out)
     for (int i = n - 1; i >= 0; i--) {
         int lb = p->u_rp[i], ub = p->u_rp[i + 1];
         for (int j = lb + 1; j < ub; j++) t[i] -= p->u_v[j] * t[p->u_ci[j]];
-        t[i] /= p->u_v[lb];
+        t[i] = divide(t[i], p->u_v[lb], g_mul_u);
     }
     for (int i = 0; i < n; i++) out[i] = t[p->perm_col[i]] / p->rscale[i];
     free(t);
@@ -525,6 +537,14 @@ static double norm2(const double *v, int n)
     return sqrt(t);
 }
 
+/* Orthogonalization: 0 = modified Gram-Schmidt as the reference
+ * (src/gmres.cu:638-641, 2356-2359); 1 = CGS2, the sharded solve's
+ * GG_SOLVE_CGS2 (csrc/kernels.hip k_multidot / k_cgs_reduce / k_cgs_update):
+ * h_k = <w, v_k> for every k from the same w, then per element
+ * w = (-h_k) v_k + w for k ascending, the same again with h2, H = h + h2. */
+static int g_orth = 0;
+void orc_set_orth(int cgs2) { g_orth = cgs2 != 0; }
+
 /* Update (src/gmres.cu:93-116): y = H(0:k,0:k)^-1 s; x += V y */
 static void update(double *x, int k, const double *H, int m, const double *s,
                    const double *V, int n)
@@ -580,6 +600,7 @@ static int gmres_core(const op_t *op, const double *b, double *x, int m,
     double *H = (double *)calloc((size_t)(m + 1) * (size_t)m, sizeof(double));
     double *V = (double *)malloc((size_t)(m + 1) * nn * sizeof(double));
     double *y = (double *)calloc(nn, sizeof(double));   /* split: Mr^-1 x */
+    double *s_cgs = (double *)calloc((size_t)m + 1, sizeof(double));
     double *acc = x;                                     /* left: update x directly */
     hist_t hs = {hist, hist_cap, 0};
     int ret = 1;
@@ -627,12 +648,27 @@ static int gmres_core(const op_t *op, const double *b, double *x, int m,
                 orc_spmv(n, op->rp, op->ci, op->v, w, ww);             /* :2144 */
                 orc_split_left(op->sp, ww, w);                         /* :2145 */
             }
-            for (k = 0; k <= i; k++) {                                 /* MGS :638-641 */
-                const double *vk = V + (size_t)k * nn;
-                double h = dot(w, vk, n);
-                H[k + i * (m + 1)] = h;
-                double a = -h;
-                for (int t = 0; t < n; t++) w[t] = a * vk[t] + w[t];
+            if (g_orth == 1) {                                         /* CGS2 (GG_SOLVE_CGS2) */
+                for (int pass = 0; pass < 2; pass++) {
+                    for (k = 0; k <= i; k++) {
+                        const double h = dot(w, V + (size_t)k * nn, n);
+                        s_cgs[k] = h;
+                        H[k + i * (m + 1)] = pass ? H[k + i * (m + 1)] + h : h;
+                    }
+                    for (int t = 0; t < n; t++) {
+                        double wt = w[t];
+                        for (k = 0; k <= i; k++) wt = (-s_cgs[k]) * V[(size_t)k * nn + t] + wt;
+                        w[t] = wt;
+                    }
+                }
+            } else {
+                for (k = 0; k <= i; k++) {                             /* MGS :638-641 */
+                    const double *vk = V + (size_t)k * nn;
+                    double h = dot(w, vk, n);
+                    H[k + i * (m + 1)] = h;
+                    double a = -h;
+                    for (int t = 0; t < n; t++) w[t] = a * vk[t] + w[t];
+                }
             }
             double hn = norm2(w, n);
             H[(i + 1) + i * (m + 1)] = hn;
@@ -687,7 +723,7 @@ out:
     if (hist_len) *hist_len = hs.len < hist_cap ? hs.len : hist_cap;
     if (inner_iters) *inner_iters = done_iters;
     free(s); free(cs); free(sn); free(w); free(ww); free(r); free(rr); free(bb);
-    free(H); free(V); free(y);
+    free(H); free(V); free(y); free(s_cgs);
     return ret;
 }
 

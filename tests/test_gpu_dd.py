@@ -147,3 +147,57 @@ def test_dd_rccl_single_rank_matches_local():
     assert np.array_equal(r0["x"], r1["x"])
     rc.close()
     loc.close()
+
+
+# ---- GG_SOLVE_CGS2: three all-gathers per inner iteration ----------------------
+CGS2_CASES = ["5pt_200x160_P2", "5pt_200x160_P4_color", "7pt_24_P4", "7pt_16x16x32_P8_upwind_color",
+              "sherman1_P4", "5pt_60x60_P1"]
+
+
+@pytest.mark.parametrize("name", CGS2_CASES)
+def test_dd_cgs2_bitexact_and_tolerance(name):
+    """CGS2 (h = V^T w, w -= V h, twice; H = h + h2) bit-identical to the oracle
+    restating it in the sharded reduction order; its first restart cycle within
+    1e-10 (north_star) of the reference's MGS in serial order; the full solve
+    converges with a true preconditioned residual below the tolerance."""
+    import ggmres
+    A, d, q, B, L, U = setup(name)
+    P = CASES[name][1]
+    b = M.rhs_ones(A)
+    segs, G = zip(*[d.dot_layout(p) for p in range(P)])
+    # the first cycle: order-matched CGS2 bit for bit, serial MGS within 1e-10
+    g1 = d.solve(b, restart=30, max_iter=30, tol=1e-300, flags=ggmres.SOLVE_CGS2)
+    O.set_dot_order_shards(list(segs), G[0])
+    O.set_orth(True)
+    try:
+        t1 = O.gmres_left(B, L, U, b[q], m=30, max_iter=30, tol=1e-300)
+        tf = O.gmres_left(B, L, U, b[q], m=30, max_iter=1500, tol=1e-10)
+    finally:
+        O.set_dot_order(None)
+        O.set_orth()
+    assert np.array_equal(g1["hist"], t1["hist"]) and np.array_equal(g1["x"][q], t1["x"])
+    s1 = O.gmres_left(B, L, U, b[q], m=30, max_iter=30, tol=1e-300)       # serial MGS
+    scale = np.max(np.abs(s1["hist"]))
+    assert g1["hist"].shape == s1["hist"].shape
+    assert np.max(np.abs(g1["hist"] - s1["hist"])) <= 1e-10 * scale
+    assert np.linalg.norm(g1["x"][q] - s1["x"]) <= 1e-10 * np.linalg.norm(s1["x"])
+    # to convergence
+    g = d.solve(b, restart=30, max_iter=1500, tol=1e-10, flags=ggmres.SOLVE_CGS2)
+    assert g["ret"] == tf["ret"] == 0 and g["iters"] == tf["iters"]
+    assert np.array_equal(g["hist"], tf["hist"]) and np.array_equal(g["x"][q], tf["x"])
+    ref = O.gmres_left(B, L, U, b[q], m=30, max_iter=1500, tol=1e-10)
+    assert abs(g["iters"] - ref["iters"]) <= max(2, ref["iters"] // 50), (g["iters"], ref["iters"])
+    normb = np.linalg.norm(O.lusolve(L, U, b[q]))
+    true = np.linalg.norm(O.lusolve(L, U, b[q] - O.spmv(B, g["x"][q]))) / normb
+    assert true < 1e-9, true
+
+
+def test_single_solver_refuses_cgs2():
+    import ggmres
+    s = ggmres.Solver(0)
+    A = M.laplacian_5pt(20)
+    s.set_matrix(A)
+    s.set_precond_ilu0()
+    with pytest.raises(ggmres.GGError):
+        s.solve(M.rhs_ones(A), restart=10, max_iter=20, flags=ggmres.SOLVE_CGS2)
+    s.close()

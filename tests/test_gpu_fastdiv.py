@@ -1,0 +1,203 @@
+"""GPU parity of the reciprocal-multiply division (gg_set_division(GG_DIV_RCP)).
+
+The reference divides every row of a non-unit triangle by its diagonal
+(LUSolve_ignoreZero, src/SpMV_compute.cpp:118-133; HostPrecond_left/right,
+src/preconditioner.cu:1094-1137).  GG_DIV_RCP has the wavefront solves compute
+x = RN(acc * RN(1/d)) instead (kernels.hip WD_MUL): within about one ulp per
+row, so it is a TOLERANCE mode.  Bars:
+  * operators: bit-exact against the oracle restated with the same multiply
+    (oracle.set_div_mode), and within 1e-13 (relative to the vector) of the
+    reference's division;
+  * GMRES: bit-identical to the order-matched oracle in the multiply mode, and
+    within north_star's 1e-10 (history scale, solution) of the SERIAL oracle
+    with the reference's division -- same return code and iteration counts --
+    on C1, the other grid matrices, the split (PG) engine, C2's first restart
+    cycle and C4's first 12 iterations.
+"""
+import numpy as np
+import pytest
+
+import ggmres
+import oracle as O
+from ggmres import matrices as M
+from helpers import device_layout, make_split, rel_err
+
+pytestmark = pytest.mark.gpu
+HIST_RTOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def solver():
+    s = ggmres.Solver(0)
+    s.set_division(ggmres.DIV_RCP)
+    yield s
+    s.close()
+
+
+def oracle_mul(run, n, nx=None, ny=None, mul=(False, True)):
+    """(serial-order oracle with the reference's division, order-matched oracle
+    with the device's division)"""
+    o_serial = run()
+    O.set_dot_order(*device_layout(n, nx, ny))
+    O.set_div_mode(*mul)
+    try:
+        o_tree = run()
+    finally:
+        O.set_dot_order(None)
+        O.set_div_mode()
+    return o_serial, o_tree
+
+
+def check_tol(g, o):
+    assert g["ret"] == o["ret"] and g["iters"] == o["iters"] and g["inner"] == o["inner"]
+    h, ho = np.asarray(g["hist"]), np.asarray(o["hist"])
+    assert h.shape == ho.shape
+    scale = np.max(np.abs(ho))
+    assert np.max(np.abs(h - ho)) <= HIST_RTOL * scale, np.max(np.abs(h - ho)) / scale
+    assert rel_err(g["x"], o["x"]) <= HIST_RTOL
+
+
+def check_exact(g, o):
+    assert g["ret"] == o["ret"] and g["iters"] == o["iters"] and g["inner"] == o["inner"]
+    assert np.array_equal(g["hist"], o["hist"])
+    assert np.array_equal(g["x"], o["x"]), rel_err(g["x"], o["x"])
+
+
+GRIDS = {
+    "c1_5pt_100x100": (lambda: M.laplacian_5pt(100), 100, None),
+    "5pt_37x64": (lambda: M.laplacian_5pt(37, 64), 37, None),
+    "5pt_300x129": (lambda: M.laplacian_5pt(300, 129), 300, None),
+    "thermal_7pt_12": (lambda: M.grid_7pt(12), 12, 12),
+    "7pt_20x30x7_upwind": (lambda: M.grid_7pt(20, 30, 7, upwind=0.1), 20, 30),
+}
+
+
+@pytest.mark.parametrize("name", sorted(GRIDS))
+@pytest.mark.parametrize("scale", [1.0, 1e-250, 1e250])
+def test_rcp_apply(solver, name, scale):
+    make, nx, ny = GRIDS[name]
+    A = make()
+    L, U = O.ilu0(A)
+    y = np.random.default_rng(3).standard_normal(A.shape[0]) * scale
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert solver.uses_wavefront
+    assert solver.division_active(0) == ggmres.DIV_EXACT      # unit L: no division
+    assert solver.division_active(1) == ggmres.DIV_RCP
+    z = solver.precond_apply(ggmres.APPLY_MINV, y)
+    O.set_div_mode(False, True)
+    try:
+        zm = O.lusolve(L, U, y)
+    finally:
+        O.set_div_mode()
+    assert np.array_equal(z, zm)
+    ze = O.lusolve(L, U, y)
+    assert rel_err(z, ze) <= 1e-13
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_rcp_skewed_apply(solver, k):
+    A = M.laplacian_5pt(100, 70)
+    L, U = O.iluk(A, k)
+    solver.set_matrix(A)
+    solver.set_precond_iluk(k)
+    assert solver.uses_wavefront and solver.division_active(1) == ggmres.DIV_RCP
+    y = np.random.default_rng(7).standard_normal(A.shape[0])
+    O.set_div_mode(False, True)
+    try:
+        zm = O.lusolve(L, U, y)
+    finally:
+        O.set_div_mode()
+    assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), zm)
+
+
+def test_rcp_not_on_dataflow_kernel(solver):
+    """other sparsity keeps the reference's division (k_trsv_flow)"""
+    A = M.power_law(3000, 33000, seed=7)
+    L, U = O.ilu0(A)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    assert not solver.uses_wavefront and solver.division_active(1) == ggmres.DIV_EXACT
+    y = np.random.default_rng(2).standard_normal(A.shape[0])
+    assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
+
+
+@pytest.mark.parametrize("name", sorted(GRIDS))
+@pytest.mark.parametrize("rhs", ["ones", "uniform"])
+def test_rcp_gmres_parity(solver, name, rhs):
+    make, nx, ny = GRIDS[name]
+    A = make()
+    n = A.shape[0]
+    b = M.rhs_ones(A) if rhs == "ones" else M.rhs_uniform(n)
+    L, U = O.ilu0(A)
+    o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=3000, tol=1e-10), n, nx, ny)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    g = solver.solve(b, restart=30, max_iter=3000, tol=1e-10)
+    check_exact(g, ot)
+    check_tol(g, o)
+
+
+def test_rcp_split_parity(solver):
+    """GMRESilu_GPU's split engine: both triangles (Ml's L, diagonal last, and
+    Mr's U, diagonal first) are non-unit and take the multiply"""
+    A = M.laplacian_5pt(40)
+    P = make_split(A, seed=9)
+    b = M.rhs_uniform(A.shape[0])
+    x0 = np.random.default_rng(3).random(A.shape[0]) * 0.1
+    solver.set_matrix(A)
+    solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    mul = (solver.division_active(0) == ggmres.DIV_RCP, solver.division_active(1) == ggmres.DIV_RCP)
+    o, ot = oracle_mul(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
+                       A.shape[0], mul=mul)
+    g = solver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
+    check_exact(g, ot)
+    check_tol(g, o)
+
+
+def test_rcp_mode_switch_back(solver):
+    """GG_DIV_EXACT restores the reference's division bit for bit"""
+    A = M.laplacian_5pt(64)
+    L, U = O.ilu0(A)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    y = np.random.default_rng(5).standard_normal(A.shape[0])
+    solver.set_division(ggmres.DIV_EXACT)
+    try:
+        assert solver.division_active(1) == ggmres.DIV_EXACT
+        assert np.array_equal(solver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
+    finally:
+        solver.set_division(ggmres.DIV_RCP)
+    with pytest.raises(ggmres.GGError):
+        solver.set_division(7)
+
+
+@pytest.mark.slow
+def test_rcp_c2_first_cycle(solver):
+    """C2 (1000 x 1000, ILU(0), GMRES(30)): the first restart cycle"""
+    A = M.laplacian_5pt(1000)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    L, U = O.ilu0(A)
+    o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=30, tol=1e-300), n, 1000)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    g = solver.solve(b, restart=30, max_iter=30, tol=1e-300)
+    assert g["iters"] == 30 and g["ret"] == 1
+    check_exact(g, ot)
+    check_tol(g, o)
+
+
+@pytest.mark.slow
+def test_rcp_c4_first_iterations(solver):
+    """C4 (216^3 7-point, 3D tile wavefront): the first 12 inner iterations"""
+    A = M.grid_7pt(216)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    L, U = O.ilu0(A)
+    o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=12, tol=1e-300), n, 216, 216)
+    solver.set_matrix(A)
+    solver.set_precond_ilu0()
+    g = solver.solve(b, restart=30, max_iter=12, tol=1e-300)
+    check_exact(g, ot)
+    check_tol(g, o)

@@ -334,3 +334,43 @@ def test_ilu0_values_split_consistent():
                 (lv if A.ci[k] < r else uv).append(fv[k])
             lv.append(1.0)
         assert np.array_equal(np.array(lv), L.v) and np.array_equal(np.array(uv), U.v)
+
+
+# ---------------------------------------- restated device modes (CPU checks)
+@pytest.mark.parametrize("name", ["5pt_10x10.mtx", "7pt_10x10x10.mtx", "sherman1.rua"])
+def test_cgs2_restatement_close_to_mgs(name):
+    """oracle.set_orth(True) (the sharded solve's GG_SOLVE_CGS2) against the
+    reference's MGS: the first restart cycle within 1e-10 of the history scale,
+    the Hessenberg columns it builds keep V orthonormal (checked through the
+    converged solution: the same iterations +- 1 and the same solution to 1e-9)."""
+    A = load(name)
+    L, U = O.ilu0(A)
+    b = M.rhs_uniform(A.shape[0])
+    mgs1 = O.gmres_left(A, L, U, b, m=30, max_iter=30, tol=1e-300)
+    O.set_orth(True)
+    try:
+        cgs1 = O.gmres_left(A, L, U, b, m=30, max_iter=30, tol=1e-300)
+        cgs = O.gmres_left(A, L, U, b, m=30, max_iter=2000, tol=1e-10)
+    finally:
+        O.set_orth()
+    scale = np.max(np.abs(mgs1["hist"]))
+    assert np.max(np.abs(cgs1["hist"] - mgs1["hist"])) <= 1e-10 * scale
+    mgs = O.gmres_left(A, L, U, b, m=30, max_iter=2000, tol=1e-10)
+    assert cgs["ret"] == mgs["ret"] == 0 and abs(cgs["iters"] - mgs["iters"]) <= 1
+    assert rel_err(cgs["x"], mgs["x"]) <= 1e-9
+
+
+def test_div_mode_restatement_within_ulps():
+    """oracle.set_div_mode (the device's GG_DIV_RCP, x = acc * RN(1/d)) against
+    the reference's division: per solve within a few ulps of the vector"""
+    A = load("7pt_10x10x10.mtx")
+    L, U = O.ilu0(A)
+    y = np.random.default_rng(4).standard_normal(A.shape[0])
+    ref = O.lusolve(L, U, y)
+    O.set_div_mode(False, True)
+    try:
+        z = O.lusolve(L, U, y)
+    finally:
+        O.set_div_mode()
+    assert not np.array_equal(z, ref)          # it is a different rounding ...
+    assert rel_err(z, ref) <= 1e-14            # ... within a few ulps

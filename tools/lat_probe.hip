@@ -77,6 +77,8 @@ __global__ void k_probe(const double *in, double *out, long long *cyc)
     TIMED(22, { double acc = (c - b * dpp_sel<0x130, 63>(x, d)) - d * x; double q0 = acc * c;
                 double q1 = __builtin_fma(-__builtin_fma(q0, a, -acc), c, q0);
                 x = __builtin_fma(-__builtin_fma(q1, a, -acc), c, q1); })
+    // the wavefront U step with GG_DIV_RCP (k_trsv_wave2d WD_MUL): DPP, mul, two subs, one mul
+    TIMED(23, x = ((c - b * dpp_old<0x130>(x, d)) - d * x) * a)
 }
 
 // shader clock vs the constant 100 MHz real-time counter over a long chain
@@ -128,7 +130,7 @@ int main()
     double h[256];
     for (int i = 0; i < 256; i++) h[i] = 1.0 + 1e-3 * i;
     double *din, *dout;
-    long long *dc, hc[32] = {0};
+    long long *dc, hc[32] = {0};   // 24 probes
     hipMalloc(&din, sizeof h);
     hipMalloc(&dout, 32 * 64 * sizeof(double));
     hipMalloc(&dc, sizeof hc);
@@ -139,8 +141,8 @@ int main()
                            "dpp only", "step+div", "step+markstein", "add x2 indep", "rcp",
                            "row_shr:1", "row_bcast:15", "quad_perm", "step(row_shr)", "wave_ror:1",
                            "row_shr+add", "shfl_up+add", "U step (WD_RCP)",
-                           "wave_shr sel", "step(wave_shr sel)", "U step (sel)"};
-    for (int i = 0; i < 23; i++) printf("%-16s %7.2f cycles/iter\n", names[i], (double)hc[i] / N);
+                           "wave_shr sel", "step(wave_shr sel)", "U step (sel)", "U step (WD_MUL)"};
+    for (int i = 0; i < 24; i++) printf("%-16s %7.2f cycles/iter\n", names[i], (double)hc[i] / N);
     for (int nw : {1, 5, 7}) {
         for (int mode = 0; mode < 3; mode++) {
             for (int rep = 0; rep < 3; rep++) {
