@@ -30,8 +30,11 @@ Multi-GPU: `--gpus N` (N > 1) without torchrun starts N rank processes (one
 per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, before the parent makes
 any GPU call) and exits with their status; under torchrun WORLD_SIZE must equal
 --gpus.  At N > 1 the default workload is the SHARDED solve of the C2 system
-(include/ggmres_dd.h: partition4 arrow ordering, one shard per GPU, RCCL
-all-gathers over xGMI; "scaling": "strong", parallelism "ddN"); `--workload dd`
+(include/ggmres_dd.h: partition4 arrow ordering, one shard per GPU,
+device-initiated all-gathers through hipIpc-mapped areas over xGMI -- --dd-comm
+rccl for RCCL collectives -- and the CGS2 orthogonalization, three all-gathers
+per inner iteration -- --dd-orth mgs for the reference's MGS; "scaling":
+"strong", parallelism "ddN"); `--workload dd`
 shards C4 (216^3 7-point) instead.  `--workload replicas` keeps the old
 independent-C2-per-rank run ("scaling": "weak", no collective on the data
 path); `--workload c5` gives each rank its own source scenario (many-RHS).
@@ -86,6 +89,12 @@ def parse():
                    help="non-unit triangular solves: rcp = x = acc * RN(1/d) on the wavefront solves "
                         "(gg_set_division GG_DIV_RCP, tolerance parity 1e-10, tests/test_gpu_fastdiv.py), "
                         "exact = RN(acc / d), the reference's division bit for bit")
+    p.add_argument("--dd-comm", choices=["ipc", "rccl"], default="ipc",
+                   help="sharded solve at N > 1: ipc = device-initiated all-gathers through hipIpc-mapped "
+                        "exchange areas over xGMI (GG_DD_IPC, default), rccl = RCCL collectives (GG_DD_RCCL)")
+    p.add_argument("--dd-orth", choices=["cgs2", "mgs"], default="cgs2",
+                   help="sharded solve: cgs2 = three all-gathers per inner iteration (GG_SOLVE_CGS2, tolerance "
+                        "parity; default), mgs = the reference's modified Gram-Schmidt (i + 2 all-gathers)")
     p.add_argument("--c5-steps", type=int, default=1000)
     p.add_argument("--c5-scenarios", type=int, default=1,
                    help="c5: independent source scenarios per GPU, solved concurrently (one solver, "
@@ -103,9 +112,11 @@ KERNEL_NAMES = {
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # bare dependent-chain latency of one wavefront step (cycles, tools/lat_probe.hip:
 # "step(dpp)" = unit L, "U step (WD_RCP)" = U with the reciprocal-FMA division)
-# and the shader clock it ran at (profiles/r01_lat_probe.txt)
-CHAIN_CYCLES = {"trsv_L": 39.2, "trsv_U": 63.4, "trsv_U_mul": 47.3}
-SHADER_GHZ = 2.396
+# and the shader clock it ran at
+# (profiles/r03_lat_probe.txt: "step(dpp)", "U step (WD_RCP)", "U step (WD_MUL)"
+# re-measured in round 3 -- round 1's probe build gave 39.2 / 63.4 cycles)
+CHAIN_CYCLES = {"trsv_L": 29.78, "trsv_U": 53.86, "trsv_U_mul": 34.30}
+SHADER_GHZ = 2.397
 
 
 def pmc_traffic(kernel, workload=None):
@@ -224,7 +235,24 @@ def bench_dd(a, torch, dist, world, rank, local):
     n = A.shape[0]
     b = M.rhs_ones(A)
     t_setup = time.perf_counter()
-    if world > 1:
+    if world > 1 and a.dd_comm == "ipc":
+        # device-initiated exchanges: the ranks' exchange-area handles are
+        # all-gathered once over a CPU (gloo) group, then every exchange is a
+        # kernel storing into the peers' areas over xGMI
+        boot = dist.new_group(backend="gloo")
+        d = DD(world, device=local, rank=rank, comm="ipc")
+
+        def allgather(hb):
+            lst = [None] * world
+            dist.all_gather_object(lst, hb, group=boot)
+            return lst
+
+        d.connect_ipc(allgather)
+        ranks, myrank = d.comm_ranks()
+        if ranks != world or myrank != rank:
+            raise SystemExit(f"bench.py: IPC exchange maps {ranks} ranks (rank {myrank}), "
+                             f"expected {world} (rank {rank})")
+    elif world > 1:
         uid = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         d = DD(world, device=local, rank=rank, uid=uid[0])
@@ -241,11 +269,14 @@ def bench_dd(a, torch, dist, world, rank, local):
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
 
+    import ggmres
+    flags = ggmres.SOLVE_CGS2 if a.dd_orth == "cgs2" else 0
+
     def step():
         dx.zero_()
         torch.cuda.synchronize()
         return d.solve_device(db.data_ptr(), dx.data_ptr(), restart=a.restart,
-                              max_iter=a.max_iter, tol=a.tol)
+                              max_iter=a.max_iter, tol=a.tol, flags=flags)
 
     def barrier():
         torch.cuda.synchronize()
@@ -277,9 +308,15 @@ def bench_dd(a, torch, dist, world, rank, local):
                                 f"the permuted matrix, GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, "
                                 f"one solve per step"),
                    "n": n, "nnz": int(A.nnz), "parts": parts,
-                   "exchange": "RCCL all-gather over xGMI" if world > 1 else
-                               f"in-process ({parts} shards on one GPU)",
-                   "rccl_ranks": ranks if world > 1 else None,
+                   "exchange": ("device-initiated all-gathers into hipIpc-mapped peer areas over xGMI "
+                                "(GG_DD_IPC)" if a.dd_comm == "ipc" else "RCCL all-gather over xGMI")
+                               if world > 1 else f"in-process ({parts} shards on one GPU)",
+                   "exchange_ranks": ranks if world > 1 else None,
+                   "orthogonalization": ("CGS2: 3 all-gathers per inner iteration (GG_SOLVE_CGS2, tolerance "
+                                         "parity 1e-10 vs MGS over the first cycle)") if a.dd_orth == "cgs2"
+                                        else "MGS (the reference's): i + 2 all-gathers per inner iteration",
+                   "all_gathers_per_iteration": (2 + 3) if a.dd_orth == "cgs2" else
+                                                "2 + (i + 2) at cycle index i",
                    "separator_rows": info["nsep"], "max_interface": info["max_iface"],
                    "wavefront_interior": info["wave_interior"],
                    "wavefront_separator": info["wave_separator"],

@@ -7,6 +7,8 @@
 // right-hand sides (its csrsv solves are commented out, :422-459) and its
 // double branch exits; here every time point is solved, and x_host is filled
 // when use_cuda_double is set.
+#include <algorithm>
+#include <cmath>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -93,8 +95,32 @@ gg_solver *make_solver(const HostCsr &A)
 
 }  // namespace
 
+// Failure (the reference aborts through checkCudaErrors): the message on
+// stderr and every requested output element set to NaN, so a caller of this
+// void entry point cannot mistake stale buffers for results (gpuData.h)
+static void fail_outputs(gpuETBR *e, int nport)
+{
+    if (!e || nport <= 0 || e->numPts <= 0) return;
+    const size_t cnt = (size_t)e->numPts * nport;
+    if (e->use_cuda_single && e->x_single_host)
+        for (size_t k = 0; k < cnt; k++) e->x_single_host[k] = std::nanf("");
+    if (e->use_cuda_double && e->x_host)
+        for (size_t k = 0; k < cnt; k++) e->x_host[k] = std::nan("");
+}
+
+static void run_wrapper(ucr_cs_dl *left, ucr_cs_dl *right, ucr_cs_dl *G, ucr_cs_dl *B, int *invPort, int nport,
+                        gpuETBR *e, bool &ok);
+
 void wrapperGMRESforPG(ucr_cs_dl *left, ucr_cs_dl *right, ucr_cs_dl *G, ucr_cs_dl *B, int *invPort, int nport,
                        gpuETBR *e)
+{
+    bool ok = false;
+    run_wrapper(left, right, G, B, invPort, nport, e, ok);
+    if (!ok) fail_outputs(e, nport);
+}
+
+static void run_wrapper(ucr_cs_dl *left, ucr_cs_dl *right, ucr_cs_dl *G, ucr_cs_dl *B, int *invPort, int nport,
+                        gpuETBR *e, bool &ok)
 {
     if (!left || !right || !G || !B || !e || (nport > 0 && !invPort)) {
         std::fprintf(stderr, "wrapperGMRESforPG: null argument\n");
@@ -106,6 +132,11 @@ void wrapperGMRESforPG(ucr_cs_dl *left, ucr_cs_dl *right, ucr_cs_dl *G, ucr_cs_d
                      n, numPts, B->m, B->n, m);
         return;
     }
+    for (int j = 0; j < nport; j++)
+        if (invPort[j] < 0 || invPort[j] >= n) {
+            std::fprintf(stderr, "wrapperGMRESforPG: port %d = node %d out of range\n", j, invPort[j]);
+            return;
+        }
     // sources in u order: the nVS voltage sources, then the nIS current sources
     std::vector<int> kind(m), ptr(m + 1, 0);
     std::vector<double> data;
@@ -115,9 +146,15 @@ void wrapperGMRESforPG(ucr_cs_dl *left, ucr_cs_dl *right, ucr_cs_dl *G, ucr_cs_d
         ptr[k + 1] = (int)data.size();
     }
     for (int k = 0; k < nIS; k++) {
-        if (e->PWLcurExist && e->PWLnumPts_host) {             // gen_PWLut_kernel
+        // per source: PWL when it has points, else PULSE when pulses are given,
+        // else 0 (the reference evaluates every source as PWL and then, when
+        // PULSEcurExist, overwrites every source with its PULSE row,
+        // src/wrapperGMRESforPG.cu:331-392 -- a mixed netlist would lose its
+        // PWL sources there; deliberate deviation, gpuData.h)
+        const int np = (e->PWLcurExist && e->PWLnumPts_host)
+                           ? std::min(std::max(e->PWLnumPts_host[k], 0), MAX_PWL_PTS) : 0;
+        if (np > 0) {                                           // gen_PWLut_kernel
             kind[nVS + k] = GG_SRC_PWL;
-            const int np = e->PWLnumPts_host[k];
             for (int p = 0; p < np; p++) {
                 data.push_back(e->PWLtime_host[(size_t)k * MAX_PWL_PTS + p]);
                 data.push_back(e->PWLval_host[(size_t)k * MAX_PWL_PTS + p]);
@@ -174,4 +211,5 @@ void wrapperGMRESforPG(ucr_cs_dl *left, ucr_cs_dl *right, ucr_cs_dl *G, ucr_cs_d
             if (e->use_cuda_single && e->x_single_host) e->x_single_host[(size_t)i * nport + j] = (float)v;
             if (e->use_cuda_double && e->x_host) e->x_host[(size_t)i * nport + j] = v;
         }
+    ok = true;
 }

@@ -236,7 +236,7 @@ class Solver:
 
     def division_active(self, which):
         """the division triangle `which` (0 = L / Ml, 1 = U / Mr) runs with"""
-        return _check(lib().gg_division_active(self.h, int(which)))
+        return _check(lib().gg_division_active(self.h, int(which)), allow_nc=True)
 
     def trsv_kernel(self, which):
         """rocprofv3 name of the kernel running triangle `which` (0 = L, 1 = U)"""

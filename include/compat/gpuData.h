@@ -25,6 +25,15 @@
  * Each system is solved with GMRES(32) + ILU(0), tol 1e-7, at most 10000
  * iterations (the PG interface's settings, src/gmres_interface_pg.cu:7,66).
  * The output arrays are the caller's (nport * numPts elements).
+ * Current sources, per source k: PWL when PWLcurExist and PWLnumPts_host[k] > 0
+ * (at most MAX_PWL_PTS points read), else PULSE when PULSEcurExist, else 0.
+ * (Deviation: the reference evaluates all nIS as PWL and then, when
+ * PULSEcurExist, overwrites all nIS with PULSE, src/wrapperGMRESforPG.cu:331-392.)
+ * Errors (bad sizes or ports, allocation / factorization / solve failure): the
+ * reference aborts (checkCudaErrors); here the message goes to stderr and every
+ * requested output element (x_single_host / x_host) is set to NaN.  A system
+ * that does not converge in 10000 iterations prints "Failed to converge." as
+ * the reference does and keeps its last iterate.
  */
 #ifndef GG_COMPAT_GPUDATA_H_
 #define GG_COMPAT_GPUDATA_H_

@@ -103,7 +103,12 @@ int gg_host_coo2csr_in(int nrows, int nz, double *val, int *row_idx, int *col_id
  * (gen_PULSEut_kernel's parameters); PWL {t0, v0, t1, v1, ...} with a point
  * (0, v0) in front when t0 != 0.  port[k] = unknown index of .print port k
  * (-1: ground or unknown name).  Arrays are malloc'd; release the whole
- * struct with gg_host_free_netlist.  GG_EINVAL if the file cannot be read. */
+ * struct with gg_host_free_netlist.  GG_EINVAL if the file cannot be read.
+ * Deliberate deviation: an R/C/L/V/I line without a name, two nodes and a
+ * value rejects the netlist (GG_EINVAL, gg_last_error names the line); the
+ * reference prints "Fail in obtaining ... value" and skips the stamp but still
+ * counts the V / L branch row (src/parser.cpp:746-762, 854-858), leaving an
+ * all-zero row in G (tests/test_netlist.py::test_netlist_short_element_line_rejected). */
 typedef struct gg_netlist {
     int n_nodes, n_l, n_v, n_i, n;
     double tstep, tstop;

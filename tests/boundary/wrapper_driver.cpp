@@ -7,7 +7,8 @@
 //
 //   wrapper_driver IN OUT
 // IN  (little-endian): int32 n, nVS, nIS, numPts, nport, is_kind (0 none,
-//     1 PWL, 2 PULSE), use_single, use_double; double tstep; then the CSC
+//     1 PWL, 2 PULSE, 3 both: the PWL block, then the PULSE block), use_single,
+//     use_double; double tstep; then the CSC
 //     matrices left, right, G, B, each int64 m, ncol, nnz, p[ncol+1], i[nnz],
 //     double x[nnz]; int32 invPort[nport]; double dcVt[nVS]; PWL: int32
 //     numPts[nIS], double time[nIS*64], value[nIS*64]; PULSE: double
@@ -82,7 +83,7 @@ int main(int argc, char **argv)
     e.dcVt_host = dc.data();
     std::vector<int> pwl_n;
     std::vector<double> pwl_t, pwl_v, pul_t, pul_v;
-    if (kind == 1) {
+    if (kind == 1 || kind == 3) {
         e.PWLcurExist = 1;
         pwl_n = rd<int>(nIS);
         pwl_t = rd<double>((size_t)nIS * MAX_PWL_PTS);
@@ -90,7 +91,8 @@ int main(int argc, char **argv)
         e.PWLnumPts_host = pwl_n.data();
         e.PWLtime_host = pwl_t.data();
         e.PWLval_host = pwl_v.data();
-    } else if (kind == 2) {
+    }
+    if (kind == 2 || kind == 3) {
         e.PULSEcurExist = 1;
         pul_t = rd<double>((size_t)nIS * 5);
         pul_v = rd<double>((size_t)nIS * 2);

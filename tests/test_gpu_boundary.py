@@ -148,33 +148,40 @@ def _mna_system(nx, h):
     return n, G, left, right, B, nIS
 
 
-@pytest.mark.parametrize("kind", ["pwl", "pulse"])
+@pytest.mark.parametrize("kind", ["pwl", "pulse", "mixed"])
 def test_wrapper_gmres_for_pg(tmp_path, kind):
+    """mixed: a netlist with both PWL and PULSE current sources -- each source
+    takes its own waveform (PWL where it has points, else its PULSE row;
+    include/compat/gpuData.h), PWL point counts above MAX_PWL_PTS clamped"""
     nx, h, numPts = 24, 1e-2, 40
     n, G, left, right, B, nIS = _mna_system(nx, h)
     nVS = 1
     ports = np.array([0, n // 3, n // 2, n - 1], np.int32)
     dc = np.array([2e-3])
-    hdr = struct.pack("<8i", n, nVS, nIS, numPts, len(ports), 1 if kind == "pwl" else 2, 1, 1) + \
-        struct.pack("<d", h)
+    code = {"pwl": 1, "pulse": 2, "mixed": 3}[kind]
+    hdr = struct.pack("<8i", n, nVS, nIS, numPts, len(ports), code, 1, 1) + struct.pack("<d", h)
     payload = hdr + b"".join(_csc_bytes(S) for S in (left, right, G, B)) + ports.tobytes() + dc.tobytes()
     srcs = [(O.SRC_DC, [dc[0]])]
-    if kind == "pwl":
-        npts = np.array([4, 3, 5, 2, 4, 3], np.int32)
+    npts = np.array([4, 3, 5, 2, 4, 3], np.int32) if kind == "pwl" else np.array([4, 0, 5, 0, 70, 0], np.int32)
+    pt = np.array([[k * h, 3 * h, 2 * h, 8 * h, 20 * h] for k in range(nIS)])   # td tr tf tw tp
+    pv = np.array([[0.0, 1e-3 * (1 + k)] for k in range(nIS)])                  # vlo vhi
+    if kind in ("pwl", "mixed"):
         tt = np.zeros((nIS, 64))
         vv = np.zeros((nIS, 64))
         for k in range(nIS):
-            t = np.cumsum(np.random.default_rng(k).uniform(2 * h, 9 * h, npts[k]))
-            v = np.random.default_rng(50 + k).uniform(-1e-3, 1e-3, npts[k])
-            tt[k, :npts[k]], vv[k, :npts[k]] = t, v
-            srcs.append((O.SRC_PWL, np.stack([t, v], 1).reshape(-1)))
+            c = min(int(npts[k]), 64)
+            t = np.cumsum(np.random.default_rng(k).uniform(2 * h, 9 * h, c))
+            v = np.random.default_rng(50 + k).uniform(-1e-3, 1e-3, c)
+            tt[k, :c], vv[k, :c] = t, v
         payload += npts.tobytes() + tt.tobytes() + vv.tobytes()
-    else:
-        pt = np.array([[k * h, 3 * h, 2 * h, 8 * h, 20 * h] for k in range(nIS)])   # td tr tf tw tp
-        pv = np.array([[0.0, 1e-3 * (1 + k)] for k in range(nIS)])                  # vlo vhi
-        for k in range(nIS):
-            srcs.append((O.SRC_PULSE, [pv[k, 0], pv[k, 1], *pt[k]]))
+    if kind in ("pulse", "mixed"):
         payload += pt.tobytes() + pv.tobytes()
+    for k in range(nIS):
+        if kind != "pulse" and npts[k] > 0:
+            c = min(int(npts[k]), 64)
+            srcs.append((O.SRC_PWL, np.stack([tt[k, :c], vv[k, :c]], 1).reshape(-1)))
+        else:
+            srcs.append((O.SRC_PULSE, [pv[k, 0], pv[k, 1], *pt[k]]))
     data, stdout = _run("wrapper_driver", payload, tmp_path, numPts * len(ports) * 12)
     xs = np.frombuffer(data, np.float32, numPts * len(ports)).reshape(numPts, len(ports))
     xd = np.frombuffer(data, np.float64, numPts * len(ports), numPts * len(ports) * 4).reshape(numPts, len(ports))
@@ -194,3 +201,18 @@ def test_wrapper_gmres_for_pg(tmp_path, kind):
     assert np.array_equal(xs, ref.astype(np.float32))
     assert np.max(np.abs(ref)) > 0 and np.max(np.abs(np.diff(ref, axis=0))) > 0     # driven, time-varying
     assert "Failed to converge" not in stdout
+
+
+def test_wrapper_failure_fills_nan(tmp_path):
+    """a failing call (here a port outside the system) cannot be mistaken for
+    results: every requested output element is NaN (include/compat/gpuData.h)"""
+    nx, h, numPts = 12, 1e-2, 5
+    n, G, left, right, B, nIS = _mna_system(nx, h)
+    ports = np.array([0, n + 5], np.int32)
+    hdr = struct.pack("<8i", n, 1, nIS, numPts, len(ports), 0, 1, 1) + struct.pack("<d", h)
+    payload = hdr + b"".join(_csc_bytes(S) for S in (left, right, G, B)) + ports.tobytes() + \
+        np.array([1e-3]).tobytes()
+    data, _ = _run("wrapper_driver", payload, tmp_path, numPts * len(ports) * 12)
+    xs = np.frombuffer(data, np.float32, numPts * len(ports))
+    xd = np.frombuffer(data, np.float64, numPts * len(ports), numPts * len(ports) * 4)
+    assert np.all(np.isnan(xs)) and np.all(np.isnan(xd))

@@ -92,7 +92,7 @@ def test_rcp_apply(solver, name, scale):
         O.set_div_mode()
     assert np.array_equal(z, zm)
     ze = O.lusolve(L, U, y)
-    assert rel_err(z, ze) <= 1e-13
+    assert rel_err(z / scale, ze / scale) <= 1e-13      # (scaled: 1e250^2 overflows the norm)
 
 
 @pytest.mark.parametrize("k", [1, 2])

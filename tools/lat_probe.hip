@@ -1,5 +1,6 @@
 // Micro-benchmark: dependent-chain latency (cycles) of fp64 VALU ops and DPP on
 // gfx950, one wave.  Diagnostics only (not part of the library).
+// Build as the library: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off lat_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
