@@ -22,6 +22,15 @@ circuit5M's n = 5,558,326 and nnz ~ 59.5M; the SuiteSparse file
 is not available offline): one step = --c3-spmvs SpMV launches, value =
 algorithmic SpMV bytes / time in GB/s (no parity claim on this matrix).
 
+--workload pg: the reference's power-grid (PG) engine, GMRESilu_GPU with an
+ILU++-style SPLIT preconditioner (src/gmres.cu:2254-2446, MyILUPPfloat
+src/preconditioner.cu:1162-1657), on the C2 grid: B = P_r D_l^-1 A D_r^-1 P_c,
+L = Lt D1 (diagonal last), U = M D1^-1 Ut (diagonal first) from the device
+ILU(0) of B, seeded scales in [0.5, 2); --pg-perm identity (default: the
+factors stay grid-shaped and take the 2D wavefront) or random (P_r = P_c^-1
+random: the level-scheduled flow solve).  The synthetic split stands in for
+ILU++'s factors (ILU++ is not built here).
+
 --workload c5: the transient loop (gg_transient: A = G + C/h on the C2 grid, 1 %
 PULSE sources, --c5-steps backward-Euler steps per step, warm start); value =
 GMRES iterations of all steps / time.
@@ -77,7 +86,9 @@ def parse():
     p.add_argument("--dd-grid", choices=["c4", "c2"], default=None,
                    help="dd workload system: c4 (216^3 7-pt, the default of --workload dd) or c2 "
                         "(1000^2 5-pt, the default sharded system at --gpus N > 1)")
-    p.add_argument("--workload", choices=["c2", "c3", "c3s", "c4", "c5", "dd", "replicas"], default=None,
+    p.add_argument("--pg-perm", choices=["identity", "random"], default="identity",
+                   help="pg: the split's row / column permutations")
+    p.add_argument("--workload", choices=["c2", "c3", "c3s", "c4", "c5", "dd", "replicas", "pg"], default=None,
                    help="default: c2 at N = 1 (one C2 solve per step, the headline), the sharded C2 "
                         "solve at N > 1; dd: the sharded solve (C4 unless --dd-grid c2); replicas: "
                         "one independent C2 solve per rank; c5: a backward-Euler transient (A = G + C/h, "
@@ -106,17 +117,16 @@ def parse():
 KERNEL_NAMES = {
     # sliced-ELL SpMV on short even rows (grids); GG_SPMV_CSR=1 keeps the CSR-stream kernel
     "spmv": "k_spmv_stream<false>" if os.environ.get("GG_SPMV_CSR") == "1" else "k_spmv_sell<false>",
-    "trsv_L": "k_trsv_wave2d<true, 0, false, false, 1>",  # lower, unit diagonal (ILU(0) L), 2D grid
-    "trsv_U": "k_trsv_wave2d<false, 2, false, false, 1>", # upper, reciprocal division (ILU(0) U), 2D grid
+    "trsv_L": "k_trsv_wave2d<true, 0, false, false, 1, false>",  # lower, unit diagonal (ILU(0) L), 2D grid
+    "trsv_U": "k_trsv_wave2d<false, 2, false, false, 1, false>", # upper, reciprocal division (ILU(0) U), 2D grid
 }
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
-# bare dependent-chain latency of one wavefront step (cycles, tools/lat_probe.hip:
-# "step(dpp)" = unit L, "U step (WD_RCP)" = U with the reciprocal-FMA division)
-# and the shader clock it ran at
-# (profiles/r03_lat_probe.txt: "step(dpp)", "U step (WD_RCP)", "U step (WD_MUL)"
-# re-measured in round 3 -- round 1's probe build gave 39.2 / 63.4 cycles)
-CHAIN_CYCLES = {"trsv_L": 29.78, "trsv_U": 53.86, "trsv_U_mul": 34.30}
-SHADER_GHZ = 2.397
+# bare dependent-chain latency of one wavefront step (cycles, tools/lat_probe.hip
+# built like the library, -ffp-contract=off, on MI355X: profiles/r03_lat_probe.txt
+# "step(dpp)" = unit L, "U step (WD_RCP)" = the bit-exact reciprocal-FMA
+# division, "U step (WD_MUL)" = GG_DIV_RCP's one multiply) and the shader clock
+CHAIN_CYCLES = {"trsv_L": 38.89, "trsv_U": 62.66, "trsv_U_mul": 43.72}
+SHADER_GHZ = 2.399
 
 
 def pmc_traffic(kernel, workload=None):
@@ -153,6 +163,36 @@ def mgs_bytes(n, m, inner_list):
             ref += 40.0 * n * (i + 1) + 24.0 * n
             iters += 1
     return fused, ref, iters
+
+
+def pg_split(A, device, seed=20261015, identity=True):
+    """Synthetic ILU++-style split of A (the PG engine's preconditioner):
+    B = P_r D_l^-1 A D_r^-1 P_c with pcol = prow^-1, (Lt, Ut) = the device ILU(0)
+    of B (leftILU semantics), L = Lt D1 (non-unit, diagonal last), U = M D1^-1 Ut
+    (diagonal first), so Ml A Mr = D1^-1 Lt^-1 B Ut^-1 D1."""
+    import scipy.sparse as sp
+    import ggmres
+    A = sp.csr_matrix(A)
+    n = A.shape[0]
+    rng = np.random.default_rng(seed)
+    prow = np.arange(n, dtype=np.int32) if identity else rng.permutation(n).astype(np.int32)
+    pcol = np.argsort(prow).astype(np.int32)
+    lscale, rscale, middle, d1 = (rng.uniform(0.5, 2.0, n) for _ in range(4))
+    Pr = sp.csr_matrix((np.ones(n), (np.arange(n), prow)), shape=(n, n))
+    B = (Pr @ sp.diags(1.0 / lscale) @ A @ sp.diags(1.0 / rscale) @ Pr.T).tocsr()
+    B.sort_indices()
+    f = ggmres.Solver(device)
+    f.set_matrix(B)
+    vals, _ = f.ilu0_device_values()
+    f.close()
+    F = sp.csr_matrix((vals, B.indices, B.indptr), shape=(n, n))
+    Lt = (sp.tril(F, -1) + sp.identity(n)).tocsr()
+    Ut = sp.triu(F).tocsr()
+    L = (Lt @ sp.diags(d1)).tocsr()
+    U = (sp.diags(middle / d1) @ Ut).tocsr()
+    L.sort_indices()
+    U.sort_indices()
+    return L, U, middle, prow, pcol, lscale, rscale
 
 
 def cpu_model():
@@ -407,6 +447,7 @@ def main():
     c5 = a.workload == "c5"
     c4 = a.workload == "c4"
     c3s = a.workload == "c3s"           # GMRES + ILU(0) on the C3 stand-in (general sparsity)
+    pg = a.workload == "pg"             # the split (PG) engine on the C2 grid
     h5 = 1e-2
     A = M.grid_7pt(a.c4_grid) if c4 else M.power_law() if c3s else M.laplacian_5pt(a.grid)
     if c5:
@@ -417,11 +458,14 @@ def main():
     t_setup = time.perf_counter()
     s.set_matrix(A)
     kilu = a.ilu_level if a.workload in ("c2", "c3s") else 0
-    if kilu:
+    if pg:
+        split = pg_split(A, local, identity=a.pg_perm == "identity")
+        s.set_precond_split(*split)
+    elif kilu:
         s.set_precond_iluk_device(kilu)
         if not c3s:
             for dom_ in ("trsv_L", "trsv_U"):              # the skewed instantiation (skew k+1)
-                KERNEL_NAMES[dom_] = KERNEL_NAMES[dom_][:-2] + f"{kilu + 1}>"
+                KERNEL_NAMES[dom_] = KERNEL_NAMES[dom_].replace(", 1, false>", f", {kilu + 1}, false>")
     else:
         s.set_precond_ilu0()
     s.set_division(ggmres.DIV_RCP if a.division == "rcp" else ggmres.DIV_EXACT)
@@ -431,6 +475,7 @@ def main():
         KERNEL_NAMES["trsv_L"] = s.trsv_kernel(0)
         KERNEL_NAMES["trsv_U"] = s.trsv_kernel(1)
     u_mul = s.division_active(1) == ggmres.DIV_RCP
+    l_mul = s.division_active(0) == ggmres.DIV_RCP
     t_setup = time.perf_counter() - t_setup
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -589,7 +634,9 @@ def main():
     # latency (tools/lat_probe.hip on MI355X, profiles/r01_lat_probe.txt)
     lat = None
     if roof and dom in ("trsv_L", "trsv_U") and s.uses_wavefront and not c5:
-        cyc = CHAIN_CYCLES["trsv_L" if dom == "trsv_L" else "trsv_U_mul" if u_mul else "trsv_U"]
+        # a non-unit L (the split engine's) divides like U
+        mul = u_mul if dom == "trsv_U" else l_mul
+        cyc = CHAIN_CYCLES["trsv_L" if dom == "trsv_L" and not pg else "trsv_U_mul" if mul else "trsv_U"]
         # the DAG's longest path (ILU(k): skew k+1; 3D: nx + ny + nz - 2, whose
         # per-step chain is the 2D one: the tile kernel's plane term is off it)
         steps = 3 * a.c4_grid - 2 if c4 else a.grid + (kilu + 1) * (a.grid - 1)
@@ -608,21 +655,28 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and a.cpu_iters > 0 and not c5 and not c4 and not c3s:
         import oracle as O
-        L, U = O.ilu0(A)
+        if pg:
+            Ls, Us, mid, pr, pc, lsc, rsc = split
+            osplit = O.Split(O.csr(Ls), O.csr(Us), mid, pr, pc, lsc, rsc)
+        else:
+            L, U = O.ilu0(A)
         # one core, pinned in-process (taskset -c 0 equivalent, no re-exec)
         aff = os.sched_getaffinity(0)
         core = min(aff)
         os.sched_setaffinity(0, {core})
         try:
             t1 = time.perf_counter()
-            o = O.gmres_left(A, L, U, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
+            if pg:
+                o = O.gmres_split(A, osplit, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
+            else:
+                o = O.gmres_left(A, L, U, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
             ct = time.perf_counter() - t1
         finally:
             os.sched_setaffinity(0, aff)
         cpu = {"value": round(o["inner"] / ct, 3), "unit": "iterations/s", "cores": 1,
                "kind": "port", "pinned_core": core, "nproc": os.cpu_count(),
                "affinity_cores": len(aff), "cpu_model": cpu_model(),
-               "sample": f"oracle/ fp64 serial C restatement of GMRES_leftILU0 on the same C2 "
+               "sample": f"oracle/ fp64 serial C restatement of {'GMRESilu (split)' if pg else 'GMRES_leftILU0'} on the same C2 "
                          f"system, first {o['inner']} inner iterations ({ct:.1f} s), one thread "
                          f"pinned to core {core}"}
 
@@ -643,14 +697,19 @@ def main():
                                 f"(no parity claim at this size), ILU({kilu}) left (device-factored; "
                                 f"C3 names ILU(1)), GMRES({a.restart}), tol {a.tol:g}, "
                                 f"b=A*1, x0=0, one solve per step") if c3s else
+                               (f"PG engine (GMRESilu_GPU) on the C2 grid: {a.grid}x{a.grid} 5-pt Laplacian, "
+                                f"synthetic ILU++-style split (device ILU(0) of P_r D_l^-1 A D_r^-1 P_c, "
+                                f"{a.pg_perm} permutations, seeded scales), GMRES({a.restart}), tol {a.tol:g}, "
+                                f"b=A*1, x0=0, one solve per step") if pg else
                                (f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU({kilu}) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step"),
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
                    "wavefront_sptrsv": s.uses_wavefront,
-                   "division": ("x = acc * RN(1/d) on the wavefront U solve (GG_DIV_RCP; tolerance "
-                                "parity 1e-10 vs the reference's division)") if u_mul else
-                               "x = RN(acc / d) (the reference's division, bit-exact)",
+                   "division": ((f"x = acc * RN(1/d) on the wavefront {'L and U solves' if l_mul else 'U solve'} "
+                                 f"(GG_DIV_RCP; tolerance parity 1e-10 vs the reference's division)")
+                                if u_mul else
+                                "x = RN(acc / d) (the reference's division, bit-exact)"),
                    "parallelism": "single" if world == 1 else f"replicas{world}",
                    "setup_s": round(t_setup, 3)},
         "roofline": roof, "latency_roofline": lat,

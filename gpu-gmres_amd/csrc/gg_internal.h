@@ -136,6 +136,10 @@ struct Wave2D {
     // edge lane's history of the neighbour band's line (forward), and T keeps
     // as many after the last row (backward)
     int skew = 1;
+    // the upper triangle's rows list the in-line term (r+1) before the line term
+    // (r+nx): the split (ILU++) U factor's ascending order (detect_wave2d's
+    // split_u); 2D, skew 1 only
+    bool u_inline_first = false;
     long long P2 = 0;        // one plane's layout length (nbands * T * 64)
     long long P = 0;         // padded layout length (nz * P2)
     // 3D tile layout (tile = true; kernels.hip k_trsv_tile3d): a wave owns a
@@ -167,7 +171,10 @@ struct Wave2D {
 // detect: L off-diagonals only at offsets {nx, nx-1, .., nx-k, 1} in this order
 // and U at {nx, nx-1, .., nx-k, 1} (canonical orders; k <= 2: ILU(0..2) of a
 // 5-point grid), no wrap-around entries; skew = k + 1.  ok=false otherwise.
-Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U);
+// split_u: U rows at {1, nx} in this order instead (ascending columns, the
+// split U factor of MyILUPP::HostPrecond_right, src/preconditioner.cu:1117-1137),
+// no fill (k = 0); sets u_inline_first.
+Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U, bool split_u = false);
 // 3D: offsets {nx*ny, nx, 1} in this order in L and in U (canonical orders),
 // no wrap-around; nz >= 2 planes of the 2D layout
 Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U);
@@ -257,6 +264,8 @@ struct DevTri {
     DBuf<double> ce1, ce2;       // skew 2/3 (ILU(1)/(2) fill): |offset| = nx-1, nx-2 coefficients
     DBuf<unsigned long long> prog;   // 3D: per (plane, band) batches stored (0 between launches)
     DBuf<int> order;             // 3D tiles: forward dependency order (the backward solve reverses it)
+    bool il = false;             // upper 2D: in-line term first (Wave2D::u_inline_first)
+    const double *osc = nullptr; // 2D, per launch: store x / osc (the split's D_r^-1 fold), null = x
     int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
     bool rcp_ok = false;         // every divisor admits WD_RCP
     bool mul_ok = false;         // every 1/d is finite and normal (WD_MUL admissible; rw uploaded)

@@ -117,7 +117,7 @@ Levels level_sets(const CanonTri &T)
     return L;
 }
 
-Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
+Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U, bool split_u)
 {
     Wave2D w;
     const int n = L.off.n;
@@ -133,7 +133,7 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
             const int o = r - L.off.ci[k];
             if (o > 1) K = std::max(K, nx - o);
         }
-    if (K > 2 || nx < K + 3) return w;
+    if (K > 2 || nx < K + 3 || (split_u && K > 0)) return w;
     // L rows: [r-nx][r-nx+1]..[r-nx+K][r-1] in this order (each may be absent),
     // no wrap: (j-1, i+a) needs i + a < nx, (j, i-1) needs i > 0
     for (int r = 0; r < n; r++) {
@@ -143,8 +143,15 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
         if (k < ub && L.off.ci[k] == r - 1 && (r % nx) != 0) k++;
         if (k != ub) return w;
     }
-    // U rows (LUSolve_ignoreZero walks from the row end): [r+nx][r+nx-1]..[r+nx-K][r+1]
-    for (int r = 0; r < n; r++) {
+    // U rows (LUSolve_ignoreZero walks from the row end): [r+nx][r+nx-1]..[r+nx-K][r+1];
+    // split_u: [r+1][r+nx] (ascending, diag-first split U)
+    for (int r = 0; split_u && r < n; r++) {
+        int lb = U.off.rp[r], ub = U.off.rp[r + 1], k = lb;
+        if (k < ub && U.off.ci[k] == r + 1 && (r % nx) != nx - 1) k++;
+        if (k < ub && U.off.ci[k] == r + nx) k++;
+        if (k != ub) return w;
+    }
+    for (int r = 0; !split_u && r < n; r++) {
         int lb = U.off.rp[r], ub = U.off.rp[r + 1], k = lb;
         for (int a = 0; a <= K; a++)
             if (k < ub && U.off.ci[k] == r + nx - a && (r % nx) - a >= 0) k++;
@@ -155,6 +162,7 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U)
     w.nx = nx;
     w.ny = n / nx;
     w.skew = K + 1;
+    w.u_inline_first = split_u;
     w.nbands = (w.ny + 63) / 64;
     // the lane skew, plus skew-1 lead-in and run-out steps (Wave2D::slot)
     w.T = (nx + 63 * w.skew + 2 * (w.skew - 1) + kWaveTAlign - 1) / kWaveTAlign * kWaveTAlign;

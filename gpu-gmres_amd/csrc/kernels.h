@@ -93,8 +93,9 @@ void launch_scatter_mul(Gate g, const double *in, const double *s, const int *pe
 
 // ---- SpMV ------------------------------------------------------------------
 // y = A x  (resid=false)  or  y = b - A x  (resid=true)
+// y = A x (resid: y = b - A x); ydiv: y[r] /= ydiv[r] (the split engine's folded row scaling)
 void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, double *y, bool resid,
-                 hipStream_t st);
+                 hipStream_t st, const double *ydiv = nullptr);
 
 // ---- triangular solves ---------------------------------------------------------
 void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st);

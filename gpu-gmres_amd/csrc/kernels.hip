@@ -272,11 +272,14 @@ __global__ void k_scatter_mul(Gate g, const double *in, const double *s, const i
 // CSR-stream: a block owns <=256 consecutive rows holding <=kSpmvCap nnz.
 // Products v*x[col] are formed with coalesced loads into LDS, then each row is
 // summed serially in CSR order (computeSpMV order, src/SpMV_compute.cpp:19-36).
-template <bool RESID>
+// YDIV: y[r] = (the row's result) / ydiv[r] -- the split engine's row gather
+// and D_l scaling (gather_divsrc, src/preconditioner.cu:1592-1626) folded into
+// the SpMV of the row-permuted matrix: the same division of the same value.
+template <bool RESID, bool YDIV = false>
 __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, const int *rp,
                                                         const int *ci, const double *v,
                                                         const double *x, const double *b,
-                                                        double *y)
+                                                        double *y, const double *ydiv)
 {
     if (gated(g)) return;
     constexpr int U = kSpmvCap / kBlock;        // products per thread
@@ -295,7 +298,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
         double acc = 0.0;
         for (int e = e0 + tid; e < e1; e += kBlock) acc += v[e] * x[ci[e]];
         acc = block_sum(acc);
-        if (tid == 0) y[r0] = RESID ? (-1.0 * acc + 1.0 * b[r0]) : acc;
+        if (tid == 0) {
+            const double o = RESID ? (-1.0 * acc + 1.0 * b[r0]) : acc;
+            y[r0] = YDIV ? o / ydiv[r0] : o;
+        }
         return;
     }
     // entries in aligned pairs (8-B index and 16-B value loads) from the even
@@ -347,7 +353,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
         }
         for (; e < z; e++) acc += prod[e];
         const int r = r0 + tid;
-        y[r] = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
+        const double o = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
+        y[r] = YDIV ? o / ydiv[r] : o;
     }
 }
 
@@ -356,13 +363,14 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
 // wave), up to 8 index/value pairs in flight before their gathers; each row is
 // summed serially in CSR order from 0.0, skipping the padding (col -1): the
 // same operations as k_spmv_stream (computeSpMV order).
-template <bool RESID>
+template <bool RESID, bool YDIV = false>
 __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice, const int *sptr,
                                                       const int *__restrict__ ci,
                                                       const double *__restrict__ v,
                                                       const double *__restrict__ x,
                                                       const double *__restrict__ b,
-                                                      double *__restrict__ y)
+                                                      double *__restrict__ y,
+                                                      const double *__restrict__ ydiv)
 {
     if (gated(g)) return;
     const int s = blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -389,7 +397,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
             if (k0 + k < w && c[k] >= 0) acc += a[k] * xv[k];
     }
     const int r = s * 64 + lane;
-    if (r < n) y[r] = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
+    if (r < n) {
+        const double o = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
+        y[r] = YDIV ? o / ydiv[r] : o;
+    }
 }
 
 // ======================================================= triangular solves
@@ -790,15 +801,22 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
     }
 }
 
-template <bool FWD, int DIV, bool TRACE, bool D3 = false, int S = 1>
+// IL: the in-line term (|offset| = 1) comes first in the row's canonical order,
+// then the line term -- the split (ILU++) U factor's ascending-column rows
+// (MyILUPP::HostPrecond_right, src/preconditioner.cu:1117-1137).  osc (2D,
+// nullable): the writer stores x / osc instead of x -- the split engine's
+// D_r^-1 scaling (gather_divdst, src/preconditioner.cu:1629-1657) folded into
+// the solve's store; the hand-off granules carry the unscaled x.
+template <bool FWD, int DIV, bool TRACE, bool D3 = false, int S = 1, bool IL = false>
 __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
     const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
     double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace,
     int nz, long long P2, const double *__restrict__ c0, unsigned long long *prog,
-    const double *__restrict__ ce1, const double *__restrict__ ce2)
+    const double *__restrict__ ce1, const double *__restrict__ ce2, const double *__restrict__ osc)
 {
     using C = WaveCfg<DIV, D3, S>;
+    static_assert(!IL || (S == 1 && !D3), "in-line-first rows: unskewed 2D grids");
     static_assert(!(TRACE && S > 1), "no trace for skewed grids");
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
     static_assert(!(D3 && TRACE), "no trace for 3D grids");
@@ -895,6 +913,12 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
         // also waits for this band's boundary values of batch bi+1: a band's
         // upstream must not hold back what it hands downstream.
         double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
+        const double2 *O2 = D3 || !osc ? nullptr : reinterpret_cast<const double2 *>(osc) + boff;
+        double2 osv[C::PBN];                // osc of the batch being stored
+        if (!D3 && O2) {
+#pragma unroll
+            for (int kk = 0; kk < C::PBN; kk++) osv[kk] = O2[(long long)(FWD ? kk : np - 1 - kk) * 64];
+        }
         [[maybe_unused]] bool bad = false;  // WD_RCP range guard (see rcp_safe)
         for (int bi = 0; bi <= nbatch; bi++) {
             if (!GG_WAVE_DECOUPLE || bi == 0) raw_barrier();
@@ -928,9 +952,19 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 if constexpr (D3) {
                     st_sc1_16(dst, v[kk]);
                 } else {
-                    *dst = v[kk];
+                    *dst = O2 ? make_double2(v[kk].x / osv[kk].x, v[kk].y / osv[kk].y) : v[kk];
                 }
                 if constexpr (DIV == WD_RCP) bad |= !rcp_safe(v[kk].x) || !rcp_safe(v[kk].y);
+            }
+            // the next batch's divisors, loaded a whole batch before their use
+            // (issued before the barrier wait: an HBM round trip is about half
+            // a batch)
+            if (!D3 && O2 && pb + 1 < nbatch) {
+#pragma unroll
+                for (int kk = 0; kk < C::PBN; kk++) {
+                    const int p = (pb + 1) * C::PBN + kk;
+                    osv[kk] = O2[(long long)(FWD ? p : np - 1 - p) * 64];
+                }
             }
             if (TRACE && lane == 0)
                 trace[(long long)band * (3 * nbatch + 8) + nbatch + 8 + pb] =
@@ -1131,7 +1165,10 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 // the neighbour line's terms oldest first (|offset| = nx, nx-1, ..),
                 // then the in-line neighbour (|offset| = 1)
                 double acc;
-                if constexpr (S == 1) {
+                if constexpr (IL) {
+                    acc = bz - p2;
+                    acc = acc - e1 * xs;
+                } else if constexpr (S == 1) {
                     acc = bz - e1 * xs;
                 } else if constexpr (S == 2) {
                     const double f1 = sx ? rg[kk][C::AE].x : rg[kk][C::AE].y;
@@ -1146,7 +1183,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 }
                 if constexpr (S >= 3) xh2 = xh1;
                 if constexpr (S >= 2) xh1 = xs;
-                acc = acc - p2;
+                if constexpr (!IL) acc = acc - p2;
                 if constexpr (DIV == WD_HW) {
                     acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
                 } else if constexpr (DIV == WD_MUL) {
@@ -2822,21 +2859,26 @@ void launch_scatter_mul(Gate g, const double *in, const double *s, const int *pe
 }
 
 void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, double *y, bool resid,
-                 hipStream_t st)
+                 hipStream_t st, const double *ydiv)
 {
     if (A.nblk == 0) return;
-    if (A.sell) {
-        const int grid = (A.nslice + kBlock / 64 - 1) / (kBlock / 64);
-        if (resid)
-            k_spmv_sell<true><<<grid, kBlock, 0, st>>>(g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, b, y);
-        else
-            k_spmv_sell<false><<<grid, kBlock, 0, st>>>(g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, b, y);
-        return;
+#define GG_SPMV(R, D)                                                                                  \
+    do {                                                                                               \
+        if (A.sell)                                                                                    \
+            k_spmv_sell<R, D><<<(A.nslice + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st>>>(        \
+                g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, b, y, ydiv);                           \
+        else                                                                                           \
+            k_spmv_stream<R, D><<<A.nblk, kBlock, 0, st>>>(g, A.blk.p, A.rp.p, A.ci.p, A.v.p, x, b, y, \
+                                                          ydiv);                                       \
+    } while (0)
+    if (ydiv) {
+        if (resid) GG_SPMV(true, true);
+        else GG_SPMV(false, true);
+    } else {
+        if (resid) GG_SPMV(true, false);
+        else GG_SPMV(false, false);
     }
-    if (resid)
-        k_spmv_stream<true><<<A.nblk, kBlock, 0, st>>>(g, A.blk.p, A.rp.p, A.ci.p, A.v.p, x, b, y);
-    else
-        k_spmv_stream<false><<<A.nblk, kBlock, 0, st>>>(g, A.blk.p, A.rp.p, A.ci.p, A.v.p, x, b, y);
+#undef GG_SPMV
 }
 
 template <bool FWD, int DIV>
@@ -2964,22 +3006,25 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
 #undef GG_TILE_LAUNCH
         } else if (w.nz == 1) {
             dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
-#define GG_WAVE_LAUNCH_S(FWD, DIV, S)                                                              \
-    k_trsv_wave2d<FWD, DIV, false, false, S><<<grid, WaveCfg<DIV, false, S>::THREADS, 0, st>>>(    \
+            const double *osc = T.osc;
+#define GG_WAVE_LAUNCH_S(FWD, DIV, S, IL)                                                          \
+    k_trsv_wave2d<FWD, DIV, false, false, S, IL><<<grid, WaveCfg<DIV, false, S>::THREADS, 0, st>>>( \
         g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr,   \
-        nullptr, T.ce1.p, T.ce2.p)
+        nullptr, T.ce1.p, T.ce2.p, osc)
 #define GG_WAVE_LAUNCH(FWD, DIV)                                                                   \
     do {                                                                                           \
-        if (T.trace && w.skew == 1)                                                                \
+        if (T.trace && w.skew == 1 && !T.il)                                                       \
             k_trsv_wave2d<FWD, DIV, true><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                 \
                 g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, T.trace, 1, w.P2,     \
-                nullptr, nullptr, nullptr, nullptr);                                               \
+                nullptr, nullptr, nullptr, nullptr, osc);                                          \
+        else if (T.il)                                                                             \
+            GG_WAVE_LAUNCH_S(FWD, DIV, 1, true);                                                   \
         else if (w.skew == 1)                                                                      \
-            GG_WAVE_LAUNCH_S(FWD, DIV, 1);                                                         \
+            GG_WAVE_LAUNCH_S(FWD, DIV, 1, false);                                                  \
         else if (w.skew == 2)                                                                      \
-            GG_WAVE_LAUNCH_S(FWD, DIV, 2);                                                         \
+            GG_WAVE_LAUNCH_S(FWD, DIV, 2, false);                                                  \
         else                                                                                       \
-            GG_WAVE_LAUNCH_S(FWD, DIV, 3);                                                         \
+            GG_WAVE_LAUNCH_S(FWD, DIV, 3, false);                                                  \
     } while (0)
             if (T.lower) {
                 if (div == WD_UNIT) GG_WAVE_LAUNCH(true, WD_UNIT);
@@ -3002,7 +3047,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         const int grid = std::min(std::min(ntask, wave3d_max_blocks<FWD, DIV>()), kTileDummyBlocks); \
         k_trsv_wave2d<FWD, DIV, false, true><<<grid, WaveCfg<DIV, true>::THREADS, 0, st>>>(        \
             g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, w.nz, w.P2,      \
-            T.c0.p, T.prog.p, nullptr, nullptr);                                                   \
+            T.c0.p, T.prog.p, nullptr, nullptr, nullptr);                                          \
     } while (0)
             if (T.lower) {
                 if (div == WD_UNIT) GG_WAVE_LAUNCH3(true, WD_UNIT);

@@ -135,6 +135,7 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
 {
     T.lower = C.lower;
     T.n = C.off.n;
+    T.il = !C.lower && wl && wl->ok && wl->u_inline_first;
     const int n = C.off.n;
     if (wl && wl->ok) {
         T.kind = DevTri::WAVE2D;
@@ -253,12 +254,24 @@ struct gg_solver {
     DBuf<long long> lay2nat, nat2lay;
     int G = 1;
 
-    DevCsr dA;
+    DevCsr dA;            // A in layout space (split: A' -- rows in prow order, columns by pcol)
     DevTri L, U;
-    // split (PG) extras, natural layout
-    DBuf<double> middle, lscale, rscale;
-    DBuf<int> prow, pcol;
-    DevCsr dUfull;
+    // Split (PG) engine, every vector in the triangles' layout (natural or
+    // wavefront).  With lay = the layout map of the triangles' row space:
+    //   A'  row lay(j) = A row prow[j], column c -> lay(pcol[c])
+    //   mid_l[lay(r)] = middle[r], ls_l[lay(j)] = lscale[prow[j]],
+    //   rs_l[lay(r)] = rscale[pcol^-1[r]]   (all three 1.0 in padding slots)
+    // so that Ml(A Mr(v)) = L^-1 (A' (U^-1 (mid_l o v) / rs_l)) / ls_l with the
+    // row gather, the column scatter and both scalings folded into the SpMV's
+    // indices and epilogue and the U solve's store (each value rounded by the
+    // same operation as in MyILUPPfloat::DevPrecond_*, src/preconditioner.cu:
+    // 1424-1657).  x lives in the same column convention: x[c] at lay(pcol[c]).
+    DBuf<double> mid_l, ls_l, rs_l;
+    // stage maps (layout slot -> natural index, -1 = padding): b in A' row
+    // order, x in the column convention; and back: x_out[c] = lay(pcol[c]),
+    // y_out[r] = lay(prow^-1[r])
+    DBuf<long long> sb_map, sx_map, sx_out, sy_out;
+    DevCsr dUfull;        // the split U factor (diagonal first) in layout space (apply_start)
 
     // workspace
     int m_alloc = -1;
@@ -335,7 +348,9 @@ Csr make_csr(int n, const int *rp, const int *ci, const double *v)
 void set_device(gg_solver *s) { GG_HIP(hipSetDevice(s->device)); }
 
 // choose the vector space and upload A in it
-void setup_space(gg_solver *s, const Wave2D *wl)
+// The solver's vector space.  prow / pcol (split engine): A' has row lay(j) =
+// A row prow[j] and column c -> lay(pcol[c]); null: A in layout space.
+void setup_space(gg_solver *s, const Wave2D *wl, const int *prow = nullptr, const int *pcol = nullptr)
 {
     const int n = s->A.n;
     s->wave = wl && wl->ok;
@@ -359,27 +374,33 @@ void setup_space(gg_solver *s, const Wave2D *wl)
     s->G = reduce_grid(s->Ppad / 2);
     const char *wf = std::getenv("GG_WIDE_FORCE");     // tests: k_arnoldi_wide at any size
     if (wf && wf[0] == '1') s->G = kWideG;
-    // A in layout space: row p = A row nat(p), columns remapped, entry order kept
-    if (!s->wave) {
+    // A in layout space: row p = A row nat(p) (split: prow[nat(p)]), columns
+    // remapped (split: through pcol), entry order kept
+    if (!s->wave && !prow) {
         Csr Ap = s->A;
         Ap.n = (int)s->P;
         s->dA.upload(Ap, s->st);
     } else {
+        auto src = [&](long long p) -> long long {
+            const long long r = l2n[p];
+            return (r < 0 || !prow) ? r : prow[r];
+        };
         Csr Ap;
         Ap.n = (int)s->P;
         Ap.rp.assign(s->P + 1, 0);
         for (long long p = 0; p < s->P; p++) {
-            long long r = l2n[p];
+            const long long r = src(p);
             Ap.rp[p + 1] = Ap.rp[p] + (r >= 0 ? s->A.rp[r + 1] - s->A.rp[r] : 0);
         }
         Ap.ci.resize(s->A.nnz());
         Ap.v.resize(s->A.nnz());
         for (long long p = 0; p < s->P; p++) {
-            long long r = l2n[p];
+            const long long r = src(p);
             if (r < 0) continue;
             int o = Ap.rp[p];
             for (int k = s->A.rp[r]; k < s->A.rp[r + 1]; k++, o++) {
-                Ap.ci[o] = (int)s->nat2lay_h[s->A.ci[k]];
+                const int c = s->A.ci[k];
+                Ap.ci[o] = (int)s->nat2lay_h[pcol ? pcol[c] : c];
                 Ap.v[o] = s->A.v[k];
             }
         }
@@ -446,28 +467,45 @@ void apply_minv(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
     trsv(s, g, s->L, GG_PROF_TRSV_L, i, in, s->t1.p);
     trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, out);
 }
-// split: Ml(v) = L^-1 P_r D_l^-1 v   (DevPrecond_left, src/preconditioner.cu:1592-1626)
+// Split engine (see gg_solver): every operand in layout space.
+// Ml(v) = L^-1 P_r D_l^-1 v (DevPrecond_left, src/preconditioner.cu:1592-1626),
+// `in` already in A' row order (b, or nothing: the SpMV folds it, spmv_left)
 void apply_left(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 {
-    const int n = s->A.n;
-    launch_gather_divsrc(g, in, s->lscale.p, s->prow.p, s->t1.p, n, s->st);
+    launch_div(g, in, s->ls_l.p, s->t1.p, (int)s->P, s->st);
     trsv(s, g, s->L, GG_PROF_TRSV_L, i, s->t1.p, out);
 }
-// split: Mr(v) = D_r^-1 P_c U^-1 M v   (DevPrecond_right, :1629-1657)
+// Mr(v) = D_r^-1 P_c U^-1 M v (DevPrecond_right, :1629-1657), out in the
+// column convention; the 2D wavefront U solve stores U^-1(..) / rs_l itself
 void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 {
-    const int n = s->A.n;
-    launch_mul(g, in, s->middle.p, s->t1.p, n, s->st);
-    trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
-    launch_gather_divdst(g, s->t2.p, s->rscale.p, s->pcol.p, out, n, s->st);
+    launch_mul(g, in, s->mid_l.p, s->t1.p, (int)s->P, s->st);
+    if (s->U.kind == DevTri::WAVE2D && s->U.wl.nz == 1) {
+        s->U.osc = s->rs_l.p;
+        trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, out);
+        s->U.osc = nullptr;
+    } else {
+        trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
+        launch_div(g, s->t2.p, s->rs_l.p, out, (int)s->P, s->st);
+    }
 }
-// split: Mr^-1(x) = M^-1 U P_c^-1 D_r x   (DevPrecond_starting_value, :1561-1589)
+// Ml(A' z) with Ml's row gather and D_l^-1 in the SpMV (resid: Ml(b - A x))
+void spmv_left(gg_solver *s, Gate g, const double *z, const double *b, double *out, int i = -1)
+{
+    int mk = prof_begin(s, GG_PROF_SPMV, i);
+    launch_spmv(g, s->dA, z, b, s->t1.p, b != nullptr, s->st, s->ls_l.p);
+    prof_end(s, mk);
+    mk = prof_begin(s, GG_PROF_PRECOND, i);
+    trsv(s, g, s->L, GG_PROF_TRSV_L, i, s->t1.p, out);
+    prof_end(s, mk);
+}
+// Mr^-1(x) = M^-1 U P_c^-1 D_r x (DevPrecond_starting_value, :1561-1589), x in
+// the column convention
 void apply_start(gg_solver *s, Gate g, const double *in, double *out)
 {
-    const int n = s->A.n;
-    launch_scatter_mul(g, in, s->rscale.p, s->pcol.p, s->t1.p, n, s->st);
+    launch_mul(g, in, s->rs_l.p, s->t1.p, (int)s->P, s->st);
     launch_spmv(g, s->dUfull, s->t1.p, nullptr, s->t2.p, false, s->st);
-    launch_div(g, s->t2.p, s->middle.p, out, n, s->st);
+    launch_div(g, s->t2.p, s->mid_l.p, out, (int)s->P, s->st);
 }
 void apply_rhs(gg_solver *s, Gate g, const double *in, double *out)
 {
@@ -521,9 +559,13 @@ void enqueue_init(gg_solver *s)
     apply_rhs(s, none, s->bv.p, s->bb.p);                                     // bb = M b
     launch_dot(none, s->bb.p, s->bb.p, s->partA.p, s->G, s->Ppad, s->st);
     launch_set_normb(s->partA.p, s->G, ds, s->st);
-    if (split) apply_start(s, none, s->xv.p, s->y.p);                          // y = Mr^-1 x0
-    launch_spmv(none, s->dA, s->xv.p, s->bv.p, s->rr.p, true, s->st);         // rr = b - A x
-    apply_rhs(s, none, s->rr.p, s->r.p);                                      // r = M rr
+    if (split) {
+        apply_start(s, none, s->xv.p, s->y.p);                                 // y = Mr^-1 x0
+        spmv_left(s, none, s->xv.p, s->bv.p, s->r.p);                          // r = Ml (b - A x)
+    } else {
+        launch_spmv(none, s->dA, s->xv.p, s->bv.p, s->rr.p, true, s->st);     // rr = b - A x
+        apply_rhs(s, none, s->rr.p, s->r.p);                                  // r = M rr
+    }
     launch_dot(none, s->r.p, s->r.p, s->partA.p, s->G, s->Ppad, s->st);
     launch_init_beta(s->partA.p, s->G, ds, s->hist.p, s->st);
 }
@@ -554,12 +596,7 @@ void enqueue_cycle(gg_solver *s, int m)
             prof_end(s, mk);
         } else {
             apply_right(s, gi, vi, s->z.p, i);                                 // z = Mr v_i
-            mk = prof_begin(s, GG_PROF_SPMV, i);
-            launch_spmv(gi, s->dA, s->z.p, nullptr, s->ww.p, false, s->st);    // ww = A z
-            prof_end(s, mk);
-            mk = prof_begin(s, GG_PROF_PRECOND, i);
-            apply_left(s, gi, s->ww.p, s->w.p, i);                             // w = Ml ww
-            prof_end(s, mk);
+            spmv_left(s, gi, s->z.p, nullptr, s->w.p, i);                      // w = Ml A z
         }
         mk = prof_begin(s, GG_PROF_MGS, i);
         if (persist) {
@@ -594,8 +631,12 @@ void enqueue_cycle(gg_solver *s, int m)
     Gate gr;
     gr.done = &ds->done;
     gr.mask = ~0;
-    launch_spmv(gr, s->dA, s->xv.p, s->bv.p, s->rr.p, true, s->st);           // rr = b - A x
-    apply_rhs(s, gr, s->rr.p, s->r.p);
+    if (split) {
+        spmv_left(s, gr, s->xv.p, s->bv.p, s->r.p);                            // r = Ml (b - A x)
+    } else {
+        launch_spmv(gr, s->dA, s->xv.p, s->bv.p, s->rr.p, true, s->st);       // rr = b - A x
+        apply_rhs(s, gr, s->rr.p, s->r.p);
+    }
     launch_dot(gr, s->r.p, s->r.p, s->partA.p, s->G, P, s->st);
     launch_end_cycle(s->partA.p, s->G, ds, s->hist.p, s->st);
 }
@@ -671,11 +712,12 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
         s->hist.alloc(need);
         s->hist_cap = need;
     }
-    // inputs into the solver's vector space
-    launch_gather(d_b, s->lay2nat.p, s->bv.p, s->Ppad, s->st);
-    launch_gather(d_x, s->lay2nat.p, s->xv.p, s->Ppad, s->st);
-    if (s->pkind == GG_PRECOND_SPLIT)
-        GG_HIP(hipMemsetAsync(s->y.p, 0, s->Ppad * sizeof(double), s->st));
+    // inputs into the solver's vector space (split: b in A' row order, x in
+    // the column convention)
+    const bool split = s->pkind == GG_PRECOND_SPLIT;
+    launch_gather(d_b, split ? s->sb_map.p : s->lay2nat.p, s->bv.p, s->Ppad, s->st);
+    launch_gather(d_x, split ? s->sx_map.p : s->lay2nat.p, s->xv.p, s->Ppad, s->st);
+    if (split) GG_HIP(hipMemsetAsync(s->y.p, 0, s->Ppad * sizeof(double), s->st));
     for (DevTri *T : {&s->L, &s->U})
         if (T->kind == DevTri::WAVE2D)
             reset_wave(T, s->st);
@@ -748,7 +790,7 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
     }
     GG_HIP(hipEventRecord(s->ev1, s->st));
     check_err(s);
-    launch_gather(s->xv.p, s->nat2lay.p, d_x, n, s->st);
+    launch_gather(s->xv.p, split ? s->sx_out.p : s->nat2lay.p, d_x, n, s->st);
     GG_HIP(hipStreamSynchronize(s->st));
     float ms = 0.f;
     GG_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -1154,19 +1196,72 @@ int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const d
     for (int i = 0; i < n; i++)
         GG_REQUIRE(perm_row[i] >= 0 && perm_row[i] < n && perm_col[i] >= 0 && perm_col[i] < n,
                    GG_EINVAL, "split: permutation index out of range");
+    std::vector<int> pcinv(n, -1), prinv(n, -1);
+    for (int i = 0; i < n; i++) {
+        GG_REQUIRE(pcinv[perm_col[i]] < 0 && prinv[perm_row[i]] < 0, GG_EINVAL,
+                   "split: perm_row / perm_col is not a permutation");
+        pcinv[perm_col[i]] = i;
+        prinv[perm_row[i]] = i;
+    }
     set_device(s);
     Csr Lf = make_csr(n, l_rp, l_ci, l_v), Uf = make_csr(n, u_rp, u_ci, u_v);
     CanonTri cl = canon_lower_lastdiag(Lf);
     CanonTri cu = canon_upper_firstdiag(Uf);
-    setup_space(s, nullptr);
-    build_tri(s->L, cl, nullptr, &s->nat2lay_h, s->Ppad, s->st);
-    build_tri(s->U, cu, nullptr, &s->nat2lay_h, s->Ppad, s->st);
-    s->middle.upload(middle, n, s->st);
-    s->lscale.upload(lscale, n, s->st);
-    s->rscale.upload(rscale, n, s->st);
-    s->prow.upload(perm_row, n, s->st);
-    s->pcol.upload(perm_col, n, s->st);
-    s->dUfull.upload(Uf, s->st);
+    // grid-shaped factors (the split of a 5-point grid in natural order) take
+    // the 2D wavefront: L rows ascending = the kernel's order, U rows ascending
+    // = in-line term first (u_inline_first)
+    Wave2D wl;
+    const char *env = std::getenv("GG_NO_WAVEFRONT");
+    if (!(env && env[0] == '1')) {
+        wl = detect_wave2d(cl, cu, true);
+        if (wl.ok && wl.nbands > 512) wl.ok = false;
+    }
+    setup_space(s, &wl, perm_row, perm_col);
+    build_tri(s->L, cl, &wl, &s->nat2lay_h, s->Ppad, s->st);
+    build_tri(s->U, cu, &wl, &s->nat2lay_h, s->Ppad, s->st);
+    const long long Pp = s->Ppad;
+    const std::vector<long long> &lay = s->nat2lay_h;
+    // padding slots: every divisor and multiplier 1.0 (apply_start divides by
+    // mid_l; a 0 there would put 0/0 into the padding of y and the wavefront
+    // carries a padding NaN into real rows through 0 * NaN)
+    std::vector<double> mid(Pp, 1.0), ls(Pp, 1.0), rs(Pp, 1.0);
+    std::vector<long long> bmap(Pp, -1), xmap(Pp, -1), xout(n), yout(n);
+    for (int r = 0; r < n; r++) {
+        const long long p = lay[r];
+        mid[p] = middle[r];
+        ls[p] = lscale[perm_row[r]];
+        rs[p] = rscale[pcinv[r]];
+        bmap[p] = perm_row[r];
+        xmap[p] = pcinv[r];
+        xout[r] = lay[perm_col[r]];
+        yout[r] = lay[prinv[r]];
+    }
+    s->mid_l.upload(mid, s->st);
+    s->ls_l.upload(ls, s->st);
+    s->rs_l.upload(rs, s->st);
+    s->sb_map.upload(bmap, s->st);
+    s->sx_map.upload(xmap, s->st);
+    s->sx_out.upload(xout, s->st);
+    s->sy_out.upload(yout, s->st);
+    // the full U (diagonal first) in layout space, entry order kept
+    Csr Ul;
+    Ul.n = (int)s->P;
+    Ul.rp.assign(s->P + 1, 0);
+    std::vector<long long> l2n(s->P, -1);
+    for (int r = 0; r < n; r++) l2n[lay[r]] = r;
+    for (long long p = 0; p < s->P; p++)
+        Ul.rp[p + 1] = Ul.rp[p] + (l2n[p] >= 0 ? Uf.rp[l2n[p] + 1] - Uf.rp[l2n[p]] : 0);
+    Ul.ci.resize(Uf.nnz());
+    Ul.v.resize(Uf.nnz());
+    for (long long p = 0; p < s->P; p++) {
+        if (l2n[p] < 0) continue;
+        int o = Ul.rp[p];
+        for (int k = Uf.rp[l2n[p]]; k < Uf.rp[l2n[p] + 1]; k++, o++) {
+            Ul.ci[o] = (int)lay[Uf.ci[k]];
+            Ul.v[o] = Uf.v[k];
+        }
+    }
+    s->dUfull.upload(Ul, s->st);
     s->pkind = GG_PRECOND_SPLIT;
     GG_HIP(hipStreamSynchronize(s->st));
     return GG_OK;
@@ -1209,7 +1304,8 @@ int gg_trsv_kernel(gg_solver *s, int which, char *name, int cap)
             k = std::string("k_trsv_tile3d<") + fwd + ", " + std::to_string(div) + ", false>";
         else
             k = std::string("k_trsv_wave2d<") + fwd + ", " + std::to_string(div) + ", false, " +
-                (T.wl.nz > 1 ? "true" : "false") + ", " + std::to_string(T.wl.nz > 1 ? 1 : T.wl.skew) + ">";
+                (T.wl.nz > 1 ? "true" : "false") + ", " + std::to_string(T.wl.nz > 1 ? 1 : T.wl.skew) + ", " +
+                (T.il ? "true" : "false") + ">";
     } else if (T.kind == DevTri::LEVEL) {
         const char *lv = std::getenv("GG_TRSV_LEVELS");
         k = (lv && atoi(lv) != 0) ? "k_trsv_level" : "k_trsv_flow";
@@ -1482,10 +1578,11 @@ int gg_spmv(gg_solver *s, const double *x, double *y)
     set_device(s);
     ensure_workspace(s, std::max(s->m_alloc, 1));
     stage_in(s, x, s->nat_in);
-    launch_gather(s->nat_in.p, s->lay2nat.p, s->xv.p, s->Ppad, s->st);
+    const bool split = s->pkind == GG_PRECOND_SPLIT;      // A' = A with rows / columns permuted
+    launch_gather(s->nat_in.p, split ? s->sx_map.p : s->lay2nat.p, s->xv.p, s->Ppad, s->st);
     launch_spmv(Gate{}, s->dA, s->xv.p, nullptr, s->ww.p, false, s->st);
     if (s->nat_out.n < (size_t)std::max(s->A.n, 1)) s->nat_out.alloc(std::max(s->A.n, 1));
-    launch_gather(s->ww.p, s->nat2lay.p, s->nat_out.p, s->A.n, s->st);
+    launch_gather(s->ww.p, split ? s->sy_out.p : s->nat2lay.p, s->nat_out.p, s->A.n, s->st);
     stage_out(s, s->nat_out, y);
     return GG_OK;
     GG_API_END
@@ -1505,7 +1602,12 @@ int gg_precond_apply(gg_solver *s, int op, const double *in, double *out)
         if (T->kind == DevTri::WAVE2D)
             reset_wave(T, s->st);
     stage_in(s, in, s->nat_in);
-    launch_gather(s->nat_in.p, s->lay2nat.p, s->xv.p, s->Ppad, s->st);
+    // operator input spaces: LEFT takes an A-row vector (A' row order), START
+    // an x (column convention), RIGHT / MINV a vector of the triangles' space
+    const long long *in_map = !split || op == GG_APPLY_RIGHT ? s->lay2nat.p
+                              : op == GG_APPLY_START        ? s->sx_map.p
+                                                            : s->sb_map.p;
+    launch_gather(s->nat_in.p, in_map, s->xv.p, s->Ppad, s->st);
     auto run = [&]() {
         GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
         Gate none;
@@ -1524,7 +1626,8 @@ int gg_precond_apply(gg_solver *s, int op, const double *in, double *out)
         run();
     }
     if (s->nat_out.n < (size_t)std::max(s->A.n, 1)) s->nat_out.alloc(std::max(s->A.n, 1));
-    launch_gather(s->ww.p, s->nat2lay.p, s->nat_out.p, s->A.n, s->st);
+    launch_gather(s->ww.p, split && op == GG_APPLY_RIGHT ? s->sx_out.p : s->nat2lay.p, s->nat_out.p,
+                  s->A.n, s->st);
     stage_out(s, s->nat_out, out);
     return GG_OK;
     GG_API_END

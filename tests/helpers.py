@@ -10,16 +10,20 @@ def csr_sp(T):
     return sp.csr_matrix((T.v, T.ci, T.rp), shape=(T.n, T.n))
 
 
-def make_split(A, seed=7):
+def make_split(A, seed=7, identity_perm=False):
     """Synthetic PG split preconditioner for A.
 
     With pcol = prow^-1, B = P_r D_l^-1 A D_r^-1 P_c is a symmetric permutation
     of a scaled A; B ~= Lt Ut (oracle ILU(0)); L = Lt D1 (non-unit, diag last),
-    U = M D1^-1 Ut (diag first) so that Ml A Mr = L^-1 B U^-1 M ~= I."""
+    U = M D1^-1 Ut (diag first) so that Ml A Mr = L^-1 B U^-1 M ~= I.
+    identity_perm: P_r = P_c = I (the factors of a grid stay grid-shaped: the
+    split engine's 2D wavefront path)."""
     A = sp.csr_matrix(A)
     n = A.shape[0]
     rng = np.random.default_rng(seed)
     prow = rng.permutation(n).astype(np.int32)
+    if identity_perm:
+        prow = np.arange(n, dtype=np.int32)
     pcol = np.argsort(prow).astype(np.int32)
     lscale = rng.uniform(0.5, 2.0, n)
     rscale = rng.uniform(0.5, 2.0, n)

@@ -421,6 +421,60 @@ def test_gmres_split_parity(solver):
     check_exact(g, ot)
 
 
+@pytest.mark.parametrize("dims", [(40, 40), (70, 130)])
+def test_split_wavefront_maps_bitexact(solver, dims):
+    """The split engine on grid-shaped factors: 2D wavefront L (non-unit, diag
+    last) and U (diag first, in-line term first), D_r^-1 folded into the U
+    solve's store, the row gather and D_l^-1 into the SpMV."""
+    A = M.laplacian_5pt(*dims)
+    P = make_split(A, seed=5, identity_perm=True)
+    solver.set_matrix(A)
+    solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    assert solver.uses_wavefront
+    rng = np.random.default_rng(6)
+    for scale in (1.0, 1e250, 1e-250):
+        v = rng.standard_normal(A.shape[0]) * scale
+        assert np.array_equal(solver.precond_apply(ggmres.APPLY_LEFT, v), P.left(v))
+        assert np.array_equal(solver.precond_apply(ggmres.APPLY_RIGHT, v), P.right(v))
+        assert np.array_equal(solver.precond_apply(ggmres.APPLY_START, v), P.start(v))
+    x = rng.standard_normal(A.shape[0])
+    assert np.array_equal(solver.spmv(x), O.spmv(A, x))
+
+
+def test_gmres_split_wavefront_parity(solver):
+    A = M.laplacian_5pt(48, 40)
+    n = A.shape[0]
+    P = make_split(A, seed=9, identity_perm=True)
+    b = M.rhs_uniform(n)
+    x0 = np.random.default_rng(3).random(n) * 0.1
+    o, ot = oracle_both(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11), n, nx=48)
+    solver.set_matrix(A)
+    solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    assert solver.uses_wavefront
+    g = solver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
+    check_gmres(g, o)
+    check_exact(g, ot)
+    # reciprocal-multiply division on both wavefront solves: tolerance parity
+    solver.set_division(ggmres.DIV_RCP)
+    try:
+        assert solver.division_active(0) == solver.division_active(1) == ggmres.DIV_RCP
+        g2 = solver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
+    finally:
+        solver.set_division(ggmres.DIV_EXACT)        # the fixture is shared by the module
+    check_gmres(g2, o)
+
+
+def test_split_random_perm_spmv(solver):
+    """gg_spmv on a split solver (A' = A with permuted rows and columns inside)"""
+    A = M.laplacian_5pt(30, 20)
+    P = make_split(A, seed=4)
+    solver.set_matrix(A)
+    solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    assert not solver.uses_wavefront
+    x = np.random.default_rng(2).standard_normal(A.shape[0])
+    assert np.array_equal(solver.spmv(x), O.spmv(A, x))
+
+
 def test_edge_cases(solver):
     A = M.laplacian_5pt(100)
     n = A.shape[0]
