@@ -265,7 +265,6 @@ struct DevTri {
     DBuf<unsigned long long> prog;   // 3D: per (plane, band) batches stored (0 between launches)
     DBuf<int> order;             // 3D tiles: forward dependency order (the backward solve reverses it)
     bool il = false;             // upper 2D: in-line term first (Wave2D::u_inline_first)
-    const double *osc = nullptr; // 2D, per launch: store x / osc (the split's D_r^-1 fold), null = x
     int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
     bool rcp_ok = false;         // every divisor admits WD_RCP
     bool mul_ok = false;         // every 1/d is finite and normal (WD_MUL admissible; rw uploaded)

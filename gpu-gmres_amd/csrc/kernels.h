@@ -85,11 +85,10 @@ void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long l
                           unsigned long long seq, long long capd, int *err, hipStream_t st);
 
 // ---- split (PG) elementwise maps -------------------------------------------
+void launch_f64_to_f32(Gate g, const double *in, float *out, int n, hipStream_t st);   // out = RN_f32(in)
+void launch_f32_to_f64(Gate g, const float *in, double *out, int n, hipStream_t st);   // out = (double)in
 void launch_mul(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in*s
 void launch_div(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in/s
-void launch_gather_divsrc(Gate g, const double *in, const double *s, const int *perm, double *out, int n, hipStream_t st);  // out[i] = in[p]/s[p]
-void launch_gather_divdst(Gate g, const double *in, const double *s, const int *perm, double *out, int n, hipStream_t st);  // out[i] = in[p]/s[i]
-void launch_scatter_mul(Gate g, const double *in, const double *s, const int *perm, double *out, int n, hipStream_t st);    // out[p] = in[i]*s[i]
 
 // ---- SpMV ------------------------------------------------------------------
 // y = A x  (resid=false)  or  y = b - A x  (resid=true)

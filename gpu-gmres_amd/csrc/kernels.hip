@@ -240,32 +240,24 @@ __global__ void k_mul(Gate g, const double *in, const double *s, double *out, in
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = in[i] * s[i];
 }
+// the user-preconditioner boundary (fp32 arrays, src/preconditioner.h:34-84)
+__global__ void k_f64_to_f32(Gate g, const double *in, float *out, int n)
+{
+    if (gated(g)) return;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (float)in[i];
+}
+__global__ void k_f32_to_f64(Gate g, const float *in, double *out, int n)
+{
+    if (gated(g)) return;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (double)in[i];
+}
 __global__ void k_div(Gate g, const double *in, const double *s, double *out, int n)
 {
     if (gated(g)) return;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = in[i] / s[i];
-}
-__global__ void k_gather_divsrc(Gate g, const double *in, const double *s, const int *perm,
-                                double *out, int n)
-{
-    if (gated(g)) return;
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) { int p = perm[i]; out[i] = in[p] / s[p]; }
-}
-__global__ void k_gather_divdst(Gate g, const double *in, const double *s, const int *perm,
-                                double *out, int n)
-{
-    if (gated(g)) return;
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = in[perm[i]] / s[i];
-}
-__global__ void k_scatter_mul(Gate g, const double *in, const double *s, const int *perm,
-                              double *out, int n)
-{
-    if (gated(g)) return;
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[perm[i]] = in[i] * s[i];
 }
 
 // ================================================================= SpMV
@@ -803,17 +795,14 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
 
 // IL: the in-line term (|offset| = 1) comes first in the row's canonical order,
 // then the line term -- the split (ILU++) U factor's ascending-column rows
-// (MyILUPP::HostPrecond_right, src/preconditioner.cu:1117-1137).  osc (2D,
-// nullable): the writer stores x / osc instead of x -- the split engine's
-// D_r^-1 scaling (gather_divdst, src/preconditioner.cu:1629-1657) folded into
-// the solve's store; the hand-off granules carry the unscaled x.
+// (MyILUPP::HostPrecond_right, src/preconditioner.cu:1117-1137).
 template <bool FWD, int DIV, bool TRACE, bool D3 = false, int S = 1, bool IL = false>
 __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
     const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
     double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace,
     int nz, long long P2, const double *__restrict__ c0, unsigned long long *prog,
-    const double *__restrict__ ce1, const double *__restrict__ ce2, const double *__restrict__ osc)
+    const double *__restrict__ ce1, const double *__restrict__ ce2)
 {
     using C = WaveCfg<DIV, D3, S>;
     static_assert(!IL || (S == 1 && !D3), "in-line-first rows: unskewed 2D grids");
@@ -913,12 +902,6 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
         // also waits for this band's boundary values of batch bi+1: a band's
         // upstream must not hold back what it hands downstream.
         double2 *X2 = reinterpret_cast<double2 *>(x) + boff;
-        const double2 *O2 = D3 || !osc ? nullptr : reinterpret_cast<const double2 *>(osc) + boff;
-        double2 osv[C::PBN];                // osc of the batch being stored
-        if (!D3 && O2) {
-#pragma unroll
-            for (int kk = 0; kk < C::PBN; kk++) osv[kk] = O2[(long long)(FWD ? kk : np - 1 - kk) * 64];
-        }
         [[maybe_unused]] bool bad = false;  // WD_RCP range guard (see rcp_safe)
         for (int bi = 0; bi <= nbatch; bi++) {
             if (!GG_WAVE_DECOUPLE || bi == 0) raw_barrier();
@@ -952,20 +935,11 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 if constexpr (D3) {
                     st_sc1_16(dst, v[kk]);
                 } else {
-                    *dst = O2 ? make_double2(v[kk].x / osv[kk].x, v[kk].y / osv[kk].y) : v[kk];
+                    *dst = v[kk];
                 }
                 if constexpr (DIV == WD_RCP) bad |= !rcp_safe(v[kk].x) || !rcp_safe(v[kk].y);
             }
-            // the next batch's divisors, loaded a whole batch before their use
-            // (issued before the barrier wait: an HBM round trip is about half
-            // a batch)
-            if (!D3 && O2 && pb + 1 < nbatch) {
-#pragma unroll
-                for (int kk = 0; kk < C::PBN; kk++) {
-                    const int p = (pb + 1) * C::PBN + kk;
-                    osv[kk] = O2[(long long)(FWD ? p : np - 1 - p) * 64];
-                }
-            }
+
             if (TRACE && lane == 0)
                 trace[(long long)band * (3 * nbatch + 8) + nbatch + 8 + pb] =
                     (long long)__builtin_amdgcn_s_memrealtime();
@@ -2834,6 +2808,14 @@ void launch_scatter_idx(const double *in, const long long *src, const long long 
     k_scatter_idx<<<blocks_for(n, kBlock, 8192), kBlock, 0, st>>>(in, src, dst, out, n);
 }
 
+void launch_f64_to_f32(Gate g, const double *in, float *out, int n, hipStream_t st)
+{
+    k_f64_to_f32<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(g, in, out, n);
+}
+void launch_f32_to_f64(Gate g, const float *in, double *out, int n, hipStream_t st)
+{
+    k_f32_to_f64<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(g, in, out, n);
+}
 void launch_mul(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st)
 {
     k_mul<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(g, in, s, out, n);
@@ -2841,21 +2823,6 @@ void launch_mul(Gate g, const double *in, const double *s, double *out, int n, h
 void launch_div(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st)
 {
     k_div<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(g, in, s, out, n);
-}
-void launch_gather_divsrc(Gate g, const double *in, const double *s, const int *perm, double *out,
-                          int n, hipStream_t st)
-{
-    k_gather_divsrc<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(g, in, s, perm, out, n);
-}
-void launch_gather_divdst(Gate g, const double *in, const double *s, const int *perm, double *out,
-                          int n, hipStream_t st)
-{
-    k_gather_divdst<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(g, in, s, perm, out, n);
-}
-void launch_scatter_mul(Gate g, const double *in, const double *s, const int *perm, double *out,
-                        int n, hipStream_t st)
-{
-    k_scatter_mul<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(g, in, s, perm, out, n);
 }
 
 void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, double *y, bool resid,
@@ -3006,17 +2973,16 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
 #undef GG_TILE_LAUNCH
         } else if (w.nz == 1) {
             dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
-            const double *osc = T.osc;
 #define GG_WAVE_LAUNCH_S(FWD, DIV, S, IL)                                                          \
     k_trsv_wave2d<FWD, DIV, false, false, S, IL><<<grid, WaveCfg<DIV, false, S>::THREADS, 0, st>>>( \
         g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr,   \
-        nullptr, T.ce1.p, T.ce2.p, osc)
+        nullptr, T.ce1.p, T.ce2.p)
 #define GG_WAVE_LAUNCH(FWD, DIV)                                                                   \
     do {                                                                                           \
         if (T.trace && w.skew == 1 && !T.il)                                                       \
             k_trsv_wave2d<FWD, DIV, true><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                 \
                 g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, T.trace, 1, w.P2,     \
-                nullptr, nullptr, nullptr, nullptr, osc);                                          \
+                nullptr, nullptr, nullptr, nullptr);                                               \
         else if (T.il)                                                                             \
             GG_WAVE_LAUNCH_S(FWD, DIV, 1, true);                                                   \
         else if (w.skew == 1)                                                                      \
@@ -3047,7 +3013,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         const int grid = std::min(std::min(ntask, wave3d_max_blocks<FWD, DIV>()), kTileDummyBlocks); \
         k_trsv_wave2d<FWD, DIV, false, true><<<grid, WaveCfg<DIV, true>::THREADS, 0, st>>>(        \
             g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, w.nz, w.P2,      \
-            T.c0.p, T.prog.p, nullptr, nullptr, nullptr);                                          \
+            T.c0.p, T.prog.p, nullptr, nullptr);                                                   \
     } while (0)
             if (T.lower) {
                 if (div == WD_UNIT) GG_WAVE_LAUNCH3(true, WD_UNIT);

@@ -272,6 +272,11 @@ struct gg_solver {
     // y_out[r] = lay(prow^-1[r])
     DBuf<long long> sb_map, sx_map, sx_out, sy_out;
     DevCsr dUfull;        // the split U factor (diagonal first) in layout space (apply_start)
+    // caller-supplied preconditioner (gg_set_precond_user): fp32 staging of its
+    // device arrays, natural order
+    gg_precond_fn ufn = nullptr;
+    void *uctx = nullptr;
+    DBuf<float> fin, fout;
 
     // workspace
     int m_alloc = -1;
@@ -455,9 +460,45 @@ void trsv(gg_solver *s, Gate g, DevTri &T, int kind, int i, const double *in, do
     prof_end(s, mk);
 }
 
+bool user_kind(const gg_solver *s) { return s->pkind == GG_PRECOND_USER || s->pkind == GG_PRECOND_USER_SPLIT; }
+
+// the control block as of the work enqueued so far (host round trip)
+DevState read_state(gg_solver *s)
+{
+    DevState h{};
+    GG_HIP(hipMemcpyAsync(&h, s->ds.p, sizeof(DevState), hipMemcpyDeviceToHost, s->st));
+    GG_HIP(hipStreamSynchronize(s->st));
+    return h;
+}
+
+// One application of the caller's operator `op` (the reference engines' calls of
+// Preconditioner::DevPrecond*, src/gmres.cu:2294-2406, 2592-2690): the gate is
+// evaluated on the host (the device is synchronized around the call anyway), the
+// fp64 input rounded to the fp32 staging array, the callback run, its fp32
+// output promoted.
+void apply_user(gg_solver *s, Gate g, int op, const double *in, double *out)
+{
+    const int n = s->A.n;
+    if (g.done || g.nit) {
+        const DevState h = read_state(s);
+        if ((g.done && (h.done & g.mask)) || (g.nit && g.i >= h.nit)) return;
+    }
+    launch_f64_to_f32(Gate{}, in, s->fin.p, n, s->st);
+    GG_HIP(hipStreamSynchronize(s->st));
+    const int rc = s->ufn(s->uctx, op, s->fin.p, s->fout.p, n);
+    GG_HIP(hipDeviceSynchronize());
+    GG_REQUIRE(rc == 0, GG_EINVAL, "user preconditioner (op " + std::to_string(op) + ") returned " +
+                                       std::to_string(rc));
+    launch_f32_to_f64(Gate{}, s->fout.p, out, n, s->st);
+}
+
 // ---- preconditioner operators (enqueue only; graph-capturable) ----------
 void apply_minv(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 {
+    if (s->pkind == GG_PRECOND_USER) {
+        apply_user(s, g, GG_APPLY_MINV, in, out);
+        return;
+    }
     if (s->pkind == GG_PRECOND_NONE) {
         Gate g2 = g;
         (void)g2;
@@ -476,18 +517,14 @@ void apply_left(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
     trsv(s, g, s->L, GG_PROF_TRSV_L, i, s->t1.p, out);
 }
 // Mr(v) = D_r^-1 P_c U^-1 M v (DevPrecond_right, :1629-1657), out in the
-// column convention; the 2D wavefront U solve stores U^-1(..) / rs_l itself
+// column convention: with the column permutation in A' the gather is gone and
+// D_r^-1 is a contiguous pass (folding it into the 2D wavefront U solve's
+// writer wave cost more than the pass: U 99.7 -> 142 us at C2)
 void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 {
     launch_mul(g, in, s->mid_l.p, s->t1.p, (int)s->P, s->st);
-    if (s->U.kind == DevTri::WAVE2D && s->U.wl.nz == 1) {
-        s->U.osc = s->rs_l.p;
-        trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, out);
-        s->U.osc = nullptr;
-    } else {
-        trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
-        launch_div(g, s->t2.p, s->rs_l.p, out, (int)s->P, s->st);
-    }
+    trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
+    launch_div(g, s->t2.p, s->rs_l.p, out, (int)s->P, s->st);
 }
 // Ml(A' z) with Ml's row gather and D_l^-1 in the SpMV (resid: Ml(b - A x))
 void spmv_left(gg_solver *s, Gate g, const double *z, const double *b, double *out, int i = -1)
@@ -510,6 +547,7 @@ void apply_start(gg_solver *s, Gate g, const double *in, double *out)
 void apply_rhs(gg_solver *s, Gate g, const double *in, double *out)
 {
     if (s->pkind == GG_PRECOND_SPLIT) apply_left(s, g, in, out);
+    else if (s->pkind == GG_PRECOND_USER_SPLIT) apply_user(s, g, GG_APPLY_RHS, in, out);
     else apply_minv(s, g, in, out);
 }
 
@@ -556,12 +594,17 @@ void enqueue_init(gg_solver *s)
     Gate none;
     DevState *ds = s->ds.p;
     const bool split = s->pkind == GG_PRECOND_SPLIT;
+    const bool usplit = s->pkind == GG_PRECOND_USER_SPLIT;
     apply_rhs(s, none, s->bv.p, s->bb.p);                                     // bb = M b
     launch_dot(none, s->bb.p, s->bb.p, s->partA.p, s->G, s->Ppad, s->st);
     launch_set_normb(s->partA.p, s->G, ds, s->st);
     if (split) {
         apply_start(s, none, s->xv.p, s->y.p);                                 // y = Mr^-1 x0
         spmv_left(s, none, s->xv.p, s->bv.p, s->r.p);                          // r = Ml (b - A x)
+    } else if (usplit) {
+        apply_user(s, none, GG_APPLY_START, s->xv.p, s->y.p);                  // y = Mr^-1 x0
+        launch_spmv(none, s->dA, s->xv.p, s->bv.p, s->rr.p, true, s->st);     // rr = b - A x
+        apply_rhs(s, none, s->rr.p, s->r.p);                                  // r = Ml rr
     } else {
         launch_spmv(none, s->dA, s->xv.p, s->bv.p, s->rr.p, true, s->st);     // rr = b - A x
         apply_rhs(s, none, s->rr.p, s->r.p);                                  // r = M rr
@@ -575,6 +618,8 @@ void enqueue_cycle(gg_solver *s, int m)
     DevState *ds = s->ds.p;
     const long long P = s->Ppad;
     const bool split = s->pkind == GG_PRECOND_SPLIT;
+    const bool usplit = s->pkind == GG_PRECOND_USER_SPLIT;
+    const bool user = user_kind(s);
     launch_init_cycle(ds, s->r.p, s->V.p, s->s.p, s->G, P, s->st);
     const bool persist = s->persist && !s->shared;
     const bool wide = s->wide && !s->shared;
@@ -586,8 +631,18 @@ void enqueue_cycle(gg_solver *s, int m)
         gi.nit = &ds->nit;
         gi.i = i;
         double *vi = s->V.p + (long long)i * P;
+        if (user) {
+            // host-driven: stop enqueueing once the cycle is over (the caller's
+            // operator would run on vectors nobody reads)
+            const DevState h = read_state(s);
+            if ((h.done & ~0) || i >= h.nit) break;
+        }
         int mk;
-        if (!split) {
+        if (usplit) {
+            apply_user(s, gi, GG_APPLY_RIGHT, vi, s->z.p);                    // z = Mr v_i
+            launch_spmv(gi, s->dA, s->z.p, nullptr, s->ww.p, false, s->st);   // ww = A z
+            apply_user(s, gi, GG_APPLY_LEFT, s->ww.p, s->w.p);                // w = Ml ww
+        } else if (!split) {
             mk = prof_begin(s, GG_PROF_SPMV, i);
             launch_spmv(gi, s->dA, vi, nullptr, s->ww.p, false, s->st);        // ww = A v_i
             prof_end(s, mk);
@@ -625,9 +680,10 @@ void enqueue_cycle(gg_solver *s, int m)
     Gate gu;
     gu.done = &ds->done;
     gu.mask = DONE_RESTART | DONE_INIT;
-    launch_update(gu, m, ds, s->H.p, s->s.p, s->ysm.p, s->V.p, P, split ? s->y.p : s->xv.p, s->G, P,
+    launch_update(gu, m, ds, s->H.p, s->s.p, s->ysm.p, s->V.p, P, split || usplit ? s->y.p : s->xv.p, s->G, P,
                   s->st);
     if (split) apply_right(s, gu, s->y.p, s->xv.p);                            // x = Mr y
+    if (usplit) apply_user(s, gu, GG_APPLY_RIGHT, s->y.p, s->xv.p);
     Gate gr;
     gr.done = &ds->done;
     gr.mask = ~0;
@@ -717,7 +773,8 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
     const bool split = s->pkind == GG_PRECOND_SPLIT;
     launch_gather(d_b, split ? s->sb_map.p : s->lay2nat.p, s->bv.p, s->Ppad, s->st);
     launch_gather(d_x, split ? s->sx_map.p : s->lay2nat.p, s->xv.p, s->Ppad, s->st);
-    if (split) GG_HIP(hipMemsetAsync(s->y.p, 0, s->Ppad * sizeof(double), s->st));
+    if (split || s->pkind == GG_PRECOND_USER_SPLIT)
+        GG_HIP(hipMemsetAsync(s->y.p, 0, s->Ppad * sizeof(double), s->st));
     for (DevTri *T : {&s->L, &s->U})
         if (T->kind == DevTri::WAVE2D)
             reset_wave(T, s->st);
@@ -1268,6 +1325,25 @@ int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const d
     GG_API_END
 }
 
+int gg_set_precond_user(gg_solver *s, int split, gg_precond_fn fn, void *ctx)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && s->have_A, GG_ESTATE, "set_precond before set_matrix");
+    GG_REQUIRE(fn, GG_EINVAL, "gg_set_precond_user: null callback");
+    GG_REQUIRE(split == 0 || split == 1, GG_EINVAL, "gg_set_precond_user: split must be 0 or 1");
+    set_device(s);
+    setup_space(s, nullptr);
+    s->L.kind = s->U.kind = DevTri::NONE;
+    s->ufn = fn;
+    s->uctx = ctx;
+    s->fin.alloc(std::max(s->A.n, 1));
+    s->fout.alloc(std::max(s->A.n, 1));
+    s->pkind = split ? GG_PRECOND_USER_SPLIT : GG_PRECOND_USER;
+    GG_HIP(hipStreamSynchronize(s->st));
+    return GG_OK;
+    GG_API_END
+}
+
 int gg_precond_kind(gg_solver *s) { return s ? s->pkind : GG_EINVAL; }
 int gg_uses_wavefront(gg_solver *s) { return (s && s->wave) ? 1 : 0; }
 int gg_set_division(gg_solver *s, int mode)
@@ -1594,7 +1670,8 @@ int gg_precond_apply(gg_solver *s, int op, const double *in, double *out)
     GG_REQUIRE(s && in && out, GG_EINVAL, "null argument");
     GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner");
     const bool split = s->pkind == GG_PRECOND_SPLIT;
-    GG_REQUIRE(split ? (op >= GG_APPLY_LEFT && op <= GG_APPLY_START) : op == GG_APPLY_MINV, GG_EINVAL,
+    const bool usplit = s->pkind == GG_PRECOND_USER_SPLIT;
+    GG_REQUIRE(split || usplit ? (op >= GG_APPLY_LEFT && op <= GG_APPLY_RHS) : op == GG_APPLY_MINV, GG_EINVAL,
                "operator not defined for this preconditioner");
     set_device(s);
     ensure_workspace(s, std::max(s->m_alloc, 1));
@@ -1613,9 +1690,11 @@ int gg_precond_apply(gg_solver *s, int op, const double *in, double *out)
         Gate none;
         switch (op) {
         case GG_APPLY_MINV: apply_minv(s, none, s->xv.p, s->ww.p); break;
-        case GG_APPLY_LEFT: apply_left(s, none, s->xv.p, s->ww.p); break;
-        case GG_APPLY_RIGHT: apply_right(s, none, s->xv.p, s->ww.p); break;
-        case GG_APPLY_START: apply_start(s, none, s->xv.p, s->ww.p); break;
+        default:
+            if (usplit) apply_user(s, none, op, s->xv.p, s->ww.p);
+            else if (op == GG_APPLY_LEFT || op == GG_APPLY_RHS) apply_left(s, none, s->xv.p, s->ww.p);
+            else if (op == GG_APPLY_RIGHT) apply_right(s, none, s->xv.p, s->ww.p);
+            else apply_start(s, none, s->xv.p, s->ww.p);
         }
         check_err(s);
     };

@@ -15,8 +15,8 @@ PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.environ.get("GGMRES_LIB") or os.path.join(PKG_ROOT, "lib", "libggmres.so")
 
 GG_OK, GG_NOT_CONVERGED = 0, 1
-PRECOND_NONE, PRECOND_ILU0, PRECOND_ILUK, PRECOND_LU, PRECOND_SPLIT = range(5)
-APPLY_MINV, APPLY_LEFT, APPLY_RIGHT, APPLY_START = range(4)
+PRECOND_NONE, PRECOND_ILU0, PRECOND_ILUK, PRECOND_LU, PRECOND_SPLIT, PRECOND_USER, PRECOND_USER_SPLIT = range(7)
+APPLY_MINV, APPLY_LEFT, APPLY_RIGHT, APPLY_START, APPLY_RHS = range(5)
 SOLVE_SHARED_DEVICE = 0x1     # gg_options.flags: other solvers share the device (ggmres.h)
 SOLVE_CGS2 = 0x2              # gg_options.flags: CGS2 orthogonalization (sharded solve only)
 
@@ -32,8 +32,11 @@ EXPORTS = [
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
     "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced",
     "gg_transient_mna", "gg_set_division", "gg_division_active",
-    "gg_trsv_kernel", "gg_mgs_kernel",
+    "gg_trsv_kernel", "gg_mgs_kernel", "gg_set_precond_user",
 ]
+# gg_precond_fn: int (*)(void *ctx, int op, const float *in, float *out, int n), device arrays
+PRECOND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_int)
 DIV_EXACT, DIV_RCP = 0, 1     # gg_div_mode
 SRC_DC, SRC_PULSE, SRC_PWL = 0, 1, 2          # gg_src_kind
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
@@ -91,6 +94,7 @@ def lib():
         L.gg_ilu0_device_values.argtypes = [_VP, _D, ctypes.POINTER(ctypes.c_double)]
         L.gg_set_precond_lu.argtypes = [_VP, _I, _I, _D, _I, _I, _D]
         L.gg_set_precond_split.argtypes = [_VP, _I, _I, _D, _I, _I, _D, _D, _I, _I, _D, _D]
+        L.gg_set_precond_user.argtypes = [_VP, ctypes.c_int, PRECOND_FN, ctypes.c_void_p]
         L.gg_solve.argtypes = [_VP, _D, _D, ctypes.POINTER(Options), ctypes.POINTER(Result)]
         L.gg_solve_device.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options),
                                       ctypes.POINTER(Result)]
@@ -228,6 +232,14 @@ class Solver:
         i = lambda a: np.ascontiguousarray(a, np.int32)
         _check(lib().gg_set_precond_split(self.h, lrp, lci, lv, urp, uci, uv, f(middle),
                                           i(perm_row), i(perm_col), f(lscale), f(rscale)))
+
+    def set_precond_user(self, fn, split=False):
+        """A caller-supplied preconditioner (the reference's Preconditioner
+        plug-in): fn(op, in_ptr, out_ptr, n) -> int works on DEVICE arrays of n
+        float32 (e.g. wrapped with torch); op is APPLY_MINV (split False) or
+        APPLY_LEFT / RIGHT / START / RHS (split True).  Kept alive on the solver."""
+        self._ufn = PRECOND_FN(lambda ctx, op, i, o, n: int(fn(op, i, o, n)))
+        _check(lib().gg_set_precond_user(self.h, 1 if split else 0, self._ufn, None))
 
     def set_division(self, mode):
         """DIV_EXACT (x = RN(acc/d), the default) or DIV_RCP (x = RN(acc * RN(1/d))

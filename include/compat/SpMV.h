@@ -8,8 +8,34 @@
 #ifndef __SPMV_H__
 #define __SPMV_H__
 
-struct SpM;
+/* src/SpMV.h:22-54: the triplet holder and the device CSR the engine ABI
+ * (GMRES_GPU(SpMatrixGPU*, SpMatrix*, ...), compat/gmres.h) receives */
+struct nzInfo {
+    int rowNum;
+    int colNum;
+    float val;
+};
+typedef struct nzInfo NZEntry;
+
+struct SpM {
+    int numRows;
+    int numCols;
+    int numNZEntries;
+    NZEntry *nzentries;
+    int *rowPtrs;
+    int *colPtrs;
+};
 typedef struct SpM SpMatrix;
+
+struct SpMGPU {
+    float *d_val;
+    int *d_indices;
+    int *d_rowIndices;
+    int *d_ins_indices;
+    int *d_ins_rowIndices;
+    int *d_ins_inputList;
+};
+typedef struct SpMGPU SpMatrixGPU;
 
 class MySpMatrix {
 public:

@@ -61,7 +61,9 @@ enum gg_precond_kind {
     GG_PRECOND_ILU0 = 1,   /* left, factored from A                        */
     GG_PRECOND_ILUK = 2,   /* left, factored from A                        */
     GG_PRECOND_LU = 3,     /* left, caller-supplied L,U                    */
-    GG_PRECOND_SPLIT = 4   /* ILU++/PG split: Ml = L^-1 P_r D_l^-1, Mr = D_r^-1 P_c U^-1 M */
+    GG_PRECOND_SPLIT = 4,  /* ILU++/PG split: Ml = L^-1 P_r D_l^-1, Mr = D_r^-1 P_c U^-1 M */
+    GG_PRECOND_USER = 5,   /* caller-supplied left operator (gg_set_precond_user)          */
+    GG_PRECOND_USER_SPLIT = 6  /* caller-supplied split operators (gg_set_precond_user)     */
 };
 
 /* which operator gg_precond_apply applies */
@@ -69,7 +71,9 @@ enum gg_precond_op {
     GG_APPLY_MINV = 0,     /* left engines: (LU)^-1           (LUSolve_gpu)                    */
     GG_APPLY_LEFT = 1,     /* split: Ml   (DevPrecond_left / _rhs)                             */
     GG_APPLY_RIGHT = 2,    /* split: Mr   (DevPrecond_right)                                   */
-    GG_APPLY_START = 3     /* split: Mr^-1 (DevPrecond_starting_value)                         */
+    GG_APPLY_START = 3,    /* split: Mr^-1 (DevPrecond_starting_value)                         */
+    GG_APPLY_RHS = 4       /* split: the right-hand side's Ml (DevPrecond_rhs; = LEFT for the
+                              built-in split, the user's own method for GG_PRECOND_USER_SPLIT) */
 };
 
 typedef struct gg_solver gg_solver;
@@ -152,6 +156,21 @@ int gg_set_precond_split(gg_solver *s,
                          const int *u_row_ptr, const int *u_col_idx, const double *u_val,
                          const double *middle, const int *perm_row, const int *perm_col,
                          const double *lscale, const double *rscale);
+/* A caller-supplied preconditioner: the reference's Preconditioner plug-in
+ * (src/preconditioner.h:34-84), whose methods the engines call --
+ * GMRES_GPU(..., Preconditioner&) (src/gmres.cu:2567-2732) DevPrecond, GMRESilu_GPU
+ * (src/gmres.cu:2254-2446) DevPrecond_rhs / _left / _right / _starting_value.
+ * The engine calls fn(ctx, op, in, out, n) with DEVICE arrays of n floats (the
+ * reference's fp32 interface: the engine's fp64 vectors are rounded to float
+ * for the call and the result promoted back), op = GG_APPLY_MINV (split = 0, the
+ * left engine) or GG_APPLY_LEFT / RIGHT / START / RHS (split = 1, the split
+ * engine).  fn runs on the calling host thread between the engine's kernels,
+ * with the device synchronized before and after it (it may launch work on any
+ * stream, or run on the host); it returns 0, or nonzero to abort the solve
+ * (GG_EINVAL).  Natural order vector space, no triangular solve of the library's
+ * own: the engine pays a host round trip per application. */
+typedef int (*gg_precond_fn)(void *ctx, int op, const float *in, float *out, int n);
+int gg_set_precond_user(gg_solver *s, int split, gg_precond_fn fn, void *ctx);
 int gg_precond_kind(gg_solver *s);
 /* Division in the non-unit triangular solves (the reference divides,
  * LUSolve_ignoreZero src/SpMV_compute.cpp:118-133, HostPrecond_left/right

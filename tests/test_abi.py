@@ -53,13 +53,23 @@ def test_reference_boundary_classes_exported(ggmres_lib):
                 "gmresInterfacePG::setPrecondPG(MySpMatrix*, MySpMatrixDouble*, MySpMatrixDouble*, "
                 "MySpMatrix*, MySpMatrix*, MySpMatrix*, MySpMatrixDouble*, MySpMatrixDouble*)",
                 "gmresInterfacePG::GMRES_host_PG()", "gmresInterfacePG::~gmresInterfacePG()",
-                "wrapperGMRESforPG(ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, int*, int, gpuETBR*)"]:
+                "wrapperGMRESforPG(ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, int*, int, gpuETBR*)",
+                # the engine ABI with the Preconditioner plug-in (src/gmres.h:356-398)
+                "GMRES_GPU(SpMGPU*, SpM*, dim3*, dim3*, float*, float const*, int, int, int*, float*, "
+                "Preconditioner&)",
+                "GMRES_GPU_tran(SpMGPU*, SpM*, dim3*, dim3*, float*, float const*, int, int, int, float, "
+                "Preconditioner&, GMRES_GPU_Data&)",
+                "GMRESilu(float const*, int const*, int const*, float*, float const*, int, int, int*, float*, "
+                "Preconditioner&)",
+                "GMRESilu_GPU(float*, int*, int*, int, float*, float*, int, int, int*, float*, Preconditioner&)"]:
         assert sig in out, sig
 
 
 @pytest.mark.parametrize("prog, sym", [
     ("pg_driver", "gmresInterfacePGfloat::GMRES_dev_PG()"),
     ("wrapper_driver", "wrapperGMRESforPG(ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, ucr_cs_dl*, int*, int, gpuETBR*)"),
+    ("engine_driver", "GMRESilu_GPU(float*, int*, int*, int, float*, float*, int, int, int*, float*, "
+                      "Preconditioner&)"),
 ])
 def test_reference_callers_link_unchanged(ggmres_lib, prog, sym):
     """The g++-built stand-ins for the reference's callers (tests/boundary/) take
@@ -89,6 +99,14 @@ def test_headers_compile_as_c_and_cpp(tmp_path):
                   'int main(){return 0;}\n')
     subprocess.check_call(["g++", "-std=c++11", "-Wall", "-fsyntax-only",
                            f"-I{REPO}/include/compat", f"-I{REPO}/include", str(cc)])
+    ce = tmp_path / "e.cpp"          # the engine ABI header, as a reference caller includes it
+    ce.write_text('#include "gmres.h"\n#include <cstddef>\n'
+                  'static_assert(sizeof(Preconditioner) == 104, "layout");\n'
+                  'static_assert(sizeof(SpMatrixGPU) == 48 && sizeof(SpMatrix) == 40, "layout");\n'
+                  'static_assert(sizeof(GMRES_GPU_Data) == 96, "layout");\n'
+                  'int main(){return 0;}\n')
+    subprocess.check_call(["g++", "-std=c++11", "-Wall", "-fsyntax-only", "-D__HIP_PLATFORM_AMD__",
+                           "-I/opt/rocm/include", f"-I{REPO}/include/compat", f"-I{REPO}/include", str(ce)])
 
 
 def test_status_strings_and_version(ggmres_lib):

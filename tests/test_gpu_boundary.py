@@ -216,3 +216,51 @@ def test_wrapper_failure_fills_nan(tmp_path):
     xs = np.frombuffer(data, np.float32, numPts * len(ports))
     xd = np.frombuffer(data, np.float64, numPts * len(ports), numPts * len(ports) * 4)
     assert np.all(np.isnan(xs)) and np.all(np.isnan(xd))
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_engine_abi_preconditioner_plugin(tmp_path, mode):
+    """GMRES_GPU / GMRES_GPU_tran / GMRESilu_GPU / GMRESilu (src/gmres.h:356-398)
+    called by a g++ program with its own Preconditioner subclass (Jacobi:
+    left M = D, split Ml = Mr = D^-1/2, start D^1/2; src/preconditioner.h:34-84).
+    The plug-in works on fp32 arrays (the reference's interface) while the
+    engine is fp64, so the check is against the oracle's GMRES with the same
+    operators in fp64 (left: L = I, U = D; split: L = U = I, D_l = D_r = D^1/2)
+    to fp32 tolerance: same convergence, iteration count within 2, x within
+    1e-5, and the plug-in called once per operator application."""
+    A64 = M.laplacian_5pt(16)
+    A64.data = A64.data + np.random.default_rng(21).uniform(-0.3, 0.3, A64.nnz)   # nonsymmetric, D != 4
+    A = sp.csr_matrix((A64.data.astype(np.float32), A64.indices, A64.indptr), shape=A64.shape)
+    Ad = sp.csr_matrix((A.data.astype(np.float64), A.indices, A.indptr), shape=A.shape)
+    n = A.shape[0]
+    b = (Ad @ np.ones(n)).astype(np.float32)
+    x0 = np.zeros(n, np.float32)
+    m, max_iter, tol = 30, 2000, 1e-5
+    hdr = struct.pack("<5if", mode, n, A.nnz, m, max_iter, tol)
+    payload = hdr + _csr_bytes(A.indptr, A.indices, A.data, np.float32) + b.tobytes() + x0.tobytes()
+    data, _ = _run("engine_driver", payload, tmp_path, 12 + 20 + 4 * n)
+    rc, it, tol_out = struct.unpack_from("<iif", data, 0)
+    calls = np.frombuffer(data, np.int32, 5, 12)
+    xg = np.frombuffer(data, np.float32, n, 32).astype(np.float64)
+    d = Ad.diagonal()
+    eye = O.csr(sp.identity(n, format="csr"))
+    if mode <= 1:
+        o = O.gmres_left(Ad, eye, O.csr(sp.diags(d).tocsr()), b.astype(np.float64), m=m, max_iter=max_iter,
+                         tol=tol)
+    else:
+        sq = np.sqrt(d)
+        ident = np.arange(n, dtype=np.int32)
+        Pj = O.Split(eye, eye, np.ones(n), ident, ident, sq, sq)
+        o = O.gmres_split(Ad, Pj, b.astype(np.float64), m=m, max_iter=max_iter, tol=tol)
+    assert rc == o["ret"] == 0
+    assert np.linalg.norm(xg - o["x"]) <= 1e-5 * np.linalg.norm(o["x"])
+    if mode == 1:        # GMRES_GPU_tran: limits by value, nothing written back
+        assert it == max_iter and tol_out == np.float32(tol)
+    else:
+        assert abs(it - o["iters"]) <= 2 and tol_out <= tol
+    iters = o["iters"]
+    if mode <= 1:        # DevPrecond: b, the initial residual, one per inner iteration
+        assert calls[0] >= iters + 2 and calls[1:].sum() == 0
+    else:                # _rhs for b and residuals, _left / _right per iteration, _starting_value once
+        assert calls[0] == 0 and calls[3] == 1 and calls[4] >= 2
+        assert abs(calls[1] - iters) <= 2 and calls[2] >= calls[1]
