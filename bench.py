@@ -304,12 +304,13 @@ def bench_dd(a, torch, dist, world, rank, local):
         d = DD(a.dd_parts, device=local)
         ranks = 1
     d.set_system(A, host.PART_BLOCKS | (host.PART_COLOR_SEP if a.dd_sep == "color" else 0))
+    import ggmres
+    d.set_division(ggmres.DIV_RCP if a.division == "rcp" else ggmres.DIV_EXACT)
     t_setup = time.perf_counter() - t_setup
     info = d.info()
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
 
-    import ggmres
     flags = ggmres.SOLVE_CGS2 if a.dd_orth == "cgs2" else 0
 
     def step():
@@ -337,6 +338,10 @@ def bench_dd(a, torch, dist, world, rank, local):
     el_max = float(t.item())
     inner = sum(r["inner"] for r in res)          # one system: every rank counts the same
     parts = world if world > 1 else a.dd_parts
+    # the exchange every sharded operator and dot pays, timed after the timed
+    # region: one dot's G partials, and CGS2's (i+1) G at i = 15
+    info_g = d.dot_layout(rank if world > 1 else 0)[1]
+    xch = {f"{c}_doubles_us": round(d.time_exchange(c, reps=200), 2) for c in (info_g, 16 * info_g)}
     out = {
         "metric": METRIC, "value": round(inner / el_max, 3), "unit": "iterations/s",
         "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -352,6 +357,8 @@ def bench_dd(a, torch, dist, world, rank, local):
                                 "(GG_DD_IPC)" if a.dd_comm == "ipc" else "RCCL all-gather over xGMI")
                                if world > 1 else f"in-process ({parts} shards on one GPU)",
                    "exchange_ranks": ranks if world > 1 else None,
+                   "exchange_latency": xch,
+                   "division": a.division,
                    "orthogonalization": ("CGS2: 3 all-gathers per inner iteration (GG_SOLVE_CGS2, tolerance "
                                          "parity 1e-10 vs MGS over the first cycle)") if a.dd_orth == "cgs2"
                                         else "MGS (the reference's): i + 2 all-gathers per inner iteration",

@@ -89,6 +89,7 @@ struct gg_dd {
     std::vector<std::unique_ptr<Shard>> sh;
     int m_alloc = -1;
     bool cgs2 = false;                      // GG_SOLVE_CGS2 for the solve in progress
+    int div_mode = GG_DIV_EXACT;            // gg_dd_set_division (the shards' wavefront solves)
     std::vector<double> last_hist;
     DBuf<double> nat_a, nat_b;
     DBuf<long long> dtmp;
@@ -219,6 +220,7 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
     auto gate = [&](Shard &s) { return gate_of(s, gi, mask); };
     for (auto &sp : d->sh) {
         Shard &s = *sp;
+        for (DevTri *T : {&s.LI, &s.LS, &s.UI, &s.US}) T->fast = d->div_mode == GG_DIV_RCP;
         launch_trsv(gate(s), s.LI, in(s), s.t1.p, s.err.p + s.p, d->st);          // y_I
     }
     halo(d, vec(&Shard::t1));                                                      // interface y
@@ -332,18 +334,30 @@ void enqueue_cycle(gg_dd *d, int m)
         if (d->cgs2) {
             // CGS2: h = V^T w, w -= V h, h2 = V^T w, w -= V h2 (+ the norm's
             // partials), H[:, i] = h + h2 -- three all-gathers
+            // (the first update and the second pass's partials in one sweep,
+            // k_cgs_update_dot, while i + 1 <= 32)
             const long long cnt = (long long)(i + 1) * d->G;
+            bool have_partials = false;
             for (int pass = 0; pass < 2; pass++) {
-                for (auto &sp : d->sh) {
-                    Shard &s = *sp;
-                    launch_multidot(gate_i(s, i), s.w.p, s.V.p, Pl, i + 1, s.partC.p + (long long)s.p * cnt, d->G,
-                                    dot_len(d, s), d->st);
+                if (!have_partials) {
+                    for (auto &sp : d->sh) {
+                        Shard &s = *sp;
+                        launch_multidot(gate_i(s, i), s.w.p, s.V.p, Pl, i + 1, s.partC.p + (long long)s.p * cnt,
+                                        d->G, dot_len(d, s), d->st);
+                    }
                 }
                 exchange(d, vec(&Shard::partC), 0, cnt);
+                have_partials = false;
                 for (auto &sp : d->sh) {
                     Shard &s = *sp;
                     launch_cgs_reduce(gate_i(s, i), s.partC.p, d->P, d->G, cnt, i + 1, s.hcgs.p, s.H.p, i, m,
                                       pass == 1, d->st);
+                    if (pass == 0 && launch_cgs_update_dot(gate_i(s, i), s.w.p, s.V.p, Pl, s.hcgs.p, i + 1, d->G,
+                                                           H0, dot_len(d, s),
+                                                           s.partC.p + (long long)s.p * cnt, d->st)) {
+                        have_partials = true;
+                        continue;
+                    }
                     launch_cgs_update(gate_i(s, i), s.w.p, s.V.p, Pl, s.hcgs.p, i + 1, d->G, H0, dot_len(d, s),
                                       pass == 1 ? s.partA.p + (long long)s.p * d->G : nullptr, d->st);
                 }
@@ -632,7 +646,12 @@ void set_system(gg_dd *d, const Csr &A, int method)
     d->S0 = agree_max(d, pi_max);
     d->H0 = d->S0 + ps;
     d->Pl = round_up(d->H0 + (long long)d->P * d->maxI, 512);
-    d->G = reduce_grid(d->H0 / 2);
+    // dot partials per shard: one 16-B unit per thread up to 1024 blocks (the
+    // single solver's reduce_grid takes 4 per thread, and a shard's vectors are
+    // P times shorter: at C2 / 8 shards 69 blocks left the shard's dot and
+    // CGS2 kernels latency-bound); the sharded restatement reads G from
+    // gg_dd_dot_layout
+    d->G = (int)std::min<long long>(1024, std::max<long long>(1, (d->H0 / 2 + kBlock - 1) / kBlock));
     // pass 2: device structures in the shard's slot space
     for (size_t k = 0; k < d->sh.size(); k++) {
         Shard &s = *d->sh[k];
@@ -974,6 +993,46 @@ int gg_dd_spmv(gg_dd *d, const double *x, double *y)
     spmv(d, -1, vec(&Shard::xv), vec(&Shard::ww));
     scatter_out(d, &Shard::ww, d->nat_b.p);
     fetch_nat(d, d->nat_b, y);
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_set_division(gg_dd *d, int mode)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d, GG_EINVAL, "null argument");
+    GG_REQUIRE(mode == GG_DIV_EXACT || mode == GG_DIV_RCP, GG_EINVAL,
+               "gg_dd_set_division: mode must be GG_DIV_EXACT or GG_DIV_RCP");
+    d->div_mode = mode;
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_time_exchange(gg_dd *d, long long cnt, int reps, double *avg_us)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && avg_us && cnt > 0 && reps > 0, GG_EINVAL, "bad argument");
+    GG_REQUIRE(d->have, GG_ESTATE, "dd: no system");
+    set_dev(d);
+    ensure_workspace(d, std::max(d->m_alloc, 1));
+    // the CGS2 partials buffer holds P slots of (m+1) G doubles per shard
+    GG_REQUIRE(cnt <= (long long)(d->m_alloc + 1) * d->G, GG_EINVAL,
+               "gg_dd_time_exchange: cnt above the exchange buffer ((m+1) * G doubles)");
+    hipEvent_t e0, e1;
+    GG_HIP(hipEventCreate(&e0));
+    GG_HIP(hipEventCreate(&e1));
+    exchange(d, vec(&Shard::partC), 0, cnt);                  // warm-up (and a rendezvous)
+    GG_HIP(hipStreamSynchronize(d->st));
+    GG_HIP(hipEventRecord(e0, d->st));
+    for (int r = 0; r < reps; r++) exchange(d, vec(&Shard::partC), 0, cnt);
+    GG_HIP(hipEventRecord(e1, d->st));
+    GG_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    GG_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (d->kind == GG_DD_IPC) ipc_check(d);
+    *avg_us = 1e3 * ms / reps;
     return GG_OK;
     GG_API_END
 }

@@ -124,6 +124,11 @@ void launch_cgs_reduce(Gate g, const double *part, int P, int G, long long cnt, 
                        int i, int m, bool add, hipStream_t st);
 void launch_cgs_update(Gate g, double *w, const double *V, long long ldv, const double *h, int nk, int G,
                        long long Ppad, long long Pdot, double *part_norm, hipStream_t st);
+// the first CGS2 update and the second pass's dot partials in one launch
+// (bit-identical to launch_cgs_update + launch_multidot); false: nk too large,
+// nothing launched
+bool launch_cgs_update_dot(Gate g, double *w, const double *V, long long ldv, const double *h, int nk, int G,
+                           long long Ppad, long long Pdot, double *part, hipStream_t st);
 void launch_arnoldi_finalize_r(Gate g, int i, int m, DevState *ds, const double *part, int nparts_in,
                                int G, const double *w, double *vnext, double *H, double *cs,
                                double *sn, double *s, double *hist, long long Ppad, hipStream_t st);

@@ -2224,6 +2224,34 @@ __global__ __launch_bounds__(kBlock) void k_cgs_reduce(Gate g, const double *par
         *hk = add ? *hk + v : v;
     }
 }
+// a = a - sum_k h[k] v_k(u), k ascending (a = (-h_k) v_k + a, the MGS AXPY's
+// rounding), the loads of eight v_k issued before their multiply-adds (a
+// thread owns one or a few units: one load round trip per eight vectors, not
+// per vector).  CACHE: default policy (the fused kernel reads v_k(u) again)
+// or non-temporal.
+template <bool CACHE>
+__device__ __forceinline__ void cgs_axpy(double2 &a, const double *__restrict__ V, long long ldv,
+                                         const double *h, int nk, long long u)
+{
+    for (int k0 = 0; k0 < nk; k0 += 8) {
+        double2 b[8];
+        double c[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            if (k0 + kk < nk) {
+                b[kk] = CACHE ? ld2(V + (long long)(k0 + kk) * ldv, u) : ld2_nt(V + (long long)(k0 + kk) * ldv, u);
+                c[kk] = -h[k0 + kk];
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            if (k0 + kk < nk) {
+                a.x = c[kk] * b[kk].x + a.x;
+                a.y = c[kk] * b[kk].y + a.y;
+            }
+        }
+    }
+}
 // w = w - sum_k h[k] v_k (per element, k ascending: w = (-h_k) v_k + w as the
 // MGS AXPY); norm: block partials of <w, w> over [0, dunits) into part_norm
 template <bool NORM>
@@ -2237,12 +2265,7 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(Gate g, double *__restric
     const long long stride = (long long)gridDim.x * kBlock;
     for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units; u += stride) {
         double2 a = ld2(w, u);
-        for (int k = 0; k < nk; k++) {
-            const double2 b = ld2_nt(V + (long long)k * ldv, u);
-            const double c = -h[k];
-            a.x = c * b.x + a.x;
-            a.y = c * b.y + a.y;
-        }
+        cgs_axpy<false>(a, V, ldv, h, nk, u);
         st2(w, u, a);
         if (NORM && u < dunits) {
             acc += a.x * a.x;
@@ -2252,6 +2275,43 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(Gate g, double *__restric
     if (NORM) {
         acc = block_sum(acc);
         if (threadIdx.x == 0) part_norm[blockIdx.x] = acc;
+    }
+}
+
+// CGS2's first update fused with the second pass's dot partials: w = w - sum_k
+// h[k] v_k (as k_cgs_update), then the block partials of <w, v_k>, k < nk, over
+// [0, dunits) into part[k*G + block] -- the same unit -> thread assignment and
+// accumulation order as k_multidot (G blocks, grid stride), so bit-identical to
+// the two launches; the second read of each v_k(u) comes from the caches.
+constexpr int kCgsFuseMax = 32;              // dots held per thread (else two launches)
+__global__ __launch_bounds__(kBlock) void k_cgs_update_dot(Gate g, double *__restrict__ w,
+                                                           const double *__restrict__ V, long long ldv,
+                                                           const double *h, int nk, long long units,
+                                                           long long dunits, double *part, int G)
+{
+    if (gated(g)) return;
+    double acc[kCgsFuseMax];
+#pragma unroll
+    for (int k = 0; k < kCgsFuseMax; k++) acc[k] = 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units; u += stride) {
+        double2 a = ld2(w, u);
+        cgs_axpy<true>(a, V, ldv, h, nk, u);
+        st2(w, u, a);
+        if (u < dunits) {
+#pragma unroll
+            for (int k = 0; k < kCgsFuseMax; k++) {
+                if (k < nk) {
+                    const double2 b = ld2_nt(V + (long long)k * ldv, u);
+                    acc[k] += a.x * b.x;
+                    acc[k] += a.y * b.y;
+                }
+            }
+        }
+    }
+    for (int k = 0; k < nk; k++) {
+        const double r = block_sum(acc[k]);
+        if (threadIdx.x == 0) part[(long long)k * G + blockIdx.x] = r;
     }
 }
 
@@ -3079,6 +3139,13 @@ void launch_cgs_update(Gate g, double *w, const double *V, long long ldv, const 
         k_cgs_update<true><<<G, kBlock, 0, st>>>(g, w, V, ldv, h, nk, Ppad / 2, Pdot / 2, part_norm);
     else
         k_cgs_update<false><<<G, kBlock, 0, st>>>(g, w, V, ldv, h, nk, Ppad / 2, Pdot / 2, nullptr);
+}
+bool launch_cgs_update_dot(Gate g, double *w, const double *V, long long ldv, const double *h, int nk, int G,
+                           long long Ppad, long long Pdot, double *part, hipStream_t st)
+{
+    if (nk > kCgsFuseMax) return false;
+    k_cgs_update_dot<<<G, kBlock, 0, st>>>(g, w, V, ldv, h, nk, Ppad / 2, Pdot / 2, part, G);
+    return true;
 }
 void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *part, int G,
                              const double *w, double *vnext, double *H, double *cs, double *sn,

@@ -26,7 +26,8 @@ EXPORTS = ["gg_dd_unique_id", "gg_dd_create", "gg_dd_destroy", "gg_dd_comm_ranks
            "gg_dd_ipc_handle", "gg_dd_ipc_connect",
            "gg_dd_set_system", "gg_dd_info",
            "gg_dd_perm", "gg_dd_dot_layout", "gg_dd_solve", "gg_dd_solve_device",
-           "gg_dd_get_history", "gg_dd_spmv", "gg_dd_precond_apply"]
+           "gg_dd_get_history", "gg_dd_spmv", "gg_dd_precond_apply", "gg_dd_set_division",
+           "gg_dd_time_exchange"]
 
 
 def _lib():
@@ -51,6 +52,8 @@ def _lib():
         L.gg_dd_get_history.argtypes = [_VP, _VP, ctypes.c_int]
         L.gg_dd_spmv.argtypes = [_VP, _D, _D]
         L.gg_dd_precond_apply.argtypes = [_VP, _D, _D]
+        L.gg_dd_set_division.argtypes = [_VP, ctypes.c_int]
+        L.gg_dd_time_exchange.argtypes = [_VP, ctypes.c_longlong, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         _done = True
     return L
 
@@ -159,6 +162,16 @@ class DD:
         y = np.zeros(self.n) if y is None else np.array(y, np.float64, copy=True)
         _check(_lib().gg_dd_spmv(self.h, np.ascontiguousarray(x, np.float64), y))
         return y
+
+    def set_division(self, mode):
+        """ggmres.DIV_EXACT / DIV_RCP for the shards' wavefront triangular solves"""
+        _check(_lib().gg_dd_set_division(self.h, int(mode)))
+
+    def time_exchange(self, cnt, reps=200):
+        """average microseconds of one all-gather of cnt doubles per shard"""
+        us = ctypes.c_double()
+        _check(_lib().gg_dd_time_exchange(self.h, int(cnt), int(reps), ctypes.byref(us)))
+        return us.value
 
     def precond_apply(self, v, out=None):
         out = np.zeros(self.n) if out is None else np.array(out, np.float64, copy=True)

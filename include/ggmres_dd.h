@@ -103,6 +103,12 @@ int gg_dd_get_history(gg_dd *d, double *out, int cap);
 /* single operators (host vectors, natural order) for parity tests */
 int gg_dd_spmv(gg_dd *d, const double *x, double *y);
 int gg_dd_precond_apply(gg_dd *d, const double *in, double *out);
+/* division in the shards' wavefront triangular solves (ggmres.h gg_set_division) */
+int gg_dd_set_division(gg_dd *d, int mode);
+/* average device time (hipEvents on the solver's stream, microseconds) of one
+ * all-gather of cnt doubles per shard over this communicator -- the exchange
+ * every sharded operator and dot pays (cnt <= (m+1) * G of the last solve) */
+int gg_dd_time_exchange(gg_dd *d, long long cnt, int reps, double *avg_us);
 
 #ifdef __cplusplus
 }

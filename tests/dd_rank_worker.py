@@ -80,6 +80,31 @@ def main():
         ranks, myrank = d.comm_ranks()
         assert (ranks, myrank) == (world, rank), (ranks, myrank)
         A, method = system(case)
+    elif mode.startswith("xtime:"):
+        # exchange latency probe (tools/ipc_exchange_probe.py): the C2 system
+        # sharded over the ranks, one short solve, then timed all-gathers
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        d = DD(world, device=0, rank=rank, comm="ipc")
+
+        def allgather(b):
+            lst = [None] * world
+            dist.all_gather_object(lst, b)
+            return lst
+
+        d.connect_ipc(allgather)
+        from ggmres import host, matrices as M
+        side = int(mode[6:])
+        A = M.laplacian_5pt(side)
+        d.set_system(A, host.PART_BLOCKS | host.PART_COLOR_SEP)
+        d.solve(M.rhs_ones(A), restart=30, max_iter=30, tol=1e-300)
+        G = d.dot_layout(rank)[1]
+        res = {c: d.time_exchange(c, reps=500) for c in (1, G, 4 * G, 16 * G, 31 * G)}
+        if rank == 0:
+            print(f"IPC all-gather, {world} processes on one GPU, G = {G}: " +
+                  ", ".join(f"{c} doubles {us:.2f} us" for c, us in res.items()), flush=True)
+        d.close()
+        dist.destroy_process_group()
+        return
     elif mode == "nccl_rccl":
         assert world == 1
         torch.cuda.set_device(0)

@@ -192,6 +192,32 @@ def test_dd_cgs2_bitexact_and_tolerance(name):
     assert true < 1e-9, true
 
 
+@pytest.mark.parametrize("name", ["5pt_200x160_P2", "7pt_24_P4", "5pt_200x160_P4_color"])
+def test_dd_division_rcp_tolerance(name):
+    """gg_dd_set_division(GG_DIV_RCP): the shards' wavefront solves multiply by
+    RN(1/d); the first restart cycle within 1e-10 (north_star) of the serial
+    oracle with the reference's division, the full solve converging in the same
+    number of iterations (MGS and CGS2)."""
+    import ggmres
+    A, d, q, B, L, U = setup(name)
+    b = M.rhs_ones(A)
+    d.set_division(ggmres.DIV_RCP)
+    try:
+        for flags in (0, ggmres.SOLVE_CGS2):
+            g1 = d.solve(b, restart=30, max_iter=30, tol=1e-300, flags=flags)
+            s1 = O.gmres_left(B, L, U, b[q], m=30, max_iter=30, tol=1e-300)
+            scale = np.max(np.abs(s1["hist"]))
+            assert g1["hist"].shape == s1["hist"].shape
+            assert np.max(np.abs(g1["hist"] - s1["hist"])) <= 1e-10 * scale
+            assert np.linalg.norm(g1["x"][q] - s1["x"]) <= 1e-10 * np.linalg.norm(s1["x"])
+            g = d.solve(b, restart=30, max_iter=1500, tol=1e-10, flags=flags)
+            ref = O.gmres_left(B, L, U, b[q], m=30, max_iter=1500, tol=1e-10)
+            assert g["ret"] == ref["ret"] == 0
+            assert abs(g["iters"] - ref["iters"]) <= max(2, ref["iters"] // 50), (g["iters"], ref["iters"])
+    finally:
+        d.set_division(ggmres.DIV_EXACT)
+
+
 def test_single_solver_refuses_cgs2():
     import ggmres
     s = ggmres.Solver(0)
