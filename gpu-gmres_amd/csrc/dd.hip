@@ -227,9 +227,14 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
     for (auto &sp : d->sh) {
         Shard &s = *sp;
         Gate g = gate(s);
-        launch_sub_seq(g, s.LSH, s.t1.p, in(s) + S0, s.t2.p + S0, d->st);         // b_S - L_SI y_I
+        // the separator solves' sentinel fills ride on the subtraction's launch
+        const bool pre = s.LS.kind == DevTri::LEVEL && s.US.kind == DevTri::LEVEL && s.LS.n == s.US.n;
+        launch_sub_seq(g, s.LSH, s.t1.p, in(s) + S0, s.t2.p + S0, d->st,                // b_S - L_SI y_I
+                       pre ? s.t1.p + S0 : nullptr, pre ? out(s) + S0 : nullptr, pre ? s.LS.n : 0);
+        s.LS.prefilled = s.US.prefilled = pre;
         launch_trsv(g, s.LS, s.t2.p + S0, s.t1.p + S0, s.err.p + s.p, d->st);     // y_S
         launch_trsv(g, s.US, s.t1.p + S0, out(s) + S0, s.err.p + s.p, d->st);     // x_S
+        s.LS.prefilled = s.US.prefilled = false;
         launch_sub_seq(g, s.UIS, out(s), s.t1.p, s.t2.p, d->st);                  // y_I - U_IS x_S
         launch_trsv(g, s.UI, s.t2.p, out(s), s.err.p + s.p, d->st);               // x_I
     }

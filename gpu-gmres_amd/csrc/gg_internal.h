@@ -269,6 +269,7 @@ struct DevTri {
     bool rcp_ok = false;         // every divisor admits WD_RCP
     bool mul_ok = false;         // every 1/d is finite and normal (WD_MUL admissible; rw uploaded)
     bool fast = false;           // the owner asked for WD_MUL (gg_set_division)
+    bool prefilled = false;      // LEVEL, per launch: x already holds the sentinel (flow kernel)
     int eff_div() const { return (fast && mul_ok && div != WD_UNIT) ? (int)WD_MUL : div; }
     DBuf<unsigned long long> bnd;  // nbands * T hand-off granules (sentinel = not ready) + 128 dummies
     long long *trace = nullptr;  // diagnostics: per band, nbatch+1 timestamps (gg_trace_precond)

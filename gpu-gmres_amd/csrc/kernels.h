@@ -70,7 +70,7 @@ void launch_dot(Gate g, const double *a, const double *b, double *part, int G, l
 // ---- sharded solve (dd.hip) --------------------------------------------------
 // out[r] = in[r] - sum_k C.v[k] * x[C.ci[k]] (sequential, listed order), r < C.n
 void launch_sub_seq(Gate g, const DevCsr &C, const double *x, const double *in, double *out,
-                    hipStream_t st);
+                    hipStream_t st, double *fill0 = nullptr, double *fill1 = nullptr, int nfill = 0);
 struct ShardPtrs { double *p[kMaxShards]; };
 // every shard's slot (b.p[s] + off + s*cnt, cnt doubles) copied to every other shard
 void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long cnt, hipStream_t st);

@@ -147,14 +147,21 @@ __global__ __launch_bounds__(kBlock) void k_dot(Gate g, const double *a, const d
 // out[r] = in[r] - v_0 x[c_0] - v_1 x[c_1] - ...  in the listed (reference) order:
 // the coupling terms a triangular row subtracts before its own triangle's terms
 // (separator rows' interior terms, interior rows' separator terms)
+// (f0, f1: nf words each set to the sentinel -- the x arrays of the two flow
+// solves that follow, whose own fill launches this saves)
 __global__ void k_sub_seq(Gate g, int n, const int *rp, const int *ci, const double *v,
-                          const double *x, const double *in, double *out)
+                          const double *x, const double *in, double *out, unsigned long long *f0,
+                          unsigned long long *f1, int nf)
 {
     if (gated(g)) return;
     for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
         double acc = in[r];
         for (int k = rp[r]; k < rp[r + 1]; k++) acc -= v[k] * x[ci[k]];
         out[r] = acc;
+    }
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < nf; r += gridDim.x * blockDim.x) {
+        if (f0) f0[r] = kSentinel;
+        if (f1) f1[r] = kSentinel;
     }
 }
 // all shards of one process: slot s of shard s' buffer (at off + s*cnt) -> every other shard
@@ -2299,19 +2306,31 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update_dot(Gate g, double *__res
         cgs_axpy<true>(a, V, ldv, h, nk, u);
         st2(w, u, a);
         if (u < dunits) {
+            // eight loads in flight, then their products (static acc indices)
 #pragma unroll
-            for (int k = 0; k < kCgsFuseMax; k++) {
-                if (k < nk) {
-                    const double2 b = ld2_nt(V + (long long)k * ldv, u);
-                    acc[k] += a.x * b.x;
-                    acc[k] += a.y * b.y;
+            for (int c = 0; c < kCgsFuseMax / 8; c++) {
+                if (c * 8 < nk) {
+                    double2 b[8];
+#pragma unroll
+                    for (int kk = 0; kk < 8; kk++)
+                        if (c * 8 + kk < nk) b[kk] = ld2_nt(V + (long long)(c * 8 + kk) * ldv, u);
+#pragma unroll
+                    for (int kk = 0; kk < 8; kk++) {
+                        if (c * 8 + kk < nk) {
+                            acc[c * 8 + kk] += a.x * b[kk].x;
+                            acc[c * 8 + kk] += a.y * b[kk].y;
+                        }
+                    }
                 }
             }
         }
     }
-    for (int k = 0; k < nk; k++) {
-        const double r = block_sum(acc[k]);
-        if (threadIdx.x == 0) part[(long long)k * G + blockIdx.x] = r;
+#pragma unroll
+    for (int k = 0; k < kCgsFuseMax; k++) {      // static indices: acc stays in registers
+        if (k < nk) {
+            const double r = block_sum(acc[k]);
+            if (threadIdx.x == 0) part[(long long)k * G + blockIdx.x] = r;
+        }
     }
 }
 
@@ -2844,10 +2863,13 @@ void launch_dot(Gate g, const double *a, const double *b, double *part, int G, l
     k_dot<<<G, kBlock, 0, st>>>(g, a, b, part, Ppad / 2);
 }
 void launch_sub_seq(Gate g, const DevCsr &C, const double *x, const double *in, double *out,
-                    hipStream_t st)
+                    hipStream_t st, double *fill0, double *fill1, int nfill)
 {
-    if (C.n == 0) return;
-    k_sub_seq<<<blocks_for(C.n, kBlock, 1 << 30), kBlock, 0, st>>>(g, C.n, C.rp.p, C.ci.p, C.v.p, x, in, out);
+    const int n = std::max(C.n, nfill);
+    if (n == 0) return;
+    k_sub_seq<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(
+        g, C.n, C.rp.p, C.ci.p, C.v.p, x, in, out, reinterpret_cast<unsigned long long *>(fill0),
+        reinterpret_cast<unsigned long long *>(fill1), nfill);
 }
 void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long cnt, hipStream_t st)
 {
@@ -2986,8 +3008,9 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
                                   : (int)std::min<long long>(8, 2 * ((per_level + wave_slots - 1) / wave_slots));
             const long long need = ((long long)T.ntask + kBlock / 64 - 1) / (kBlock / 64);   // a wave per task
             const int blocks = (int)std::min<long long>(std::min<long long>(flow_blocks, (long long)bpc * std::max(cus, 1)), need);
-            k_fill_gated<<<blocks_for(nrows, kBlock, 8192), kBlock, 0, st>>>(
-                g, reinterpret_cast<unsigned long long *>(x), nrows, kSentinel);
+            if (!T.prefilled)
+                k_fill_gated<<<blocks_for(nrows, kBlock, 8192), kBlock, 0, st>>>(
+                    g, reinterpret_cast<unsigned long long *>(x), nrows, kSentinel);
             k_trsv_flow<<<blocks, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p, T.off.ci.p,
                                                    T.off.v.p, T.d.p, b, x, err);
             return;

@@ -13,4 +13,6 @@ timeout -k 10 300 python -u bench.py --workload dd --dd-parts 8 > $O/r03_dd_c4_p
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_dd4 -o run -f csv -- python3 -u bench.py --workload dd --dd-grid c2 --dd-parts 4 --steps 1 --warmup 0 > $O/r03_dd_prof4.json 2> $O/r03_dd_prof4.err &&
 find /tmp/prof_dd4 -name '*kernel_stats.csv' -exec cp {} $O/r03_kernel_stats_dd_c2_local4_cgs2_rcp.csv \; &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_dd8 -o run -f csv -- python3 -u bench.py --workload dd --dd-grid c2 --dd-parts 8 --steps 1 --warmup 0 > $O/r03_dd_prof8.json 2> $O/r03_dd_prof8.err &&
-find /tmp/prof_dd8 -name '*kernel_stats.csv' -exec cp {} $O/r03_kernel_stats_dd_c2_local8_cgs2_rcp.csv \;
+find /tmp/prof_dd8 -name '*kernel_stats.csv' -exec cp {} $O/r03_kernel_stats_dd_c2_local8_cgs2_rcp.csv \; &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_dd2 -o run -f csv -- python3 -u bench.py --workload dd --dd-grid c2 --dd-parts 2 --steps 1 --warmup 0 > $O/r03_dd_prof2.json 2> $O/r03_dd_prof2.err &&
+find /tmp/prof_dd2 -name '*kernel_stats.csv' -exec cp {} $O/r03_kernel_stats_dd_c2_local2_cgs2_rcp.csv \;
