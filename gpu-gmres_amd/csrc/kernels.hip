@@ -2533,7 +2533,14 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
 // units, per thread ascending j, block_sum, G partials summed in sum_partials
 // order), so it is bit-identical to the per-step path.  Needs every block
 // co-resident (host: kWideG blocks, two per CU).
-constexpr int kWideJR = 40, kWideJL = 5, kWideD = 8;
+// kWideJS of a thread's units of v_{k+1} are kept in LDS from step k, where they
+// are streamed for the next dot, to step k+1, where they are v_k (and v_0 from
+// the first dot to step 0): that share of the basis is read from HBM once per
+// step instead of twice (LDS: 2 blocks x (kWideJL + kWideJS) x 256 x 16 B)
+#ifndef GG_WIDE_STASH
+#define GG_WIDE_STASH 14
+#endif
+constexpr int kWideJR = 40, kWideJL = 5, kWideD = 8, kWideJS = GG_WIDE_STASH;
 #ifndef GG_WIDE_NEXT_NT
 #define GG_WIDE_NEXT_NT 0
 #endif
@@ -2548,6 +2555,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
     constexpr int J = kWideJR + kWideJL;
     if (gated(g)) return;
     __shared__ double2 wl[kWideJL * kBlock];
+    __shared__ double2 vst[(kWideJS > 0 ? kWideJS : 1) * kBlock];   // v_{k+1} (then v_k) of units j < kWideJS
     const int G = gridDim.x;
     const int stride = G * kBlock;                      // units (vectors < 2^31 units: host check)
     const int u0 = blockIdx.x * kBlock + threadIdx.x;
@@ -2570,10 +2578,15 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
     // v_{k+1} is read again as v_k in the next step: GG_WIDE_NEXT_NT=0 reads it
     // with the default policy (it may stay in the Infinity Cache for that
     // second read), 1 streams it non-temporally like v_k's last read
-    auto fetch = [&](int j, int ub, const double2 *vkp, const double2 *vnp) {
+    // stash: v_k's units j < kWideJS come from LDS (written one step earlier)
+    auto fetch = [&](int j, int ub, const double2 *vkp, const double2 *vnp, bool stash) {
         if (j < J && j < nval) {
-            const dbl2v a = __builtin_nontemporal_load(reinterpret_cast<const dbl2v *>(vkp) + ub + j * stride);
-            pk[j % kWideD] = make_double2(a.x, a.y);
+            if (stash && j < kWideJS) {
+                pk[j % kWideD] = vst[j * kBlock + threadIdx.x];
+            } else {
+                const dbl2v a = __builtin_nontemporal_load(reinterpret_cast<const dbl2v *>(vkp) + ub + j * stride);
+                pk[j % kWideD] = make_double2(a.x, a.y);
+            }
             if (vnp) {
                 if constexpr (GG_WIDE_NEXT_NT) {
                     const dbl2v c = __builtin_nontemporal_load(reinterpret_cast<const dbl2v *>(vnp) + ub + j * stride);
@@ -2590,7 +2603,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         int ub = u0;
         asm volatile("" : "+v"(ub));
 #pragma unroll
-        for (int j = 0; j < kWideD; j++) fetch(j, ub, vec(V), nullptr);
+        for (int j = 0; j < kWideD; j++) fetch(j, ub, vec(V), nullptr, false);
 #pragma unroll
         for (int j = 0; j < J; j++) {
             if (j < nval) {
@@ -2599,8 +2612,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
                 const double2 v0 = pk[j % kWideD];
                 acc += wv.x * v0.x;
                 acc += wv.y * v0.y;
+                if (j < kWideJS) vst[j * kBlock + threadIdx.x] = v0;     // v_0 again at step 0
             }
-            fetch(j + kWideD, ub, vec(V), nullptr);
+            fetch(j + kWideD, ub, vec(V), nullptr, false);
         }
     }
     publish(0, acc);                                          // <w, v_0>
@@ -2610,7 +2624,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         int ub = u0;
         asm volatile("" : "+v"(ub));
 #pragma unroll
-        for (int j = 0; j < kWideD; j++) fetch(j, ub, vkp, vnp);    // in flight during the sum
+        for (int j = 0; j < kWideD; j++) fetch(j, ub, vkp, vnp, true);    // in flight during the sum
         const double h = gather_sum(gran + (long long)k * G, G, err);
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
@@ -2626,8 +2640,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
                 const double2 o = vnp ? pn[j % kWideD] : wv;    // next dot: v_{k+1}, or the norm
                 acc += wv.x * o.x;
                 acc += wv.y * o.y;
+                if (vnp && j < kWideJS) vst[j * kBlock + threadIdx.x] = o;   // v_k of the next step
             }
-            fetch(j + kWideD, ub, vkp, vnp);
+            fetch(j + kWideD, ub, vkp, vnp, true);
         }
         publish(k + 1, acc);
     }
