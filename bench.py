@@ -62,6 +62,9 @@ sys.path.insert(0, os.path.join(REPO, "gpu-gmres_amd"))
 import numpy as np
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# tests only (tests/test_gpu_bench_ranks.py): every rank on GPU 0 and a gloo
+# process group -- the multi-rank control flow on a one-GPU box
+ONE_GPU = os.environ.get("GG_BENCH_ONE_GPU") == "1"
 METRIC = "fp64 GMRES iterations/sec + SpMV HBM GB/s, 1M-row CSR @1/2/4/8 MI355X"
 
 
@@ -275,24 +278,36 @@ def bench_dd(a, torch, dist, world, rank, local):
     n = A.shape[0]
     b = M.rhs_ones(A)
     t_setup = time.perf_counter()
-    if world > 1 and a.dd_comm == "ipc":
+    comm = a.dd_comm
+    if world > 1 and comm == "ipc":
         # device-initiated exchanges: the ranks' exchange-area handles are
         # all-gathered once over a CPU (gloo) group, then every exchange is a
         # kernel storing into the peers' areas over xGMI
+        import ggmres
         boot = dist.new_group(backend="gloo")
-        d = DD(world, device=local, rank=rank, comm="ipc")
+        d, ok = None, 1
+        try:
+            d = DD(world, device=local, rank=rank, comm="ipc")
 
-        def allgather(hb):
-            lst = [None] * world
-            dist.all_gather_object(lst, hb, group=boot)
-            return lst
+            def allgather(hb):
+                lst = [None] * world
+                dist.all_gather_object(lst, hb, group=boot)
+                return lst
 
-        d.connect_ipc(allgather)
-        ranks, myrank = d.comm_ranks()
-        if ranks != world or myrank != rank:
-            raise SystemExit(f"bench.py: IPC exchange maps {ranks} ranks (rank {myrank}), "
-                             f"expected {world} (rank {rank})")
-    elif world > 1:
+            d.connect_ipc(allgather)
+            ranks, myrank = d.comm_ranks()
+            ok = int(ranks == world and myrank == rank)
+        except ggmres.GGError as e:
+            print(f"bench.py rank {rank}: IPC exchange unavailable ({e})", file=sys.stderr, flush=True)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=boot)
+        if not int(flag.item()):
+            # every rank falls back together: RCCL collectives
+            if d is not None:
+                d.close()
+            comm = "rccl"
+    if world > 1 and comm == "rccl":
         uid = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         d = DD(world, device=local, rank=rank, uid=uid[0])
@@ -300,7 +315,7 @@ def bench_dd(a, torch, dist, world, rank, local):
         if ranks != world or myrank != rank:
             raise SystemExit(f"bench.py: RCCL communicator has {ranks} ranks (rank {myrank}), "
                              f"expected {world} (rank {rank})")
-    else:
+    elif world == 1:
         d = DD(a.dd_parts, device=local)
         ranks = 1
     d.set_system(A, host.PART_BLOCKS | (host.PART_COLOR_SEP if a.dd_sep == "color" else 0))
@@ -332,7 +347,7 @@ def bench_dd(a, torch, dist, world, rank, local):
     res = [step() for _ in range(a.steps)]
     barrier()
     el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    t = torch.tensor([el], dtype=torch.float64, device="cpu" if ONE_GPU else "cuda")
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
@@ -354,7 +369,9 @@ def bench_dd(a, torch, dist, world, rank, local):
                                 f"one solve per step"),
                    "n": n, "nnz": int(A.nnz), "parts": parts,
                    "exchange": ("device-initiated all-gathers into hipIpc-mapped peer areas over xGMI "
-                                "(GG_DD_IPC)" if a.dd_comm == "ipc" else "RCCL all-gather over xGMI")
+                                "(GG_DD_IPC)" if comm == "ipc" else
+                                "RCCL all-gather over xGMI" + (" (IPC unavailable: fallback)"
+                                                               if a.dd_comm == "ipc" else ""))
                                if world > 1 else f"in-process ({parts} shards on one GPU)",
                    "exchange_ranks": ranks if world > 1 else None,
                    "exchange_latency": xch,
@@ -390,7 +407,7 @@ def spawn_ranks(n, argv, visible=None):
     import subprocess
     if visible is None:
         import torch
-        visible = torch.cuda.device_count()
+        visible = n if ONE_GPU else torch.cuda.device_count()
     if visible < n:
         print(f"bench.py: --gpus {n} but only {visible} GPU(s) visible", file=sys.stderr, flush=True)
         return 2
@@ -399,7 +416,7 @@ def spawn_ranks(n, argv, visible=None):
         port = sk.getsockname()[1]
     procs = []
     for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0" if ONE_GPU else str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen(argv, env=env))
     rc = 0
@@ -442,7 +459,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if ONE_GPU:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import ggmres
     from ggmres import matrices as M
