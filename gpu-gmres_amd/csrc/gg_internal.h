@@ -147,7 +147,8 @@ struct Wave2D {
     // plane k = 8K + c, with the Gray code g(c) = c ^ (c >> 1): consecutive
     // planes sit in half-rows that differ in one bit, i.e. one DPP row_ror:8,
     // v_permlane16_swap or v_permlane32_swap apart.  Point (i, j, k) runs at
-    // step t = i + a + 2c of its tile (a plane lags its predecessor by 2 steps,
+    // step t = i + a + c of its tile (a plane lags its predecessor by 1 step, as a
+    // line lags its neighbour line: the DAG's own skew; round 2 used 2 steps,
     // so the cross-lane move is off the recurrence); tiles K-major (band =
     // K*NJ + J), each stored as a 2D band of T steps (nbands = NJ * NK; nz
     // stays the grid's plane count).
@@ -160,7 +161,7 @@ struct Wave2D {
         const long long k = r / nxy, q = r % nxy;
         if (tile) {
             const int j = (int)(q / nx), i = (int)(q % nx), a = j & 7, c = (int)(k & 7);
-            const int l = a + 8 * (c ^ (c >> 1)), t = i + a + 2 * c;
+            const int l = a + 8 * (c ^ (c >> 1)), t = i + a + c;
             const long long band = (k >> 3) * NJ + (j >> 3);
             return ((band * (T / 2) + t / 2) * 64 + l) * 2 + (t & 1);
         }

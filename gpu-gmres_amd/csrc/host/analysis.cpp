@@ -210,12 +210,12 @@ Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U)
     w.nz = (int)(n / nxy);
     const char *pl = std::getenv("GG_WAVE3D_PLANES");     // the (plane, band) pipeline instead
     if (!(pl && pl[0] == '1')) {
-        // 8-line x 8-plane tiles (Wave2D::slot); the lane skew is a + 2c <= 21 steps
+        // 8-line x 8-plane tiles (Wave2D::slot); the lane skew is a + c <= 14 steps
         w.tile = true;
         w.NJ = (w.ny + 7) / 8;
         w.NK = (w.nz + 7) / 8;
         w.nbands = w.NJ * w.NK;
-        w.T = (w.nx + 21 + kTileTAlign - 1) / kTileTAlign * kTileTAlign;
+        w.T = (w.nx + 14 + kTileTAlign - 1) / kTileTAlign * kTileTAlign;
         w.P2 = (long long)w.nbands * w.T * 64;
         w.P = w.P2;
         return w;

@@ -1221,24 +1221,27 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 // ================================================ 3D 7-point grids: tile wavefront
 // Layout (gg_internal.h Wave2D, tile = true): one wave owns a tile of 8 lines
 // x 8 planes, lane l = a + 8 g(c) with the Gray code g(c) = c ^ (c >> 1) for
-// plane c = 0..7, and runs point (i, j, k) at step t = i + a + 2c.  Every term
+// plane c = 0..7, and runs point (i, j, k) at step t = i + a + c.  Every term
 // of a row is then a recent value of a neighbouring lane: the in-line term the
 // lane's own previous step; the line term the previous step one lane down its
 // 8-lane half-row (DPP row_shr:1, backward row_shl:1; the half-row's edge lane
 // takes the neighbouring tile's value -- as the DPP `old` in half-row 0 of a
-// row, by a select in half-row 1); the plane term the value of TWO steps back
-// in the predecessor plane's half-row, which differs in one bit of g: one DPP
+// row, by a select in half-row 1); the plane term the previous step's value in
+// the predecessor plane's half-row, which differs in one bit of g: one DPP
 // row_ror:8 (bit 0), in-place v_permlane16_swap (bit 1) or v_permlane32_swap
-// (bit 2) plus selects, computed a step ahead, off the recurrence, whose chain
-// is the 2D one (DPP, multiply, two subtractions, the division).  The first
-// plane's half-row takes the neighbouring tile's value.  The dependency chain
+// (bit 2) plus selects.  The first plane's half-row takes the neighbouring
+// tile's value.  Round 2 skewed planes by two steps so that the plane move ran
+// a step ahead, off the recurrence; but the step is issue-bound (≈ 30
+// instructions), not chain-bound, and the extra skew cost a K hop 16 steps and
+// one more batch of granularity instead of 8: with skew 1 the plane move sits
+// on the chain and every hop is 8 steps + one batch.  The dependency chain
 // (nx + ny + nz - 2 steps) crosses a workgroup boundary every 8 lines and every
 // 8 planes: 26 + 26 hand-offs at 216^3 (round 1: 216 plane hops through HBM).
 // Hand-off granules (8 B, value = flag, kSentinel = not ready, re-armed by the
 // consumer): per tile and step 16 words, [0, 8) the last plane's half-row for
 // tile (J, K +- 1), [8, 16) the eight planes' edge lanes for tile (J +- 1, K).
-// The consumer's step t needs the plane granules of step t +- 14 and the line
-// granules of step t +- 7 (same point i, skew a + 2c).
+// The consumer's step t needs the plane and the line granules of step t +- 7
+// (same point i, skew a + c).
 // Roles as k_trsv_wave2d: wave 0 computes, 1 polls the granules, 2 stores x
 // and publishes, 3 streams b, c1, c2 (, d (, RN(1/d))), c0 into the LDS ring.
 // Persistent grid, every workgroup co-resident, tiles taken in dependency
@@ -1460,7 +1463,7 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
             if (e >= C::B * NG || bj >= nbatch) return nullptr;
             const int t = FWD ? bj * C::B + tt : (T - 1) - (bj * C::B + tt);
             const bool pl = idx < 8;
-            const int tp = pl ? (FWD ? t + 14 : t - 14) : (FWD ? t + 7 : t - 7);
+            const int tp = FWD ? t + 7 : t - 7;
             if (!(pl ? has_k : has_j) || tp < 0 || tp >= T) return nullptr;
             return (pl ? gk : gj) + (long long)tp * NG + idx;
         };
@@ -1595,7 +1598,7 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     const int cs = FWD ? cp : cp + 1;           // the plane whose predecessor move applies
     const TileMasks tm{(FWD ? cp == 0 : cp == 7) ? ~0u : 0u, (cs & 1) ? ~0u : 0u, (cs & 3) == 2 ? ~0u : 0u,
                        (lane & 15) == (FWD ? 8 : 7) ? ~0u : 0u};
-    double xp = 0.0, xq = 0.0;              // this lane's values of the previous two steps
+    double xp = 0.0;                        // this lane's value of the previous step
     double2 rg[C::PBN][C::A];
     raw_barrier();                          // barrier 0: batch 0 is in LDS
     if (TRACE && lane == 0) {
@@ -1603,9 +1606,9 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
         trace[(long long)band * TS + 2] = blockIdx.x;
     }
     for (int bi = 0; bi < nbatch; bi++) {
-        // the first step's plane neighbour (two steps back) is moved before the
-        // barrier; only the first plane's row waits for the boundary value
-        const double xzp = plane_move(xq, 0.0, tm);
+        // the first step's plane neighbour (the previous step) is moved before
+        // the barrier; only the first plane's row waits for the boundary value
+        const double xzp = plane_move(xp, 0.0, tm);
         if (bi > 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // x staging of batch bi-1 written
             raw_barrier();                  // batch bi's data and boundary values
@@ -1631,8 +1634,8 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
         }
         __builtin_amdgcn_sched_barrier(0);
         double xv[C::B];
-        // the plane neighbour's value for the batch's first step (two steps back)
-        double xzn = bfi64(tm.kb, bk[0].x, xzp);
+        // the plane neighbour's value for the batch's first step
+        const double xz0 = bfi64(tm.kb, bk[0].x, xzp);
 #pragma unroll
         for (int kk = 0; kk < C::PBN; kk++) {
 #pragma unroll
@@ -1644,12 +1647,10 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                 const double e2 = sx ? rg[kk][2].x : rg[kk][2].y;
                 const double e0 = sx ? rg[kk][C::AC0].x : rg[kk][C::AC0].y;
                 const double oj = h ? bj[kk].y : bj[kk].x;      // boundary entries by sweep step
-                const double xz = xzn;
+                // the plane neighbour: the predecessor plane's value of the previous step
+                const double xz = tt == 0 ? xz0 : plane_move(xp, h ? bk[kk].y : bk[kk].x, tm);
                 const double p2 = e2 * xp;
                 const double xs = bfi64(tm.lfix, oj, dpp_shift_old<ctrl>(xp, oj));
-                // the next step's plane neighbour: this lane's row predecessor's
-                // value of the previous step (xp), moved while the chain runs
-                if (tt + 1 < C::B) xzn = plane_move(xp, h ? bk[kk + 1].x : bk[kk].y, tm);
                 if constexpr (kWaveShadow) {
                     __builtin_amdgcn_sched_barrier(0);
                     if (h == 0 && kk + C::LOOK < C::PBN) {
@@ -1678,7 +1679,6 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                     const double q1 = __builtin_fma(-__builtin_fma(q0, d, -acc), y, q0);
                     acc = __builtin_fma(-__builtin_fma(q1, d, -acc), y, q1);
                 }
-                xq = xp;
                 xp = acc;
                 xv[tt] = acc;
             }

@@ -112,15 +112,17 @@ void DevCsr::copy_from(const DevCsr &o, hipStream_t st)
 long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
 
 // Tiles of a 3D layout in a forward dependency order: tile (J, K) waits on
-// (J-1, K) and (J, K-1), whose hand-offs lag it by about 2 and 3 batches
-// (k_trsv_tile3d), so tiles are taken by that expected start, 2J + 3K, then J.
+// (J-1, K) and (J, K-1), whose hand-offs lag it by about the same time since
+// planes are skewed by one step like lines (k_trsv_tile3d, traced: 3.7-4.2 and
+// 4.2-4.8 us), so tiles are taken by that expected start, 7J + 8K, then J
+// (round 2's two-step plane skew: 2J + 3K).
 // Any order that lists a tile after both its sources keeps the persistent grid
 // deadlock-free (every workgroup takes its tiles in list order).
 std::vector<int> tile_order(const Wave2D &w)
 {
     std::vector<int> ord(w.nbands);
     for (int q = 0; q < w.nbands; q++) ord[q] = q;
-    auto key = [&](int q) { return 2LL * (q % w.NJ) + 3LL * (q / w.NJ); };
+    auto key = [&](int q) { return 7LL * (q % w.NJ) + 8LL * (q / w.NJ); };
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
         const long long ka = key(a), kb = key(b);
         return ka != kb ? ka < kb : (a % w.NJ) < (b % w.NJ);

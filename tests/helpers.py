@@ -73,19 +73,19 @@ def device_layout(n, nx=None, ny=None, skew=1):
         slots = np.arange(n, dtype=np.int64)
     elif ny is not None and n // (nx * ny) >= 2:
         # 3D: 8-line x 8-plane tiles (gg_internal.h Wave2D::slot, tile = true):
-        # lane a + 8*g(c), g(c) = c ^ (c >> 1); step t = i + a + 2c;
-        # T = roundup(nx + 21, 16); tiles K-major
+        # lane a + 8*g(c), g(c) = c ^ (c >> 1); step t = i + a + c;
+        # T = roundup(nx + 14, 16); tiles K-major
         nxy = nx * ny
         nz = n // nxy
         NJ, NK = (ny + 7) // 8, (nz + 7) // 8
-        T = (nx + 21 + 15) // 16 * 16
+        T = (nx + 14 + 15) // 16 * 16
         P = NJ * NK * T * 64
         r = np.arange(n, dtype=np.int64)
         k, q = r // nxy, r % nxy
         j, i = q // nx, q % nx
         a, c = j % 8, k % 8
         lane = a + 8 * (c ^ (c >> 1))
-        t = i + a + 2 * c
+        t = i + a + c
         band = (k // 8) * NJ + j // 8
         slots = ((band * (T // 2) + t // 2) * 64 + lane) * 2 + t % 2
     else:

@@ -245,7 +245,7 @@ def test_wave_layout_matches_restatement(ggmres_lib, dims):
     assert info[0] == (3 if nz > 1 else 2) and tuple(info[1:4]) == (nx, ny, nz)
     if nz > 1:
         assert info[6] == (ny + 7) // 8 and info[7] == (nz + 7) // 8 and info[4] == info[6] * info[7]
-        assert info[5] == (nx + 21 + 15) // 16 * 16
+        assert info[5] == (nx + 14 + 15) // 16 * 16
     assert len(np.unique(slot)) == n
     lay2nat, _ = device_layout(n, nx, ny if nz > 1 else None)
     assert np.array_equal(lay2nat[slot], np.arange(n))

@@ -71,7 +71,7 @@ for which in (0, 1):
         for bi in range(1, nbt - 3):
             need = []
             if 0 <= sk < NK:
-                kb = (KB * bi + KB - 1 + 14) // KB
+                kb = (KB * bi + KB - 1 + 7) // KB     # plane granules: step t + 7 (skew a + c)
                 if kb < nbt:
                     need.append(pub[sk * NJ + J, kb])
             if 0 <= sj < NJ:
