@@ -646,7 +646,7 @@ def main():
                      if os.environ.get("GG_TRSV_LEVELS") == "1" else "k_trsv_flow")
         else:
             kname = KERNEL_NAMES[dom]
-        pmc_wl = "c4" if c4 else "c3s" if c3s else None
+        pmc_wl = "c4" if c4 else "c3s" if c3s else "pg" if pg else None
         roof = {"kernel": kname, "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),

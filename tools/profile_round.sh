@@ -1,6 +1,6 @@
 #!/bin/bash
 # Refresh the committed profile set on a GPU box (run through gpurun from the repo root):
-#   tools/profile_round.sh TAG [WORKLOAD]        (WORKLOAD: c2 (default) or c4)
+#   tools/profile_round.sh TAG [WORKLOAD]        (WORKLOAD: c2 (default), c4, pg, c5, c3s)
 # writes gpurun_out/prof_TAG[_WORKLOAD]/{bench.json, kernel_stats.csv, pmc_traffic.json}
 # Each GPU step has its own time limit; the steps are chained with && so the
 # script ends at the first failure.
@@ -21,5 +21,6 @@ timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o r
     python3 -u bench.py $ARGS --steps 1 --warmup 0 --cpu-iters 0 --max-iter 600 --no-profile > /dev/null 2> $OUT/write.err
 python3 profiles/pmc_traffic.py $OUT/fetch $OUT/write $OUT/pmc_traffic.json
 find $OUT -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/kernel_stats.csv
-rm -rf $OUT/fetch $OUT/write
+# the per-dispatch traces are tens of MB at C2 (gpurun_out comes back only under 64 MiB)
+rm -rf $OUT/fetch $OUT/write $OUT/stats
 echo "profile $TAG $WL done"
