@@ -8,6 +8,7 @@
 //                                       splitLU_csr :481-541)
 //   iluk_itsol  lofC + ilukC            src/iluk.cpp:56-334
 #include <algorithm>
+#include <memory>
 #include <atomic>
 #include <cmath>
 #include <numeric>
@@ -188,6 +189,73 @@ void iluk_symbolic(const Csr &A, int lof, std::vector<std::vector<int>> &Lja,
     }
 }
 
+// Row i of the ILU(k) pattern for k >= 2 without any other row's result, by
+// incomplete fill paths (Hysom & Pothen, "Level-based incomplete LU
+// factorization: graph model and algorithms", the incomplete fill-path
+// theorem): entry (i, j) has level L - 1 exactly when the shortest path
+// i -> ... -> j in G(A) whose interior vertices are all below min(i, j) has L
+// edges -- lofC's sum rule lev(i,j) = min_k lev(i,k) + lev(k,j) + 1 unrolled.
+// Per row a layered min-max search: M_L(x) = the smallest largest interior
+// vertex over walks of exactly L edges from i to x with every interior vertex
+// below i (M_1 = -1 on row i of A), M_{L+1}(y) = min over edges x -> y, x < i,
+// of max(M_L(x), x); j > i joins at the first L where M_L(j) exists, j < i at
+// the first L with M_L(j) < j (a walk shortens to a path with no larger
+// interior, so walks never report a level below the true one).  Rows are
+// independent: built over host threads like k = 1.
+struct FillPathScratch {
+    std::vector<int> mcur, mnext, lev;          // per vertex; kUnset outside the row's search
+    std::vector<int> fcur, fnext, touched;
+    static constexpr int kUnset = 0x7fffffff;
+    explicit FillPathScratch(int n) : mcur(n, kUnset), mnext(n, kUnset), lev(n, kUnset) {}
+};
+static void fillpath_row(const Csr &A, int lof, int i, FillPathScratch &w, std::vector<int> &row)
+{
+    constexpr int U = FillPathScratch::kUnset;
+    w.fcur.clear();
+    w.touched.clear();
+    for (int e = A.rp[i]; e < A.rp[i + 1]; e++) {
+        const int x = A.ci[e];
+        if (x == i || w.mcur[x] != U) continue;
+        w.mcur[x] = -1;                             // an original entry: level 0
+        w.fcur.push_back(x);
+        if (w.lev[x] == U) {
+            w.lev[x] = 0;
+            w.touched.push_back(x);
+        }
+    }
+    for (int L = 1; L <= lof && !w.fcur.empty(); L++) {
+        w.fnext.clear();
+        for (int x : w.fcur) {
+            if (x >= i) continue;                   // only vertices below i are interior
+            const int m = std::max(w.mcur[x], x);
+            for (int e = A.rp[x]; e < A.rp[x + 1]; e++) {
+                const int y = A.ci[e];
+                if (y == i || m >= w.mnext[y]) continue;
+                if (w.mnext[y] == U) w.fnext.push_back(y);
+                w.mnext[y] = m;
+            }
+        }
+        for (int x : w.fcur) w.mcur[x] = U;
+        for (int y : w.fnext) {
+            if (w.lev[y] == U && (y > i || w.mnext[y] < y)) {
+                w.lev[y] = L;
+                w.touched.push_back(y);
+            }
+            w.mcur[y] = w.mnext[y];
+            w.mnext[y] = U;
+        }
+        w.fcur.swap(w.fnext);
+    }
+    for (int x : w.fcur) w.mcur[x] = U;
+    row.clear();
+    row.push_back(i);
+    for (int x : w.touched) {
+        row.push_back(x);                           // every recorded level is <= lof
+        w.lev[x] = U;
+    }
+    std::sort(row.begin(), row.end());
+}
+
 // The ILU(k) pattern as flat rows (each row ascending: L part, the diagonal,
 // U part) -- the order-free content of lofC's output (src/iluk.cpp:193-334:
 // its L part is built in leftmost-pivot = ascending order, its U part is
@@ -198,15 +266,16 @@ void iluk_symbolic(const Csr &A, int lof, std::vector<std::vector<int>> &Lja,
 //     path has level >= 2), so row i's pattern is A(i) united with U_A(k) over
 //     k in L_A(i): independent of every other row's fill, built row-parallel
 //     over `threads` host threads (dynamic blocks of 1024 rows);
-//   k >= 2: lofC itself (serial: a row's fill depends on earlier rows' fill
-//     levels), flattened.
+//   k >= 2: the incomplete fill paths of each row (fillpath_row), row-parallel
+//     the same way (GG_ILUK_SERIAL=1: lofC itself, serial, flattened).
 void iluk_pattern(const Csr &A, int lof, int threads, std::vector<long long> &prow, std::vector<int> &nl,
                   std::vector<int> &pcol)
 {
     const int n = A.n;
     prow.assign((size_t)n + 1, 0);
     nl.assign(n, 0);
-    if (lof != 1) {
+    const char *ser = std::getenv("GG_ILUK_SERIAL");
+    if (lof == 0 || (lof >= 2 && ser && ser[0] == '1')) {
         std::vector<std::vector<int>> Lja, Uja;
         iluk_symbolic(A, lof, Lja, Uja);
         for (int i = 0; i < n; i++) {
@@ -230,11 +299,18 @@ void iluk_pattern(const Csr &A, int lof, int threads, std::vector<long long> &pr
     std::atomic<int> next{0};
     auto work = [&]() {
         std::vector<int> mark(n, -1), row;
+        std::unique_ptr<FillPathScratch> fp(lof >= 2 ? new FillPathScratch(n) : nullptr);
         for (int b; (b = next.fetch_add(1)) < nblk;) {
             const int r0 = b * kRows, r1 = std::min(n, r0 + kRows);
             std::vector<int> &cols = bcols[b], &len = blen[b];
             len.resize(r1 - r0);
             for (int i = r0; i < r1; i++) {
+                if (fp) {
+                    fillpath_row(A, lof, i, *fp, row);
+                    len[i - r0] = (int)row.size();
+                    cols.insert(cols.end(), row.begin(), row.end());
+                    continue;
+                }
                 row.clear();
                 mark[i] = i;
                 row.push_back(i);

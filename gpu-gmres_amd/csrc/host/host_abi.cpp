@@ -68,6 +68,28 @@ int gg_host_iluk(int level, int n, const int *rp, const int *ci, const double *v
     }
 }
 
+int gg_host_iluk_pattern(int level, int n, const int *rp, const int *ci, int threads, int *prow, int **pcol)
+{
+    if (n < 0 || level < 0 || !rp || !prow || !pcol) return GG_EINVAL;
+    try {
+        std::vector<double> v((size_t)rp[n], 0.0);
+        const Csr A = wrap(n, rp, ci, v.data());
+        std::vector<long long> pr;
+        std::vector<int> nl, pc;
+        iluk_pattern(A, level, std::max(1, threads), pr, nl, pc);
+        GG_REQUIRE(pr[n] < (1LL << 31), GG_EINVAL, "pattern above 2^31 entries");
+        for (int r = 0; r <= n; r++) prow[r] = (int)pr[r];
+        *pcol = static_cast<int *>(std::malloc(sizeof(int) * std::max<size_t>(pc.size(), 1)));
+        if (!*pcol) return GG_ENOMEM;
+        std::copy(pc.begin(), pc.end(), *pcol);
+        return GG_OK;
+    } catch (const Error &e) {
+        return e.code;
+    } catch (...) {
+        return GG_EINVAL;
+    }
+}
+
 int gg_host_wave2d(int n, const int *l_rp, const int *l_ci, const double *l_v, const int *u_rp,
                    const int *u_ci, const double *u_v, int *nx, int *ny)
 {

@@ -32,6 +32,13 @@ int gg_host_ilu0(int n, const int *row_ptr, const int *col_idx, const double *va
 int gg_host_iluk(int level, int n, const int *row_ptr, const int *col_idx, const double *val,
                  int *l_row_ptr, int **l_col_idx, double **l_val,
                  int *u_row_ptr, int **u_col_idx, double **u_val);
+/* The ILU(level) pattern as flat rows (each row ascending, diagonal included):
+ * lofC's level-of-fill pattern (src/iluk.cpp:193-334), built row-parallel over
+ * `threads` host threads -- level 1 by the original L x U entries, level >= 2
+ * by incomplete fill paths; prow[n+1] caller-allocated, *pcol
+ * malloc'd (gg_host_free).  The symbolic phase of gg_set_precond_iluk_device. */
+int gg_host_iluk_pattern(int level, int n, const int *row_ptr, const int *col_idx, int threads,
+                         int *prow, int **pcol);
 /* For ILU factors (L unit-lower diag last, U diag first): 1 and the grid
  * line length / count if the wavefront path applies, else 0. */
 int gg_host_wave2d(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,

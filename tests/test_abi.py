@@ -186,6 +186,57 @@ def test_host_iluk_bitexact_vs_oracle(ggmres_lib, name, k):
         assert np.array_equal(a.v, b.v)
 
 
+def host_iluk_pattern(lib, A, level, threads):
+    A = O.csr(A)
+    prow = np.zeros(A.n + 1, np.int32)
+    pcol = PI()
+    rc = lib.gg_host_iluk_pattern(ctypes.c_int(level), ctypes.c_int(A.n), A.rp.ctypes.data_as(PI),
+                                  A.ci.ctypes.data_as(PI), ctypes.c_int(threads),
+                                  prow.ctypes.data_as(PI), ctypes.byref(pcol))
+    assert rc == 0
+    nnz = int(prow[-1])
+    cols = np.ctypeslib.as_array(pcol, (max(nnz, 1),))[:nnz].copy()
+    lib.gg_host_free(ctypes.cast(pcol, ctypes.c_void_p))
+    return prow, cols
+
+
+def random_nonsym(n, per_row, seed):
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    rows = np.repeat(np.arange(n), per_row)
+    cols = rng.integers(0, n, n * per_row)
+    A = sp.csr_matrix((rng.standard_normal(n * per_row), (rows, cols)), shape=(n, n))
+    A = A + sp.diags(np.abs(A).sum(axis=1).A1 + 1.0)
+    A.sum_duplicates()
+    A.sort_indices()
+    return A.tocsr()
+
+
+@pytest.mark.parametrize("case", CASES + ["rand300", "rand1000"])
+def test_host_iluk_pattern_row_parallel(ggmres_lib, case):
+    """The row-parallel symbolic phase (level 1 by L x U, level >= 2 by
+    incomplete fill paths) equals lofC's pattern (src/iluk.cpp:193-334) row by
+    row, for any thread count."""
+    A = (random_nonsym(300, 4, 11) if case == "rand300" else
+         random_nonsym(1000, 3, 12) if case == "rand1000" else load(case))
+    for k in (0, 1, 2, 3, 4):
+        try:
+            Lo, Uo = O.iluk(A, k)
+        except ZeroDivisionError:
+            continue
+        ref_rp = np.zeros(Lo.n + 1, np.int64)
+        ref_ci = []
+        for r in range(Lo.n):
+            row = np.union1d(Lo.ci[Lo.rp[r]:Lo.rp[r + 1]], Uo.ci[Uo.rp[r]:Uo.rp[r + 1]])
+            ref_ci.append(row)
+            ref_rp[r + 1] = ref_rp[r] + row.size
+        ref_ci = np.concatenate(ref_ci)
+        for threads in (1, 4):
+            prow, cols = host_iluk_pattern(ggmres_lib, A, k, threads)
+            assert np.array_equal(prow, ref_rp), (case, k, threads)
+            assert np.array_equal(cols, ref_ci), (case, k, threads)
+
+
 def test_host_iluk_zero_pivot(ggmres_lib):
     import scipy.sparse as sp
     A = sp.csr_matrix(np.array([[0.0, 1.0], [1.0, 1.0]]))
