@@ -59,6 +59,12 @@ struct Shard {
     DBuf<int> err;                          // P words (slot p is this shard's)
     double bytes_spmv = 0, bytes_trsv = 0;
     std::vector<long long> slot2perm;       // host: slot -> permuted global row (-1 pad), H0
+    // the separator step as one k_sep_flow launch (LEVEL separator triangles):
+    // tasks {first, count, phase} over rows = [L rows | U rows | interface rows]
+    bool sepflow = false;
+    int sf_ntask = 0;
+    DBuf<int4> sf_tasks;
+    DBuf<int> sf_rows;
 };
 
 using Get = std::function<double *(Shard &)>;
@@ -203,7 +209,6 @@ void halo(gg_dd *d, const Get &x, hipStream_t st)
     }
     exchange(d, x, d->H0, d->maxI, st);
 }
-void halo(gg_dd *d, const Get &x) { halo(d, x, d->st); }
 
 Get vec(DBuf<double> Shard::*m) { return [m](Shard &s) { return (s.*m).p; }; }
 
@@ -223,10 +228,35 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
         for (DevTri *T : {&s.LI, &s.LS, &s.UI, &s.US}) T->fast = d->div_mode == GG_DIV_RCP;
         launch_trsv(gate(s), s.LI, in(s), s.t1.p, s.err.p + s.p, d->st);          // y_I
     }
-    halo(d, vec(&Shard::t1));                                                      // interface y
+    // interface y (halo); the fused separator step's sentinel fills ride on the gathers
+    const bool xch = d->maxI > 0 && d->P > 1;
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        double *f0 = s.sepflow ? s.t1.p + S0 : nullptr, *f1 = s.sepflow ? out(s) + S0 : nullptr;
+        if (xch)
+            launch_gather(s.t1.p, s.iface_slot.p, s.t1.p + d->H0 + (long long)s.p * d->maxI, d->maxI, d->st, f0, f1,
+                          s.sepflow ? s.nS : 0);
+        else if (s.sepflow)
+            launch_gather(s.t1.p, s.iface_slot.p, s.t1.p, 0, d->st, f0, f1, s.nS);
+    }
+    if (xch) exchange(d, vec(&Shard::t1), d->H0, d->maxI, d->st);
     for (auto &sp : d->sh) {
         Shard &s = *sp;
         Gate g = gate(s);
+        if (s.sepflow) {
+            // b_S - L_SI y_I and the separator L solve, the separator U solve,
+            // y_I - U_IS x_S (in place in t1): one launch, the same bits
+            SepFlow f;
+            f.ph[0] = SepPhase{s.LS.off.rp.p, s.LS.off.ci.p, s.LS.off.v.p, s.t1.p + S0, s.LSH.rp.p, s.LSH.ci.p,
+                               s.LSH.v.p, s.t1.p, in(s) + S0, s.LS.d.p, s.t1.p + S0, false};
+            f.ph[1] = SepPhase{s.US.off.rp.p, s.US.off.ci.p, s.US.off.v.p, out(s) + S0, nullptr, nullptr,
+                               nullptr, nullptr, s.t1.p + S0, s.US.d.p, out(s) + S0, true};
+            f.ph[2] = SepPhase{s.UIS.rp.p, s.UIS.ci.p, s.UIS.v.p, out(s), nullptr, nullptr,
+                               nullptr, nullptr, s.t1.p, nullptr, s.t1.p, false};
+            launch_sep_flow(g, s.sf_ntask, s.sf_tasks.p, s.sf_rows.p, f, s.err.p + s.p, d->st);
+            launch_trsv(g, s.UI, s.t1.p, out(s), s.err.p + s.p, d->st);               // x_I
+            continue;
+        }
         // the separator solves' sentinel fills ride on the subtraction's launch
         const bool pre = s.LS.kind == DevTri::LEVEL && s.US.kind == DevTri::LEVEL && s.LS.n == s.US.n;
         launch_sub_seq(g, s.LSH, s.t1.p, in(s) + S0, s.t2.p + S0, d->st,                // b_S - L_SI y_I
@@ -613,6 +643,42 @@ Csr slot_csr(const Csr &C, const std::vector<long long> &slot, long long nslots,
     return O;
 }
 
+// the fused separator step (k_sep_flow) when both separator triangles are
+// level-scheduled with short rows: rows of the three phases in their launch
+// order (L and U in level order, then the interior rows with U_IS terms),
+// cut into runs of up to 64 (GG_DD_SEPFLOW=0 keeps the four launches)
+void build_sepflow(Shard &s, const DDShardHost &H, const Csr &uis, hipStream_t st)
+{
+    s.sepflow = false;
+    const char *e = std::getenv("GG_DD_SEPFLOW");
+    if ((e && e[0] == '0') || s.nS == 0 || s.LS.kind != DevTri::LEVEL || s.US.kind != DevTri::LEVEL ||
+        s.LS.n != s.US.n)
+        return;
+    for (const CanonTri *C : {&H.LS, &H.US})
+        for (int r = 0; r < C->off.n; r++)
+            if (C->off.rp[r + 1] - C->off.rp[r] > kFlowLong) return;
+    std::vector<int> rows;
+    std::vector<int4> tasks;
+    auto add_phase = [&](const std::vector<int> &pr, int phase) {
+        for (size_t q = 0; q < pr.size(); q += 64) {
+            const int cnt = (int)std::min<size_t>(64, pr.size() - q);
+            tasks.push_back(make_int4((int)(rows.size() + q), cnt, phase, 0));
+        }
+        rows.insert(rows.end(), pr.begin(), pr.end());
+    };
+    add_phase(level_sets(H.LS).rows, 0);
+    add_phase(level_sets(H.US).rows, 1);
+    std::vector<int> ifr;
+    for (int r = 0; r < uis.n; r++)
+        if (uis.rp[r + 1] > uis.rp[r]) ifr.push_back(r);
+    add_phase(ifr, 2);
+    s.sf_ntask = (int)tasks.size();
+    s.sf_tasks.upload(tasks, st);
+    s.sf_rows.upload(rows, st);
+    GG_HIP(hipStreamSynchronize(st));           // the host vectors end here
+    s.sepflow = true;
+}
+
 void set_system(gg_dd *d, const Csr &A, int method)
 {
     DDPlan plan = dd_plan(A, d->P, method);
@@ -699,6 +765,7 @@ void set_system(gg_dd *d, const Csr &A, int method)
         s.LSH.upload(lsh, d->st);
         Csr uis = slot_csr(H.UIS, s.slotI, s.PIr, [&](int c) { return S0 + s.slotS[c]; });
         s.UIS.upload(uis, d->st);
+        build_sepflow(s, H, uis, d->st);
         // interface slots, natural rows of the slots, rows written back
         std::vector<long long> ifs(std::max(d->maxI, 1), -1);
         for (size_t t = 0; t < H.iface.size(); t++) ifs[t] = s.slotI[H.iface[t]];

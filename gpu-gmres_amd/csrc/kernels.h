@@ -63,7 +63,9 @@ void launch_iluk_scatter(int n, const int *arp, const int *aci, const double *av
 void launch_iluk_wave(int n, const long long *prow, const int *nl, const int *pcol, double *val, double *dinv,
                       int *done, const int *rows_short, int nshort, const int *rows_long, int nlong,
                       int long_blocks, int *scratch, int *err, int blocks, hipStream_t st);
-void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st);  // out[i] = idx[i]<0 ? 0 : in[idx[i]]
+// out[i] = idx[i]<0 ? 0 : in[idx[i]]  (+ fill0/fill1[0, nfill) = the sentinel)
+void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st,
+                   double *fill0 = nullptr, double *fill1 = nullptr, long long nfill = 0);
 void launch_copy(const double *in, double *out, long long n, hipStream_t st);
 void launch_dot(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, hipStream_t st);
 
@@ -71,6 +73,20 @@ void launch_dot(Gate g, const double *a, const double *b, double *part, int G, l
 // out[r] = in[r] - sum_k C.v[k] * x[C.ci[k]] (sequential, listed order), r < C.n
 void launch_sub_seq(Gate g, const DevCsr &C, const double *x, const double *in, double *out,
                     hipStream_t st, double *fill0 = nullptr, double *fill1 = nullptr, int nfill = 0);
+// the sharded solve's fused separator step (kernels.hip k_sep_flow): per phase,
+// row r: acc = b[r] (polled when bpoll) - prefix terms (plain loads of px) -
+// own terms (polled sources src[ci]); x[r] = d ? acc / d[r] : acc
+struct SepPhase {
+    const int *rp = nullptr, *ci = nullptr;
+    const double *v = nullptr, *src = nullptr;
+    const int *prp = nullptr, *pci = nullptr;
+    const double *pv = nullptr, *px = nullptr;
+    const double *b = nullptr, *d = nullptr;
+    double *x = nullptr;
+    bool bpoll = false;
+};
+struct SepFlow { SepPhase ph[3]; };
+void launch_sep_flow(Gate g, int ntask, const int4 *tasks, const int *rows, const SepFlow &f, int *err, hipStream_t st);
 struct ShardPtrs { double *p[kMaxShards]; };
 // every shard's slot (b.p[s] + off + s*cnt, cnt doubles) copied to every other shard
 void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long cnt, hipStream_t st);
@@ -138,17 +154,18 @@ void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *p
 // persistent Arnoldi orthogonalization (one launch per inner iteration):
 // units per thread (1/2/4/8, 0 = too many), how many blocks can be resident
 int arnoldi_persist_units(int G, long long Ppad);
-int arnoldi_persist_max_blocks();
+int arnoldi_persist_max_blocks(int J);
 void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
                             long long ldv, double *H, double *cs, double *sn, double *s,
-                            double *hist, unsigned long long *gran, int G, long long Ppad, int *err,
-                            hipStream_t st);
+                            double *hist, unsigned long long *gran, unsigned long long *hg, int G,
+                            long long Ppad, int *err, hipStream_t st);
 // the same for long vectors (w on chip, the basis streamed): kWideG blocks
 constexpr int kWideG = 512;
 bool arnoldi_wide_ok(int G, long long Ppad);
 void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, double *V, long long ldv,
                          double *H, double *cs, double *sn, double *s, double *hist,
-                         unsigned long long *gran, int G, long long Ppad, int *err, hipStream_t st);
+                         unsigned long long *gran, unsigned long long *hg, int G, long long Ppad, int *err,
+                         hipStream_t st);
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
                    const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st);
 void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st);

@@ -100,12 +100,19 @@ __global__ void k_fill_u64(unsigned long long *p, long long n, unsigned long lon
         p[i] = v;
 }
 
-__global__ void k_gather(const double *in, const long long *idx, double *out, long long n)
+__global__ void k_gather(const double *in, const long long *idx, double *out, long long n,
+                         unsigned long long *f0, unsigned long long *f1, long long nf)
 {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x) {
         long long s = idx[i];
         out[i] = s < 0 ? 0.0 : in[s];
+    }
+    // (sentinel fills riding on the launch: the x arrays of a flow solve that follows)
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nf;
+         i += (long long)gridDim.x * blockDim.x) {
+        f0[i] = kSentinel;
+        f1[i] = kSentinel;
     }
 }
 
@@ -567,6 +574,78 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                 }
                 if (k == k1) {
                     st_agent(xu + r, (unsigned long long)__double_as_longlong(acc / dr));
+                    pending = false;
+                }
+            }
+            if (__any(pending)) {
+                __builtin_amdgcn_s_sleep(4);
+                if (++spins > kSpinLimit) {
+                    if (pending) atomicOr(err, 1);
+                    pending = false;
+                }
+            }
+        }
+    }
+}
+
+// The sharded solve's separator step in ONE launch (dd.hip apply_minv): the
+// three row phases of SepFlow -- separator L rows (b_S - L_SI y_I, then the
+// separator triangle's terms, / d), separator U rows (y_S, then the triangle's
+// terms, / d), interface rows of the interior (y_I - U_IS x_S, in place) -- as
+// one dataflow task list in that order (each phase in level order), short rows
+// one per lane as in k_trsv_flow.  Every row runs the operations and order of
+// the launches it replaces (k_sub_seq, k_trsv_flow, k_trsv_flow, k_sub_seq),
+// so the result is the same bit for bit.  Values a row polls: its own-phase
+// sources (sentinel = not ready) and, in the U phase, b = y_S.
+__global__ __launch_bounds__(kBlock) void k_sep_flow(Gate g, int ntask, const int4 *__restrict__ tasks,
+                                                     const int *__restrict__ rows, SepFlow f, int *err)
+{
+    if (gated(g)) return;
+    const int lane = threadIdx.x & 63;
+    const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
+    for (long long t = wid; t < ntask; t += nw) {
+        const int4 tk = tasks[t];
+        const SepPhase &P = f.ph[tk.z];
+        const unsigned long long *src = reinterpret_cast<const unsigned long long *>(P.src);
+        const int r = lane < tk.y ? rows[tk.x + lane] : -1;
+        bool pending = r >= 0;
+        int k = pending ? P.rp[r] : 0;
+        const int k1 = pending ? P.rp[r + 1] : 0;
+        double acc = 0.0;
+        bool have_b = !pending;
+        if (pending && !P.bpoll) {
+            acc = P.b[r];
+            if (P.prp)
+                for (int q = P.prp[r]; q < P.prp[r + 1]; q++) acc -= P.pv[q] * P.px[P.pci[q]];
+            have_b = true;
+        }
+        int spins = 0;
+        while (__any(pending)) {
+            if (pending && !have_b) {
+                const unsigned long long u = ld_agent(reinterpret_cast<const unsigned long long *>(P.b) + r);
+                if (u != kSentinel) {
+                    acc = __longlong_as_double((long long)u);
+                    have_b = true;
+                }
+            }
+            if (pending && have_b) {
+                bool stop = false;
+                while (!stop && k < k1) {
+                    unsigned long long u[4];            // up to 4 polls in flight
+#pragma unroll
+                    for (int j = 0; j < 4; j++) u[j] = k + j < k1 ? ld_agent(src + P.ci[k + j]) : 0ull;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        if (stop || k >= k1) break;
+                        if (u[j] == kSentinel) { stop = true; break; }
+                        acc = acc - P.v[k] * __longlong_as_double((long long)u[j]);
+                        k++;
+                    }
+                }
+                if (k == k1) {
+                    const double o = P.d ? acc / P.d[r] : acc;
+                    st_agent(reinterpret_cast<unsigned long long *>(P.x) + r, (unsigned long long)__double_as_longlong(o));
                     pending = false;
                 }
             }
@@ -2413,23 +2492,49 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
 // every block sums them in sum_partials' fixed order, so h is bit-identical to
 // the per-step kernels'.  Needs all G blocks resident (checked on the host);
 // every spin is bounded (err bit 0).
+__device__ __forceinline__ unsigned long long poll_granule(const unsigned long long *p, int *err)
+{
+    unsigned long long a = ld_agent(p);
+    int spins = 0;
+    while (a == kSentinel) {
+        __builtin_amdgcn_s_sleep(1);
+        a = ld_agent(p);
+        if (++spins > kSpinLimit) {
+            atomicOr(err, 1);
+            break;
+        }
+    }
+    return a;
+}
+
 __device__ __forceinline__ double gather_sum(const unsigned long long *row, int G, int *err)
 {
     double v = 0.0;
-    for (int q = threadIdx.x; q < G; q += kBlock) {
-        unsigned long long b = ld_agent(row + q);
-        int spins = 0;
-        while (b == kSentinel) {
-            __builtin_amdgcn_s_sleep(1);
-            b = ld_agent(row + q);
-            if (++spins > kSpinLimit) {
-                atomicOr(err, 1);
-                break;
-            }
-        }
-        v += __longlong_as_double((long long)b);
-    }
+    for (int q = threadIdx.x; q < G; q += kBlock) v += __longlong_as_double((long long)poll_granule(row + q, err));
     return block_sum(v);
+}
+
+// The sum of step k's partials as every block needs it.  LEADER: block 0
+// alone gathers the row (gather_sum: the same order, the same bits) and
+// publishes the sum in one granule hg; the other blocks' thread 0 polls that
+// granule and hands the value over through LDS -- G line requests per poll
+// round instead of G x G/32 on the few channels that hold the row, for one
+// more hop.  Measured (C2 / C4, profiles/r03_gather_ab.txt): k_arnoldi_wide
+// (C4, streaming the basis beside the polls) 472.5 -> 456.6 us, so it leads;
+// k_arnoldi_persist (C2) 73.2 -> 77.5 us, so every block gathers there.
+template <bool LEADER>
+__device__ __forceinline__ double gather_h(const unsigned long long *row, unsigned long long *hg, int k, int G,
+                                           int *err)
+{
+    if (!LEADER || blockIdx.x == 0) {
+        const double h = gather_sum(row, G, err);
+        if (LEADER && threadIdx.x == 0) st_agent(hg, (unsigned long long)__double_as_longlong(h));
+        return h;
+    }
+    __shared__ double hb[2];                    // alternating: steps k and k+2 are a block_sum apart
+    if (threadIdx.x == 0) hb[k & 1] = __longlong_as_double((long long)poll_granule(hg, err));
+    __syncthreads();
+    return hb[k & 1];
 }
 
 template <int J>
@@ -2438,8 +2543,8 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
                                                             double *__restrict__ V, long long ldv,
                                                             double *H, double *cs, double *sn,
                                                             double *s, double *hist,
-                                                            unsigned long long *gran, long long units,
-                                                            int *err)
+                                                            unsigned long long *gran, unsigned long long *hg,
+                                                            long long units, int *err)
 {
     if (gated(g)) return;
     const int G = gridDim.x;
@@ -2473,7 +2578,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             for (int j = 0; j < J; j++)
                 if (u0 + j * stride < units) vn[j] = ld2_nt(vnp, u0 + j * stride);   // streamed
         }
-        const double h = gather_sum(gran + (long long)k * G, G, err);
+        const double h = gather_h<false>(gran + (long long)k * G, hg + k, k, G, err);
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         acc = 0.0;
@@ -2490,7 +2595,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(gather_sum(gran + (long long)(i + 1) * G, G, err));
+    const double hn = sqrt(gather_h<false>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err));
     if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
@@ -2549,8 +2654,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
                                                             double *__restrict__ V, long long ldv,
                                                             double *H, double *cs, double *sn,
                                                             double *s, double *hist,
-                                                            unsigned long long *gran, long long units,
-                                                            int *err)
+                                                            unsigned long long *gran, unsigned long long *hg,
+                                                            long long units, int *err)
 {
     constexpr int J = kWideJR + kWideJL;
     if (gated(g)) return;
@@ -2625,7 +2730,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         asm volatile("" : "+v"(ub));
 #pragma unroll
         for (int j = 0; j < kWideD; j++) fetch(j, ub, vkp, vnp, true);    // in flight during the sum
-        const double h = gather_sum(gran + (long long)k * G, G, err);
+        const double h = gather_h<true>(gran + (long long)k * G, hg + k, k, G, err);
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         acc = 0.0;
@@ -2646,7 +2751,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(gather_sum(gran + (long long)(i + 1) * G, G, err));
+    const double hn = sqrt(gather_h<true>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err));
     if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
@@ -2778,13 +2883,16 @@ inline int blocks_for(long long n, int bs = kBlock, int cap = 65535)
 }  // namespace
 
 // ======================================================= host launchers
+#ifndef GG_REDUCE_UPT
+#define GG_REDUCE_UPT 4
+#endif
 int reduce_grid(long long units)
 {
     // vectors too long for k_arnoldi_persist's registers at 1024 blocks (more
     // than 8 units per thread) reduce over kWideG blocks, two per CU, so that
     // k_arnoldi_wide can keep w on chip with the same tree
     if (units > (long long)1024 * kBlock * 8) return kWideG;
-    long long g = (units + kBlock * 4 - 1) / (kBlock * 4);   // >= 8 elements / thread
+    long long g = (units + kBlock * GG_REDUCE_UPT - 1) / (kBlock * GG_REDUCE_UPT);   // >= 2*UPT elements / thread
     if (g < 1) g = 1;
     if (g > 1024) g = 1024;
     return (int)g;
@@ -2864,9 +2972,13 @@ void launch_iluk_wave(int n, const long long *prow, const int *nl, const int *pc
     k_iluk_wave<<<blocks, kBlock, 0, st>>>(n, prow, nl, pcol, val, dinv, done, rows_short, nshort, rows_long,
                                            nlong, long_blocks, scratch, err);
 }
-void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st)
+void launch_gather(const double *in, const long long *idx, double *out, long long n, hipStream_t st,
+                   double *fill0, double *fill1, long long nfill)
 {
-    k_gather<<<blocks_for(n, kBlock, 8192), kBlock, 0, st>>>(in, idx, out, n);
+    if (!fill0 || !fill1) nfill = 0;
+    k_gather<<<blocks_for(std::max(n, nfill), kBlock, 8192), kBlock, 0, st>>>(
+        in, idx, out, n, reinterpret_cast<unsigned long long *>(fill0), reinterpret_cast<unsigned long long *>(fill1),
+        nfill);
 }
 void launch_copy(const double *in, double *out, long long n, hipStream_t st)
 {
@@ -2885,6 +2997,23 @@ void launch_sub_seq(Gate g, const DevCsr &C, const double *x, const double *in, 
     k_sub_seq<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(
         g, C.n, C.rp.p, C.ci.p, C.v.p, x, in, out, reinterpret_cast<unsigned long long *>(fill0),
         reinterpret_cast<unsigned long long *>(fill1), nfill);
+}
+
+void launch_sep_flow(Gate g, int ntask, const int4 *tasks, const int *rows, const SepFlow &f, int *err, hipStream_t st)
+{
+    if (ntask <= 0) return;
+    // one block per CU at most (every waiting lane polls; all co-resident), a wave per task
+    static const int cap = [] {
+        int dev = 0, c = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_sep_flow, kBlock, 0) != hipSuccess) per = 0;
+        return per > 0 ? c : 0;
+    }();
+    GG_REQUIRE(cap > 0, GG_EHIP, "k_sep_flow cannot be resident");
+    const long long need = ((long long)ntask + kBlock / 64 - 1) / (kBlock / 64);
+    const int blocks = (int)std::min<long long>(cap, need);
+    k_sep_flow<<<blocks, kBlock, 0, st>>>(g, ntask, tasks, rows, f, err);
 }
 void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long cnt, hipStream_t st)
 {
@@ -3205,14 +3334,19 @@ int arnoldi_persist_units(int G, long long Ppad)
     return J <= 1 ? 1 : J <= 2 ? 2 : J <= 4 ? 4 : J <= 8 ? 8 : 0;
 }
 
-int arnoldi_persist_max_blocks()
+// blocks of the J-unit instantiation that can be resident at once
+int arnoldi_persist_max_blocks(int J)
 {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_arnoldi_persist<8>, kBlock, 0) != hipSuccess)
-        return 0;
-    return cus * per;
+    auto occ = [&](const void *f) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) == hipSuccess; };
+    const bool ok = J == 1   ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<1>))
+                    : J == 2 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<2>))
+                    : J == 4 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<4>))
+                    : J == 8 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<8>))
+                             : false;
+    return ok ? cus * per : 0;
 }
 
 // k_arnoldi_wide: usable when G = kWideG blocks of kWideJR + kWideJL units per
@@ -3234,20 +3368,21 @@ bool arnoldi_wide_ok(int G, long long Ppad)
 
 void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, double *V, long long ldv,
                          double *H, double *cs, double *sn, double *s, double *hist,
-                         unsigned long long *gran, int G, long long Ppad, int *err, hipStream_t st)
+                         unsigned long long *gran, unsigned long long *hg, int G, long long Ppad, int *err,
+                         hipStream_t st)
 {
-    k_arnoldi_wide<<<G, kBlock, 0, st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, Ppad / 2, err);
+    k_arnoldi_wide<<<G, kBlock, 0, st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2, err);
 }
 
 void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
                             long long ldv, double *H, double *cs, double *sn, double *s,
-                            double *hist, unsigned long long *gran, int G, long long Ppad, int *err,
-                            hipStream_t st)
+                            double *hist, unsigned long long *gran, unsigned long long *hg, int G, long long Ppad,
+                            int *err, hipStream_t st)
 {
     const int J = arnoldi_persist_units(G, Ppad);
 #define GG_PERSIST(JJ)                                                                       \
     k_arnoldi_persist<JJ><<<G, kBlock, 0, st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, \
-                                                 Ppad / 2, err)
+                                                 hg, Ppad / 2, err)
     if (J == 1) GG_PERSIST(1);
     else if (J == 2) GG_PERSIST(2);
     else if (J == 4) GG_PERSIST(4);

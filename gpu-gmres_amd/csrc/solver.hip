@@ -296,7 +296,8 @@ struct gg_solver {
     // transient tap-node statistics (gg_transient_set_taps / _get_taps)
     std::vector<int> taps;
     std::vector<double> tap_max, tap_min, tap_avg;
-    DBuf<unsigned long long> gran;      // m * (m+2) * G hand-off granules, re-armed per cycle
+    DBuf<unsigned long long> gran;      // m * (m+2) * G hand-off granules, then m * (m+2) sums
+                                        // (gather_h), re-armed per cycle
     DBuf<double> hist;
     long long hist_cap = 0;
     DBuf<DevState> ds;
@@ -434,10 +435,10 @@ void ensure_workspace(gg_solver *s, int m)
         const bool off = e && e[0] == '1';
         const char *wf = std::getenv("GG_WIDE_FORCE");
         const bool force_wide = wf && wf[0] == '1';
-        s->persist = !off && !force_wide && arnoldi_persist_units(s->G, s->Ppad) != 0 &&
-                     s->G <= arnoldi_persist_max_blocks();
+        const int pj = arnoldi_persist_units(s->G, s->Ppad);
+        s->persist = !off && !force_wide && pj != 0 && s->G <= arnoldi_persist_max_blocks(pj);
         s->wide = !off && !s->persist && arnoldi_wide_ok(s->G, s->Ppad);   // long vectors: w on chip
-        if (s->persist || s->wide) s->gran.alloc((size_t)m * (m + 2) * s->G);
+        if (s->persist || s->wide) s->gran.alloc((size_t)m * (m + 2) * (s->G + 1));
     }
     s->H.alloc((size_t)(m + 1) * m);
     GG_HIP(hipMemsetAsync(s->H.p, 0, (size_t)(m + 1) * m * sizeof(double), s->st));
@@ -615,6 +616,12 @@ void enqueue_init(gg_solver *s)
     launch_init_beta(s->partA.p, s->G, ds, s->hist.p, s->st);
 }
 
+// inner iteration i's sum granules (gather_h): after the m * (m+2) * G partials
+unsigned long long *hgran(gg_solver *s, int m, int i)
+{
+    return s->gran.p + (size_t)m * (m + 2) * s->G + (size_t)i * (m + 2);
+}
+
 void enqueue_cycle(gg_solver *s, int m)
 {
     DevState *ds = s->ds.p;
@@ -658,12 +665,12 @@ void enqueue_cycle(gg_solver *s, int m)
         mk = prof_begin(s, GG_PROF_MGS, i);
         if (persist) {
             launch_arnoldi_persist(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
-                                   s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, s->G, P,
-                                   s->err.p, s->st);
+                                   s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
+                                   P, s->err.p, s->st);
         } else if (wide) {
             launch_arnoldi_wide(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
-                                s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, s->G, P, s->err.p,
-                                s->st);
+                                s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
+                                P, s->err.p, s->st);
         } else {
             double *pin = s->partA.p, *pout = s->partB.p;
             launch_dot(gi, s->w.p, s->V.p, pin, s->G, P, s->st);               // <w, v_0>
