@@ -1328,8 +1328,11 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 #ifndef GG_TILE_BATCH
 #define GG_TILE_BATCH 8
 #endif
+// 3 slots: 59-70 KiB of LDS, two workgroups per CU -- at the C4 wavefront's
+// peak more tiles are ready than there are CUs (C4 L 227 -> 222 us, U 234 ->
+// 233 us against 5 slots, profiles/r03_tile_ring.txt)
 #ifndef GG_TILE_RING
-#define GG_TILE_RING GG_WAVE_RING
+#define GG_TILE_RING 3
 #endif
 // boundary wave retries: 0 = one poll at a time, n > 0 = two generations in
 // flight, the second issued s_sleep(n) after the first (measured at C4: L/U
