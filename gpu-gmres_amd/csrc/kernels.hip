@@ -47,6 +47,29 @@ __device__ __forceinline__ double block_sum(double v)
     return r;
 }
 
+// block_sum of acc[k] for every k < nk at once, stored by thread k at
+// part[k * kstride]: the same wave_sum per wave and (0 + 1) + (2 + 3) as
+// block_sum, so the same bits, with one barrier instead of three per value.
+// Once per kernel (its LDS is not re-armed).
+template <int NK>
+__device__ __forceinline__ void block_sum_store(const double (&acc)[NK], int nk, double *part, long long kstride)
+{
+    __shared__ double sh[kBlock / 64][NK];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        if (k < nk) {
+            const double v = wave_sum(acc[k]);
+            if (lane == 0) sh[w][k] = v;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nk) {
+        const int k = threadIdx.x;
+        part[k * kstride] = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+    }
+}
+
 // Sum of G per-block partials, identical (bit-for-bit) in every block.
 __device__ __forceinline__ double sum_partials(const double *part, int G)
 {
@@ -918,7 +941,8 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     // round-robin over the XCDs) the bands share one XCD and its L2 --
     // placement is for speed only, the hand-off protocol is the same.
     // Measured on C2: U 121.0 -> 117.9 us, while L (3 streamed arrays) slows
-    // 88.9 -> 90.0 us, so the forward solve keeps one workgroup per band.
+    // 88.9 -> 90.0 us (round 3, re-measured: 89.4 / 90.3 -> 89.9 / 90.4 us), so
+    // the forward solve keeps one workgroup per band.
     constexpr int XS = (D3 || FWD) ? 1 : GG_WAVE_XCD;
     if (XS > 1 && blockIdx.x % XS) return;
     const int blk = blockIdx.x / XS;
@@ -2291,10 +2315,7 @@ __global__ __launch_bounds__(kBlock) void k_multidot(Gate g, const double *__res
             }
         }
     }
-    for (int kk = 0; kk < kc; kk++) {
-        const double r = block_sum(acc[kk]);
-        if (threadIdx.x == 0) part[(long long)(k0 + kk) * G + blockIdx.x] = r;
-    }
+    block_sum_store<kCgsKC>(acc, kc, part + (long long)k0 * G + blockIdx.x, G);
 }
 // h[k] = sum of every shard's partials of dot k (shard q's at part + q*cnt + k*G,
 // summed in sum_partials' order over the P*G partials, shard-major);
@@ -2407,13 +2428,7 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update_dot(Gate g, double *__res
             }
         }
     }
-#pragma unroll
-    for (int k = 0; k < kCgsFuseMax; k++) {      // static indices: acc stays in registers
-        if (k < nk) {
-            const double r = block_sum(acc[k]);
-            if (threadIdx.x == 0) part[(long long)k * G + blockIdx.x] = r;
-        }
-    }
+    block_sum_store<kCgsFuseMax>(acc, nk, part + blockIdx.x, G);   // static indices: acc stays in registers
 }
 
 __device__ __forceinline__ void apply_rot(double &dx, double &dy, double cs, double sn)
