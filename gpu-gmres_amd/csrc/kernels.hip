@@ -392,6 +392,20 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
 // wave), up to 8 index/value pairs in flight before their gathers; each row is
 // summed serially in CSR order from 0.0, skipping the padding (col -1): the
 // same operations as k_spmv_stream (computeSpMV order).
+// GG_SPMV_XCD: blocks b, b+8, ... (one XCD under round-robin dispatch, for
+// speed only) take consecutive slices, so the x lines that neighbouring slices
+// share are fetched into one L2 (the 3D tile layout's line and plane
+// neighbours are 64 and 13,824 rows away)
+#ifndef GG_SPMV_XCD
+#define GG_SPMV_XCD 1
+#endif
+__device__ __forceinline__ int xcd_block()
+{
+    if (!GG_SPMV_XCD) return blockIdx.x;
+    const int nb = gridDim.x, q = nb >> 3, rem = nb & 7, x = blockIdx.x & 7;
+    return x * q + (x < rem ? x : rem) + (blockIdx.x >> 3);
+}
+
 template <bool RESID, bool YDIV = false>
 __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice, const int *sptr,
                                                       const int *__restrict__ ci,
@@ -402,7 +416,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
                                                       const double *__restrict__ ydiv)
 {
     if (gated(g)) return;
-    const int s = blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int s = xcd_block() * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (s >= nslice) return;
     const int lane = threadIdx.x & 63;
     const int off = sptr[s], w = (sptr[s + 1] - off) >> 6;
