@@ -2349,30 +2349,22 @@ __global__ __launch_bounds__(kBlock) void k_cgs_reduce(Gate g, const double *par
     }
 }
 // a = a - sum_k h[k] v_k(u), k ascending (a = (-h_k) v_k + a, the MGS AXPY's
-// rounding), the loads of eight v_k issued before their multiply-adds (a
-// thread owns one or a few units: one load round trip per eight vectors, not
-// per vector).  CACHE: default policy (the fused kernel reads v_k(u) again)
-// or non-temporal.
-template <bool CACHE>
-__device__ __forceinline__ void cgs_axpy(double2 &a, const double *__restrict__ V, long long ldv,
-                                         const double *h, int nk, long long u)
+// rounding), the loads of up to kCgsChunk v_k issued before their
+// multiply-adds (a thread owns one or a few units: one load round trip per
+// chunk, not per vector); the chunk's values are left in b for the caller.
+constexpr int kCgsChunk = 32;
+__device__ __forceinline__ void cgs_axpy_chunk(double2 &a, double2 (&b)[kCgsChunk], const double *__restrict__ V,
+                                               long long ldv, const double *h, int k0, int nk, long long u)
 {
-    for (int k0 = 0; k0 < nk; k0 += 8) {
-        double2 b[8];
-        double c[8];
 #pragma unroll
-        for (int kk = 0; kk < 8; kk++) {
-            if (k0 + kk < nk) {
-                b[kk] = CACHE ? ld2(V + (long long)(k0 + kk) * ldv, u) : ld2_nt(V + (long long)(k0 + kk) * ldv, u);
-                c[kk] = -h[k0 + kk];
-            }
-        }
+    for (int kk = 0; kk < kCgsChunk; kk++)
+        if (k0 + kk < nk) b[kk] = ld2_nt(V + (long long)(k0 + kk) * ldv, u);
 #pragma unroll
-        for (int kk = 0; kk < 8; kk++) {
-            if (k0 + kk < nk) {
-                a.x = c[kk] * b[kk].x + a.x;
-                a.y = c[kk] * b[kk].y + a.y;
-            }
+    for (int kk = 0; kk < kCgsChunk; kk++) {
+        if (k0 + kk < nk) {
+            const double c = -h[k0 + kk];
+            a.x = c * b[kk].x + a.x;
+            a.y = c * b[kk].y + a.y;
         }
     }
 }
@@ -2389,7 +2381,8 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(Gate g, double *__restric
     const long long stride = (long long)gridDim.x * kBlock;
     for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units; u += stride) {
         double2 a = ld2(w, u);
-        cgs_axpy<false>(a, V, ldv, h, nk, u);
+        double2 b[kCgsChunk];
+        for (int k0 = 0; k0 < nk; k0 += kCgsChunk) cgs_axpy_chunk(a, b, V, ldv, h, k0, nk, u);
         st2(w, u, a);
         if (NORM && u < dunits) {
             acc += a.x * a.x;
@@ -2406,8 +2399,9 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(Gate g, double *__restric
 // h[k] v_k (as k_cgs_update), then the block partials of <w, v_k>, k < nk, over
 // [0, dunits) into part[k*G + block] -- the same unit -> thread assignment and
 // accumulation order as k_multidot (G blocks, grid stride), so bit-identical to
-// the two launches; the second read of each v_k(u) comes from the caches.
-constexpr int kCgsFuseMax = 32;              // dots held per thread (else two launches)
+// the two launches; each v_k(u) is read once (kept in registers between the
+// update and the dots).
+constexpr int kCgsFuseMax = kCgsChunk;       // dots held per thread (else two launches)
 __global__ __launch_bounds__(kBlock) void k_cgs_update_dot(Gate g, double *__restrict__ w,
                                                            const double *__restrict__ V, long long ldv,
                                                            const double *h, int nk, long long units,
@@ -2420,24 +2414,15 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update_dot(Gate g, double *__res
     const long long stride = (long long)gridDim.x * kBlock;
     for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units; u += stride) {
         double2 a = ld2(w, u);
-        cgs_axpy<true>(a, V, ldv, h, nk, u);
+        double2 b[kCgsChunk];
+        cgs_axpy_chunk(a, b, V, ldv, h, 0, nk, u);
         st2(w, u, a);
         if (u < dunits) {
-            // eight loads in flight, then their products (static acc indices)
 #pragma unroll
-            for (int c = 0; c < kCgsFuseMax / 8; c++) {
-                if (c * 8 < nk) {
-                    double2 b[8];
-#pragma unroll
-                    for (int kk = 0; kk < 8; kk++)
-                        if (c * 8 + kk < nk) b[kk] = ld2_nt(V + (long long)(c * 8 + kk) * ldv, u);
-#pragma unroll
-                    for (int kk = 0; kk < 8; kk++) {
-                        if (c * 8 + kk < nk) {
-                            acc[c * 8 + kk] += a.x * b[kk].x;
-                            acc[c * 8 + kk] += a.y * b[kk].y;
-                        }
-                    }
+            for (int k = 0; k < kCgsFuseMax; k++) {
+                if (k < nk) {
+                    acc[k] += a.x * b[k].x;
+                    acc[k] += a.y * b[k].y;
                 }
             }
         }
