@@ -383,7 +383,9 @@ def bench_dd(a, torch, dist, world, rank, local):
                                                 "2 + (i + 2) at cycle index i",
                    "separator_rows": info["nsep"], "max_interface": info["max_iface"],
                    "wavefront_interior": info["wave_interior"],
-                   "wavefront_separator": info["wave_separator"],
+                   "wavefront_separator": int(info["wave_separator"] >= 2),
+                   "separator_step": {0: "level launches", 1: "fused dataflow launch (k_sep_flow)",
+                                      2: "2D wavefront", 3: "3D tile wavefront"}.get(info["wave_separator"]),
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
                    "parallelism": f"dd{parts}", "setup_s": round(t_setup, 3)},
         "roofline": None,

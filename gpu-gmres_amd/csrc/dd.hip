@@ -988,7 +988,7 @@ int gg_dd_info(gg_dd *d, int *info)
     info[3] = d->maxI;
     info[4] = s.nI;
     info[5] = s.wI.ok ? (s.wI.nz > 1 ? 3 : 2) : 0;
-    info[6] = s.wS.ok ? (s.wS.nz > 1 ? 3 : 2) : 0;
+    info[6] = s.wS.ok ? (s.wS.nz > 1 ? 3 : 2) : s.sepflow ? 1 : 0;
     info[7] = (int)d->Pl;
     info[8] = (int)d->sh.size();
     info[9] = d->P * d->maxI;

@@ -82,9 +82,11 @@ int gg_dd_comm_ranks(gg_dd *d, int *ranks, int *rank);
 int gg_dd_set_system(gg_dd *d, int n, const int *row_ptr, const int *col_idx, const double *val,
                      int method);
 /* info[0..9]: n, nparts, separator rows, max interface per shard, this
- * process's first shard: interior rows, wavefront interior (0/1), wavefront
- * separator (0/1), local vector length (slots), shards in this process, halo
- * doubles exchanged per all-gather (received, per shard) */
+ * process's first shard: interior rows, interior solves (0 level-scheduled,
+ * 2 / 3 the 2D / 3D wavefront), separator solves (0 level-scheduled launches,
+ * 1 the fused separator step, 2 / 3 wavefront), local vector length (slots),
+ * shards in this process, halo doubles exchanged per all-gather (received,
+ * per shard) */
 int gg_dd_info(gg_dd *d, int *info);
 /* the arrow permutation in use: pinv[j] = new index of node j; q = its inverse */
 int gg_dd_perm(gg_dd *d, int *pinv, int *q);

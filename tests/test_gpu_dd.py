@@ -30,10 +30,11 @@ CASES = {
     "sherman1_P4": (lambda: M.read_rua(fixture_path("sherman1.rua")), 4, host.PART_BISECT, None, None),
     "5pt_60x60_P1": (lambda: M.laplacian_5pt(60, 60), 1, host.PART_BLOCKS, 2, 0),
     # the separator ordered by a greedy colouring (GG_PART_COLOR_SEP): a
-    # few-level separator solve on the dataflow kernel
-    "5pt_200x160_P4_color": (lambda: M.laplacian_5pt(200, 160), 4, host.PART_BLOCKS | host.PART_COLOR_SEP, 2, 0),
+    # few-level separator solve, fused with its coupling terms into one
+    # dataflow launch (k_sep_flow, separator kind 1)
+    "5pt_200x160_P4_color": (lambda: M.laplacian_5pt(200, 160), 4, host.PART_BLOCKS | host.PART_COLOR_SEP, 2, 1),
     "7pt_16x16x32_P8_upwind_color": (lambda: M.grid_7pt(16, 16, 32, upwind=0.1), 8,
-                                     host.PART_BLOCKS | host.PART_COLOR_SEP, 3, 0),
+                                     host.PART_BLOCKS | host.PART_COLOR_SEP, 3, 1),
 }
 
 _cache = {}
@@ -63,6 +64,21 @@ def test_dd_layout(name):
         assert inf["wave_separator"] == ws, inf
     plan = host.DDPlan(A, P, CASES[name][2])          # the host plan agrees with the solver's
     assert np.array_equal(plan.q, q) and inf["nsep"] == plan.nsep
+
+
+def test_dd_separator_four_launches_match_fused(monkeypatch):
+    """GG_DD_SEPFLOW=0 keeps the four separator launches (k_sub_seq, two
+    k_trsv_flow, k_sub_seq): the same bits as the fused step."""
+    A, d, q, B, L, U = setup("5pt_200x160_P4_color")
+    monkeypatch.setenv("GG_DD_SEPFLOW", "0")
+    d0 = DD(4, device=0)
+    d0.set_system(A, CASES["5pt_200x160_P4_color"][2])
+    assert d0.info()["wave_separator"] == 0 and d.info()["wave_separator"] == 1
+    rng = np.random.default_rng(11)
+    v = rng.standard_normal(A.shape[0])
+    z0, z1 = d0.precond_apply(v), d.precond_apply(v)
+    assert np.array_equal(z0, z1)
+    assert np.array_equal(z1[q], O.lusolve(L, U, v[q]))
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
