@@ -66,6 +66,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # process group -- the multi-rank control flow on a one-GPU box
 ONE_GPU = os.environ.get("GG_BENCH_ONE_GPU") == "1"
 METRIC = "fp64 GMRES iterations/sec + SpMV HBM GB/s, 1M-row CSR @1/2/4/8 MI355X"
+# --division -> ggmres.DIV_EXACT / DIV_RCP / DIV_FMA (ggmres.h gg_div_mode)
+DIV_MODES = {"exact": 0, "rcp": 1, "fma": 2}
 
 
 def parse():
@@ -99,10 +101,12 @@ def parse():
     p.add_argument("--dd-sep", choices=["color", "natural"], default="color",
                    help="dd: separator order -- a greedy colouring of its graph (GG_PART_COLOR_SEP, "
                         "default: a few-level separator solve) or partition4's ascending index")
-    p.add_argument("--division", choices=["rcp", "exact"], default="rcp",
-                   help="non-unit triangular solves: rcp = x = acc * RN(1/d) on the wavefront solves "
-                        "(gg_set_division GG_DIV_RCP, tolerance parity 1e-10, tests/test_gpu_fastdiv.py), "
-                        "exact = RN(acc / d), the reference's division bit for bit")
+    p.add_argument("--division", choices=["fma", "rcp", "exact"], default="fma",
+                   help="triangular-solve rows: fma = two fused multiply-adds per row on the unskewed "
+                        "2D-grid wavefronts, U pre-scaled by RN(1/d), rcp elsewhere (gg_set_division "
+                        "GG_DIV_FMA, default); rcp = x = acc * RN(1/d) on the wavefront solves "
+                        "(GG_DIV_RCP); both tolerance parity 1e-10 (tests/test_gpu_fastdiv.py); "
+                        "exact = the reference's row arithmetic bit for bit")
     p.add_argument("--dd-comm", choices=["ipc", "rccl"], default="ipc",
                    help="sharded solve at N > 1: ipc = device-initiated all-gathers through hipIpc-mapped "
                         "exchange areas over xGMI (GG_DD_IPC, default), rccl = RCCL collectives (GG_DD_RCCL)")
@@ -127,8 +131,11 @@ PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # bare dependent-chain latency of one wavefront step (cycles, tools/lat_probe.hip
 # built like the library, -ffp-contract=off, on MI355X: profiles/r03_lat_probe.txt
 # "step(dpp)" = unit L, "U step (WD_RCP)" = the bit-exact reciprocal-FMA
-# division, "U step (WD_MUL)" = GG_DIV_RCP's one multiply) and the shader clock
-CHAIN_CYCLES = {"trsv_L": 38.89, "trsv_U": 62.66, "trsv_U_mul": 43.72}
+# division, "U step (WD_MUL)" = GG_DIV_RCP's one multiply; "L step (UFMA)" /
+# "U step (SFMA)" = GG_DIV_FMA's fused rows, profiles/r03_lat_probe_fma.txt) and
+# the shader clock
+CHAIN_CYCLES = {"trsv_L": 38.89, "trsv_U": 62.66, "trsv_U_mul": 43.72,
+                "trsv_L_fma": 29.19, "trsv_U_fma": 29.58}
 SHADER_GHZ = 2.399
 
 
@@ -320,7 +327,10 @@ def bench_dd(a, torch, dist, world, rank, local):
         ranks = 1
     d.set_system(A, host.PART_BLOCKS | (host.PART_COLOR_SEP if a.dd_sep == "color" else 0))
     import ggmres
-    d.set_division(ggmres.DIV_RCP if a.division == "rcp" else ggmres.DIV_EXACT)
+    # the sharded solve multiplies by RN(1/d) at most (gg_dd_set_division has no
+    # GG_DIV_FMA: its restatement, oracle/dd.py, has no fused rows)
+    dd_div = "rcp" if a.division == "fma" else a.division
+    d.set_division(DIV_MODES[dd_div])
     t_setup = time.perf_counter() - t_setup
     info = d.info()
     db = torch.from_numpy(b).cuda()
@@ -375,7 +385,7 @@ def bench_dd(a, torch, dist, world, rank, local):
                                if world > 1 else f"in-process ({parts} shards on one GPU)",
                    "exchange_ranks": ranks if world > 1 else None,
                    "exchange_latency": xch,
-                   "division": a.division,
+                   "division": dd_div,
                    "orthogonalization": ("CGS2: 3 all-gathers per inner iteration (GG_SOLVE_CGS2, tolerance "
                                          "parity 1e-10 vs MGS over the first cycle)") if a.dd_orth == "cgs2"
                                         else "MGS (the reference's): i + 2 all-gathers per inner iteration",
@@ -497,14 +507,15 @@ def main():
                 KERNEL_NAMES[dom_] = KERNEL_NAMES[dom_].replace(", 1, false>", f", {kilu + 1}, false>")
     else:
         s.set_precond_ilu0()
-    s.set_division(ggmres.DIV_RCP if a.division == "rcp" else ggmres.DIV_EXACT)
+    s.set_division(DIV_MODES[a.division])
     if s.uses_wavefront:
         # the kernels the solver launches for L and U (2D band / 3D tile
         # wavefront, skew, division mode), as rocprofv3 names them
         KERNEL_NAMES["trsv_L"] = s.trsv_kernel(0)
         KERNEL_NAMES["trsv_U"] = s.trsv_kernel(1)
-    u_mul = s.division_active(1) == ggmres.DIV_RCP
-    l_mul = s.division_active(0) == ggmres.DIV_RCP
+    u_mode, l_mode = s.division_active(1), s.division_active(0)
+    u_mul, l_mul = u_mode != ggmres.DIV_EXACT, l_mode != ggmres.DIV_EXACT     # not the reference's division
+    u_fma, l_fma = u_mode == ggmres.DIV_FMA, l_mode == ggmres.DIV_FMA
     t_setup = time.perf_counter() - t_setup
     db = torch.from_numpy(b).cuda()
     dx = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -520,7 +531,7 @@ def main():
             s2 = ggmres.Solver(local)
             s2.set_matrix(A)
             s2.set_precond_ilu0()
-            s2.set_division(ggmres.DIV_RCP if a.division == "rcp" else ggmres.DIV_EXACT)
+            s2.set_division(DIV_MODES[a.division])
             solvers.append(s2)
         flags = ggmres.SOLVE_SHARED_DEVICE if S > 1 else 0
 
@@ -665,7 +676,9 @@ def main():
     if roof and dom in ("trsv_L", "trsv_U") and s.uses_wavefront and not c5:
         # a non-unit L (the split engine's) divides like U
         mul = u_mul if dom == "trsv_U" else l_mul
-        cyc = CHAIN_CYCLES["trsv_L" if dom == "trsv_L" and not pg else "trsv_U_mul" if mul else "trsv_U"]
+        fm = u_fma if dom == "trsv_U" else l_fma
+        cyc = CHAIN_CYCLES[(dom + "_fma") if fm else
+                           "trsv_L" if dom == "trsv_L" and not pg else "trsv_U_mul" if mul else "trsv_U"]
         # the DAG's longest path (ILU(k): skew k+1; 3D: nx + ny + nz - 2, whose
         # per-step chain is the 2D one: the tile kernel's plane term is off it)
         steps = 3 * a.c4_grid - 2 if c4 else a.grid + (kilu + 1) * (a.grid - 1)
@@ -735,7 +748,10 @@ def main():
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
                    "wavefront_sptrsv": s.uses_wavefront,
-                   "division": ((f"x = acc * RN(1/d) on the wavefront {'L and U solves' if l_mul else 'U solve'} "
+                   "division": (("rows as two fused multiply-adds, in-line term first, U's b and "
+                                 "coefficients pre-scaled by RN(1/d) (GG_DIV_FMA; tolerance parity "
+                                 "1e-10 vs the reference's arithmetic)") if u_fma else
+                                (f"x = acc * RN(1/d) on the wavefront {'L and U solves' if l_mul else 'U solve'} "
                                  f"(GG_DIV_RCP; tolerance parity 1e-10 vs the reference's division)")
                                 if u_mul else
                                 "x = RN(acc / d) (the reference's division, bit-exact)"),

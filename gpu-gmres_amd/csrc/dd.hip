@@ -225,7 +225,7 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
     auto gate = [&](Shard &s) { return gate_of(s, gi, mask); };
     for (auto &sp : d->sh) {
         Shard &s = *sp;
-        for (DevTri *T : {&s.LI, &s.LS, &s.UI, &s.US}) T->fast = d->div_mode == GG_DIV_RCP;
+        for (DevTri *T : {&s.LI, &s.LS, &s.UI, &s.US}) T->fast = d->div_mode;
         launch_trsv(gate(s), s.LI, in(s), s.t1.p, s.err.p + s.p, d->st);          // y_I
     }
     // interface y (halo); the fused separator step's sentinel fills ride on the gathers

@@ -240,8 +240,11 @@ struct DevCsr {
 
 // wavefront division modes: unit diagonal, IEEE division, reciprocal + FMA
 // corrections (both RN(acc/d)), multiply by the reciprocal (gg_set_division
-// GG_DIV_RCP: RN(acc * RN(1/d)), tolerance parity)
-enum WaveDiv { WD_UNIT = 0, WD_HW = 1, WD_RCP = 2, WD_MUL = 3 };
+// GG_DIV_RCP: RN(acc * RN(1/d)), tolerance parity); gg_set_division GG_DIV_FMA
+// on an unskewed 2D grid: the row as two fused multiply-adds, in-line term
+// first -- unit (WD_UFMA) or with the coefficients and b pre-scaled by RN(1/d)
+// (WD_SFMA), tolerance parity
+enum WaveDiv { WD_UNIT = 0, WD_HW = 1, WD_RCP = 2, WD_MUL = 3, WD_UFMA = 4, WD_SFMA = 5 };
 
 // device triangular solve
 struct DevTri {
@@ -261,6 +264,7 @@ struct DevTri {
     // WAVE2D (layout arrays, length P)
     Wave2D wl;
     DBuf<double> c1, c2, dw, rw; // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor, rw: RN(1/dw)
+    DBuf<double> c1s, c2s;       // WD_SFMA: RN(c1 * rw), RN(c2 * rw)
     DBuf<double> c0;             // 3D: |offset| = nx*ny coefficient
     DBuf<double> ce1, ce2;       // skew 2/3 (ILU(1)/(2) fill): |offset| = nx-1, nx-2 coefficients
     DBuf<unsigned long long> prog;   // 3D: per (plane, band) batches stored (0 between launches)
@@ -269,14 +273,19 @@ struct DevTri {
     int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
     bool rcp_ok = false;         // every divisor admits WD_RCP
     bool mul_ok = false;         // every 1/d is finite and normal (WD_MUL admissible; rw uploaded)
-    bool fast = false;           // the owner asked for WD_MUL (gg_set_division)
+    bool fma_ok = false;         // unskewed 2D grid, canonical order, unit or mul_ok (c1s / c2s uploaded)
+    int fast = 0;                // the owner's gg_set_division mode (GG_DIV_RCP: WD_MUL, GG_DIV_FMA: WD_*FMA)
     bool prefilled = false;      // LEVEL, per launch: x already holds the sentinel (flow kernel)
-    int eff_div() const { return (fast && mul_ok && div != WD_UNIT) ? (int)WD_MUL : div; }
+    int eff_div() const
+    {
+        if (fast == 2 && fma_ok) return div == WD_UNIT ? (int)WD_UFMA : (int)WD_SFMA;
+        return (fast && mul_ok && div != WD_UNIT) ? (int)WD_MUL : div;
+    }
     DBuf<unsigned long long> bnd;  // nbands * T hand-off granules (sentinel = not ready) + 128 dummies
     long long *trace = nullptr;  // diagnostics: per band, nbatch+1 timestamps (gg_trace_precond)
     double bytes = 0;            // algorithmic bytes per solve
     double bytes_mul = 0;        // the same with WD_MUL (y streamed in place of d (, y))
-    double alg_bytes() const { return eff_div() == WD_MUL ? bytes_mul : bytes; }
+    double alg_bytes() const { const int e = eff_div(); return (e == WD_MUL || e == WD_SFMA) ? bytes_mul : bytes; }
 };
 
 // device triangle from a canonical one: WAVE2D when `wl` is an active grid

@@ -803,10 +803,10 @@ struct WaveCfg {
     // streamed arrays: b, c1, c2 (, d (, RN(1/d))); a skewed 2D grid (ILU(S-1))
     // adds the fill coefficients of offsets nx-1 .. nx-S+1; a 3D grid adds the
     // plane coefficient c0 and the previous plane's x
-    static constexpr int AE = DIV == WD_UNIT ? 3 : DIV == WD_RCP ? 5 : 4;   // first fill array (WD_MUL streams y as d)
+    static constexpr int AE = (DIV == WD_UNIT || DIV == WD_UFMA) ? 3 : DIV == WD_RCP ? 5 : 4;   // first fill array (WD_MUL / WD_SFMA stream y as d)
     static constexpr int A2 = AE + (S - 1);
     static constexpr int A = A2 + (D3 ? 2 : 0);
-    static constexpr int B16 = DIV == WD_UNIT ? GG_WAVE_BATCH_UNIT
+    static constexpr int B16 = (DIV == WD_UNIT || DIV == WD_UFMA) ? GG_WAVE_BATCH_UNIT
                              : DIV == WD_RCP  ? GG_WAVE_BATCH_RCP
                                               : GG_WAVE_BATCH_HW;
     // steps per batch: 8 where 16-step slots of A arrays would not leave room for 3 slots
@@ -929,6 +929,8 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 {
     using C = WaveCfg<DIV, D3, S>;
     static_assert(!IL || (S == 1 && !D3), "in-line-first rows: unskewed 2D grids");
+    constexpr bool FM = DIV == WD_UFMA || DIV == WD_SFMA;     // GG_DIV_FMA rows
+    static_assert(!FM || (S == 1 && !D3 && !IL), "fused rows: unskewed 2D grids, canonical order");
     static_assert(!(TRACE && S > 1), "no trace for skewed grids");
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
     static_assert(!(D3 && TRACE), "no trace for 3D grids");
@@ -1234,7 +1236,16 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 const double e1 = sx ? rg[kk][1].x : rg[kk][1].y;
                 const double e2 = sx ? rg[kk][2].x : rg[kk][2].y;
                 const double old = h ? bv[kk].y : bv[kk].x;
-                const double p2 = e2 * xp;
+                const double p2 = FM ? 0.0 : e2 * xp;
+                // GG_DIV_FMA: the in-line term first, fused, while the line
+                // value crosses lanes; b pre-scaled by y = RN(1/d) for U (the
+                // coefficients arrive pre-scaled), off the recurrence
+                double tf = 0.0;
+                if constexpr (FM) {
+                    double by = bb;
+                    if constexpr (DIV == WD_SFMA) by = bb * (sx ? rg[kk][3].x : rg[kk][3].y);
+                    tf = __builtin_fma(-e2, xp, by);
+                }
                 // 3D: the plane neighbour comes first in the canonical order
                 // (|offset| = nx*ny); its term is off the recurrence
                 double bz = bb;
@@ -1263,7 +1274,9 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 // the neighbour line's terms oldest first (|offset| = nx, nx-1, ..),
                 // then the in-line neighbour (|offset| = 1)
                 double acc;
-                if constexpr (IL) {
+                if constexpr (FM) {
+                    acc = __builtin_fma(-e1, xs, tf);
+                } else if constexpr (IL) {
                     acc = bz - p2;
                     acc = acc - e1 * xs;
                 } else if constexpr (S == 1) {
@@ -1281,7 +1294,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 }
                 if constexpr (S >= 3) xh2 = xh1;
                 if constexpr (S >= 2) xh1 = xs;
-                if constexpr (!IL) acc = acc - p2;
+                if constexpr (!IL && !FM) acc = acc - p2;
                 if constexpr (DIV == WD_HW) {
                     acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
                 } else if constexpr (DIV == WD_MUL) {
@@ -3137,6 +3150,8 @@ int wave_batch_steps(int div, bool d3, int skew)
     if (skew == 3)
         return div == WD_UNIT ? WaveCfg<WD_UNIT, false, 3>::B : hw ? WaveCfg<WD_HW, false, 3>::B
                                                                    : WaveCfg<WD_RCP, false, 3>::B;
+    if (div == WD_UFMA) return WaveCfg<WD_UFMA>::B;
+    if (div == WD_SFMA) return WaveCfg<WD_SFMA>::B;
     return div == WD_UNIT ? WaveCfg<WD_UNIT>::B : hw ? WaveCfg<WD_HW>::B : WaveCfg<WD_RCP>::B;
 }
 
@@ -3185,10 +3200,25 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
     } else if (T.kind == DevTri::WAVE2D) {
         const Wave2D &w = T.wl;
         const int div = T.eff_div();
-        // WD_MUL streams y = RN(1/d) in d's place
-        const double *dv = div == WD_UNIT ? nullptr : div == WD_MUL ? T.rw.p : T.dw.p;
+        // WD_MUL / WD_SFMA stream y = RN(1/d) in d's place
+        const double *dv = (div == WD_UNIT || div == WD_UFMA) ? nullptr
+                         : (div == WD_MUL || div == WD_SFMA) ? T.rw.p : T.dw.p;
         const double *rv = div == WD_RCP ? T.rw.p : nullptr;
-        if (w.tile) {
+        if (div == WD_UFMA || div == WD_SFMA) {
+            // GG_DIV_FMA (build_tri admits unskewed 2D grids in canonical order only)
+            dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
+            const double *k1 = div == WD_SFMA ? T.c1s.p : T.c1.p, *k2 = div == WD_SFMA ? T.c2s.p : T.c2.p;
+            if (T.lower && div == WD_UFMA)
+                k_trsv_wave2d<true, WD_UFMA, false><<<grid, WaveCfg<WD_UFMA>::THREADS, 0, st>>>(
+                    g, w.T, w.nbands, b, k1, k2, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr, nullptr,
+                    nullptr, nullptr);
+            else if (!T.lower && div == WD_SFMA)
+                k_trsv_wave2d<false, WD_SFMA, false><<<grid, WaveCfg<WD_SFMA>::THREADS, 0, st>>>(
+                    g, w.T, w.nbands, b, k1, k2, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr, nullptr,
+                    nullptr, nullptr);
+            else
+                std::abort();   // build_tri: the unit L or the non-unit U only
+        } else if (w.tile) {
             // 3D tiles: persistent, every workgroup co-resident (tiles wait on tiles)
             const int ntask = w.nbands;
 #define GG_TILE_LAUNCH(FWD, DIV)                                                                   \

@@ -190,6 +190,18 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
             if (T.rcp_ok || T.mul_ok) T.rw.upload(rv, st);
             T.div = T.rcp_ok ? WD_RCP : WD_HW;
         }
+        // GG_DIV_FMA: unskewed 2D grids in the canonical row order (the line
+        // term, then the in-line term), the unit L or a U whose 1/d are normal
+        T.fma_ok = !d3 && K == 0 && !T.il && (C.lower ? unit : (!unit && mul_ok));
+        if (T.fma_ok && !unit) {
+            std::vector<double> s1(Ppad, 0.0), s2(Ppad, 0.0);
+            for (long long p = 0; p < Ppad; p++) {
+                s1[p] = c1[p] * rv[p];
+                s2[p] = c2[p] * rv[p];
+            }
+            T.c1s.upload(s1, st);
+            T.c2s.upload(s2, st);
+        }
         // one hand-off granule per band (tile) and step, then per workgroup 64
         // zero granules (dummy reads) and 64 write-only ones (dummy re-arms),
         // for up to kTileDummyBlocks workgroups: one line that every boundary
@@ -458,7 +470,7 @@ void prof_end(gg_solver *s, int mark);
 void trsv(gg_solver *s, Gate g, DevTri &T, int kind, int i, const double *in, double *out)
 {
     const int mk = i >= 0 ? prof_begin(s, kind, i) : -1;
-    T.fast = s->div_mode == GG_DIV_RCP;
+    T.fast = s->div_mode;
     launch_trsv(g, T, in, out, s->err.p, s->st);
     prof_end(s, mk);
 }
@@ -1358,8 +1370,8 @@ int gg_uses_wavefront(gg_solver *s) { return (s && s->wave) ? 1 : 0; }
 int gg_set_division(gg_solver *s, int mode)
 {
     if (!s) return GG_EINVAL;
-    if (mode != GG_DIV_EXACT && mode != GG_DIV_RCP) {
-        set_error("gg_set_division: mode must be GG_DIV_EXACT or GG_DIV_RCP");
+    if (mode != GG_DIV_EXACT && mode != GG_DIV_RCP && mode != GG_DIV_FMA) {
+        set_error("gg_set_division: mode must be GG_DIV_EXACT, GG_DIV_RCP or GG_DIV_FMA");
         return GG_EINVAL;
     }
     s->div_mode = mode;
@@ -1380,7 +1392,7 @@ int gg_trsv_kernel(gg_solver *s, int which, char *name, int cap)
 {
     if (!s || (which != 0 && which != 1) || !name || cap <= 0) return GG_EINVAL;
     DevTri &T = which == 0 ? s->L : s->U;
-    T.fast = s->div_mode == GG_DIV_RCP;
+    T.fast = s->div_mode;
     std::string k;
     if (T.kind == DevTri::WAVE2D) {
         const char *fwd = T.lower ? "true" : "false";
@@ -1402,8 +1414,10 @@ int gg_division_active(gg_solver *s, int which)
 {
     if (!s || (which != 0 && which != 1)) return GG_EINVAL;
     DevTri &T = which == 0 ? s->L : s->U;
-    T.fast = s->div_mode == GG_DIV_RCP;
-    return (T.kind == DevTri::WAVE2D && T.eff_div() == WD_MUL) ? GG_DIV_RCP : GG_DIV_EXACT;
+    T.fast = s->div_mode;
+    if (T.kind != DevTri::WAVE2D) return GG_DIV_EXACT;
+    const int e = T.eff_div();
+    return e == WD_MUL ? GG_DIV_RCP : (e == WD_UFMA || e == WD_SFMA) ? GG_DIV_FMA : GG_DIV_EXACT;
 }
 int gg_spmv_sliced(gg_solver *s) { return (s && s->dA.sell) ? 1 : 0; }
 
@@ -1824,7 +1838,7 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     GG_HIP(hipMemsetAsync(s->err.p, 0, sizeof(int), s->st));
     T.trace = buf.p;
     Gate none;
-    T.fast = s->div_mode == GG_DIV_RCP;
+    T.fast = s->div_mode;
     launch_trsv(none, T, s->bv.p, s->t1.p, s->err.p, s->st);
     T.trace = nullptr;
     GG_HIP(hipMemcpyAsync(out, buf.p, need * sizeof(long long), hipMemcpyDeviceToHost, s->st));
@@ -1870,14 +1884,14 @@ double gg_bytes_spmv(gg_solver *s)
 double gg_bytes_precond(gg_solver *s)
 {
     if (!s || s->pkind < 0) return 0.0;
-    s->L.fast = s->U.fast = s->div_mode == GG_DIV_RCP;
+    s->L.fast = s->U.fast = s->div_mode;
     return s->L.alg_bytes() + s->U.alg_bytes();
 }
 
 double gg_bytes_trsv(gg_solver *s, int which)
 {
     if (!s || s->pkind < 0 || (which != 0 && which != 1)) return 0.0;
-    s->L.fast = s->U.fast = s->div_mode == GG_DIV_RCP;
+    s->L.fast = s->U.fast = s->div_mode;
     return which == 0 ? s->L.alg_bytes() : s->U.alg_bytes();
 }
 

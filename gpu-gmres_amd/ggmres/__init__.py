@@ -37,7 +37,7 @@ EXPORTS = [
 # gg_precond_fn: int (*)(void *ctx, int op, const float *in, float *out, int n), device arrays
 PRECOND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_int)
-DIV_EXACT, DIV_RCP = 0, 1     # gg_div_mode
+DIV_EXACT, DIV_RCP, DIV_FMA = 0, 1, 2     # gg_div_mode
 SRC_DC, SRC_PULSE, SRC_PWL = 0, 1, 2          # gg_src_kind
 PROF_SPMV, PROF_PRECOND, PROF_MGS, PROF_TRSV_L, PROF_TRSV_U = range(5)
 PROF_NKINDS = 5
@@ -242,8 +242,10 @@ class Solver:
         _check(lib().gg_set_precond_user(self.h, 1 if split else 0, self._ufn, None))
 
     def set_division(self, mode):
-        """DIV_EXACT (x = RN(acc/d), the default) or DIV_RCP (x = RN(acc * RN(1/d))
-        on the wavefront triangular solves, tolerance parity) -- ggmres.h"""
+        """DIV_EXACT (x = RN(acc/d), the default), DIV_RCP (x = RN(acc * RN(1/d))
+        on the wavefront triangular solves) or DIV_FMA (rows as two fused
+        multiply-adds, U pre-scaled by RN(1/d), on unskewed 2D-grid wavefronts;
+        DIV_RCP elsewhere); both tolerance parity -- ggmres.h"""
         _check(lib().gg_set_division(self.h, int(mode)))
 
     def division_active(self, which):

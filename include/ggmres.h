@@ -183,12 +183,24 @@ int gg_precond_kind(gg_solver *s);
  *                           five-operation correctly rounded quotient, and one
  *                           streamed array fewer.  Tolerance parity (north_star
  *                           1e-10 on the residual history); the dataflow solve
- *                           of other sparsity keeps dividing.
+ *                           of other sparsity keeps dividing;
+ *   GG_DIV_FMA              on an unskewed 2D-grid wavefront (ILU(0) of a
+ *                           5-point grid) every row is two fused multiply-adds,
+ *                           in-line term first: x = fma(-c_l, x_l, fma(-c_i, x_i,
+ *                           b)) for the unit L, and with c and b pre-scaled by
+ *                           y = RN(1/d) (c' = RN(c*y), RN(b*y)) for U -- one
+ *                           dependent FMA after the cross-lane move per step
+ *                           instead of multiply, two subtractions and the
+ *                           multiply by y.  A few ulps per row; tolerance parity
+ *                           as GG_DIV_RCP, which the other wavefront solves fall
+ *                           back to.
  * Applies to every later solve / apply of this solver. */
-enum gg_div_mode { GG_DIV_EXACT = 0, GG_DIV_RCP = 1 };
+enum gg_div_mode { GG_DIV_EXACT = 0, GG_DIV_RCP = 1, GG_DIV_FMA = 2 };
 int gg_set_division(gg_solver *s, int mode);
 /* the division the last-set mode gives triangle `which` (0 = L / Ml, 1 = U /
- * Mr): GG_DIV_RCP only on a non-unit wavefront triangle whose 1/d are normal */
+ * Mr): GG_DIV_RCP only on a non-unit wavefront triangle whose 1/d are normal,
+ * GG_DIV_FMA only on an unskewed 2D-grid wavefront triangle (the unit L, or a
+ * non-unit U whose 1/d are normal) */
 int gg_division_active(gg_solver *s, int which);
 /* the kernel (rocprofv3 name) that runs triangle `which` (0 = L / Ml, 1 = U /
  * Mr) under the current division mode, into name[cap]; returns its length

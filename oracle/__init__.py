@@ -218,10 +218,12 @@ def set_dot_order_shards(segments, G):
 
 
 def set_div_mode(mul_l=False, mul_u=False):
-    """Division of the non-unit triangles: False = x / d (the reference), True =
-    x * (1.0 / d) (the device's GG_DIV_RCP on a wavefront triangle); for
+    """Division of the non-unit triangles: False / 0 = x / d (the reference),
+    True / 1 = x * (1.0 / d) (the device's GG_DIV_RCP on a wavefront triangle),
+    2 = the device's GG_DIV_FMA rows (lusolve only: b and the coefficients
+    pre-scaled by 1.0 / d, the nearest term first, fused multiply-adds); for
     order-matched checks only -- reset with set_div_mode()."""
-    lib().orc_set_div_mode(int(bool(mul_l)), int(bool(mul_u)))
+    lib().orc_set_div_mode(int(mul_l), int(mul_u))
 
 
 def set_orth(cgs2=False):

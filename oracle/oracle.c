@@ -329,12 +329,16 @@ int orc_iluk(int lofM, int n, const int *rp, const int *ci, const double *v,
 /* Division mode of the non-unit triangles (the device's gg_set_division):
  * 0 = x / d as the reference; 1 = x * (1.0 / d), the device's WD_MUL
  * (x = RN(acc * RN(1/d))), per triangle (L = the lower / Ml one, U = the upper
- * / Mr one).  Only for order-matched checks of GG_DIV_RCP solves. */
+ * / Mr one).  Only for order-matched checks of GG_DIV_RCP solves.
+ * 2 = the device's GG_DIV_FMA rows (kernels.hip WD_UFMA / WD_SFMA; orc_lusolve
+ * only): with y = RN(1/d) (y = 1 for the unit L), acc = RN(b*y) (b for the
+ * unit L), then for the off-diagonal terms nearest first (|i - col|
+ * ascending) acc = fma(-RN(c*y), x[col], acc) (c for the unit L). */
 static int g_mul_l = 0, g_mul_u = 0;
 void orc_set_div_mode(int mul_l, int mul_u)
 {
-    g_mul_l = mul_l != 0;
-    g_mul_u = mul_u != 0;
+    g_mul_l = mul_l < 0 ? 0 : mul_l > 2 ? 2 : mul_l;
+    g_mul_u = mul_u < 0 ? 0 : mul_u > 2 ? 2 : mul_u;
 }
 static double divide(double a, double d, int mul) { return mul ? a * (1.0 / d) : a / d; }
 
@@ -347,6 +351,14 @@ void orc_lusolve(int n, const int *l_rp, const int *l_ci, const double *l_v,
     double *w = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
     memcpy(w, y, (size_t)n * sizeof(double));
     for (int i = 0; i < n; i++) {
+        if (g_mul_l == 2) {         /* GG_DIV_FMA: nearest term first, fused */
+            int j = l_rp[i];
+            while (j < l_rp[i + 1] && l_ci[j] < i) j++;
+            double acc = w[i];
+            for (j--; j >= l_rp[i]; j--) acc = fma(-l_v[j], w[l_ci[j]], acc);
+            w[i] = acc;
+            continue;
+        }
         for (int j = l_rp[i]; j < l_rp[i + 1]; j++) {
             if (l_ci[j] >= i) break;
             w[i] -= l_v[j] * w[l_ci[j]];
@@ -354,6 +366,17 @@ void orc_lusolve(int n, const int *l_rp, const int *l_ci, const double *l_v,
     }
     memcpy(x, w, (size_t)n * sizeof(double));
     for (int i = n - 1; i >= 0; i--) {
+        if (g_mul_u == 2) {         /* GG_DIV_FMA: pre-scaled by RN(1/d), nearest term first */
+            int j = u_rp[i];
+            while (j < u_rp[i + 1] && u_ci[j] < i) j++;
+            double yd = 1.0;
+            if (j < u_rp[i + 1] && u_ci[j] == i && !is_zero(u_v[j])) yd = 1.0 / u_v[j];
+            if (j < u_rp[i + 1] && u_ci[j] == i) j++;
+            double acc = x[i] * yd;
+            for (; j < u_rp[i + 1]; j++) acc = fma(-(u_v[j] * yd), x[u_ci[j]], acc);
+            x[i] = acc;
+            continue;
+        }
         int lb = u_rp[i], j = u_rp[i + 1] - 1;
         for (; j >= lb; j--) {
             if (u_ci[j] <= i) break;

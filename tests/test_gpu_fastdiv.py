@@ -201,3 +201,156 @@ def test_rcp_c4_first_iterations(solver):
     g = solver.solve(b, restart=30, max_iter=12, tol=1e-300)
     check_exact(g, ot)
     check_tol(g, o)
+
+
+# ---------------------------------------------------------------- GG_DIV_FMA
+# The unskewed 2D-grid wavefront solves as two fused multiply-adds per row (the
+# in-line term first; U's b and coefficients pre-scaled by RN(1/d), kernels.hip
+# WD_UFMA / WD_SFMA), restated by oracle.set_div_mode(2, 2).  The other
+# wavefront solves (3D tiles, skewed ILU(k) grids, the split engine's
+# in-line-first U and non-unit L) fall back to GG_DIV_RCP's multiply.  Bars as
+# above: bit-exact vs the order-matched restatement, within 1e-10 of the serial
+# oracle with the reference's arithmetic.
+@pytest.fixture(scope="module")
+def fsolver():
+    s = ggmres.Solver(0)
+    s.set_division(ggmres.DIV_FMA)
+    yield s
+    s.close()
+
+
+def modes(s):
+    """per-triangle oracle mode (0 divide, 1 multiply, 2 fused) of the active solve"""
+    m = {ggmres.DIV_EXACT: 0, ggmres.DIV_RCP: 1, ggmres.DIV_FMA: 2}
+    return m[s.division_active(0)], m[s.division_active(1)]
+
+
+FMA_2D = [k for k in sorted(GRIDS) if "7pt" not in k]
+
+
+@pytest.mark.parametrize("name", FMA_2D)
+@pytest.mark.parametrize("scale", [1.0, 1e-250, 1e250])
+def test_fma_apply(fsolver, name, scale):
+    make, nx, ny = GRIDS[name]
+    A = make()
+    L, U = O.ilu0(A)
+    y = np.random.default_rng(3).standard_normal(A.shape[0]) * scale
+    fsolver.set_matrix(A)
+    fsolver.set_precond_ilu0()
+    assert fsolver.uses_wavefront
+    assert modes(fsolver) == (2, 2)
+    assert "k_trsv_wave2d<true, 4," in fsolver.trsv_kernel(0)
+    assert "k_trsv_wave2d<false, 5," in fsolver.trsv_kernel(1)
+    z = fsolver.precond_apply(ggmres.APPLY_MINV, y)
+    O.set_div_mode(2, 2)
+    try:
+        zm = O.lusolve(L, U, y)
+    finally:
+        O.set_div_mode()
+    assert np.array_equal(z, zm)
+    ze = O.lusolve(L, U, y)
+    assert rel_err(z / scale, ze / scale) <= 1e-12
+
+
+def test_fma_fallbacks(fsolver):
+    """3D tiles, skewed ILU(1) grids and other sparsity: GG_DIV_RCP / the division"""
+    A = M.grid_7pt(12)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_ilu0()
+    assert modes(fsolver) == (0, 1)
+    A = M.laplacian_5pt(100, 70)
+    L, U = O.iluk(A, 1)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_iluk(1)
+    assert fsolver.uses_wavefront and modes(fsolver) == (0, 1)
+    y = np.random.default_rng(7).standard_normal(A.shape[0])
+    O.set_div_mode(0, 1)
+    try:
+        zm = O.lusolve(L, U, y)
+    finally:
+        O.set_div_mode()
+    assert np.array_equal(fsolver.precond_apply(ggmres.APPLY_MINV, y), zm)
+    A = M.power_law(3000, 33000, seed=7)
+    L, U = O.ilu0(A)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_ilu0()
+    assert not fsolver.uses_wavefront and modes(fsolver) == (0, 0)
+    y = np.random.default_rng(2).standard_normal(3000)
+    assert np.array_equal(fsolver.precond_apply(ggmres.APPLY_MINV, y), O.lusolve(L, U, y))
+
+
+@pytest.mark.parametrize("name", sorted(GRIDS))
+@pytest.mark.parametrize("rhs", ["ones", "uniform"])
+def test_fma_gmres_parity(fsolver, name, rhs):
+    make, nx, ny = GRIDS[name]
+    A = make()
+    n = A.shape[0]
+    b = M.rhs_ones(A) if rhs == "ones" else M.rhs_uniform(n)
+    L, U = O.ilu0(A)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_ilu0()
+    md = modes(fsolver)
+    assert md == ((0, 1) if "7pt" in name else (2, 2))
+    o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=3000, tol=1e-10), n, nx, ny, mul=md)
+    g = fsolver.solve(b, restart=30, max_iter=3000, tol=1e-10)
+    check_exact(g, ot)
+    check_tol(g, o)
+
+
+def test_fma_split_parity(fsolver):
+    """the split engine's triangles are not admitted: GG_DIV_RCP's multiply"""
+    A = M.laplacian_5pt(40)
+    P = make_split(A, seed=9)
+    b = M.rhs_uniform(A.shape[0])
+    x0 = np.random.default_rng(3).random(A.shape[0]) * 0.1
+    fsolver.set_matrix(A)
+    fsolver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    md = modes(fsolver)
+    assert 2 not in md
+    o, ot = oracle_mul(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
+                       A.shape[0], mul=md)
+    g = fsolver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
+    check_exact(g, ot)
+    check_tol(g, o)
+
+
+@pytest.mark.slow
+def test_fma_c2_first_cycle(fsolver):
+    """C2 (1000 x 1000, ILU(0), GMRES(30)): the first restart cycle"""
+    A = M.laplacian_5pt(1000)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    L, U = O.ilu0(A)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_ilu0()
+    assert modes(fsolver) == (2, 2)
+    o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=30, tol=1e-300), n, 1000,
+                       mul=(2, 2))
+    g = fsolver.solve(b, restart=30, max_iter=30, tol=1e-300)
+    assert g["iters"] == 30 and g["ret"] == 1
+    check_exact(g, ot)
+    check_tol(g, o)
+
+
+@pytest.mark.slow
+def test_fma_c2_full_solve_tolerance(fsolver):
+    """C2 solved to 1e-8 (the bench's tolerance): same return code, iteration
+    counts within 1 % of the serial oracle's divide-mode solve is not asserted
+    (the serial oracle takes minutes at this size); instead the device's
+    GG_DIV_FMA solve is compared with its own GG_DIV_EXACT solve: same
+    convergence, histories within 1e-10 over the first 300 iterations"""
+    A = M.laplacian_5pt(1000)
+    b = M.rhs_ones(A)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_ilu0()
+    g = fsolver.solve(b, restart=30, max_iter=20000, tol=1e-8)
+    fsolver.set_division(ggmres.DIV_EXACT)
+    try:
+        e = fsolver.solve(b, restart=30, max_iter=20000, tol=1e-8)
+    finally:
+        fsolver.set_division(ggmres.DIV_FMA)
+    assert g["ret"] == e["ret"] == 0
+    assert abs(g["iters"] - e["iters"]) <= 0.01 * e["iters"]
+    h, he = np.asarray(g["hist"])[:300], np.asarray(e["hist"])[:300]
+    assert np.max(np.abs(h - he)) <= HIST_RTOL * np.max(np.abs(he))
+    assert rel_err(g["x"], e["x"]) <= 1e-6      # both stop at relres 1e-8

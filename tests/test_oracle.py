@@ -374,3 +374,18 @@ def test_div_mode_restatement_within_ulps():
         O.set_div_mode()
     assert not np.array_equal(z, ref)          # it is a different rounding ...
     assert rel_err(z, ref) <= 1e-14            # ... within a few ulps
+
+
+def test_fma_oracle_differs_from_divide():
+    """the restatement is a different rounding, not the reference's bits (so the
+    bit-exact checks above do test the fused rows)"""
+    A = M.laplacian_5pt(64)
+    L, U = O.ilu0(A)
+    y = np.random.default_rng(11).standard_normal(A.shape[0])
+    O.set_div_mode(2, 2)
+    try:
+        zf = O.lusolve(L, U, y)
+    finally:
+        O.set_div_mode()
+    ze = O.lusolve(L, U, y)
+    assert not np.array_equal(zf, ze) and rel_err(zf, ze) <= 1e-13

@@ -80,6 +80,10 @@ __global__ void k_probe(const double *in, double *out, long long *cyc)
                 x = __builtin_fma(-__builtin_fma(q1, a, -acc), c, q1); })
     // the wavefront U step with GG_DIV_RCP (k_trsv_wave2d WD_MUL): DPP, mul, two subs, one mul
     TIMED(23, x = ((c - b * dpp_old<0x130>(x, d)) - d * x) * a)
+    // GG_DIV_FMA (k_trsv_wave2d WD_UFMA / WD_SFMA): in-line term fused first, then
+    // the line term fused after the DPP move (U: b and coefficients pre-scaled)
+    TIMED(24, x = __builtin_fma(-b, dpp_old<0x138>(x, d), __builtin_fma(-d, x, c)))
+    TIMED(25, x = __builtin_fma(-b, dpp_old<0x130>(x, d), __builtin_fma(-d, x, c * a)))
 }
 
 // shader clock vs the constant 100 MHz real-time counter over a long chain
@@ -131,7 +135,7 @@ int main()
     double h[256];
     for (int i = 0; i < 256; i++) h[i] = 1.0 + 1e-3 * i;
     double *din, *dout;
-    long long *dc, hc[32] = {0};   // 24 probes
+    long long *dc, hc[32] = {0};   // 26 probes
     hipMalloc(&din, sizeof h);
     hipMalloc(&dout, 32 * 64 * sizeof(double));
     hipMalloc(&dc, sizeof hc);
@@ -142,8 +146,9 @@ int main()
                            "dpp only", "step+div", "step+markstein", "add x2 indep", "rcp",
                            "row_shr:1", "row_bcast:15", "quad_perm", "step(row_shr)", "wave_ror:1",
                            "row_shr+add", "shfl_up+add", "U step (WD_RCP)",
-                           "wave_shr sel", "step(wave_shr sel)", "U step (sel)", "U step (WD_MUL)"};
-    for (int i = 0; i < 24; i++) printf("%-16s %7.2f cycles/iter\n", names[i], (double)hc[i] / N);
+                           "wave_shr sel", "step(wave_shr sel)", "U step (sel)", "U step (WD_MUL)",
+                           "L step (UFMA)", "U step (SFMA)"};
+    for (int i = 0; i < 26; i++) printf("%-16s %7.2f cycles/iter\n", names[i], (double)hc[i] / N);
     for (int nw : {1, 5, 7}) {
         for (int mode = 0; mode < 3; mode++) {
             for (int rep = 0; rep < 3; rep++) {
