@@ -327,9 +327,7 @@ def bench_dd(a, torch, dist, world, rank, local):
         ranks = 1
     d.set_system(A, host.PART_BLOCKS | (host.PART_COLOR_SEP if a.dd_sep == "color" else 0))
     import ggmres
-    # the sharded solve multiplies by RN(1/d) at most (gg_dd_set_division has no
-    # GG_DIV_FMA: its restatement, oracle/dd.py, has no fused rows)
-    dd_div = "rcp" if a.division == "fma" else a.division
+    dd_div = a.division
     d.set_division(DIV_MODES[dd_div])
     t_setup = time.perf_counter() - t_setup
     info = d.info()

@@ -1073,8 +1073,8 @@ int gg_dd_set_division(gg_dd *d, int mode)
 {
     GG_API_BEGIN
     GG_REQUIRE(d, GG_EINVAL, "null argument");
-    GG_REQUIRE(mode == GG_DIV_EXACT || mode == GG_DIV_RCP, GG_EINVAL,
-               "gg_dd_set_division: mode must be GG_DIV_EXACT or GG_DIV_RCP");
+    GG_REQUIRE(mode == GG_DIV_EXACT || mode == GG_DIV_RCP || mode == GG_DIV_FMA, GG_EINVAL,
+               "gg_dd_set_division: mode must be GG_DIV_EXACT, GG_DIV_RCP or GG_DIV_FMA");
     d->div_mode = mode;
     return GG_OK;
     GG_API_END

@@ -264,7 +264,7 @@ struct DevTri {
     // WAVE2D (layout arrays, length P)
     Wave2D wl;
     DBuf<double> c1, c2, dw, rw; // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor, rw: RN(1/dw)
-    DBuf<double> c1s, c2s;       // WD_SFMA: RN(c1 * rw), RN(c2 * rw)
+    DBuf<double> c1s, c2s, c0s;  // WD_SFMA: RN(c1 * rw), RN(c2 * rw) (3D tiles: RN(c0 * rw))
     DBuf<double> c0;             // 3D: |offset| = nx*ny coefficient
     DBuf<double> ce1, ce2;       // skew 2/3 (ILU(1)/(2) fill): |offset| = nx-1, nx-2 coefficients
     DBuf<unsigned long long> prog;   // 3D: per (plane, band) batches stored (0 between launches)
@@ -273,7 +273,7 @@ struct DevTri {
     int div = WD_UNIT;           // division mode (kernels.hip k_trsv_wave2d)
     bool rcp_ok = false;         // every divisor admits WD_RCP
     bool mul_ok = false;         // every 1/d is finite and normal (WD_MUL admissible; rw uploaded)
-    bool fma_ok = false;         // unskewed 2D grid, canonical order, unit or mul_ok (c1s / c2s uploaded)
+    bool fma_ok = false;         // unskewed 2D grid / 3D tiles, canonical order, unit L or mul_ok U (c*s uploaded)
     int fast = 0;                // the owner's gg_set_division mode (GG_DIV_RCP: WD_MUL, GG_DIV_FMA: WD_*FMA)
     bool prefilled = false;      // LEVEL, per launch: x already holds the sentinel (flow kernel)
     int eff_div() const

@@ -1394,7 +1394,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
 #endif
 template <int DIV>
 struct TileCfg {
-    static constexpr int A = DIV == WD_UNIT ? 4 : DIV == WD_RCP ? 6 : 5;   // WD_MUL streams y as d
+    static constexpr int A = (DIV == WD_UNIT || DIV == WD_UFMA) ? 4 : DIV == WD_RCP ? 6 : 5;   // WD_MUL / WD_SFMA stream y as d
     static constexpr int AC0 = A - 1;                   // the plane coefficient streams last
     static constexpr int B = GG_TILE_BATCH;
     static constexpr int PBN = B / 2;
@@ -1782,7 +1782,7 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                 const double oj = h ? bj[kk].y : bj[kk].x;      // boundary entries by sweep step
                 // the plane neighbour: the predecessor plane's value of the previous step
                 const double xz = tt == 0 ? xz0 : plane_move(xp, h ? bk[kk].y : bk[kk].x, tm);
-                const double p2 = e2 * xp;
+                const double p2 = (DIV == WD_UFMA || DIV == WD_SFMA) ? 0.0 : e2 * xp;
                 const double xs = bfi64(tm.lfix, oj, dpp_shift_old<ctrl>(xp, oj));
                 if constexpr (kWaveShadow) {
                     __builtin_amdgcn_sched_barrier(0);
@@ -1797,10 +1797,21 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                // canonical order: plane term, line term, in-line term
-                double acc = bb - e0 * xz;
-                acc = acc - e1 * xs;
-                acc = acc - p2;
+                // canonical order: plane term, line term, in-line term;
+                // GG_DIV_FMA: nearest first, fused (in-line, line, plane: the
+                // order the operands arrive in), b pre-scaled for U
+                double acc;
+                if constexpr (DIV == WD_UFMA || DIV == WD_SFMA) {
+                    double by = bb;
+                    if constexpr (DIV == WD_SFMA) by = bb * (sx ? rg[kk][3].x : rg[kk][3].y);
+                    acc = __builtin_fma(-e2, xp, by);
+                    acc = __builtin_fma(-e1, xs, acc);
+                    acc = __builtin_fma(-e0, xz, acc);
+                } else {
+                    acc = bb - e0 * xz;
+                    acc = acc - e1 * xs;
+                    acc = acc - p2;
+                }
                 if constexpr (DIV == WD_HW) {
                     acc = acc / (sx ? rg[kk][3].x : rg[kk][3].y);
                 } else if constexpr (DIV == WD_MUL) {
@@ -3204,36 +3215,46 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         const double *dv = (div == WD_UNIT || div == WD_UFMA) ? nullptr
                          : (div == WD_MUL || div == WD_SFMA) ? T.rw.p : T.dw.p;
         const double *rv = div == WD_RCP ? T.rw.p : nullptr;
-        if (div == WD_UFMA || div == WD_SFMA) {
-            // GG_DIV_FMA (build_tri admits unskewed 2D grids in canonical order only)
+        if ((div == WD_UFMA || div == WD_SFMA) && !w.tile) {
+            // GG_DIV_FMA on a 2D grid (build_tri admits unskewed ones in canonical order)
             dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
             const double *k1 = div == WD_SFMA ? T.c1s.p : T.c1.p, *k2 = div == WD_SFMA ? T.c2s.p : T.c2.p;
-            if (T.lower && div == WD_UFMA)
-                k_trsv_wave2d<true, WD_UFMA, false><<<grid, WaveCfg<WD_UFMA>::THREADS, 0, st>>>(
-                    g, w.T, w.nbands, b, k1, k2, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr, nullptr,
-                    nullptr, nullptr);
-            else if (!T.lower && div == WD_SFMA)
-                k_trsv_wave2d<false, WD_SFMA, false><<<grid, WaveCfg<WD_SFMA>::THREADS, 0, st>>>(
-                    g, w.T, w.nbands, b, k1, k2, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr, nullptr,
-                    nullptr, nullptr);
-            else
+#define GG_FMA_LAUNCH(FWD, DIV, TR)                                                                \
+    k_trsv_wave2d<FWD, DIV, TR><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                           \
+        g, w.T, w.nbands, b, k1, k2, dv, rv, x, T.bnd.p, err, T.trace, 1, w.P2, nullptr, nullptr,   \
+        nullptr, nullptr)
+            if (T.lower && div == WD_UFMA) {
+                if (T.trace) GG_FMA_LAUNCH(true, WD_UFMA, true);
+                else GG_FMA_LAUNCH(true, WD_UFMA, false);
+            } else if (!T.lower && div == WD_SFMA) {
+                if (T.trace) GG_FMA_LAUNCH(false, WD_SFMA, true);
+                else GG_FMA_LAUNCH(false, WD_SFMA, false);
+            } else
+#undef GG_FMA_LAUNCH
                 std::abort();   // build_tri: the unit L or the non-unit U only
         } else if (w.tile) {
             // 3D tiles: persistent, every workgroup co-resident (tiles wait on tiles)
             const int ntask = w.nbands;
+            const bool sc = div == WD_SFMA;     // GG_DIV_FMA's U: coefficients pre-scaled by RN(1/d)
+            const double *k1 = sc ? T.c1s.p : T.c1.p, *k2 = sc ? T.c2s.p : T.c2.p, *k0 = sc ? T.c0s.p : T.c0.p;
 #define GG_TILE_LAUNCH(FWD, DIV)                                                                   \
     do {                                                                                           \
         const int grid = std::min(std::min(ntask, tile3d_max_blocks<FWD, DIV>()), kTileDummyBlocks);  \
         if (T.trace)                                                                               \
             k_trsv_tile3d<FWD, DIV, true><<<grid, TileCfg<DIV>::THREADS, 0, st>>>(                 \
-                g, w.T, w.NJ, w.NK, T.order.p, b, T.c1.p, T.c2.p, dv, rv, T.c0.p, x, T.bnd.p, err,  \
+                g, w.T, w.NJ, w.NK, T.order.p, b, k1, k2, dv, rv, k0, x, T.bnd.p, err,              \
                 T.trace);                                                                          \
         else                                                                                       \
             k_trsv_tile3d<FWD, DIV><<<grid, TileCfg<DIV>::THREADS, 0, st>>>(                       \
-                g, w.T, w.NJ, w.NK, T.order.p, b, T.c1.p, T.c2.p, dv, rv, T.c0.p, x, T.bnd.p, err,  \
+                g, w.T, w.NJ, w.NK, T.order.p, b, k1, k2, dv, rv, k0, x, T.bnd.p, err,              \
                 nullptr);                                                                          \
     } while (0)
-            if (T.lower) {
+            if (div == WD_UFMA || div == WD_SFMA) {
+                // GG_DIV_FMA (build_tri admits the unit L and a non-unit U)
+                if (T.lower && div == WD_UFMA) GG_TILE_LAUNCH(true, WD_UFMA);
+                else if (!T.lower && div == WD_SFMA) GG_TILE_LAUNCH(false, WD_SFMA);
+                else std::abort();
+            } else if (T.lower) {
                 if (div == WD_UNIT) GG_TILE_LAUNCH(true, WD_UNIT);
                 else if (div == WD_HW) GG_TILE_LAUNCH(true, WD_HW);
                 else if (div == WD_MUL) GG_TILE_LAUNCH(true, WD_MUL);

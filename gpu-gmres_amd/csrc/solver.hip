@@ -190,17 +190,24 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
             if (T.rcp_ok || T.mul_ok) T.rw.upload(rv, st);
             T.div = T.rcp_ok ? WD_RCP : WD_HW;
         }
-        // GG_DIV_FMA: unskewed 2D grids in the canonical row order (the line
-        // term, then the in-line term), the unit L or a U whose 1/d are normal
-        T.fma_ok = !d3 && K == 0 && !T.il && (C.lower ? unit : (!unit && mul_ok));
+        // GG_DIV_FMA: unskewed 2D grids and 3D tiles in the canonical row order
+        // (the plane term, the line term, the in-line term), the unit L or a U
+        // whose 1/d are normal
+        // GG_FMA_TILE (diagnostics, default 3): bit 0 / 1 admits the 3D tiles' L / U
+        const char *ft = std::getenv("GG_FMA_TILE");
+        const int ftm = ft ? atoi(ft) : 3;
+        const bool tile_ok = wl->tile && (ftm & (C.lower ? 1 : 2));
+        T.fma_ok = (!d3 || tile_ok) && K == 0 && !T.il && (C.lower ? unit : (!unit && mul_ok));
         if (T.fma_ok && !unit) {
-            std::vector<double> s1(Ppad, 0.0), s2(Ppad, 0.0);
+            std::vector<double> s1(Ppad, 0.0), s2(Ppad, 0.0), s0(d3 ? Ppad : 0, 0.0);
             for (long long p = 0; p < Ppad; p++) {
                 s1[p] = c1[p] * rv[p];
                 s2[p] = c2[p] * rv[p];
+                if (d3) s0[p] = c0[p] * rv[p];
             }
             T.c1s.upload(s1, st);
             T.c2s.upload(s2, st);
+            if (d3) T.c0s.upload(s0, st);
         }
         // one hand-off granule per band (tile) and step, then per workgroup 64
         // zero granules (dummy reads) and 64 write-only ones (dummy re-arms),

@@ -164,7 +164,7 @@ class DD:
         return y
 
     def set_division(self, mode):
-        """ggmres.DIV_EXACT / DIV_RCP for the shards' wavefront triangular solves"""
+        """ggmres.DIV_EXACT / DIV_RCP / DIV_FMA for the shards' wavefront triangular solves"""
         _check(_lib().gg_dd_set_division(self.h, int(mode)))
 
     def time_exchange(self, cnt, reps=200):

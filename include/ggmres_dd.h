@@ -105,7 +105,9 @@ int gg_dd_get_history(gg_dd *d, double *out, int cap);
 /* single operators (host vectors, natural order) for parity tests */
 int gg_dd_spmv(gg_dd *d, const double *x, double *y);
 int gg_dd_precond_apply(gg_dd *d, const double *in, double *out);
-/* division in the shards' wavefront triangular solves (ggmres.h gg_set_division) */
+/* division in the shards' wavefront triangular solves (ggmres.h gg_set_division:
+ * GG_DIV_FMA fuses the rows of the interiors' unskewed 2D-grid wavefronts, the
+ * other wavefronts multiply as GG_DIV_RCP; the separator's solves divide) */
 int gg_dd_set_division(gg_dd *d, int mode);
 /* average device time (hipEvents on the solver's stream, microseconds) of one
  * all-gather of cnt doubles per shard over this communicator -- the exchange

@@ -208,16 +208,18 @@ def test_dd_cgs2_bitexact_and_tolerance(name):
     assert true < 1e-9, true
 
 
+@pytest.mark.parametrize("mode", ["rcp", "fma"])
 @pytest.mark.parametrize("name", ["5pt_200x160_P2", "7pt_24_P4", "5pt_200x160_P4_color"])
-def test_dd_division_rcp_tolerance(name):
+def test_dd_division_rcp_tolerance(name, mode):
     """gg_dd_set_division(GG_DIV_RCP): the shards' wavefront solves multiply by
-    RN(1/d); the first restart cycle within 1e-10 (north_star) of the serial
-    oracle with the reference's division, the full solve converging in the same
-    number of iterations (MGS and CGS2)."""
+    RN(1/d); GG_DIV_FMA: the 2D interiors' rows are two fused multiply-adds (U
+    pre-scaled by RN(1/d)); the first restart cycle within 1e-10 (north_star) of
+    the serial oracle with the reference's division, the full solve converging
+    in the same number of iterations (MGS and CGS2)."""
     import ggmres
     A, d, q, B, L, U = setup(name)
     b = M.rhs_ones(A)
-    d.set_division(ggmres.DIV_RCP)
+    d.set_division(ggmres.DIV_RCP if mode == "rcp" else ggmres.DIV_FMA)
     try:
         for flags in (0, ggmres.SOLVE_CGS2):
             g1 = d.solve(b, restart=30, max_iter=30, tol=1e-300, flags=flags)

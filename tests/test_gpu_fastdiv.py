@@ -204,13 +204,13 @@ def test_rcp_c4_first_iterations(solver):
 
 
 # ---------------------------------------------------------------- GG_DIV_FMA
-# The unskewed 2D-grid wavefront solves as two fused multiply-adds per row (the
-# in-line term first; U's b and coefficients pre-scaled by RN(1/d), kernels.hip
-# WD_UFMA / WD_SFMA), restated by oracle.set_div_mode(2, 2).  The other
-# wavefront solves (3D tiles, skewed ILU(k) grids, the split engine's
-# in-line-first U and non-unit L) fall back to GG_DIV_RCP's multiply.  Bars as
-# above: bit-exact vs the order-matched restatement, within 1e-10 of the serial
-# oracle with the reference's arithmetic.
+# The unskewed 2D-grid and 3D-tile wavefront solves as fused multiply-adds per
+# row (nearest term first; U's b and coefficients pre-scaled by RN(1/d),
+# kernels.hip WD_UFMA / WD_SFMA), restated by oracle.set_div_mode(2, 2).  The
+# other wavefront solves (skewed ILU(k) grids, the split engine's in-line-first
+# U and non-unit L) fall back to GG_DIV_RCP's multiply.  Bars as above:
+# bit-exact vs the order-matched restatement, within 1e-10 of the serial oracle
+# with the reference's arithmetic.
 @pytest.fixture(scope="module")
 def fsolver():
     s = ggmres.Solver(0)
@@ -225,10 +225,19 @@ def modes(s):
     return m[s.division_active(0)], m[s.division_active(1)]
 
 
-FMA_2D = [k for k in sorted(GRIDS) if "7pt" not in k]
+def fused_expected(s):
+    """(2, 2) where the triangles take the 2D band or the 3D tile kernel"""
+    k0, k1 = s.trsv_kernel(0), s.trsv_kernel(1)
+    if k0.startswith("k_trsv_tile3d"):
+        assert k0.startswith("k_trsv_tile3d<true, 4,") and k1.startswith("k_trsv_tile3d<false, 5,")
+        return True
+    if ", false, 1, false>" in k0:          # unskewed 2D band kernel
+        assert k0.startswith("k_trsv_wave2d<true, 4,") and k1.startswith("k_trsv_wave2d<false, 5,")
+        return True
+    return False
 
 
-@pytest.mark.parametrize("name", FMA_2D)
+@pytest.mark.parametrize("name", sorted(GRIDS))
 @pytest.mark.parametrize("scale", [1.0, 1e-250, 1e250])
 def test_fma_apply(fsolver, name, scale):
     make, nx, ny = GRIDS[name]
@@ -238,9 +247,7 @@ def test_fma_apply(fsolver, name, scale):
     fsolver.set_matrix(A)
     fsolver.set_precond_ilu0()
     assert fsolver.uses_wavefront
-    assert modes(fsolver) == (2, 2)
-    assert "k_trsv_wave2d<true, 4," in fsolver.trsv_kernel(0)
-    assert "k_trsv_wave2d<false, 5," in fsolver.trsv_kernel(1)
+    assert fused_expected(fsolver) and modes(fsolver) == (2, 2)
     z = fsolver.precond_apply(ggmres.APPLY_MINV, y)
     O.set_div_mode(2, 2)
     try:
@@ -253,11 +260,7 @@ def test_fma_apply(fsolver, name, scale):
 
 
 def test_fma_fallbacks(fsolver):
-    """3D tiles, skewed ILU(1) grids and other sparsity: GG_DIV_RCP / the division"""
-    A = M.grid_7pt(12)
-    fsolver.set_matrix(A)
-    fsolver.set_precond_ilu0()
-    assert modes(fsolver) == (0, 1)
+    """skewed ILU(1) grids and other sparsity: GG_DIV_RCP / the division"""
     A = M.laplacian_5pt(100, 70)
     L, U = O.iluk(A, 1)
     fsolver.set_matrix(A)
@@ -290,7 +293,7 @@ def test_fma_gmres_parity(fsolver, name, rhs):
     fsolver.set_matrix(A)
     fsolver.set_precond_ilu0()
     md = modes(fsolver)
-    assert md == ((0, 1) if "7pt" in name else (2, 2))
+    assert fused_expected(fsolver) and md == (2, 2)
     o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=3000, tol=1e-10), n, nx, ny, mul=md)
     g = fsolver.solve(b, restart=30, max_iter=3000, tol=1e-10)
     check_exact(g, ot)
@@ -354,3 +357,20 @@ def test_fma_c2_full_solve_tolerance(fsolver):
     h, he = np.asarray(g["hist"])[:300], np.asarray(e["hist"])[:300]
     assert np.max(np.abs(h - he)) <= HIST_RTOL * np.max(np.abs(he))
     assert rel_err(g["x"], e["x"]) <= 1e-6      # both stop at relres 1e-8
+
+
+@pytest.mark.slow
+def test_fma_c4_first_iterations(fsolver):
+    """C4 (216^3 7-point, 3D tile wavefront): the first 12 inner iterations"""
+    A = M.grid_7pt(216)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    L, U = O.ilu0(A)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_ilu0()
+    assert fused_expected(fsolver) and modes(fsolver) == (2, 2)
+    o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=12, tol=1e-300), n, 216, 216,
+                       mul=(2, 2))
+    g = fsolver.solve(b, restart=30, max_iter=12, tol=1e-300)
+    check_exact(g, ot)
+    check_tol(g, o)

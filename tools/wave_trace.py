@@ -15,11 +15,14 @@ from ggmres import matrices as M        # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--grid", type=int, default=1000)
+ap.add_argument("--division", choices=["exact", "rcp", "fma"], default="fma")
 args = ap.parse_args()
 A = M.laplacian_5pt(args.grid)
 s = G.Solver()
 s.set_matrix(A)
 s.set_precond_ilu0()
+s.set_division({"exact": G.DIV_EXACT, "rcp": G.DIV_RCP, "fma": G.DIV_FMA}[args.division])
+print("division", args.division, "kernels", s.trsv_kernel(0), "/", s.trsv_kernel(1))
 b = np.ones(A.shape[0])
 s.precond_apply(0, b)
 print("precond apply avg ms", s.time_precond(20))
