@@ -930,7 +930,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     using C = WaveCfg<DIV, D3, S>;
     static_assert(!IL || (S == 1 && !D3), "in-line-first rows: unskewed 2D grids");
     constexpr bool FM = DIV == WD_UFMA || DIV == WD_SFMA;     // GG_DIV_FMA rows
-    static_assert(!FM || (S == 1 && !D3 && !IL), "fused rows: unskewed 2D grids, canonical order");
+    static_assert(!FM || (S == 1 && !D3 && !IL), "fused rows: unskewed 2D grids (one order for both IL)");
     static_assert(!(TRACE && S > 1), "no trace for skewed grids");
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
     static_assert(!(D3 && TRACE), "no trace for 3D grids");
@@ -3223,15 +3223,19 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
     k_trsv_wave2d<FWD, DIV, TR><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                           \
         g, w.T, w.nbands, b, k1, k2, dv, rv, x, T.bnd.p, err, T.trace, 1, w.P2, nullptr, nullptr,   \
         nullptr, nullptr)
+            // (T.il needs no instantiation of its own: the fused rows take the
+            // in-line term first in either canonical order)
             if (T.lower && div == WD_UFMA) {
                 if (T.trace) GG_FMA_LAUNCH(true, WD_UFMA, true);
                 else GG_FMA_LAUNCH(true, WD_UFMA, false);
             } else if (!T.lower && div == WD_SFMA) {
                 if (T.trace) GG_FMA_LAUNCH(false, WD_SFMA, true);
                 else GG_FMA_LAUNCH(false, WD_SFMA, false);
+            } else if (T.lower && div == WD_SFMA) {
+                GG_FMA_LAUNCH(true, WD_SFMA, false);      // the split engine's non-unit L
             } else
 #undef GG_FMA_LAUNCH
-                std::abort();   // build_tri: the unit L or the non-unit U only
+                std::abort();   // build_tri: no unit upper triangle
         } else if (w.tile) {
             // 3D tiles: persistent, every workgroup co-resident (tiles wait on tiles)
             const int ntask = w.nbands;

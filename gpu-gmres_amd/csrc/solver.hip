@@ -196,8 +196,11 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         // GG_FMA_TILE (diagnostics, default 3): bit 0 / 1 admits the 3D tiles' L / U
         const char *ft = std::getenv("GG_FMA_TILE");
         const int ftm = ft ? atoi(ft) : 3;
-        const bool tile_ok = wl->tile && (ftm & (C.lower ? 1 : 2));
-        T.fma_ok = (!d3 || tile_ok) && K == 0 && !T.il && (C.lower ? unit : (!unit && mul_ok));
+        const bool tile_ok = wl->tile && (ftm & (C.lower ? 1 : 2)) && (!C.lower || unit);
+        // (the fused rows take the in-line term first whatever the canonical
+        // order, so the split engine's in-line-first U is admitted too, and
+        // its non-unit L as a pre-scaled lower triangle)
+        T.fma_ok = (!d3 || tile_ok) && K == 0 && (unit ? C.lower : mul_ok);
         if (T.fma_ok && !unit) {
             std::vector<double> s1(Ppad, 0.0), s2(Ppad, 0.0), s0(d3 ? Ppad : 0, 0.0);
             for (long long p = 0; p < Ppad; p++) {
@@ -1409,7 +1412,7 @@ int gg_trsv_kernel(gg_solver *s, int which, char *name, int cap)
         else
             k = std::string("k_trsv_wave2d<") + fwd + ", " + std::to_string(div) + ", false, " +
                 (T.wl.nz > 1 ? "true" : "false") + ", " + std::to_string(T.wl.nz > 1 ? 1 : T.wl.skew) + ", " +
-                (T.il ? "true" : "false") + ">";
+                ((T.il && div != WD_UFMA && div != WD_SFMA) ? "true" : "false") + ">";   // fused rows: one order
     } else if (T.kind == DevTri::LEVEL) {
         const char *lv = std::getenv("GG_TRSV_LEVELS");
         k = (lv && atoi(lv) != 0) ? "k_trsv_level" : "k_trsv_flow";

@@ -331,9 +331,9 @@ int orc_iluk(int lofM, int n, const int *rp, const int *ci, const double *v,
  * (x = RN(acc * RN(1/d))), per triangle (L = the lower / Ml one, U = the upper
  * / Mr one).  Only for order-matched checks of GG_DIV_RCP solves.
  * 2 = the device's GG_DIV_FMA rows (kernels.hip WD_UFMA / WD_SFMA; orc_lusolve
- * only): with y = RN(1/d) (y = 1 for the unit L), acc = RN(b*y) (b for the
- * unit L), then for the off-diagonal terms nearest first (|i - col|
- * ascending) acc = fma(-RN(c*y), x[col], acc) (c for the unit L). */
+ * and the split engine's two solves): with y = RN(1/d) (y = 1 for the unit L),
+ * acc = RN(b*y) (b for the unit L), then for the off-diagonal terms nearest
+ * first (|i - col| ascending) acc = fma(-RN(c*y), x[col], acc) (c for the unit L). */
 static int g_mul_l = 0, g_mul_u = 0;
 void orc_set_div_mode(int mul_l, int mul_u)
 {
@@ -397,6 +397,12 @@ void orc_split_left(const orc_split_t *p, const double *in, double *out)
     for (int i = 0; i < n; i++) out[i] = t[p->perm_row[i]];
     for (int i = 0; i < n; i++) {
         int lb = p->l_rp[i], ub = p->l_rp[i + 1];
+        if (g_mul_l == 2) {         /* GG_DIV_FMA: pre-scaled, nearest term first */
+            double yd = 1.0 / p->l_v[ub - 1], acc = out[i] * yd;
+            for (int j = ub - 2; j >= lb; j--) acc = fma(-(p->l_v[j] * yd), out[p->l_ci[j]], acc);
+            out[i] = acc;
+            continue;
+        }
         for (int j = lb; j < ub - 1; j++) out[i] -= p->l_v[j] * out[p->l_ci[j]];
         out[i] = divide(out[i], p->l_v[ub - 1], g_mul_l);
     }
@@ -411,6 +417,12 @@ void orc_split_right(const orc_split_t *p, const double *in, double *out)
     for (int i = 0; i < n; i++) t[i] = in[i] * p->middle[i];
     for (int i = n - 1; i >= 0; i--) {
         int lb = p->u_rp[i], ub = p->u_rp[i + 1];
+        if (g_mul_u == 2) {         /* GG_DIV_FMA: pre-scaled, nearest term first */
+            double yd = 1.0 / p->u_v[lb], acc = t[i] * yd;
+            for (int j = lb + 1; j < ub; j++) acc = fma(-(p->u_v[j] * yd), t[p->u_ci[j]], acc);
+            t[i] = acc;
+            continue;
+        }
         for (int j = lb + 1; j < ub; j++) t[i] -= p->u_v[j] * t[p->u_ci[j]];
         t[i] = divide(t[i], p->u_v[lb], g_mul_u);
     }

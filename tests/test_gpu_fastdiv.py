@@ -300,18 +300,26 @@ def test_fma_gmres_parity(fsolver, name, rhs):
     check_tol(g, o)
 
 
-def test_fma_split_parity(fsolver):
-    """the split engine's triangles are not admitted: GG_DIV_RCP's multiply"""
-    A = M.laplacian_5pt(40)
-    P = make_split(A, seed=9)
+@pytest.mark.parametrize("perm", ["random", "identity"])
+def test_fma_split_parity(fsolver, perm):
+    """GMRESilu_GPU's split engine: with identity permutations both factors are
+    grid-shaped (2D wavefront) and both non-unit: Ml's L pre-scaled as a lower
+    triangle, Mr's in-line-first U as the canonical one (the fused rows take
+    the in-line term first either way); random permutations keep the dataflow
+    kernel and the reference's division"""
+    A = M.laplacian_5pt(48, 40)
+    P = make_split(A, seed=9, identity_perm=perm == "identity")
     b = M.rhs_uniform(A.shape[0])
     x0 = np.random.default_rng(3).random(A.shape[0]) * 0.1
     fsolver.set_matrix(A)
     fsolver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
     md = modes(fsolver)
-    assert 2 not in md
+    assert md == ((2, 2) if perm == "identity" else (0, 0))
+    if perm == "identity":
+        assert fsolver.trsv_kernel(0).startswith("k_trsv_wave2d<true, 5,")
+        assert fsolver.trsv_kernel(1).startswith("k_trsv_wave2d<false, 5,")
     o, ot = oracle_mul(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
-                       A.shape[0], mul=md)
+                       A.shape[0], nx=48 if perm == "identity" else None, mul=md)
     g = fsolver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
     check_exact(g, ot)
     check_tol(g, o)
