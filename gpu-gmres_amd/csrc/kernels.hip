@@ -797,6 +797,10 @@ constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 #ifndef GG_WAVE_XCD
 #define GG_WAVE_XCD 8
 #endif
+// the same placement for the forward solve (1: one workgroup per band)
+#ifndef GG_WAVE_XCD_L
+#define GG_WAVE_XCD_L 1
+#endif
 
 template <int DIV, bool D3 = false, int S = 1>
 struct WaveCfg {
@@ -959,7 +963,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     // Measured on C2: U 121.0 -> 117.9 us, while L (3 streamed arrays) slows
     // 88.9 -> 90.0 us (round 3, re-measured: 89.4 / 90.3 -> 89.9 / 90.4 us), so
     // the forward solve keeps one workgroup per band.
-    constexpr int XS = (D3 || FWD) ? 1 : GG_WAVE_XCD;
+    constexpr int XS = D3 ? 1 : FWD ? GG_WAVE_XCD_L : GG_WAVE_XCD;
     if (XS > 1 && blockIdx.x % XS) return;
     const int blk = blockIdx.x / XS;
     const int ntask = nz * nbands;
@@ -3217,7 +3221,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         const double *rv = div == WD_RCP ? T.rw.p : nullptr;
         if ((div == WD_UFMA || div == WD_SFMA) && !w.tile) {
             // GG_DIV_FMA on a 2D grid (build_tri admits unskewed ones in canonical order)
-            dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
+            dim3 grid(w.nbands * (T.lower ? GG_WAVE_XCD_L : GG_WAVE_XCD));
             const double *k1 = div == WD_SFMA ? T.c1s.p : T.c1.p, *k2 = div == WD_SFMA ? T.c2s.p : T.c2.p;
 #define GG_FMA_LAUNCH(FWD, DIV, TR)                                                                \
     k_trsv_wave2d<FWD, DIV, TR><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                           \
@@ -3271,7 +3275,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
             }
 #undef GG_TILE_LAUNCH
         } else if (w.nz == 1) {
-            dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
+            dim3 grid(w.nbands * (T.lower ? GG_WAVE_XCD_L : GG_WAVE_XCD));
 #define GG_WAVE_LAUNCH_S(FWD, DIV, S, IL)                                                          \
     k_trsv_wave2d<FWD, DIV, false, false, S, IL><<<grid, WaveCfg<DIV, false, S>::THREADS, 0, st>>>( \
         g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr,   \
