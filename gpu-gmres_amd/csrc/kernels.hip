@@ -47,6 +47,24 @@ __device__ __forceinline__ double block_sum(double v)
     return r;
 }
 
+// block_sum with one barrier instead of three, the same bits (the same
+// wave_sum per wave and (0 + 1) + (2 + 3)), every thread forming the sum from
+// the four wave sums itself: the wave sums alternate between two LDS rows
+// (`par`, uniform, flipped per call), so a call's writes never meet the
+// previous call's reads -- between a call and the one after next there is
+// always the barrier of the call in between.
+__device__ __forceinline__ double block_sum_pp(double v, int &par)
+{
+    __shared__ double sh[2][kBlock / 64];
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) sh[par][w] = v;
+    __syncthreads();
+    const double r = (sh[par][0] + sh[par][1]) + (sh[par][2] + sh[par][3]);
+    par ^= 1;
+    return r;
+}
+
 // block_sum of acc[k] for every k < nk at once, stored by thread k at
 // part[k * kstride]: the same wave_sum per wave and (0 + 1) + (2 + 3) as
 // block_sum, so the same bits, with one barrier instead of three per value.
@@ -2552,11 +2570,11 @@ __device__ __forceinline__ unsigned long long poll_granule(const unsigned long l
     return a;
 }
 
-__device__ __forceinline__ double gather_sum(const unsigned long long *row, int G, int *err)
+__device__ __forceinline__ double gather_sum(const unsigned long long *row, int G, int *err, int &par)
 {
     double v = 0.0;
     for (int q = threadIdx.x; q < G; q += kBlock) v += __longlong_as_double((long long)poll_granule(row + q, err));
-    return block_sum(v);
+    return block_sum_pp(v, par);
 }
 
 // The sum of step k's partials as every block needs it.  LEADER: block 0
@@ -2569,10 +2587,10 @@ __device__ __forceinline__ double gather_sum(const unsigned long long *row, int 
 // k_arnoldi_persist (C2) 73.2 -> 77.5 us, so every block gathers there.
 template <bool LEADER>
 __device__ __forceinline__ double gather_h(const unsigned long long *row, unsigned long long *hg, int k, int G,
-                                           int *err)
+                                           int *err, int &par)
 {
     if (!LEADER || blockIdx.x == 0) {
-        const double h = gather_sum(row, G, err);
+        const double h = gather_sum(row, G, err, par);
         if (LEADER && threadIdx.x == 0) st_agent(hg, (unsigned long long)__double_as_longlong(h));
         return h;
     }
@@ -2604,8 +2622,9 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             vk[j] = ld2(V, u);
         }
     }
+    int par = 0;                                              // block_sum_pp's LDS row
     auto publish = [&](int k, double acc) {
-        acc = block_sum(acc);
+        acc = block_sum_pp(acc, par);
         if (threadIdx.x == 0) st_agent(gran + (long long)k * G + blockIdx.x, (unsigned long long)__double_as_longlong(acc));
     };
     double acc = 0.0;
@@ -2623,7 +2642,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             for (int j = 0; j < J; j++)
                 if (u0 + j * stride < units) vn[j] = ld2_nt(vnp, u0 + j * stride);   // streamed
         }
-        const double h = gather_h<false>(gran + (long long)k * G, hg + k, k, G, err);
+        const double h = gather_h<false>(gran + (long long)k * G, hg + k, k, G, err, par);
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         acc = 0.0;
@@ -2640,7 +2659,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(gather_h<false>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err));
+    const double hn = sqrt(gather_h<false>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par));
     if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
@@ -2717,8 +2736,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         if (j < kWideJR) wr[j] = v;
         else wl[(j - kWideJR) * kBlock + threadIdx.x] = v;
     };
+    int gpar = 0;                                       // block_sum_pp's LDS row
     auto publish = [&](int k, double acc) {
-        acc = block_sum(acc);
+        acc = block_sum_pp(acc, gpar);
         if (threadIdx.x == 0) st_agent(gran + (long long)k * G + blockIdx.x, (unsigned long long)__double_as_longlong(acc));
     };
     // streaming ring: slot j % kWideD holds unit j's v_k (and v_{k+1}).  The
@@ -2775,7 +2795,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         asm volatile("" : "+v"(ub));
 #pragma unroll
         for (int j = 0; j < kWideD; j++) fetch(j, ub, vkp, vnp, true);    // in flight during the sum
-        const double h = gather_h<true>(gran + (long long)k * G, hg + k, k, G, err);
+        const double h = gather_h<true>(gran + (long long)k * G, hg + k, k, G, err, gpar);
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         acc = 0.0;
@@ -2796,7 +2816,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(gather_h<true>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err));
+    const double hn = sqrt(gather_h<true>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, gpar));
     if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
