@@ -566,7 +566,11 @@ def main():
 
     FAMS = (("spmv", ggmres.PROF_SPMV, lambda: s.bytes_spmv()),
             ("ilu0_apply", ggmres.PROF_PRECOND, lambda: s.bytes_precond()),
-            ("trsv_L", ggmres.PROF_TRSV_L, lambda: s.bytes_trsv(0)),
+            # with the SpMV fused into the forward solve's launch (GG_FUSE_SPMV) that
+            # launch also moves the SpMV's bytes
+            ("trsv_L", ggmres.PROF_TRSV_L,
+             lambda: s.bytes_trsv(0) + (s.bytes_spmv() if s.trsv_kernel(0).startswith("k_trsv_wave2d_spmv")
+                                        else 0)),
             ("trsv_U", ggmres.PROF_TRSV_U, lambda: s.bytes_trsv(1)),
             ("mgs_givens", ggmres.PROF_MGS, None))
 
@@ -746,6 +750,7 @@ def main():
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
                    "wavefront_sptrsv": s.uses_wavefront,
+                   "spmv_fused_into_forward_solve": s.trsv_kernel(0).startswith("k_trsv_wave2d_spmv"),
                    "division": (("rows as two fused multiply-adds, in-line term first, U's b and "
                                  "coefficients pre-scaled by RN(1/d) (GG_DIV_FMA; tolerance parity "
                                  "1e-10 vs the reference's arithmetic)") if u_fma else

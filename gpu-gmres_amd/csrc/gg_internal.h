@@ -282,6 +282,7 @@ struct DevTri {
         return (fast && mul_ok && div != WD_UNIT) ? (int)WD_MUL : div;
     }
     DBuf<unsigned long long> bnd;  // nbands * T hand-off granules (sentinel = not ready) + 128 dummies
+    DBuf<unsigned long long> fcnt; // fused SpMV (forward solve): per slice group, 1 = stored (0 between launches)
     long long *trace = nullptr;  // diagnostics: per band, nbatch+1 timestamps (gg_trace_precond)
     double bytes = 0;            // algorithmic bytes per solve
     double bytes_mul = 0;        // the same with WD_MUL (y streamed in place of d (, y))

@@ -938,18 +938,94 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
     }
 }
 
+// The SpMV fused into the forward solve's launch (GG_FUSE_SPMV, k_trsv_wave2d_spmv):
+// b = A v is produced by extra workgroups of the same launch (blocks >= nbands)
+// while the bands run.  Slices (64 layout rows, the sliced-ELL copy of A) are
+// taken kFsGroup at a time in band-major order, each row summed exactly as
+// k_spmv_sell sums it (entry order, no contraction), stored write-through
+// (agent scope) and counted per band once drained; a band's loader wave waits
+// for its band's count before its first batch (no DMA in flight then), re-arms
+// the counter and streams b with the coherent (sc1) policy.  The SpMV blocks
+// never wait on anything, so they need no co-residency.
+struct FusedSpmv {
+    const int *sptr = nullptr, *sci = nullptr;
+    const double *sv = nullptr, *v = nullptr;
+    double *w = nullptr;                    // = the solve's b
+    unsigned long long *cnt = nullptr;      // per slice group: 1 = stored (0 between launches)
+    const double *ydiv = nullptr;           // split engine: row divisors (k_spmv_sell's YDIV)
+    int n = 0;                              // rows of A (layout space)
+};
+constexpr int kFsGroup = 4;                 // slices per group (kWaveTAlign is a multiple)
+
+__device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands, int T, int nwv)
+{
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int NW = ((int)gridDim.x - nbands) * nwv;
+    const int gpb = T / kFsGroup;
+    const int ngroups = nbands * gpb;
+    for (int q = ((int)blockIdx.x - nbands) * nwv + wv; q < ngroups; q += NW) {
+        const int s0 = q * kFsGroup;
+        int off[kFsGroup], wd[kFsGroup];
+        int wmax = 0;
+#pragma unroll
+        for (int j = 0; j < kFsGroup; j++) {
+            off[j] = fs.sptr[s0 + j];
+            wd[j] = (fs.sptr[s0 + j + 1] - off[j]) >> 6;
+            wmax = wd[j] > wmax ? wd[j] : wmax;
+        }
+        double acc[kFsGroup];
+#pragma unroll
+        for (int j = 0; j < kFsGroup; j++) acc[j] = 0.0;
+        for (int k0 = 0; k0 < wmax; k0 += 8) {
+            int c[kFsGroup][8];
+            double a[kFsGroup][8], xv[kFsGroup][8];
+#pragma unroll
+            for (int j = 0; j < kFsGroup; j++)
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (k0 + k < wd[j]) {
+                        c[j][k] = __builtin_nontemporal_load(fs.sci + off[j] + lane + (k0 + k) * 64);
+                        a[j][k] = __builtin_nontemporal_load(fs.sv + off[j] + lane + (k0 + k) * 64);
+                    }
+#pragma unroll
+            for (int j = 0; j < kFsGroup; j++)
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (k0 + k < wd[j] && c[j][k] >= 0) xv[j][k] = fs.v[c[j][k]];
+#pragma unroll
+            for (int j = 0; j < kFsGroup; j++)
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (k0 + k < wd[j] && c[j][k] >= 0) acc[j] += a[j][k] * xv[j][k];
+        }
+#pragma unroll
+        for (int j = 0; j < kFsGroup; j++) {
+            const int r = (s0 + j) * 64 + lane;
+            if (r < fs.n) {
+                const double o = fs.ydiv ? acc[j] / fs.ydiv[r] : acc[j];
+                st_agent(reinterpret_cast<unsigned long long *>(fs.w) + r, (unsigned long long)__double_as_longlong(o));
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the group's rows stored
+        if (lane == 0) st_agent(fs.cnt + q, 1ull);          // one word per group: no contention
+    }
+}
+
 // IL: the in-line term (|offset| = 1) comes first in the row's canonical order,
 // then the line term -- the split (ILU++) U factor's ascending-column rows
 // (MyILUPP::HostPrecond_right, src/preconditioner.cu:1117-1137).
-template <bool FWD, int DIV, bool TRACE, bool D3 = false, int S = 1, bool IL = false>
-__global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
+// FS: the SpMV fused into the launch (see FusedSpmv; forward unskewed 2D only).
+template <bool FWD, int DIV, bool TRACE, bool D3, int S, bool IL, bool FS>
+__device__ __forceinline__ void trsv_wave2d_body(
     Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
     const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
     double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace,
     int nz, long long P2, const double *__restrict__ c0, unsigned long long *prog,
-    const double *__restrict__ ce1, const double *__restrict__ ce2)
+    const double *__restrict__ ce1, const double *__restrict__ ce2, const FusedSpmv &fs)
 {
     using C = WaveCfg<DIV, D3, S>;
+    static_assert(!FS || (FWD && !D3 && S == 1 && !TRACE && C::LOADERS == 1), "fused SpMV: forward 2D, one loader");
     static_assert(!IL || (S == 1 && !D3), "in-line-first rows: unskewed 2D grids");
     constexpr bool FM = DIV == WD_UFMA || DIV == WD_SFMA;     // GG_DIV_FMA rows
     static_assert(!FM || (S == 1 && !D3 && !IL), "fused rows: unskewed 2D grids (one order for both IL)");
@@ -957,6 +1033,12 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
     static_assert(!(D3 && TRACE), "no trace for 3D grids");
     if (gated(g)) return;
+    if constexpr (FS) {
+        if ((int)blockIdx.x >= nbands) {
+            fused_spmv_role(fs, nbands, T, C::THREADS / 64);
+            return;
+        }
+    }
     // one LDS object: data ring [R][A][C::PBN][64] double2, 2 x 64 boundary values
     // (lanes 0..C::B-1 of each half are used), x staging [2][C::PBN][64]
     __shared__ double2 lds[C::LDS2];
@@ -985,7 +1067,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
     if (XS > 1 && blockIdx.x % XS) return;
     const int blk = blockIdx.x / XS;
     const int ntask = nz * nbands;
-    for (int task = blk; task < ntask; task += gridDim.x / XS) {
+    for (int task = blk; task < ntask; task += (FS ? nbands : (int)gridDim.x / XS)) {
     const int kq = task / nbands, bq = task % nbands;
     const int band = FWD ? bq : (nbands - 1 - bq);
     const int kp = FWD ? kq : (nz - 1 - kq);    // plane
@@ -1029,10 +1111,35 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                 }
             }
         }
+        if constexpr (FS) {
+            // this band's b rows all stored by the SpMV blocks (no DMA in flight
+            // yet: a blocking poll is free); the counter is re-armed after the
+            // stream (a store in flight would upset the loader's vmcnt count)
+            const int gpb = T / kFsGroup;
+            const unsigned long long *fl = fs.cnt + (long long)band * gpb;
+            auto all_stored = [&]() {
+                bool ok = true;
+                for (int k = lane; k < gpb; k += 64) ok &= ld_agent(fl + k) != 0ull;
+                return __all(ok);
+            };
+            int spins = 0;
+            while (!all_stored()) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinLimit) {
+                    if (lane == 0) atomicOr(err, 1);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
         if constexpr (C::LOADERS == 1) {
-            wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN, D3 ? C::A2 + 1 : -1>(src, lds, np, nbatch);
+            wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN, D3 ? C::A2 + 1 : FS ? 0 : -1>(src, lds, np, nbatch);
         } else {
             wave_loader<FWD, C::R, C::SLOT, 1, C::PBN>(src + (wave - 3), lds + (wave - 3) * PB, np, nbatch);
+        }
+        if constexpr (FS) {
+            const int gpb = T / kFsGroup;
+            for (int k = lane; k < gpb; k += 64) st_agent(fs.cnt + (long long)band * gpb + k, 0ull);   // re-arm
         }
         raw_barrier();                      // final barrier (the writer drains the last batch)
         continue;
@@ -1368,6 +1475,30 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
         for (int k = 0; k < 4; k++) tr[nbatch + 1 + k] = ph[k];
     }
     }   // task loop
+}
+
+template <bool FWD, int DIV, bool TRACE, bool D3 = false, int S = 1, bool IL = false>
+__global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
+    Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
+    const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
+    double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace,
+    int nz, long long P2, const double *__restrict__ c0, unsigned long long *prog,
+    const double *__restrict__ ce1, const double *__restrict__ ce2)
+{
+    trsv_wave2d_body<FWD, DIV, TRACE, D3, S, IL, false>(g, T, nbands, b, c1, c2, dv, rv, x, bnd, err, trace, nz,
+                                                        P2, c0, prog, ce1, ce2, FusedSpmv{});
+}
+
+// forward 2D solve with b = A v computed by the launch's blocks >= nbands (FusedSpmv)
+template <int DIV>
+__global__ __launch_bounds__((WaveCfg<DIV>::THREADS)) void k_trsv_wave2d_spmv(
+    Gate g, int T, int nbands, const double *__restrict__ c1, const double *__restrict__ c2,
+    const double *__restrict__ dv, const double *__restrict__ rv, double *__restrict__ x,
+    unsigned long long *bnd, int *err, long long P2, FusedSpmv fs)
+{
+    trsv_wave2d_body<true, DIV, false, false, 1, false, true>(g, T, nbands, fs.w, c1, c2, dv, rv, x, bnd, err,
+                                                              nullptr, 1, P2, nullptr, nullptr, nullptr, nullptr,
+                                                              fs);
 }
 
 // ================================================ 3D 7-point grids: tile wavefront
@@ -3188,6 +3319,48 @@ int wave_batch_steps(int div, bool d3, int skew)
     if (div == WD_UFMA) return WaveCfg<WD_UFMA>::B;
     if (div == WD_SFMA) return WaveCfg<WD_SFMA>::B;
     return div == WD_UNIT ? WaveCfg<WD_UNIT>::B : hw ? WaveCfg<WD_HW>::B : WaveCfg<WD_RCP>::B;
+}
+
+bool fused_spmv_ok(const DevTri &T, const DevCsr &A)
+{
+    const Wave2D &w = T.wl;
+    return T.kind == DevTri::WAVE2D && T.lower && w.ok && !w.tile && w.nz == 1 && w.skew == 1 && !T.trace &&
+           (T.eff_div() == WD_UFMA || T.eff_div() == WD_SFMA) && A.sell && w.T % kFsGroup == 0 &&
+           (long long)A.nslice >= (long long)w.nbands * w.T && (long long)A.n >= (long long)w.nbands * w.T * 64;
+}
+
+void launch_trsv_spmv(Gate g, DevTri &T, const DevCsr &A, const double *v, double *w, double *x, int *err,
+                      hipStream_t st, const double *ydiv)
+{
+    const Wave2D &wl = T.wl;
+    const size_t nflag = (size_t)wl.nbands * (wl.T / kFsGroup);
+    if (T.fcnt.n < nflag) {
+        T.fcnt.alloc(nflag);
+        GG_HIP(hipMemsetAsync(T.fcnt.p, 0, nflag * sizeof(unsigned long long), st));
+    }
+    // every CU the bands leave free computes b (the SpMV blocks wait on nothing)
+    static const int cus = [] {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return c;
+    }();
+    const int ns = std::max(64, cus - wl.nbands);
+    FusedSpmv fs;
+    fs.sptr = A.sptr.p;
+    fs.sci = A.sci.p;
+    fs.sv = A.sv.p;
+    fs.v = v;
+    fs.w = w;
+    fs.cnt = T.fcnt.p;
+    fs.ydiv = ydiv;
+    fs.n = A.n;
+    if (T.eff_div() == WD_UFMA)
+        k_trsv_wave2d_spmv<WD_UFMA><<<wl.nbands + ns, WaveCfg<WD_UFMA>::THREADS, 0, st>>>(
+            g, wl.T, wl.nbands, T.c1.p, T.c2.p, nullptr, nullptr, x, T.bnd.p, err, wl.P2, fs);
+    else   // the split engine's non-unit L, coefficients and b pre-scaled by RN(1/d)
+        k_trsv_wave2d_spmv<WD_SFMA><<<wl.nbands + ns, WaveCfg<WD_SFMA>::THREADS, 0, st>>>(
+            g, wl.T, wl.nbands, T.c1s.p, T.c2s.p, T.rw.p, nullptr, x, T.bnd.p, err, wl.P2, fs);
 }
 
 void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st)

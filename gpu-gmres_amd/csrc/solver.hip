@@ -552,8 +552,18 @@ void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1
     launch_div(g, s->t2.p, s->rs_l.p, out, (int)s->P, s->st);
 }
 // Ml(A' z) with Ml's row gather and D_l^-1 in the SpMV (resid: Ml(b - A x))
-void spmv_left(gg_solver *s, Gate g, const double *z, const double *b, double *out, int i = -1)
+void spmv_left(gg_solver *s, Gate g, const double *z, const double *b, double *out, int i = -1,
+               bool fuse = false)
 {
+    if (fuse && !b) {
+        // A' z and its row scaling computed inside the forward solve's launch (GG_FUSE_SPMV)
+        const int mk = prof_begin(s, GG_PROF_PRECOND, i);
+        const int ml = prof_begin(s, GG_PROF_TRSV_L, i);
+        launch_trsv_spmv(g, s->L, s->dA, z, s->t1.p, out, s->err.p, s->st, s->ls_l.p);
+        prof_end(s, ml);
+        prof_end(s, mk);
+        return;
+    }
     int mk = prof_begin(s, GG_PROF_SPMV, i);
     launch_spmv(g, s->dA, z, b, s->t1.p, b != nullptr, s->st, s->ls_l.p);
     prof_end(s, mk);
@@ -644,6 +654,18 @@ unsigned long long *hgran(gg_solver *s, int m, int i)
     return s->gran.p + (size_t)m * (m + 2) * s->G + (size_t)i * (m + 2);
 }
 
+// The inner iteration's SpMV runs inside the forward solve's launch (FusedSpmv,
+// kernels.hip) on the 2D wavefront with GG_DIV_FMA's unit L; GG_FUSE_SPMV=0 keeps
+// the separate k_spmv_sell launch.  Same bits either way (the rows summed alike).
+bool fuse_spmv_active(gg_solver *s)
+{
+    const char *e = std::getenv("GG_FUSE_SPMV");
+    if (e && e[0] == '0') return false;
+    if (s->shared || s->pkind == GG_PRECOND_NONE || user_kind(s)) return false;
+    s->L.fast = s->div_mode;
+    return fused_spmv_ok(s->L, s->dA);
+}
+
 void enqueue_cycle(gg_solver *s, int m)
 {
     DevState *ds = s->ds.p;
@@ -655,6 +677,7 @@ void enqueue_cycle(gg_solver *s, int m)
     const bool persist = s->persist && !s->shared;
     const bool wide = s->wide && !s->shared;
     if (persist || wide) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
+    const bool fuse = fuse_spmv_active(s);
     for (int i = 0; i < m; i++) {
         Gate gi;
         gi.done = &ds->done;
@@ -673,6 +696,14 @@ void enqueue_cycle(gg_solver *s, int m)
             apply_user(s, gi, GG_APPLY_RIGHT, vi, s->z.p);                    // z = Mr v_i
             launch_spmv(gi, s->dA, s->z.p, nullptr, s->ww.p, false, s->st);   // ww = A z
             apply_user(s, gi, GG_APPLY_LEFT, s->ww.p, s->w.p);                // w = Ml ww
+        } else if (fuse && !split) {
+            // ww = A v_i computed inside the forward solve's launch (GG_FUSE_SPMV)
+            mk = prof_begin(s, GG_PROF_PRECOND, i);
+            const int ml = prof_begin(s, GG_PROF_TRSV_L, i);
+            launch_trsv_spmv(gi, s->L, s->dA, vi, s->ww.p, s->t1.p, s->err.p, s->st);
+            prof_end(s, ml);
+            trsv(s, gi, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->w.p);              // w = M^-1 ww
+            prof_end(s, mk);
         } else if (!split) {
             mk = prof_begin(s, GG_PROF_SPMV, i);
             launch_spmv(gi, s->dA, vi, nullptr, s->ww.p, false, s->st);        // ww = A v_i
@@ -682,7 +713,7 @@ void enqueue_cycle(gg_solver *s, int m)
             prof_end(s, mk);
         } else {
             apply_right(s, gi, vi, s->z.p, i);                                 // z = Mr v_i
-            spmv_left(s, gi, s->z.p, nullptr, s->w.p, i);                      // w = Ml A z
+            spmv_left(s, gi, s->z.p, nullptr, s->w.p, i, fuse);                // w = Ml A z
         }
         mk = prof_begin(s, GG_PROF_MGS, i);
         if (persist) {
@@ -733,6 +764,7 @@ void enqueue_cycle(gg_solver *s, int m)
 void reset_wave(DevTri *T, hipStream_t st)
 {
     launch_fill_u64(T->bnd.p, T->wl.ngran(), kSentinel, st);
+    if (T->fcnt.p) GG_HIP(hipMemsetAsync(T->fcnt.p, 0, T->fcnt.n * sizeof(unsigned long long), st));
     if (T->prog.p) GG_HIP(hipMemsetAsync(T->prog.p, 0, T->prog.n * sizeof(unsigned long long), st));
 }
 
@@ -1404,7 +1436,9 @@ int gg_trsv_kernel(gg_solver *s, int which, char *name, int cap)
     DevTri &T = which == 0 ? s->L : s->U;
     T.fast = s->div_mode;
     std::string k;
-    if (T.kind == DevTri::WAVE2D) {
+    if (which == 0 && fuse_spmv_active(s)) {
+        k = "k_trsv_wave2d_spmv<" + std::to_string(T.eff_div()) + ">";
+    } else if (T.kind == DevTri::WAVE2D) {
         const char *fwd = T.lower ? "true" : "false";
         const int div = T.eff_div();
         if (T.wl.tile)

@@ -231,6 +231,9 @@ def fused_expected(s):
     if k0.startswith("k_trsv_tile3d"):
         assert k0.startswith("k_trsv_tile3d<true, 4,") and k1.startswith("k_trsv_tile3d<false, 5,")
         return True
+    if k0.startswith("k_trsv_wave2d_spmv<"):  # the forward solve with the SpMV fused in
+        assert k0 == "k_trsv_wave2d_spmv<4>" and k1.startswith("k_trsv_wave2d<false, 5,")
+        return True
     if ", false, 1, false>" in k0:          # unskewed 2D band kernel
         assert k0.startswith("k_trsv_wave2d<true, 4,") and k1.startswith("k_trsv_wave2d<false, 5,")
         return True
@@ -316,7 +319,8 @@ def test_fma_split_parity(fsolver, perm):
     md = modes(fsolver)
     assert md == ((2, 2) if perm == "identity" else (0, 0))
     if perm == "identity":
-        assert fsolver.trsv_kernel(0).startswith("k_trsv_wave2d<true, 5,")
+        # A' z fused into the L launch where A' has the sliced-ELL copy (not at this size)
+        assert fsolver.trsv_kernel(0) in ("k_trsv_wave2d_spmv<5>", "k_trsv_wave2d<true, 5, false, false, 1, false>")
         assert fsolver.trsv_kernel(1).startswith("k_trsv_wave2d<false, 5,")
     o, ot = oracle_mul(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
                        A.shape[0], nx=48 if perm == "identity" else None, mul=md)
@@ -382,3 +386,32 @@ def test_fma_c4_first_iterations(fsolver):
     g = fsolver.solve(b, restart=30, max_iter=12, tol=1e-300)
     check_exact(g, ot)
     check_tol(g, o)
+
+
+@pytest.mark.parametrize("engine", ["left", "split"])
+@pytest.mark.parametrize("shape", [(600, 128), (1000, 192)])
+def test_fused_spmv_same_bits(fsolver, monkeypatch, shape, engine):
+    """GG_FUSE_SPMV: the inner iteration's A v (split engine: A' z with D_l^-1)
+    computed by the forward solve's own launch (extra workgroups, per-band
+    counters) gives the bits of the separate k_spmv_sell launch, solve after
+    solve (the counters re-arm)"""
+    nx, ny = shape
+    A = M.laplacian_5pt(nx, ny)
+    b = M.rhs_uniform(A.shape[0])
+    fsolver.set_matrix(A)
+    if engine == "left":
+        fsolver.set_precond_ilu0()
+    else:
+        P = make_split(A, seed=9, identity_perm=True)
+        fsolver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    monkeypatch.delenv("GG_FUSE_SPMV", raising=False)
+    assert fsolver.trsv_kernel(0) == ("k_trsv_wave2d_spmv<4>" if engine == "left" else "k_trsv_wave2d_spmv<5>")
+    g = fsolver.solve(b, restart=30, max_iter=400, tol=1e-12)
+    g2 = fsolver.solve(b, restart=30, max_iter=400, tol=1e-12)
+    monkeypatch.setenv("GG_FUSE_SPMV", "0")
+    assert fsolver.trsv_kernel(0).startswith("k_trsv_wave2d<true, ")
+    e = fsolver.solve(b, restart=30, max_iter=400, tol=1e-12)
+    for r in (g, g2):
+        assert r["ret"] == e["ret"] and r["iters"] == e["iters"] and r["inner"] == e["inner"]
+        assert np.array_equal(r["hist"], e["hist"])
+        assert np.array_equal(r["x"], e["x"])
