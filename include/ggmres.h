@@ -91,7 +91,10 @@ typedef struct gg_options {
  * needs the whole device co-resident (the orthogonalization takes the
  * per-step kernels instead of the persistent launch); it requires the 2D
  * wavefront triangular solve or no preconditioner (else GG_EINVAL), whose
- * workgroups only wait on workgroups dispatched before them. */
+ * workgroups only wait on workgroups dispatched before them; for the same
+ * reason the inner iteration's SpMV stays a launch of its own (without the
+ * flag it runs inside the forward solve's launch on the GG_DIV_FMA 2D path;
+ * environment GG_FUSE_SPMV=0 turns that off). */
 #define GG_SOLVE_SHARED_DEVICE 0x1
 /* gg_options.flags, the sharded solve (ggmres_dd.h) only: orthogonalize each
  * Arnoldi vector by classical Gram-Schmidt with one re-orthogonalization
