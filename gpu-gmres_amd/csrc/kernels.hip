@@ -955,7 +955,9 @@ struct FusedSpmv {
     const double *ydiv = nullptr;           // split engine: row divisors (k_spmv_sell's YDIV)
     int n = 0;                              // rows of A (layout space)
 };
-constexpr int kFsGroup = 4;                 // slices per group (kWaveTAlign is a multiple)
+// slices per group: C2 fused L 92.5 / 87.0 / 85.8 us at 8 / 4 / 2 (a group's
+// chain is shorter with fewer loads per lane; profiles/r03_fs_knobs.txt)
+constexpr int kFsGroup = 2;                 // (kWaveTAlign is a multiple)
 
 __device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands, int T, int nwv)
 {
