@@ -274,6 +274,26 @@ def bench_c3(a, torch, dist, world, rank, local):
         dist.destroy_process_group()
 
 
+def lockstep(torch, dist, group, rank, steps):
+    """Run `steps` ([(name, fn)]) in lockstep over the CPU `group`: after each
+    local step every rank learns (MIN all-reduce) whether every rank succeeded,
+    and all stop at the first step that failed anywhere.  A rank whose step
+    raised still joins the agreement, so no rank is left waiting in a
+    collective of a later step.  True iff every step succeeded on every rank."""
+    for name, fn in steps:
+        try:
+            fn()
+            ok = 1
+        except Exception as e:          # noqa: BLE001 -- any failure: every rank falls back together
+            print(f"bench.py rank {rank}: IPC {name} failed ({e})", file=sys.stderr, flush=True)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if not int(flag.item()):
+            return False
+    return True
+
+
 def bench_dd(a, torch, dist, world, rank, local):
     """The sharded solve (include/ggmres_dd.h): ONE system split over the ranks
     (torchrun: one shard per GPU, RCCL exchanges; one process: --dd-parts
@@ -292,24 +312,30 @@ def bench_dd(a, torch, dist, world, rank, local):
         # kernel storing into the peers' areas over xGMI
         import ggmres
         boot = dist.new_group(backend="gloo")
-        d, ok = None, 1
-        try:
+        d, hb = None, None
+
+        def create():
+            nonlocal d, hb
+            if os.environ.get("GG_BENCH_IPC_FAIL") == f"create:{rank}":      # fault injection (tests)
+                raise RuntimeError("injected")
             d = DD(world, device=local, rank=rank, comm="ipc")
+            hb = d.ipc_handle()
 
-            def allgather(hb):
-                lst = [None] * world
-                dist.all_gather_object(lst, hb, group=boot)
-                return lst
+        def connect():
+            lst = [None] * world
+            dist.all_gather_object(lst, hb, group=boot)     # every rank reaches this together
+            if os.environ.get("GG_BENCH_IPC_FAIL") == f"connect:{rank}":
+                raise RuntimeError("injected")
+            d.ipc_connect(lst)
 
-            d.connect_ipc(allgather)
-            ranks, myrank = d.comm_ranks()
-            ok = int(ranks == world and myrank == rank)
-        except ggmres.GGError as e:
-            print(f"bench.py rank {rank}: IPC exchange unavailable ({e})", file=sys.stderr, flush=True)
-            ok = 0
-        flag = torch.tensor([ok], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=boot)
-        if not int(flag.item()):
+        def check():
+            ranks, myrank = d.comm_ranks()                  # an exchange: bounded (30 s) on the device
+            if ranks != world or myrank != rank:
+                raise RuntimeError(f"{ranks} ranks mapped (rank {myrank})")
+
+        ok = lockstep(torch, dist, boot, rank, [("exchange area", create), ("connect", connect),
+                                                ("rank check", check)])
+        if not ok:
             # every rank falls back together: RCCL collectives
             if d is not None:
                 d.close()

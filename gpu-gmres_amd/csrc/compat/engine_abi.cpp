@@ -5,11 +5,14 @@
 // becomes a gg_set_precond_user callback (its Dev* methods with device arrays,
 // or -- GMRESilu, the host engine -- its Host* methods with host arrays), the
 // matrix and vectors are promoted from fp32 to the fp64 engine, x is rounded
-// back.  Errors print to stderr and return 1 (the reference exits on
-// checkCudaErrors).
+// back.  The solver is kept across calls (one setup per matrix; see Ctx).
+// Errors print to stderr and return 1 (the reference exits on checkCudaErrors).
+#include <algorithm>
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -86,50 +89,163 @@ bool fetch(void *dst, const void *src, size_t bytes, bool device)
     return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess;
 }
 
+// The engine state kept across calls (src/gmres.h:82-112: GMRES_GPU_Data exists
+// so that a transient caller reuses one workspace across time steps,
+// src_thermal/main2.cu:470-506).  One solver per (caller's CSR arrays, n, nnz,
+// engine, device; for GMRES_GPU_tran also the caller's GMRES_GPU_Data): the
+// first call sets the matrix up (one gg_set_matrix: upload, layout), later
+// calls only check that the arrays were not changed in place (an
+// order-independent fingerprint of values, row pointers and column indices,
+// computed on the device for device arrays) and solve, with b and x promoted
+// and x rounded back on the device (gg_solve_device_f32).  A changed matrix
+// is set up again.  At most kCacheCap solvers are kept (least recently used
+// first out); the reference's engines are not reentrant, neither is this cache
+// (one mutex).
+struct Ctx {
+    gg_solver *s = nullptr;
+    int dev = 0, n = 0, nnz = 0, split = 0;
+    bool device = false;
+    const void *val = nullptr, *rp = nullptr, *ci = nullptr, *owner = nullptr;
+    unsigned long long fp = 0;
+    unsigned long long used = 0;
+    Plugin pl{nullptr, false, {}, {}};
+    ~Ctx()
+    {
+        if (s) gg_destroy(s);
+    }
+};
+constexpr size_t kCacheCap = 8;
+std::mutex g_mu;
+std::vector<std::unique_ptr<Ctx>> g_cache;
+unsigned long long g_tick = 0;
+
+unsigned long long host_fingerprint(const void *p, size_t bytes)
+{
+    // the device fingerprint's formula (gg_device_fingerprint) on host memory
+    const unsigned *w = static_cast<const unsigned *>(p);
+    unsigned long long acc = 0;
+    for (size_t k = 0; k < bytes / 4; k++) acc += (unsigned long long)w[k] * (unsigned long long)(2 * k + 1);
+    return acc;
+}
+
+// fingerprint of the caller's CSR (values, row pointers, column indices)
+bool csr_fingerprint(bool device, const float *val, const int *rp, const int *ci, int n, int nnz,
+                     unsigned long long &fp)
+{
+    const size_t b[3] = {sizeof(float) * (size_t)nnz, sizeof(int) * ((size_t)n + 1), sizeof(int) * (size_t)nnz};
+    const void *p[3] = {val, rp, ci};
+    fp = 0;
+    for (int k = 0; k < 3; k++) {
+        unsigned long long f = 0;
+        if (device) {
+            if (gg_device_fingerprint(p[k], b[k], &f) != GG_OK) return false;
+        } else {
+            f = host_fingerprint(p[k], b[k]);
+        }
+        fp = fp * 0x9E3779B97F4A7C15ull + f;
+    }
+    return true;
+}
+
+// the cached solver for this call, set up if missing or stale (nullptr: error reported)
+Ctx *context(const char *who, bool device, int split, const float *val, const int *rp, const int *ci, int n,
+             const void *owner)
+{
+    auto fail = [&](const char *what, int rc) -> Ctx * {
+        std::fprintf(stderr, "%s: %s: %s (%s)\n", who, what, gg_strerror(rc), gg_last_error());
+        return nullptr;
+    };
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    int r0 = 0, rn = 0;
+    if (!fetch(&r0, rp, sizeof(int), device) || !fetch(&rn, rp + n, sizeof(int), device))
+        return fail("row pointers", GG_EHIP);
+    const int nnz = rn - r0;
+    if (nnz < 0) return fail("row pointers", GG_EINVAL);
+    unsigned long long fp = 0;
+    if (!csr_fingerprint(device, val + r0, rp, ci + r0, n, nnz, fp)) return fail("fingerprint", GG_EHIP);
+    Ctx *c = nullptr;
+    for (auto &e : g_cache)
+        if (e->dev == dev && e->device == device && e->split == split && e->val == val && e->rp == rp &&
+            e->ci == ci && e->n == n && e->nnz == nnz && e->owner == owner) {
+            c = e.get();
+            break;
+        }
+    if (c && c->fp == fp) {
+        c->used = ++g_tick;
+        return c;
+    }
+    if (!c) {
+        if (g_cache.size() >= kCacheCap) {
+            auto lru = std::min_element(g_cache.begin(), g_cache.end(),
+                                        [](const std::unique_ptr<Ctx> &a, const std::unique_ptr<Ctx> &b) {
+                                            return a->used < b->used;
+                                        });
+            g_cache.erase(lru);
+        }
+        g_cache.push_back(std::make_unique<Ctx>());
+        c = g_cache.back().get();
+        c->dev = dev;
+        c->device = device;
+        c->split = split;
+        c->val = val;
+        c->rp = rp;
+        c->ci = ci;
+        c->n = n;
+        c->nnz = nnz;
+        c->owner = owner;
+        int rc = gg_create(dev, &c->s);
+        if (rc != GG_OK) {
+            g_cache.pop_back();
+            return fail("gg_create", rc);
+        }
+    }
+    // (re)build: the matrix in fp64 (the reference's float values promoted)
+    std::vector<int> hrp(n + 1), hci(nnz);
+    std::vector<float> hv(nnz);
+    if (!fetch(hrp.data(), rp, sizeof(int) * (n + 1), device) ||
+        !fetch(hci.data(), ci + r0, sizeof(int) * nnz, device) || !fetch(hv.data(), val + r0, sizeof(float) * nnz, device))
+        return fail("copy in", GG_EHIP);
+    for (int &r : hrp) r -= r0;
+    std::vector<double> dv(hv.begin(), hv.end());
+    c->fp = 0;   // invalid until set up
+    int rc = gg_set_matrix(c->s, n, hrp.data(), hci.data(), dv.data());
+    if (rc == GG_OK) rc = gg_set_precond_user(c->s, split, call_plugin, &c->pl);
+    if (rc != GG_OK) return fail("setup", rc);
+    c->fp = fp;
+    c->used = ++g_tick;
+    return c;
+}
+
 // one solve: CSR (fp32 values), b, x (in/out) in device or host memory
 int engine(const char *who, bool device, int split, const float *val, const int *rp, const int *ci, int n,
            float *x, const float *b, int m, int max_iter_in, float tol_in, Preconditioner &P, int *iters_out,
-           float *tol_out)
+           float *tol_out, const void *owner = nullptr)
 {
-    auto fail = [&](const char *what, int rc) {
-        std::fprintf(stderr, "%s: %s: %s (%s)\n", who, what, gg_strerror(rc), gg_last_error());
-        return 1;
-    };
     if (n <= 0 || m < 1) {
         std::fprintf(stderr, "%s: bad sizes n=%d m=%d\n", who, n, m);
         return 1;
     }
-    std::vector<int> hrp(n + 1);
-    if (!fetch(hrp.data(), rp, sizeof(int) * (n + 1), device)) return fail("row pointers", GG_EHIP);
-    const int nnz = hrp[n] - hrp[0];
-    std::vector<int> hci(nnz);
-    std::vector<float> hv(nnz), hx(n), hb(n);
-    if (!fetch(hci.data(), ci + hrp[0], sizeof(int) * nnz, device) ||
-        !fetch(hv.data(), val + hrp[0], sizeof(float) * nnz, device) ||
-        !fetch(hx.data(), x, sizeof(float) * n, device) || !fetch(hb.data(), b, sizeof(float) * n, device))
-        return fail("copy in", GG_EHIP);
-    const int base = hrp[0];
-    for (int &r : hrp) r -= base;
-    std::vector<double> dv(hv.begin(), hv.end()), dx(hx.begin(), hx.end()), db(hb.begin(), hb.end());
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    gg_solver *s = nullptr;
-    int rc = gg_create(dev, &s);
-    if (rc != GG_OK) return fail("gg_create", rc);
-    Plugin pl{&P, !device, {}, {}};
+    std::lock_guard<std::mutex> lock(g_mu);
+    Ctx *c = context(who, device, split, val, rp, ci, n, owner);
+    if (!c) return 1;
+    c->pl.p = &P;                                // the caller's object of THIS call
+    c->pl.host = !device;
+    gg_options o{m, max_iter_in, (double)tol_in, 0};
     gg_result res{};
-    rc = gg_set_matrix(s, n, hrp.data(), hci.data(), dv.data());
-    if (rc == GG_OK) rc = gg_set_precond_user(s, split, call_plugin, &pl);
-    if (rc == GG_OK) {
-        gg_options o{m, max_iter_in, (double)tol_in, 0};
-        rc = gg_solve(s, db.data(), dx.data(), &o, &res);
+    int rc;
+    if (device) {
+        rc = gg_solve_device_f32(c->s, b, x, &o, &res);
+    } else {
+        std::vector<double> dx(x, x + n), db(b, b + n);
+        rc = gg_solve(c->s, db.data(), dx.data(), &o, &res);
+        if (rc >= 0)
+            for (int i = 0; i < n; i++) x[i] = (float)dx[i];
     }
-    gg_destroy(s);
-    if (rc < 0) return fail("solve", rc);
-    for (int i = 0; i < n; i++) hx[i] = (float)dx[i];
-    if (device ? hipMemcpy(x, hx.data(), sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess
-               : (std::memcpy(x, hx.data(), sizeof(float) * n), false))
-        return fail("copy out", GG_EHIP);
+    if (rc < 0) {
+        std::fprintf(stderr, "%s: solve: %s (%s)\n", who, gg_strerror(rc), gg_last_error());
+        return 1;
+    }
     if (iters_out) *iters_out = res.iters;
     if (tol_out) *tol_out = (float)res.relres;
     return res.status == GG_OK ? 0 : 1;
@@ -160,13 +276,13 @@ int GMRES_GPU_tran(SpMatrixGPU *Sparse, SpMatrix *spm, dim3 *grid, dim3 *block, 
     (void)spm;
     (void)grid;
     (void)block;
-    (void)gmres_gpu_data;
     if (!Sparse) {
         std::fprintf(stderr, "GMRES_GPU_tran: null argument\n");
         return 1;
     }
+    // the solver hangs off the caller's workspace object: one setup per time loop
     return engine("GMRES_GPU_tran", true, 0, Sparse->d_val, Sparse->d_rowIndices, Sparse->d_indices, n, d_x, d_b,
-                  m, max_iter, tol, preconditioner, nullptr, nullptr);
+                  m, max_iter, tol, preconditioner, nullptr, nullptr, &gmres_gpu_data);
 }
 
 // src/gmres.cu:2069-2252 -- the split engine on host arrays, Host* methods

@@ -84,6 +84,10 @@ struct gg_dd {
     bool ipc_connected = false;
     unsigned long long ipc_seq = 0;
     DBuf<int> xerr;
+    // a peer timed out (xerr bit 4): the ranks' sequence numbers may now
+    // differ, so the communicator is unusable -- every later exchange is
+    // refused with GG_ESTATE (create a new gg_dd to recover)
+    bool ipc_broken = false;
     hipStream_t st = nullptr;
     hipStream_t st2 = nullptr;              // the SpMV's interface exchange, beside the interior rows
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evx = nullptr, evh = nullptr;
@@ -138,6 +142,8 @@ Gate gate_mask(Shard &s, int mask)
 void ipc_allgather(gg_dd *d, double *buf, long long cnt, hipStream_t st)
 {
     GG_REQUIRE(d->ipc_connected, GG_ESTATE, "dd: IPC exchange used before gg_dd_ipc_connect");
+    GG_REQUIRE(!d->ipc_broken, GG_ESTATE,
+               "dd: IPC communicator unusable after a peer timeout (create a new gg_dd)");
     GG_REQUIRE(cnt <= d->ipc_capd, GG_EINVAL,
                "dd: IPC exchange of " + std::to_string(cnt) + " doubles exceeds the area's " +
                    std::to_string(d->ipc_capd) + " per rank (GG_DD_IPC_CAP)");
@@ -148,7 +154,11 @@ void ipc_check(gg_dd *d)
     int e = 0;
     GG_HIP(hipMemcpyAsync(&e, d->xerr.p, sizeof(int), hipMemcpyDeviceToHost, d->st));
     GG_HIP(hipStreamSynchronize(d->st));
-    GG_REQUIRE((e & 4) == 0, GG_ETIMEOUT, "dd: IPC exchange: a peer did not arrive within 30 s");
+    if (e & 4) {
+        d->ipc_broken = true;
+        throw Error{GG_ETIMEOUT, "dd: IPC exchange: a peer did not arrive within 30 s "
+                                 "(the communicator is unusable from here on)"};
+    }
 }
 // GG_DD_IPC, host-synchronous (setup, error checks): every rank's value
 std::vector<long long> ipc_allgather_host(gg_dd *d, long long v)
@@ -491,6 +501,9 @@ void reset_waves(gg_dd *d)
         for (DevTri *T : {&sp->LI, &sp->LS, &sp->UI, &sp->US}) {
             if (T->kind != DevTri::WAVE2D) continue;
             launch_fill_u64(T->bnd.p, T->wl.ngran(), kSentinel, d->st);
+            if (T->wl.tile)     // the tile kernel's task queue
+                GG_HIP(hipMemsetAsync(T->bnd.p + T->wl.ngran() + 128LL * kTileDummyBlocks, 0,
+                                      64 * sizeof(unsigned long long), d->st));
             if (T->prog.p) GG_HIP(hipMemsetAsync(T->prog.p, 0, T->prog.n * sizeof(unsigned long long), d->st));
         }
         GG_HIP(hipMemsetAsync(sp->err.p, 0, d->P * sizeof(int), d->st));

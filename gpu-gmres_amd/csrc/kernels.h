@@ -10,7 +10,8 @@ namespace gg {
 // enqueued with a single host sync per cycle.
 struct DevState {
     double normb, beta, resid, tol;
-    int done;       // bit flags: 1 inner-converged, 2 restart-converged, 4 converged at start
+    int done;       // bit flags: 1 inner-converged, 2 restart-converged, 4 converged at start,
+                    // 8 cycle aborted (a persistent grid was not co-resident: rerun)
     int conv_i;     // inner index of convergence
     int j;          // reference iteration counter at the start of the cycle
     int max_iter;
@@ -21,7 +22,7 @@ struct DevState {
     int err;        // device-side error (1 = wavefront wait timed out)
     int pad;
 };
-constexpr int DONE_INNER = 1, DONE_RESTART = 2, DONE_INIT = 4;
+constexpr int DONE_INNER = 1, DONE_RESTART = 2, DONE_INIT = 4, DONE_ABORT = 8;
 
 // A kernel is skipped when (*done & mask) != 0, or (nit && i >= *nit).
 struct Gate {
@@ -102,6 +103,8 @@ void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long l
 
 // ---- split (PG) elementwise maps -------------------------------------------
 void launch_f64_to_f32(Gate g, const double *in, float *out, int n, hipStream_t st);   // out = RN_f32(in)
+// *out += sum over the nw 32-bit words w_k of p of w_k * (2k + 1) (mod 2^64)
+void launch_fingerprint(const void *p, long long nw, unsigned long long *out, hipStream_t st);
 void launch_f32_to_f64(Gate g, const float *in, double *out, int n, hipStream_t st);   // out = (double)in
 void launch_mul(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in*s
 void launch_div(Gate g, const double *in, const double *s, double *out, int n, hipStream_t st);            // out = in/s

@@ -296,6 +296,16 @@ __global__ void k_mul(Gate g, const double *in, const double *s, double *out, in
     if (i < n) out[i] = in[i] * s[i];
 }
 // the user-preconditioner boundary (fp32 arrays, src/preconditioner.h:34-84)
+// order-independent fingerprint: sum of w_k * (2k + 1) over 32-bit words, mod 2^64
+__global__ __launch_bounds__(kBlock) void k_fingerprint(const unsigned *p, long long nw, unsigned long long *out)
+{
+    unsigned long long acc = 0;
+    for (long long k = blockIdx.x * (long long)kBlock + threadIdx.x; k < nw; k += (long long)gridDim.x * kBlock)
+        acc += (unsigned long long)p[k] * (unsigned long long)(2 * k + 1);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);      // integer adds: any order, same sum
+}
+
 __global__ void k_f64_to_f32(Gate g, const double *in, float *out, int n)
 {
     if (gated(g)) return;
@@ -946,7 +956,11 @@ __device__ __forceinline__ void wave_loader(const double2 *const *src, double2 *
 // (agent scope) and counted per band once drained; a band's loader wave waits
 // for its band's count before its first batch (no DMA in flight then), re-arms
 // the counter and streams b with the coherent (sc1) policy.  The SpMV blocks
-// never wait on anything, so they need no co-residency.
+// never wait on anything and take the LOW block indices, so they are dispatched
+// before the bands that wait on them: with more bands than resident slots the
+// SpMV blocks still finish and the bands run in dispatch order, each waiting
+// only on blocks dispatched before it (with the bands first, a grid
+// of nbands >= resident slots would spin on never-dispatched SpMV blocks).
 struct FusedSpmv {
     const int *sptr = nullptr, *sci = nullptr;
     const double *sv = nullptr, *v = nullptr;
@@ -954,6 +968,7 @@ struct FusedSpmv {
     unsigned long long *cnt = nullptr;      // per slice group: 1 = stored (0 between launches)
     const double *ydiv = nullptr;           // split engine: row divisors (k_spmv_sell's YDIV)
     int n = 0;                              // rows of A (layout space)
+    int ns = 0;                             // SpMV blocks: blockIdx < ns, the bands after them
 };
 // slices per group: C2 fused L 92.5 / 87.0 / 85.8 us at 8 / 4 / 2 (a group's
 // chain is shorter with fewer loads per lane; profiles/r03_fs_knobs.txt)
@@ -963,10 +978,10 @@ __device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands,
 {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int NW = ((int)gridDim.x - nbands) * nwv;
+    const int NW = fs.ns * nwv;
     const int gpb = T / kFsGroup;
     const int ngroups = nbands * gpb;
-    for (int q = ((int)blockIdx.x - nbands) * nwv + wv; q < ngroups; q += NW) {
+    for (int q = (int)blockIdx.x * nwv + wv; q < ngroups; q += NW) {
         const int s0 = q * kFsGroup;
         int off[kFsGroup], wd[kFsGroup];
         int wmax = 0;
@@ -1035,11 +1050,13 @@ __device__ __forceinline__ void trsv_wave2d_body(
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
     static_assert(!(D3 && TRACE), "no trace for 3D grids");
     if (gated(g)) return;
+    int bid = (int)blockIdx.x;                  // this workgroup among the bands
     if constexpr (FS) {
-        if ((int)blockIdx.x >= nbands) {
+        if (bid < fs.ns) {
             fused_spmv_role(fs, nbands, T, C::THREADS / 64);
             return;
         }
+        bid -= fs.ns;
     }
     // one LDS object: data ring [R][A][C::PBN][64] double2, 2 x 64 boundary values
     // (lanes 0..C::B-1 of each half are used), x staging [2][C::PBN][64]
@@ -1066,8 +1083,8 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // 88.9 -> 90.0 us (round 3, re-measured: 89.4 / 90.3 -> 89.9 / 90.4 us), so
     // the forward solve keeps one workgroup per band.
     constexpr int XS = D3 ? 1 : FWD ? GG_WAVE_XCD_L : GG_WAVE_XCD;
-    if (XS > 1 && blockIdx.x % XS) return;
-    const int blk = blockIdx.x / XS;
+    if (XS > 1 && bid % XS) return;
+    const int blk = bid / XS;
     const int ntask = nz * nbands;
     for (int task = blk; task < ntask; task += (FS ? nbands : (int)gridDim.x / XS)) {
     const int kq = task / nbands, bq = task % nbands;
@@ -1491,7 +1508,7 @@ __global__ __launch_bounds__((WaveCfg<DIV, D3, S>::THREADS)) void k_trsv_wave2d(
                                                         P2, c0, prog, ce1, ce2, FusedSpmv{});
 }
 
-// forward 2D solve with b = A v computed by the launch's blocks >= nbands (FusedSpmv)
+// forward 2D solve with b = A v computed by the launch's blocks < fs.ns (FusedSpmv)
 template <int DIV>
 __global__ __launch_bounds__((WaveCfg<DIV>::THREADS)) void k_trsv_wave2d_spmv(
     Gate g, int T, int nbands, const double *__restrict__ c1, const double *__restrict__ c2,
@@ -1660,7 +1677,19 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     // hot spot on one memory channel
     unsigned long long *dummy_ld = gran + (long long)ntask * tgran + (long long)blockIdx.x * 128 + lane;
     unsigned long long *dummy_st = dummy_ld + 64;
-    for (int task = blockIdx.x; task < ntask; task += gridDim.x) {
+    // Tiles are CLAIMED in dependency order from a queue (one agent-scope
+    // atomic per tile, issued one tile ahead by the compute wave), not dealt
+    // statically: a workgroup claims a tile only while it runs, and the
+    // smallest unfinished tile's owner has finished every tile it claimed
+    // before it, whose sources all precede it -- so any grid drains, resident
+    // or not (the occupancy API is not trusted).  q[0] = next tile,
+    // q[8] = workgroups finished; the last one re-arms both for the next launch.
+    unsigned long long *q = gran + (long long)ntask * tgran + 128LL * kTileDummyBlocks;
+    __shared__ int tq[2];                       // the current and the next claimed tile
+    if (threadIdx.x == 0) tq[0] = (int)atomicAdd(q, 1ull);
+    __syncthreads();
+    int kq = 0;                                 // tiles this workgroup has run
+    for (int task = tq[0]; task < ntask; task = tq[++kq & 1]) {
     const int band = order[FWD ? task : ntask - 1 - task];
     const int J = band % NJ, K = band / NJ;
     const long long boff = (long long)band * np * 64 + lane;     // double2 units
@@ -1889,6 +1918,10 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     double xp = 0.0;                        // this lane's value of the previous step
     double2 rg[C::PBN][C::A];
     raw_barrier();                          // barrier 0: batch 0 is in LDS
+    // the next tile, claimed now (its latency hides in this tile's batches)
+    // and handed to every wave through LDS before the task's final barrier
+    int next_task = 0;
+    if (lane == 0) next_task = (int)atomicAdd(q, 1ull);
     if (TRACE && lane == 0) {
         trace[(long long)band * TS + 0] = (long long)__builtin_amdgcn_s_memrealtime();
         trace[(long long)band * TS + 2] = blockIdx.x;
@@ -1997,10 +2030,19 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
             __hip_atomic_store(&xdone, seq + bi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     seq += nbatch;
+    if (lane == 0) tq[(kq + 1) & 1] = next_task;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();                          // final barrier: the writer drains the last batch
     if (TRACE && lane == 0) trace[(long long)band * TS + 1] = (long long)__builtin_amdgcn_s_memrealtime();
     }   // task loop
+    // every claim of this workgroup has returned: count it out; the last
+    // workgroup re-arms the queue (the next launch follows a kernel boundary)
+    if (threadIdx.x == 0) {
+        if (atomicAdd(q + 8, 1ull) == (unsigned long long)gridDim.x - 1) {
+            st_agent(q, 0ull);
+            st_agent(q + 8, 0ull);
+        }
+    }
 }
 
 // ================================================ ILU(0) factorization (device)
@@ -2688,13 +2730,45 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
 // every block sums them in sum_partials' fixed order, so h is bit-identical to
 // the per-step kernels'.  Needs all G blocks resident (checked on the host);
 // every spin is bounded (err bit 0).
-__device__ __forceinline__ unsigned long long poll_granule(const unsigned long long *p, int *err)
+// Co-residency: the grid is sized from the occupancy API, which
+// has over-promised on this pool (profiles/r03_gather_ab.txt).  So the kernels
+// do not trust it: the FIRST all-gather of a launch waits at most kResidSpin
+// polls; a block that times out there sets DONE_ABORT in the control block
+// (agent-scope atomic, drained before the block exits) and leaves.  A block
+// entering the kernel returns at once when DONE_ABORT is set -- a block that
+// was not resident can only be dispatched after some block exited, and only
+// an aborting block exits early -- and every later poll that has to retry
+// checks the flag every 256 retries, so the grid drains either way.
+// DONE_ABORT gates the rest of the enqueued cycle off; the host restores the
+// control block and reruns the cycle on the per-step kernels (same bits).
+constexpr int kResidSpin = 1 << 13;         // ~10 ms: far beyond any resident grid's first gather
+__device__ __forceinline__ int ld_agent_int(const int *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the whole block: was the cycle aborted?  (entry check, one sc1 load)
+__device__ __forceinline__ bool block_aborted(const DevState *ds)
+{
+    __shared__ int ab;
+    if (threadIdx.x == 0) ab = ld_agent_int(&ds->done) & DONE_ABORT;
+    __syncthreads();
+    return ab != 0;
+}
+__device__ __forceinline__ void set_abort(DevState *ds)
+{
+    atomicOr(&ds->done, DONE_ABORT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // performed before this block exits
+}
+
+__device__ __forceinline__ unsigned long long poll_granule(const unsigned long long *p, int *err,
+                                                          const int *abortw = nullptr)
 {
     unsigned long long a = ld_agent(p);
     int spins = 0;
     while (a == kSentinel) {
         __builtin_amdgcn_s_sleep(1);
         a = ld_agent(p);
+        if (abortw && (spins & 255) == 255 && (ld_agent_int(abortw) & DONE_ABORT)) break;
         if (++spins > kSpinLimit) {
             atomicOr(err, 1);
             break;
@@ -2703,11 +2777,38 @@ __device__ __forceinline__ unsigned long long poll_granule(const unsigned long l
     return a;
 }
 
-__device__ __forceinline__ double gather_sum(const unsigned long long *row, int G, int *err, int &par)
+__device__ __forceinline__ double gather_sum(const unsigned long long *row, int G, int *err, int &par,
+                                             const int *abortw = nullptr)
 {
     double v = 0.0;
-    for (int q = threadIdx.x; q < G; q += kBlock) v += __longlong_as_double((long long)poll_granule(row + q, err));
+    for (int q = threadIdx.x; q < G; q += kBlock)
+        v += __longlong_as_double((long long)poll_granule(row + q, err, abortw));
     return block_sum_pp(v, par);
+}
+
+// The launch's first all-gather with the co-residency bound: false = this
+// block timed out (DONE_ABORT set) and must return (block-uniform)
+__device__ __forceinline__ bool gather_first(const unsigned long long *row, int G, DevState *ds, int &par,
+                                             double &h)
+{
+    double v = 0.0;
+    int miss = 0;
+    for (int q = threadIdx.x; q < G; q += kBlock) {
+        unsigned long long a = ld_agent(row + q);
+        int spins = 0;
+        while (a == kSentinel && !miss) {
+            __builtin_amdgcn_s_sleep(1);
+            a = ld_agent(row + q);
+            if (++spins > kResidSpin) miss = 1;
+        }
+        v += __longlong_as_double((long long)a);
+    }
+    if (__syncthreads_or(miss)) {
+        if (threadIdx.x == 0) set_abort(ds);
+        return false;
+    }
+    h = block_sum_pp(v, par);
+    return true;
 }
 
 // The sum of step k's partials as every block needs it.  LEADER: block 0
@@ -2720,17 +2821,48 @@ __device__ __forceinline__ double gather_sum(const unsigned long long *row, int 
 // k_arnoldi_persist (C2) 73.2 -> 77.5 us, so every block gathers there.
 template <bool LEADER>
 __device__ __forceinline__ double gather_h(const unsigned long long *row, unsigned long long *hg, int k, int G,
-                                           int *err, int &par)
+                                           int *err, int &par, const int *abortw)
 {
     if (!LEADER || blockIdx.x == 0) {
-        const double h = gather_sum(row, G, err, par);
+        const double h = gather_sum(row, G, err, par, abortw);
         if (LEADER && threadIdx.x == 0) st_agent(hg, (unsigned long long)__double_as_longlong(h));
         return h;
     }
     __shared__ double hb[2];                    // alternating: steps k and k+2 are a block_sum apart
-    if (threadIdx.x == 0) hb[k & 1] = __longlong_as_double((long long)poll_granule(hg, err));
+    if (threadIdx.x == 0) hb[k & 1] = __longlong_as_double((long long)poll_granule(hg, err, abortw));
     __syncthreads();
     return hb[k & 1];
+}
+// step 0 of a launch: gather_h with the co-residency bound on every wait
+// (LEADER: block 0 gathers with the bound, the others' poll of its sum granule
+// is bounded alike -- whichever block is missing, every waiting block times out)
+template <bool LEADER>
+__device__ __forceinline__ bool gather_h_first(const unsigned long long *row, unsigned long long *hg, int G,
+                                               DevState *ds, int &par, double &h)
+{
+    if (!LEADER || blockIdx.x == 0) {
+        if (!gather_first(row, G, ds, par, h)) return false;
+        if (LEADER && threadIdx.x == 0) st_agent(hg, (unsigned long long)__double_as_longlong(h));
+        return true;
+    }
+    __shared__ double hb0;
+    int miss = 0;
+    if (threadIdx.x == 0) {
+        unsigned long long a = ld_agent(hg);
+        int spins = 0;
+        while (a == kSentinel && !miss) {
+            __builtin_amdgcn_s_sleep(1);
+            a = ld_agent(hg);
+            if (++spins > kResidSpin) miss = 1;
+        }
+        hb0 = __longlong_as_double((long long)a);
+    }
+    if (__syncthreads_or(miss)) {
+        if (threadIdx.x == 0) set_abort(ds);
+        return false;
+    }
+    h = hb0;
+    return true;
 }
 
 template <int J>
@@ -2743,9 +2875,11 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
                                                             long long units, int *err)
 {
     if (gated(g)) return;
+    if (block_aborted(ds)) return;                            // co-residency (gather_first)
     const int G = gridDim.x;
     const long long stride = (long long)G * kBlock;
     const long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x;
+    const int *abortw = &ds->done;
     double2 w[J], vk[J], vn[J];
 #pragma unroll
     for (int j = 0; j < J; j++) {
@@ -2775,7 +2909,12 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             for (int j = 0; j < J; j++)
                 if (u0 + j * stride < units) vn[j] = ld2_nt(vnp, u0 + j * stride);   // streamed
         }
-        const double h = gather_h<false>(gran + (long long)k * G, hg + k, k, G, err, par);
+        double h;
+        if (k == 0) {
+            if (!gather_h_first<false>(gran, hg, G, ds, par, h)) return;
+        } else {
+            h = gather_h<false>(gran + (long long)k * G, hg + k, k, G, err, par, abortw);
+        }
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         acc = 0.0;
@@ -2792,7 +2931,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(gather_h<false>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par));
+    const double hn = sqrt(gather_h<false>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par, abortw));
     if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
@@ -2856,6 +2995,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
 {
     constexpr int J = kWideJR + kWideJL;
     if (gated(g)) return;
+    if (block_aborted(ds)) return;                            // co-residency (gather_first)
+    const int *abortw = &ds->done;
     __shared__ double2 wl[kWideJL * kBlock];
     __shared__ double2 vst[(kWideJS > 0 ? kWideJS : 1) * kBlock];   // v_{k+1} (then v_k) of units j < kWideJS
     const int G = gridDim.x;
@@ -2928,7 +3069,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         asm volatile("" : "+v"(ub));
 #pragma unroll
         for (int j = 0; j < kWideD; j++) fetch(j, ub, vkp, vnp, true);    // in flight during the sum
-        const double h = gather_h<true>(gran + (long long)k * G, hg + k, k, G, err, gpar);
+        double h;
+        if (k == 0) {
+            if (!gather_h_first<true>(gran, hg, G, ds, gpar, h)) return;
+        } else {
+            h = gather_h<true>(gran + (long long)k * G, hg + k, k, G, err, gpar, abortw);
+        }
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         acc = 0.0;
@@ -2949,7 +3095,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(gather_h<true>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, gpar));
+    const double hn = sqrt(gather_h<true>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, gpar, abortw));
     if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
@@ -3232,6 +3378,11 @@ void launch_scatter_idx(const double *in, const long long *src, const long long 
     k_scatter_idx<<<blocks_for(n, kBlock, 8192), kBlock, 0, st>>>(in, src, dst, out, n);
 }
 
+void launch_fingerprint(const void *p, long long nw, unsigned long long *out, hipStream_t st)
+{
+    if (nw <= 0) return;
+    k_fingerprint<<<blocks_for(nw, kBlock, 2048), kBlock, 0, st>>>(static_cast<const unsigned *>(p), nw, out);
+}
 void launch_f64_to_f32(Gate g, const double *in, float *out, int n, hipStream_t st)
 {
     k_f64_to_f32<<<blocks_for(n, kBlock, 1 << 30), kBlock, 0, st>>>(g, in, out, n);
@@ -3306,6 +3457,22 @@ int tile3d_max_blocks()
 
 int tile_batch_steps() { return GG_TILE_BATCH; }
 
+// tests: GG_TILE_GRID = workgroups of the tile solve (beyond what can be
+// resident: the task queue must still drain it)
+static int tile_grid_override(int g)
+{
+    const char *e = std::getenv("GG_TILE_GRID");
+    return e && atoi(e) > 0 ? atoi(e) : g;
+}
+// tests: GG_PERSIST_TEST_LDS = dynamic LDS bytes added to the persistent
+// orthogonalization launches, so that fewer blocks fit than the grid needs
+// (the co-residency abort and the per-step rerun, kernels.hip gather_first)
+static size_t persist_test_lds()
+{
+    const char *e = std::getenv("GG_PERSIST_TEST_LDS");
+    return e ? (size_t)std::max(0, atoi(e)) : 0;
+}
+
 int wave_batch_steps(int div, bool d3, int skew)
 {
     // WD_MUL streams as many arrays as WD_HW (y in d's place): the same batches
@@ -3357,6 +3524,7 @@ void launch_trsv_spmv(Gate g, DevTri &T, const DevCsr &A, const double *v, doubl
     fs.cnt = T.fcnt.p;
     fs.ydiv = ydiv;
     fs.n = A.n;
+    fs.ns = ns;
     if (T.eff_div() == WD_UFMA)
         k_trsv_wave2d_spmv<WD_UFMA><<<wl.nbands + ns, WaveCfg<WD_UFMA>::THREADS, 0, st>>>(
             g, wl.T, wl.nbands, T.c1.p, T.c2.p, nullptr, nullptr, x, T.bnd.p, err, wl.P2, fs);
@@ -3442,7 +3610,8 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
             const double *k1 = sc ? T.c1s.p : T.c1.p, *k2 = sc ? T.c2s.p : T.c2.p, *k0 = sc ? T.c0s.p : T.c0.p;
 #define GG_TILE_LAUNCH(FWD, DIV)                                                                   \
     do {                                                                                           \
-        const int grid = std::min(std::min(ntask, tile3d_max_blocks<FWD, DIV>()), kTileDummyBlocks);  \
+        const int grid = std::min(std::min(ntask, tile_grid_override(tile3d_max_blocks<FWD, DIV>())), \
+                                  kTileDummyBlocks);                                                     \
         if (T.trace)                                                                               \
             k_trsv_tile3d<FWD, DIV, true><<<grid, TileCfg<DIV>::THREADS, 0, st>>>(                 \
                 g, w.T, w.NJ, w.NK, T.order.p, b, k1, k2, dv, rv, k0, x, T.bnd.p, err,              \
@@ -3642,7 +3811,8 @@ void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, do
                          unsigned long long *gran, unsigned long long *hg, int G, long long Ppad, int *err,
                          hipStream_t st)
 {
-    k_arnoldi_wide<<<G, kBlock, 0, st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2, err);
+    k_arnoldi_wide<<<G, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg,
+                                                          Ppad / 2, err);
 }
 
 void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
@@ -3652,7 +3822,7 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
 {
     const int J = arnoldi_persist_units(G, Ppad);
 #define GG_PERSIST(JJ)                                                                       \
-    k_arnoldi_persist<JJ><<<G, kBlock, 0, st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, \
+    k_arnoldi_persist<JJ><<<G, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, \
                                                  hg, Ppad / 2, err)
     if (J == 1) GG_PERSIST(1);
     else if (J == 2) GG_PERSIST(2);

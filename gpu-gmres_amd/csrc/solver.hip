@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <cmath>
 #include <cstdio>
@@ -216,11 +217,12 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         // zero granules (dummy reads) and 64 write-only ones (dummy re-arms),
         // for up to kTileDummyBlocks workgroups: one line that every boundary
         // wave polled and re-armed would be a hot spot on one memory channel
+        // (+ 64 words: the 3D tile kernel's task queue, k_trsv_tile3d)
         const long long ngran = wl->ngran();
         const long long ndummy = 128LL * kTileDummyBlocks;
-        T.bnd.alloc((size_t)(ngran + ndummy));
+        T.bnd.alloc((size_t)(ngran + ndummy + 64));
         launch_fill_u64(T.bnd.p, ngran, kSentinel, st);
-        launch_fill_u64(T.bnd.p + ngran, ndummy, 0ull, st);
+        launch_fill_u64(T.bnd.p + ngran, ndummy + 64, 0ull, st);
         // algorithmic bytes: b, two coefficients, (divisor (, reciprocal)), x per grid point
         T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
         T.bytes_mul = (double)n * (8.0 * ((unit ? 4 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
@@ -315,6 +317,7 @@ struct gg_solver {
     // round trip per restart cycle reads both)
     DevState *h_state = nullptr;
     int *h_err = nullptr;
+    int resid_fallbacks = 0;            // cycles rerun after a persistent grid was not co-resident
     // transient tap-node statistics (gg_transient_set_taps / _get_taps)
     std::vector<int> taps;
     std::vector<double> tap_max, tap_min, tap_avg;
@@ -741,7 +744,7 @@ void enqueue_cycle(gg_solver *s, int m)
     }
     Gate gu;
     gu.done = &ds->done;
-    gu.mask = DONE_RESTART | DONE_INIT;
+    gu.mask = DONE_RESTART | DONE_INIT | DONE_ABORT;
     launch_update(gu, m, ds, s->H.p, s->s.p, s->ysm.p, s->V.p, P, split || usplit ? s->y.p : s->xv.p, s->G, P,
                   s->st);
     if (split) apply_right(s, gu, s->y.p, s->xv.p);                            // x = Mr y
@@ -764,6 +767,8 @@ void enqueue_cycle(gg_solver *s, int m)
 void reset_wave(DevTri *T, hipStream_t st)
 {
     launch_fill_u64(T->bnd.p, T->wl.ngran(), kSentinel, st);
+    if (T->wl.tile)     // the tile kernel's task queue (a launch cut short would leave it armed)
+        GG_HIP(hipMemsetAsync(T->bnd.p + T->wl.ngran() + 128LL * kTileDummyBlocks, 0, 64 * sizeof(unsigned long long), st));
     if (T->fcnt.p) GG_HIP(hipMemsetAsync(T->fcnt.p, 0, T->fcnt.n * sizeof(unsigned long long), st));
     if (T->prog.p) GG_HIP(hipMemsetAsync(T->prog.p, 0, T->prog.n * sizeof(unsigned long long), st));
 }
@@ -800,6 +805,28 @@ void demote_rcp(gg_solver *s)
 {
     for (DevTri *T : {&s->L, &s->U})
         if (T->kind == DevTri::WAVE2D && T->div == WD_RCP) T->div = WD_HW;
+}
+
+// A persistent orthogonalization grid that was not co-resident aborted the
+// cycle (DONE_ABORT, kernels.hip gather_first): everything after the abort
+// point was gated off and x, r, j, hist_len are as before the cycle.  Restore
+// the control block (done = 0, resid = beta / normb as k_init_beta /
+// k_end_cycle left it), drop the persistent kernels for the solver's life and
+// run the cycle again on the per-step kernels (the same reduction tree: the
+// same bits).  Returns the state after the cycle.
+DevState rerun_aborted_cycle(gg_solver *s, int m, DevState h)
+{
+    s->persist = false;
+    s->wide = false;
+    s->resid_fallbacks++;
+    prof_collect(s, 0);                 // the aborted cycle's marks
+    h.done = 0;
+    h.resid = h.beta / h.normb;
+    GG_HIP(hipMemcpyAsync(s->ds.p, &h, sizeof(DevState), hipMemcpyHostToDevice, s->st));
+    enqueue_cycle(s, m);
+    h = read_state_checked(s);
+    GG_REQUIRE((h.done & DONE_ABORT) == 0, GG_EHIP, "gg_solve: per-step cycle aborted");
+    return h;
 }
 
 int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
@@ -858,6 +885,7 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
     bool first = opt->max_iter >= 1;
     if (first) enqueue_cycle(s, m);
     h = read_state_checked(s);
+    if (first && (h.done & DONE_ABORT)) h = rerun_aborted_cycle(s, m, h);
     int ret = 1, iters = 0, inner = 0, restarts = 0;
     long long hist_len = 1;
     double relres = h.resid;
@@ -886,6 +914,7 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
                 enqueue_cycle(s, m);
                 prev = h;
                 h = read_state_checked(s);
+                if (h.done & DONE_ABORT) h = rerun_aborted_cycle(s, m, h);
             }
             prof_collect(s, (h.done & DONE_INNER) ? h.conv_i + 1 : h.nit);
             if (h.done & DONE_INNER) {
@@ -1020,10 +1049,14 @@ int gg_destroy(gg_solver *s)
     return GG_OK;
 }
 
+static std::atomic<long long> g_set_matrix_calls{0};
+long long gg_set_matrix_count(void) { return g_set_matrix_calls.load(); }
+
 int gg_set_matrix(gg_solver *s, int n, const int *row_ptr, const int *col_idx, const double *val)
 {
     GG_API_BEGIN
     GG_REQUIRE(s, GG_EINVAL, "null solver");
+    g_set_matrix_calls++;
     check_csr(n, row_ptr, col_idx, val, "A");
     set_device(s);
     s->A = make_csr(n, row_ptr, col_idx, val);
@@ -1702,6 +1735,41 @@ int gg_solve(gg_solver *s, const double *b, double *x, const gg_options *opt, gg
     int rc = solve_device(s, s->nat_in.p, s->nat_out.p, opt, res);
     stage_out(s, s->nat_out, x);
     return rc;
+    GG_API_END
+}
+
+int gg_solve_device_f32(gg_solver *s, const float *d_b, float *d_x, const gg_options *opt, gg_result *res)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(s && d_b && d_x, GG_EINVAL, "null argument");
+    GG_REQUIRE(s->have_A, GG_ESTATE, "gg_solve: no matrix");
+    set_device(s);
+    const int n = s->A.n;
+    for (DBuf<double> *d : {&s->nat_in, &s->nat_out})
+        if (d->n < (size_t)std::max(n, 1)) d->alloc(std::max(n, 1));
+    launch_f32_to_f64(Gate{}, d_b, s->nat_in.p, n, s->st);
+    launch_f32_to_f64(Gate{}, d_x, s->nat_out.p, n, s->st);
+    const int rc = solve_device(s, s->nat_in.p, s->nat_out.p, opt, res);
+    launch_f64_to_f32(Gate{}, s->nat_out.p, d_x, n, s->st);
+    GG_HIP(hipStreamSynchronize(s->st));
+    return rc;
+    GG_API_END
+}
+
+int gg_device_fingerprint(const void *d_p, unsigned long long bytes, unsigned long long *fp)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(fp && (d_p || bytes == 0) && bytes % 4 == 0, GG_EINVAL, "gg_device_fingerprint: bad argument");
+    *fp = 0;
+    if (bytes == 0) return GG_OK;
+    // one 8-byte accumulator per host thread, never freed (a thread_local
+    // destructor would run after the HIP runtime's own teardown)
+    static thread_local unsigned long long *acc = nullptr;
+    if (!acc) GG_HIP(hipMalloc(reinterpret_cast<void **>(&acc), sizeof(unsigned long long)));
+    GG_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long), nullptr));
+    launch_fingerprint(d_p, (long long)(bytes / 4), acc, nullptr);
+    GG_HIP(hipMemcpy(fp, acc, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return GG_OK;
     GG_API_END
 }
 

@@ -32,7 +32,8 @@ EXPORTS = [
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
     "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced",
     "gg_transient_mna", "gg_set_division", "gg_division_active",
-    "gg_trsv_kernel", "gg_mgs_kernel", "gg_set_precond_user",
+    "gg_trsv_kernel", "gg_mgs_kernel", "gg_set_precond_user", "gg_solve_device_f32",
+    "gg_device_fingerprint", "gg_set_matrix_count",
 ]
 # gg_precond_fn: int (*)(void *ctx, int op, const float *in, float *out, int n), device arrays
 PRECOND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -95,6 +96,9 @@ def lib():
         L.gg_set_precond_lu.argtypes = [_VP, _I, _I, _D, _I, _I, _D]
         L.gg_set_precond_split.argtypes = [_VP, _I, _I, _D, _I, _I, _D, _D, _I, _I, _D, _D]
         L.gg_set_precond_user.argtypes = [_VP, ctypes.c_int, PRECOND_FN, ctypes.c_void_p]
+        L.gg_solve_device_f32.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options), ctypes.POINTER(Result)]
+        L.gg_device_fingerprint.argtypes = [_VP, ctypes.c_ulonglong, ctypes.POINTER(ctypes.c_ulonglong)]
+        L.gg_set_matrix_count.restype = ctypes.c_longlong
         L.gg_solve.argtypes = [_VP, _D, _D, ctypes.POINTER(Options), ctypes.POINTER(Result)]
         L.gg_solve_device.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options),
                                       ctypes.POINTER(Result)]
@@ -237,8 +241,19 @@ class Solver:
         """A caller-supplied preconditioner (the reference's Preconditioner
         plug-in): fn(op, in_ptr, out_ptr, n) -> int works on DEVICE arrays of n
         float32 (e.g. wrapped with torch); op is APPLY_MINV (split False) or
-        APPLY_LEFT / RIGHT / START / RHS (split True).  Kept alive on the solver."""
-        self._ufn = PRECOND_FN(lambda ctx, op, i, o, n: int(fn(op, i, o, n)))
+        APPLY_LEFT / RIGHT / START / RHS (split True).  Kept alive on the solver.
+        An exception raised by fn is reported to the solver as status -1 (a
+        ctypes callback that raises would return 0, i.e. success) and kept in
+        self.user_exc."""
+        self.user_exc = None
+
+        def call(ctx, op, i, o, n):
+            try:
+                return int(fn(op, i, o, n))
+            except BaseException as e:          # noqa: BLE001 -- must not cross the C frame
+                self.user_exc = e
+                return -1
+        self._ufn = PRECOND_FN(call)
         _check(lib().gg_set_precond_user(self.h, 1 if split else 0, self._ufn, None))
 
     def set_division(self, mode):

@@ -223,6 +223,18 @@ int gg_solve(gg_solver *s, const double *b, double *x, const gg_options *opt,
              gg_result *res);
 int gg_solve_device(gg_solver *s, const double *d_b, double *d_x,
                     const gg_options *opt, gg_result *res);
+/* fp32 device vectors (the reference's float* x / b, src/gmres.h:356-398): b
+ * and x promoted to fp64 and x rounded back to fp32 ON the device (no host
+ * round trip), natural order; otherwise as gg_solve_device */
+int gg_solve_device_f32(gg_solver *s, const float *d_b, float *d_x, const gg_options *opt,
+                        gg_result *res);
+/* order-independent 64-bit fingerprint of `bytes` (a multiple of 4) of device
+ * memory: sum over 32-bit words w_k of w_k * (2k + 1) modulo 2^64 (the engine
+ * ABI's check that a cached matrix was not changed in place) */
+int gg_device_fingerprint(const void *d_p, unsigned long long bytes, unsigned long long *fp);
+/* gg_set_matrix calls in this process (diagnostics: the engine ABI's setup
+ * cache, compat/engine_abi.cpp) */
+long long gg_set_matrix_count(void);
 /* residual history of the last solve: [beta0/normb, |s[i+1]|/normb per inner
  * iteration, beta/normb after each restart ...] in event order.  Returns the
  * number of entries (may exceed cap; only cap are written). */

@@ -13,6 +13,14 @@
 //     rp[n+1] ci[nnz] float val[nnz] float b[n] float x0[n]
 // OUT int32 return code, int32 max_iter (out), float tol (out), int32 calls[5]
 //     (DevPrecond/HostPrecond, _left, _right, _starting_value, _rhs), float x[n]
+// mode 4 (a transient caller, src_thermal/main2.cu:470-506): kSteps time steps
+//     of GMRES_GPU_tran with ONE GMRES_GPU_Data, b_t = b (1 + t/100), x warm-
+//     started; then the same steps through the C ABI directly (one gg_solver set
+//     up once, gg_solve_device_f32, the same plug-in as a gg_precond_fn).
+//     OUT int32 rc (last step), int32 gg_set_matrix calls during the
+//     GMRES_GPU_tran loop, double ms per step (GMRES_GPU_tran), double ms per
+//     step (C ABI), float x[n] (GMRES_GPU_tran's last step), float x[n] (C ABI)
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -21,6 +29,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "ggmres.h"
 #include "gmres.h"
 
 namespace {
@@ -94,6 +103,93 @@ T *to_dev(const std::vector<T> &h)
     return static_cast<T *>(p);
 }
 
+// the plug-in as a C-ABI operator (gg_set_precond_user): the left engine's DevPrecond
+int jacobi_fn(void *ctx, int op, const float *in, float *out, int n)
+{
+    (void)op;
+    (void)n;
+    static_cast<Jacobi *>(ctx)->DevPrecond(in, out);
+    return 0;
+}
+
+constexpr int kSteps = 100;
+
+int transient(int n, int nnz, int m, int max_it, float tol, const std::vector<int> &rp, const std::vector<int> &ci,
+              const std::vector<float> &val, const std::vector<float> &b, const std::vector<float> &x0, Jacobi &P,
+              const char *outp)
+{
+    float *d_val = to_dev(val), *d_x = to_dev(x0), *d_b = to_dev(b);
+    int *d_rp = to_dev(rp), *d_ci = to_dev(ci);
+    SpMatrixGPU Sparse;
+    std::memset(&Sparse, 0, sizeof Sparse);
+    Sparse.d_val = d_val;
+    Sparse.d_indices = d_ci;
+    Sparse.d_rowIndices = d_rp;
+    SpMatrix spm;
+    std::memset(&spm, 0, sizeof spm);
+    spm.numRows = spm.numCols = n;
+    spm.numNZEntries = nnz;
+    dim3 grid(1), block(256);
+    GMRES_GPU_Data ws;
+    ws.Initilize(m, n);
+    std::vector<float> bt(n);
+    auto rhs = [&](int t) {
+        for (int i = 0; i < n; i++) bt[i] = b[i] * (1.0f + 0.01f * (float)t);
+        check(hipMemcpy(d_b, bt.data(), sizeof(float) * n, hipMemcpyHostToDevice), "H2D b");
+    };
+    using clk = std::chrono::steady_clock;
+    // step 0 sets the engine up (the caller's first call); the timed steps follow
+    rhs(0);
+    int ret = GMRES_GPU_tran(&Sparse, &spm, &grid, &block, d_x, d_b, n, m, max_it, tol, P, ws);
+    const long long setups0 = gg_set_matrix_count();
+    auto t0 = clk::now();
+    for (int t = 1; t <= kSteps; t++) {
+        rhs(t);
+        ret = GMRES_GPU_tran(&Sparse, &spm, &grid, &block, d_x, d_b, n, m, max_it, tol, P, ws);
+    }
+    const double tran_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count() / kSteps;
+    const int setups = (int)(gg_set_matrix_count() - setups0);
+    std::vector<float> xt(n), xc(n);
+    check(hipMemcpy(xt.data(), d_x, sizeof(float) * n, hipMemcpyDeviceToHost), "D2H x");
+    // the C ABI alone: one solver, set up once, the same steps
+    check(hipMemcpy(d_x, x0.data(), sizeof(float) * n, hipMemcpyHostToDevice), "H2D x");
+    int dev = 0;
+    check(hipGetDevice(&dev), "device");
+    gg_solver *s = nullptr;
+    std::vector<double> dv(val.begin(), val.end());
+    if (gg_create(dev, &s) != GG_OK || gg_set_matrix(s, n, rp.data(), ci.data(), dv.data()) != GG_OK ||
+        gg_set_precond_user(s, 0, jacobi_fn, &P) != GG_OK) {
+        std::fprintf(stderr, "engine_driver: C ABI setup: %s\n", gg_last_error());
+        return 3;
+    }
+    gg_options o{m, max_it, (double)tol, 0};
+    gg_result res{};
+    rhs(0);
+    (void)gg_solve_device_f32(s, d_b, d_x, &o, &res);
+    t0 = clk::now();
+    for (int t = 1; t <= kSteps; t++) {
+        rhs(t);
+        if (gg_solve_device_f32(s, d_b, d_x, &o, &res) < 0) {
+            std::fprintf(stderr, "engine_driver: gg_solve_device_f32: %s\n", gg_last_error());
+            return 3;
+        }
+    }
+    const double direct_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count() / kSteps;
+    check(hipMemcpy(xc.data(), d_x, sizeof(float) * n, hipMemcpyDeviceToHost), "D2H x");
+    gg_destroy(s);
+    for (void *p : {(void *)d_val, (void *)d_x, (void *)d_b, (void *)d_rp, (void *)d_ci}) (void)hipFree(p);
+    FILE *out = std::fopen(outp, "wb");
+    if (!out) return 2;
+    std::fwrite(&ret, sizeof ret, 1, out);
+    std::fwrite(&setups, sizeof setups, 1, out);
+    std::fwrite(&tran_ms, sizeof tran_ms, 1, out);
+    std::fwrite(&direct_ms, sizeof direct_ms, 1, out);
+    std::fwrite(xt.data(), sizeof(float), n, out);
+    std::fwrite(xc.data(), sizeof(float), n, out);
+    std::fclose(out);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv)
@@ -122,6 +218,7 @@ int main(int argc, char **argv)
     Jacobi P;
     P.Initilize(A);
 
+    if (mode == 4) return transient(n, nnz, m, max_it, tol, rp, ci, val, b, x, P, argv[2]);
     int ret = 1;
     if (mode == 3) {                                // host engine, host arrays
         ret = GMRESilu(val.data(), rp.data(), ci.data(), x.data(), b.data(), n, m, &max_it, &tol, P);

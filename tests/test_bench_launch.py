@@ -68,3 +68,48 @@ def test_bench_refuses_bad_world(argv, env, code):
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == code, p.stderr[-2000:]
     assert "bench.py:" in p.stderr
+
+
+LOCKSTEP = r"""
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+import torch, torch.distributed as dist
+import bench
+dist.init_process_group("gloo", init_method="env://")
+rank = dist.get_rank()
+fail = sys.argv[3]                   # "<phase>:<rank>" or "none"
+ran = []
+
+def step(name):
+    def fn():
+        ran.append(name)
+        if name == "connect":        # a collective inside a step, as bench_dd's all_gather_object
+            lst = [None] * dist.get_world_size()
+            dist.all_gather_object(lst, rank)
+        if fail == f"{name}:{rank}":
+            raise RuntimeError("injected")
+    return fn
+
+ok = bench.lockstep(torch, dist, None, rank, [(n, step(n)) for n in ("create", "connect", "check")])
+with open(os.path.join(sys.argv[2], f"r{rank}.json"), "w") as f:
+    json.dump({"ok": ok, "ran": ran}, f)
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("fail", ["none", "create:1", "connect:0", "check:1"])
+def test_ipc_setup_lockstep_fallback(tmp_path, fail):
+    """bench_dd's IPC setup (bench.lockstep): a step failing on ONE rank takes
+    every rank to the RCCL fallback at that step -- no rank is left waiting in a
+    later step's collective (2 gloo ranks on CPU)"""
+    script = tmp_path / "lockstep.py"
+    script.write_text(LOCKSTEP)
+    t0 = time.time()
+    rc = bench.spawn_ranks(2, [sys.executable, str(script), REPO, str(tmp_path), fail], visible=2)
+    assert rc == 0 and time.time() - t0 < 120
+    res = [json.loads((tmp_path / f"r{r}.json").read_text()) for r in range(2)]
+    order = ["create", "connect", "check"]
+    stop = order.index(fail.split(":")[0]) + 1 if fail != "none" else 3
+    for r in res:
+        assert r["ok"] == (fail == "none")
+        assert r["ran"] == order[:stop]          # every rank stopped after the same step

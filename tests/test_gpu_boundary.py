@@ -264,3 +264,29 @@ def test_engine_abi_preconditioner_plugin(tmp_path, mode):
     else:                # _rhs for b and residuals, _left / _right per iteration, _starting_value once
         assert calls[0] == 0 and calls[3] == 1 and calls[4] >= 2
         assert abs(calls[1] - iters) <= 2 and calls[2] >= calls[1]
+
+
+def test_engine_abi_tran_keeps_its_solver(tmp_path):
+    """a transient caller (src_thermal/main2.cu:470-506) runs
+    100 GMRES_GPU_tran steps with one GMRES_GPU_Data: the engine is set up by the
+    first call only (no gg_set_matrix during the 100 steps), each step costs
+    within 10 % of the same solve through the C ABI alone (one gg_solver set up
+    once, gg_solve_device_f32, the same plug-in), and both give the same bits"""
+    A64 = M.laplacian_5pt(64)
+    A64.data = A64.data + np.random.default_rng(5).uniform(-0.3, 0.3, A64.nnz)
+    A = sp.csr_matrix((A64.data.astype(np.float32), A64.indices, A64.indptr), shape=A64.shape)
+    n = A.shape[0]
+    b = (sp.csr_matrix((A.data.astype(np.float64), A.indices, A.indptr), shape=A.shape) @ np.ones(n))
+    b = b.astype(np.float32)
+    x0 = np.zeros(n, np.float32)
+    hdr = struct.pack("<5if", 4, n, A.nnz, 30, 2000, 1e-5)
+    payload = hdr + _csr_bytes(A.indptr, A.indices, A.data, np.float32) + b.tobytes() + x0.tobytes()
+    data, _ = _run("engine_driver", payload, tmp_path, 8 + 16 + 8 * n)
+    rc, setups = struct.unpack_from("<ii", data, 0)
+    tran_ms, direct_ms = struct.unpack_from("<dd", data, 8)
+    xt = np.frombuffer(data, np.float32, n, 24)
+    xc = np.frombuffer(data, np.float32, n, 24 + 4 * n)
+    print(f"GMRES_GPU_tran {tran_ms:.3f} ms/step, C ABI alone {direct_ms:.3f} ms/step, setups {setups}")
+    assert rc == 0 and setups == 0
+    assert tran_ms <= 1.10 * direct_ms + 0.05, (tran_ms, direct_ms)
+    assert np.array_equal(xt, xc)
