@@ -103,7 +103,7 @@ bool fetch(void *dst, const void *src, size_t bytes, bool device)
 // (one mutex).
 struct Ctx {
     gg_solver *s = nullptr;
-    int dev = 0, n = 0, nnz = 0, split = 0;
+    int dev = 0, n = 0, nnz = 0, r0 = 0, split = 0;
     bool device = false;
     const void *val = nullptr, *rp = nullptr, *ci = nullptr, *owner = nullptr;
     unsigned long long fp = 0;
@@ -132,18 +132,16 @@ unsigned long long host_fingerprint(const void *p, size_t bytes)
 bool csr_fingerprint(bool device, const float *val, const int *rp, const int *ci, int n, int nnz,
                      unsigned long long &fp)
 {
-    const size_t b[3] = {sizeof(float) * (size_t)nnz, sizeof(int) * ((size_t)n + 1), sizeof(int) * (size_t)nnz};
+    const unsigned long long b[3] = {sizeof(float) * (unsigned long long)nnz,
+                                     sizeof(int) * ((unsigned long long)n + 1), sizeof(int) * (unsigned long long)nnz};
     const void *p[3] = {val, rp, ci};
-    fp = 0;
-    for (int k = 0; k < 3; k++) {
-        unsigned long long f = 0;
-        if (device) {
-            if (gg_device_fingerprint(p[k], b[k], &f) != GG_OK) return false;
-        } else {
-            f = host_fingerprint(p[k], b[k]);
-        }
-        fp = fp * 0x9E3779B97F4A7C15ull + f;
+    unsigned long long f[3] = {0, 0, 0};
+    if (device) {
+        if (gg_device_fingerprint(p, b, 3, f) != GG_OK) return false;
+    } else {
+        for (int k = 0; k < 3; k++) f[k] = host_fingerprint(p[k], b[k]);
     }
+    fp = (f[0] * 0x9E3779B97F4A7C15ull + f[1]) * 0x9E3779B97F4A7C15ull + f[2];
     return true;
 }
 
@@ -157,6 +155,23 @@ Ctx *context(const char *who, bool device, int split, const float *val, const in
     };
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    Ctx *c = nullptr;
+    for (auto &e : g_cache)
+        if (e->dev == dev && e->device == device && e->split == split && e->val == val && e->rp == rp &&
+            e->ci == ci && e->n == n && e->owner == owner) {
+            c = e.get();
+            break;
+        }
+    // a cached entry: one fingerprint round trip over its extent (a changed
+    // rp[0] / rp[n] changes the row pointers' fingerprint)
+    if (c && c->fp) {
+        unsigned long long fp = 0;
+        if (!csr_fingerprint(device, val + c->r0, rp, ci + c->r0, n, c->nnz, fp)) return fail("fingerprint", GG_EHIP);
+        if (fp == c->fp) {
+            c->used = ++g_tick;
+            return c;
+        }
+    }
     int r0 = 0, rn = 0;
     if (!fetch(&r0, rp, sizeof(int), device) || !fetch(&rn, rp + n, sizeof(int), device))
         return fail("row pointers", GG_EHIP);
@@ -164,17 +179,6 @@ Ctx *context(const char *who, bool device, int split, const float *val, const in
     if (nnz < 0) return fail("row pointers", GG_EINVAL);
     unsigned long long fp = 0;
     if (!csr_fingerprint(device, val + r0, rp, ci + r0, n, nnz, fp)) return fail("fingerprint", GG_EHIP);
-    Ctx *c = nullptr;
-    for (auto &e : g_cache)
-        if (e->dev == dev && e->device == device && e->split == split && e->val == val && e->rp == rp &&
-            e->ci == ci && e->n == n && e->nnz == nnz && e->owner == owner) {
-            c = e.get();
-            break;
-        }
-    if (c && c->fp == fp) {
-        c->used = ++g_tick;
-        return c;
-    }
     if (!c) {
         if (g_cache.size() >= kCacheCap) {
             auto lru = std::min_element(g_cache.begin(), g_cache.end(),
@@ -192,7 +196,6 @@ Ctx *context(const char *who, bool device, int split, const float *val, const in
         c->rp = rp;
         c->ci = ci;
         c->n = n;
-        c->nnz = nnz;
         c->owner = owner;
         int rc = gg_create(dev, &c->s);
         if (rc != GG_OK) {
@@ -200,6 +203,8 @@ Ctx *context(const char *who, bool device, int split, const float *val, const in
             return fail("gg_create", rc);
         }
     }
+    c->r0 = r0;
+    c->nnz = nnz;
     // (re)build: the matrix in fp64 (the reference's float values promoted)
     std::vector<int> hrp(n + 1), hci(nnz);
     std::vector<float> hv(nnz);

@@ -1756,19 +1756,22 @@ int gg_solve_device_f32(gg_solver *s, const float *d_b, float *d_x, const gg_opt
     GG_API_END
 }
 
-int gg_device_fingerprint(const void *d_p, unsigned long long bytes, unsigned long long *fp)
+int gg_device_fingerprint(const void *const *d_p, const unsigned long long *bytes, int count,
+                          unsigned long long *fp)
 {
     GG_API_BEGIN
-    GG_REQUIRE(fp && (d_p || bytes == 0) && bytes % 4 == 0, GG_EINVAL, "gg_device_fingerprint: bad argument");
-    *fp = 0;
-    if (bytes == 0) return GG_OK;
-    // one 8-byte accumulator per host thread, never freed (a thread_local
-    // destructor would run after the HIP runtime's own teardown)
+    constexpr int kMax = 16;
+    GG_REQUIRE(d_p && bytes && fp && count >= 0 && count <= kMax, GG_EINVAL, "gg_device_fingerprint: bad argument");
+    for (int i = 0; i < count; i++)
+        GG_REQUIRE((d_p[i] || bytes[i] == 0) && bytes[i] % 4 == 0, GG_EINVAL, "gg_device_fingerprint: bad buffer");
+    if (count == 0) return GG_OK;
+    // kMax accumulators per host thread, never freed (a thread_local destructor
+    // would run after the HIP runtime's own teardown)
     static thread_local unsigned long long *acc = nullptr;
-    if (!acc) GG_HIP(hipMalloc(reinterpret_cast<void **>(&acc), sizeof(unsigned long long)));
-    GG_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long), nullptr));
-    launch_fingerprint(d_p, (long long)(bytes / 4), acc, nullptr);
-    GG_HIP(hipMemcpy(fp, acc, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (!acc) GG_HIP(hipMalloc(reinterpret_cast<void **>(&acc), kMax * sizeof(unsigned long long)));
+    GG_HIP(hipMemsetAsync(acc, 0, count * sizeof(unsigned long long), nullptr));
+    for (int i = 0; i < count; i++) launch_fingerprint(d_p[i], (long long)(bytes[i] / 4), acc + i, nullptr);
+    GG_HIP(hipMemcpy(fp, acc, count * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return GG_OK;
     GG_API_END
 }

@@ -97,7 +97,8 @@ def lib():
         L.gg_set_precond_split.argtypes = [_VP, _I, _I, _D, _I, _I, _D, _D, _I, _I, _D, _D]
         L.gg_set_precond_user.argtypes = [_VP, ctypes.c_int, PRECOND_FN, ctypes.c_void_p]
         L.gg_solve_device_f32.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options), ctypes.POINTER(Result)]
-        L.gg_device_fingerprint.argtypes = [_VP, ctypes.c_ulonglong, ctypes.POINTER(ctypes.c_ulonglong)]
+        L.gg_device_fingerprint.argtypes = [ctypes.POINTER(_VP), ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_ulonglong)]
         L.gg_set_matrix_count.restype = ctypes.c_longlong
         L.gg_solve.argtypes = [_VP, _D, _D, ctypes.POINTER(Options), ctypes.POINTER(Result)]
         L.gg_solve_device.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options),

@@ -228,10 +228,12 @@ int gg_solve_device(gg_solver *s, const double *d_b, double *d_x,
  * round trip), natural order; otherwise as gg_solve_device */
 int gg_solve_device_f32(gg_solver *s, const float *d_b, float *d_x, const gg_options *opt,
                         gg_result *res);
-/* order-independent 64-bit fingerprint of `bytes` (a multiple of 4) of device
- * memory: sum over 32-bit words w_k of w_k * (2k + 1) modulo 2^64 (the engine
- * ABI's check that a cached matrix was not changed in place) */
-int gg_device_fingerprint(const void *d_p, unsigned long long bytes, unsigned long long *fp);
+/* order-independent 64-bit fingerprints of `count` device buffers (bytes[i] a
+ * multiple of 4): fp[i] = sum over the 32-bit words w_k of d_p[i] of
+ * w_k * (2k + 1) modulo 2^64 -- one host round trip for all of them (the
+ * engine ABI's check that a cached matrix was not changed in place) */
+int gg_device_fingerprint(const void *const *d_p, const unsigned long long *bytes, int count,
+                          unsigned long long *fp);
 /* gg_set_matrix calls in this process (diagnostics: the engine ABI's setup
  * cache, compat/engine_abi.cpp) */
 long long gg_set_matrix_count(void);

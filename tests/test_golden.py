@@ -70,15 +70,20 @@ def test_golden_independent_checks(gold, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("division", ["exact", "fma"])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_device_matches_golden(gold, name):
+def test_device_matches_golden(gold, name, division):
     """The device solve against the committed vectors: same return code and
     iteration count, residual history within 1e-10 of its scale, solution
-    within 1e-10 relative."""
+    within 1e-10 relative -- with the reference's division (exact) and with
+    the bench's default arithmetic (fma: GG_DIV_FMA's fused rows where the
+    wavefront admits them)."""
     import ggmres
     A = CASES[name]()
     s = ggmres.Solver(0)
     try:
+        if division == "fma":
+            s.set_division(ggmres.DIV_FMA)
         s.set_matrix(A)
         s.set_precond_ilu0()
         for rn, rf in RHS.items():

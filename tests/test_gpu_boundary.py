@@ -272,7 +272,8 @@ def test_engine_abi_tran_keeps_its_solver(tmp_path):
     first call only (no gg_set_matrix during the 100 steps), each step costs
     within 10 % of the same solve through the C ABI alone (one gg_solver set up
     once, gg_solve_device_f32, the same plug-in), and both give the same bits"""
-    A64 = M.laplacian_5pt(64)
+    A64 = (M.laplacian_5pt(64) + 2.0 * sp.identity(64 * 64)).tocsr()     # diagonally dominant: ~20 iterations
+    A64.sort_indices()
     A64.data = A64.data + np.random.default_rng(5).uniform(-0.3, 0.3, A64.nnz)
     A = sp.csr_matrix((A64.data.astype(np.float32), A64.indices, A64.indptr), shape=A64.shape)
     n = A.shape[0]
