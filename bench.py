@@ -312,7 +312,7 @@ def bench_dd(a, torch, dist, world, rank, local):
         # kernel storing into the peers' areas over xGMI
         import ggmres
         boot = dist.new_group(backend="gloo")
-        d, hb = None, None
+        d, hb, ranks = None, None, None
 
         def create():
             nonlocal d, hb
@@ -329,6 +329,7 @@ def bench_dd(a, torch, dist, world, rank, local):
             d.ipc_connect(lst)
 
         def check():
+            nonlocal ranks
             ranks, myrank = d.comm_ranks()                  # an exchange: bounded (30 s) on the device
             if ranks != world or myrank != rank:
                 raise RuntimeError(f"{ranks} ranks mapped (rank {myrank})")
@@ -374,18 +375,76 @@ def bench_dd(a, torch, dist, world, rank, local):
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
-        step()
+    from ggmres import dd as DDM
+
+    def families(inner_run, el):
+        """this rank's per-family event timing (every inner iteration's families
+        bracketed; the shards of this process)"""
+        fam = {}
+        for k, name in enumerate(DDM.PROF_NAMES):
+            cnt, ms = d.profile_get(k)
+            if cnt == 0:
+                continue
+            fam[name] = {"launches": cnt, "avg_us": round(ms * 1e3 / cnt, 3),
+                         "share_of_step": round(ms / (el * 1e3), 4)}
+            if k in (DDM.PROF_SPMV, DDM.PROF_TRSV_L, DDM.PROF_TRSV_U):
+                byt = d.bytes(k)
+                fam[name]["alg_bytes_per_launch"] = byt
+                fam[name]["achieved_gbs"] = round(byt / (ms * 1e-3 / cnt) / 1e9, 1)
+        return fam
+
+    # per-family breakdown in the last warmup step (events around every family
+    # cost time, so that pass stays out of the timed region); then only the
+    # dominant single-kernel family (SpMV, interior L, interior U) is bracketed
+    # inside the timed region, for the roofline
+    fam = {}
+    for w in range(a.warmup):
+        if w == a.warmup - 1 and not a.no_profile:
+            d.profile(True)
+            barrier()
+            t1 = time.perf_counter()
+            r0 = step()
+            barrier()
+            fam = families(r0["inner"], time.perf_counter() - t1)
+            d.profile(False)
+        else:
+            step()
+    single = {k: v for k, v in fam.items() if "alg_bytes_per_launch" in v}
+    dom = max(single, key=lambda k: single[k]["share_of_step"]) if single else None
+    if dom:
+        d.profile(True, kinds=[DDM.PROF_NAMES.index(dom)])
     barrier()
     t0 = time.perf_counter()
     res = [step() for _ in range(a.steps)]
     barrier()
     el = time.perf_counter() - t0
+    timed = families(None, el) if dom else {}
+    d.profile(False)
     t = torch.tensor([el], dtype=torch.float64, device="cpu" if ONE_GPU else "cuda")
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el_max = float(t.item())
     inner = sum(r["inner"] for r in res)          # one system: every rank counts the same
+    roof = None
+    wi = d.info()["wave_interior"]
+    kname = {"spmv": "k_spmv_sell<false> / k_spmv_stream<false> (interior + separator rows)",
+             "trsv_L": {2: "k_trsv_wave2d (interior L, 2D band wavefront)",
+                        3: "k_trsv_tile3d (interior L, 3D tile wavefront)"}.get(wi, "k_trsv_flow (interior L)"),
+             "trsv_U": {2: "k_trsv_wave2d (interior U, 2D band wavefront)",
+                        3: "k_trsv_tile3d (interior U, 3D tile wavefront)"}.get(wi, "k_trsv_flow (interior U)")}
+    if dom and dom in timed:
+        f = timed[dom]
+        roof = {"kernel": kname[dom], "bound": "hbm", "achieved": f["achieved_gbs"], "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
+                "launches_timed": f["launches"], "rank": rank,
+                "note": "per rank (its own shard), event-timed inside the timed region on the solver's stream"}
+    # every rank's breakdown next to the exchange latency (rank 0 prints them)
+    per_rank = [{"rank": rank, "kernels": fam}]
+    if dist:
+        lst = [None] * world
+        dist.all_gather_object(lst, per_rank[0])
+        per_rank = lst
     parts = world if world > 1 else a.dd_parts
     # the exchange every sharded operator and dot pays, timed after the timed
     # region: one dot's G partials, and CGS2's (i+1) G at i = 15
@@ -422,7 +481,9 @@ def bench_dd(a, torch, dist, world, rank, local):
                                       2: "2D wavefront", 3: "3D tile wavefront"}.get(info["wave_separator"]),
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
                    "parallelism": f"dd{parts}", "setup_s": round(t_setup, 3)},
-        "roofline": None,
+        "roofline": roof,
+        "kernels_per_rank": per_rank,
+        "kernels_from": "one profiled warmup step per rank, every family bracketed by hipEvents",
         "cpu_baseline": None,
     }
     if rank == 0:

@@ -103,6 +103,16 @@ struct gg_dd {
     std::vector<double> last_hist;
     DBuf<double> nat_a, nat_b;
     DBuf<long long> dtmp;
+    // in-solve timing (gg_dd_profile_*): hipEvent pairs on the solver's stream
+    // around each family of an inner iteration, accounted for the iterations
+    // that really ran (as the single solver's gg_profile_*)
+    int prof_mask = 0;
+    std::vector<hipEvent_t> prof_pool;
+    size_t prof_used = 0;
+    struct Mark { int kind, i, e0, e1; };
+    std::vector<Mark> marks;
+    double prof_ms[GG_DD_PROF_NKINDS] = {};
+    long long prof_cnt[GG_DD_PROF_NKINDS] = {};
 };
 
 namespace {
@@ -222,6 +232,41 @@ void halo(gg_dd *d, const Get &x, hipStream_t st)
 
 Get vec(DBuf<double> Shard::*m) { return [m](Shard &s) { return (s.*m).p; }; }
 
+// ---- in-solve profiling ------------------------------------------------------
+int prof_event(gg_dd *d)
+{
+    if (d->prof_used == d->prof_pool.size()) {
+        hipEvent_t e;
+        GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));   // timing only
+        d->prof_pool.push_back(e);
+    }
+    GG_HIP(hipEventRecord(d->prof_pool[d->prof_used], d->st));
+    return (int)d->prof_used++;
+}
+int prof_begin(gg_dd *d, int kind, int i)
+{
+    if (i < 0 || !((d->prof_mask >> kind) & 1)) return -1;
+    d->marks.push_back({kind, i, prof_event(d), -1});
+    return (int)d->marks.size() - 1;
+}
+void prof_end(gg_dd *d, int mark)
+{
+    if (mark >= 0) d->marks[mark].e1 = prof_event(d);
+}
+void prof_collect(gg_dd *d, int executed)
+{
+    if (!d->prof_mask) return;
+    for (const auto &mk : d->marks) {
+        if (mk.i >= executed || mk.e1 < 0) continue;
+        float ms = 0.f;
+        GG_HIP(hipEventElapsedTime(&ms, d->prof_pool[mk.e0], d->prof_pool[mk.e1]));
+        d->prof_ms[mk.kind] += ms;
+        d->prof_cnt[mk.kind]++;
+    }
+    d->marks.clear();
+    d->prof_used = 0;
+}
+
 // gate of a phase: inner iteration gi (>= 0), else the done-mask (0 = ungated)
 Gate gate_of(Shard &s, int gi, int mask)
 {
@@ -233,11 +278,14 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
 {
     const long long S0 = d->S0;
     auto gate = [&](Shard &s) { return gate_of(s, gi, mask); };
+    int mk = prof_begin(d, GG_DD_PROF_TRSV_L, gi);
     for (auto &sp : d->sh) {
         Shard &s = *sp;
         for (DevTri *T : {&s.LI, &s.LS, &s.UI, &s.US}) T->fast = d->div_mode;
         launch_trsv(gate(s), s.LI, in(s), s.t1.p, s.err.p + s.p, d->st);          // y_I
     }
+    prof_end(d, mk);
+    mk = prof_begin(d, GG_DD_PROF_SEP, gi);
     // interface y (halo); the fused separator step's sentinel fills ride on the gathers
     const bool xch = d->maxI > 0 && d->P > 1;
     for (auto &sp : d->sh) {
@@ -264,7 +312,6 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
             f.ph[2] = SepPhase{s.UIS.rp.p, s.UIS.ci.p, s.UIS.v.p, out(s), nullptr, nullptr,
                                nullptr, nullptr, s.t1.p, nullptr, s.t1.p, false};
             launch_sep_flow(g, s.sf_ntask, s.sf_tasks.p, s.sf_rows.p, f, s.err.p + s.p, d->st);
-            launch_trsv(g, s.UI, s.t1.p, out(s), s.err.p + s.p, d->st);               // x_I
             continue;
         }
         // the separator solves' sentinel fills ride on the subtraction's launch
@@ -276,8 +323,14 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
         launch_trsv(g, s.US, s.t1.p + S0, out(s) + S0, s.err.p + s.p, d->st);     // x_S
         s.LS.prefilled = s.US.prefilled = false;
         launch_sub_seq(g, s.UIS, out(s), s.t1.p, s.t2.p, d->st);                  // y_I - U_IS x_S
-        launch_trsv(g, s.UI, s.t2.p, out(s), s.err.p + s.p, d->st);               // x_I
     }
+    prof_end(d, mk);
+    mk = prof_begin(d, GG_DD_PROF_TRSV_U, gi);
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        launch_trsv(gate(s), s.UI, s.sepflow ? s.t1.p : s.t2.p, out(s), s.err.p + s.p, d->st);   // x_I
+    }
+    prof_end(d, mk);
 }
 
 // y = A x (b = null) or y = b - A x: the interior rows reference only their
@@ -374,8 +427,11 @@ void enqueue_cycle(gg_dd *d, int m)
     for (auto &sp : d->sh) launch_init_cycle(sp->ds.p, sp->r.p, sp->V.p, sp->s.p, d->G, H0, d->st);
     for (int i = 0; i < m; i++) {
         const Get vi = [i, Pl](Shard &s) { return s.V.p + (long long)i * Pl; };
+        int mk = prof_begin(d, GG_DD_PROF_SPMV, i);
         spmv(d, i, vi, vec(&Shard::ww));                                        // ww = A v_i
+        prof_end(d, mk);
         apply_minv(d, i, 0, vec(&Shard::ww), vec(&Shard::w));                   // w = M^-1 ww
+        mk = prof_begin(d, GG_DD_PROF_ORTH, i);
         if (d->cgs2) {
             // CGS2: h = V^T w, w -= V h, h2 = V^T w, w -= V h2 (+ the norm's
             // partials), H[:, i] = h + h2 -- three all-gathers
@@ -414,6 +470,7 @@ void enqueue_cycle(gg_dd *d, int m)
                                           s.V.p + (long long)(i + 1) * Pl, s.H.p, s.cs.p, s.sn.p, s.s.p,
                                           s.hist.p, H0, d->st);
             }
+            prof_end(d, mk);
             continue;
         }
         dot(d, i, 0, vec(&Shard::w), [](Shard &s) { return s.V.p; }, &Shard::partA);
@@ -436,6 +493,7 @@ void enqueue_cycle(gg_dd *d, int m)
                                       s.V.p + (long long)(i + 1) * Pl, s.H.p, s.cs.p, s.sn.p, s.s.p,
                                       s.hist.p, H0, d->st);
         }
+        prof_end(d, mk);
     }
     for (auto &sp : d->sh) {
         Shard &s = *sp;
@@ -461,7 +519,11 @@ DevState read_state(gg_dd *d)
     return h[0];
 }
 
-struct RcpFallback {};
+// err bit 1: WD_RCP range (divide instead), bit 3: a static tile grid was not
+// co-resident (claim tiles from the queue) -- apply_fallback, then repeat
+struct Fallback {
+    int bits;
+};
 void check_err(gg_dd *d)
 {
     int any = 0;
@@ -486,14 +548,17 @@ void check_err(gg_dd *d)
         GG_HIP(hipStreamSynchronize(d->st));
         for (int v : e) any |= v;
     }
+    if (any & 8) throw Fallback{any};
     GG_REQUIRE((any & 1) == 0, GG_ETIMEOUT, "dd: wavefront triangular solve: boundary wait timed out");
-    if (any & 2) throw RcpFallback{};
+    if (any & 2) throw Fallback{any};
 }
-void demote_rcp(gg_dd *d)
+void apply_fallback(gg_dd *d, const Fallback &f)
 {
     for (auto &sp : d->sh)
-        for (DevTri *T : {&sp->LI, &sp->LS, &sp->UI, &sp->US})
-            if (T->kind == DevTri::WAVE2D && T->div == WD_RCP) T->div = WD_HW;
+        for (DevTri *T : {&sp->LI, &sp->LS, &sp->UI, &sp->US}) {
+            if ((f.bits & 2) && T->kind == DevTri::WAVE2D && T->div == WD_RCP) T->div = WD_HW;
+            if ((f.bits & 8) && T->kind == DevTri::WAVE2D && T->wl.tile) T->tile_queue = true;
+        }
 }
 void reset_waves(gg_dd *d)
 {
@@ -569,6 +634,7 @@ int solve_once(gg_dd *d, const double *d_b, double *d_x, const gg_options *opt, 
             DevState prev = h;
             h = read_state(d);
             check_err(d);
+            prof_collect(d, (h.done & DONE_INNER) ? h.conv_i + 1 : h.nit);
             if (h.done & DONE_INNER) {
                 ret = 0;
                 iters = prev.j + h.conv_i;
@@ -612,11 +678,13 @@ int solve_once(gg_dd *d, const double *d_b, double *d_x, const gg_options *opt, 
 
 int solve_dev(gg_dd *d, const double *d_b, double *d_x, const gg_options *opt, gg_result *res)
 {
-    try {
-        return solve_once(d, d_b, d_x, opt, res);
-    } catch (RcpFallback &) {
-        demote_rcp(d);
-        return solve_once(d, d_b, d_x, opt, res);
+    for (int attempt = 0;; attempt++) {
+        try {
+            return solve_once(d, d_b, d_x, opt, res);
+        } catch (Fallback &f) {
+            if (attempt >= 2) throw Error{GG_EHIP, "gg_dd_solve: fallbacks exhausted"};
+            apply_fallback(d, f);
+        }
     }
 }
 
@@ -1122,6 +1190,51 @@ int gg_dd_time_exchange(gg_dd *d, long long cnt, int reps, double *avg_us)
     GG_API_END
 }
 
+int gg_dd_profile_enable(gg_dd *d, int kinds)
+{
+    if (!d) return GG_EINVAL;
+    d->prof_mask = kinds & ((1 << GG_DD_PROF_NKINDS) - 1);
+    return GG_OK;
+}
+int gg_dd_profile_reset(gg_dd *d)
+{
+    if (!d) return GG_EINVAL;
+    for (int k = 0; k < GG_DD_PROF_NKINDS; k++) {
+        d->prof_ms[k] = 0;
+        d->prof_cnt[k] = 0;
+    }
+    return GG_OK;
+}
+int gg_dd_profile_get(gg_dd *d, int kind, int *launches, double *total_ms)
+{
+    if (!d || kind < 0 || kind >= GG_DD_PROF_NKINDS || !launches || !total_ms) return GG_EINVAL;
+    *launches = (int)d->prof_cnt[kind];
+    *total_ms = d->prof_ms[kind];
+    return GG_OK;
+}
+int gg_dd_bytes(gg_dd *d, int kind, double *bytes)
+{
+    if (!d || !bytes || !d->have) return GG_EINVAL;
+    // algorithmic bytes of one family launch for the shards of this process
+    // (each operand once, each result once)
+    double b = 0;
+    for (auto &sp : d->sh) {
+        Shard &s = *sp;
+        if (kind == GG_DD_PROF_SPMV) {
+            for (const DevCsr *A : {&s.AI, &s.AS})
+                b += 12.0 * A->nnz + 4.0 * (A->n + 1) + 16.0 * A->n;
+        } else if (kind == GG_DD_PROF_TRSV_L) {
+            b += s.LI.alg_bytes();
+        } else if (kind == GG_DD_PROF_TRSV_U) {
+            b += s.UI.alg_bytes();
+        } else {
+            return GG_EINVAL;
+        }
+    }
+    *bytes = b;
+    return GG_OK;
+}
+
 int gg_dd_precond_apply(gg_dd *d, const double *in, double *out)
 {
     GG_API_BEGIN
@@ -1137,11 +1250,14 @@ int gg_dd_precond_apply(gg_dd *d, const double *in, double *out)
         apply_minv(d, -1, 0, vec(&Shard::xv), vec(&Shard::ww));
         check_err(d);
     };
-    try {
-        run();
-    } catch (RcpFallback &) {
-        demote_rcp(d);
-        run();
+    for (int attempt = 0;; attempt++) {
+        try {
+            run();
+            break;
+        } catch (Fallback &f) {
+            if (attempt >= 2) throw Error{GG_EHIP, "gg_dd_precond_apply: fallbacks exhausted"};
+            apply_fallback(d, f);
+        }
     }
     scatter_out(d, &Shard::ww, d->nat_b.p);
     fetch_nat(d, d->nat_b, out);

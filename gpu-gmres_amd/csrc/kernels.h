@@ -32,6 +32,17 @@ struct Gate {
     int i = 0;
 };
 
+// Which 16-B units (slot pairs) of a solver's vector space hold at least one
+// real row: the wavefront layouts pad every line to T steps (C2: 10 %, C4:
+// 11 % of the slots), and every vector is +0 there, so the orthogonalization
+// and the update skip those units -- the same sums, bit for bit (a +0 term
+// never changes a partial that starts at +0), fewer bytes
+struct UnitMap {
+    int kind = -1;        // -1 every unit, 0 natural order (n rows), 1 2D band wavefront, 2 3D tiles
+    int nx = 0, ny = 0, nz = 1, T = 0, skew = 1, NJ = 0, nbands = 0;
+    long long n = 0;
+};
+
 constexpr int kBlock = 256;
 constexpr unsigned long long kSentinel = 0x7FF4DEAD0000BEEFull;  // sNaN payload: "not ready"
 
@@ -163,19 +174,27 @@ void launch_arnoldi_finalize(Gate g, int i, int m, DevState *ds, const double *p
 // units per thread (1/2/4/8, 0 = too many), how many blocks can be resident
 int arnoldi_persist_units(int G, long long Ppad);
 int arnoldi_persist_max_blocks(int J);
+// xb: per inner step kMgsXcdWords words (the XCD-local gather's slots, kernels.hip
+// gather_xcd; re-armed with the granules), elect: kMgsElectWords words (zeroed
+// once), seq: strictly increasing per launch
+constexpr int kMgsXcdWords = 8 * 16, kMgsElectWords = 8 * 16;
+int mgs_gather_form();   // GG_MGS_GATHER: 0 every block gathers, 2 XCD-local reducers
+int mgs_prefetch();      // GG_MGS_PREFETCH: 1 v_{k+1} streamed during the gather, 0 after it
 void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
                             long long ldv, double *H, double *cs, double *sn, double *s,
                             double *hist, unsigned long long *gran, unsigned long long *hg, int G,
-                            long long Ppad, int *err, hipStream_t st);
+                            long long Ppad, int *err, unsigned long long *xb, unsigned long long *elect,
+                            unsigned long long seq, const UnitMap &um, hipStream_t st);
 // the same for long vectors (w on chip, the basis streamed): kWideG blocks
 constexpr int kWideG = 512;
 bool arnoldi_wide_ok(int G, long long Ppad);
 void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, double *V, long long ldv,
                          double *H, double *cs, double *sn, double *s, double *hist,
                          unsigned long long *gran, unsigned long long *hg, int G, long long Ppad, int *err,
-                         hipStream_t st);
+                         const UnitMap &um, hipStream_t st);
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
-                   const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st);
+                   const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st,
+                   const UnitMap &um = UnitMap{});
 void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st);
 
 }  // namespace gg

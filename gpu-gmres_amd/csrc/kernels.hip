@@ -96,6 +96,41 @@ __device__ __forceinline__ double sum_partials(const double *part, int G)
     return block_sum(v);
 }
 
+// UnitMap (kernels.h): does unit u (slots 2u, 2u+1) hold a real row?
+__device__ __forceinline__ bool unit_real(const UnitMap &m, long long u)
+{
+    if (m.kind < 0) return true;
+    if (m.kind == 0) return 2 * u < m.n;
+    const int lane = (int)(u & 63);
+    const long long q = u >> 6;
+    const int th = m.T >> 1;
+    int j, k, lo;
+    long long tp;
+    if (m.kind == 1) {
+        // 2D band layout (gg_internal.h Wave2D::slot): q = plane*nbands*T/2 + band*T/2 + t/2
+        const long long per_plane = (long long)m.nbands * th;
+        const long long kpl = q / per_plane;
+        const long long r = q - kpl * per_plane;
+        const int band = (int)(r / th);
+        tp = r - (long long)band * th;
+        j = band * 64 + lane;
+        k = (int)kpl;
+        lo = m.skew * lane + (m.skew - 1);              // the line's first real step
+    } else {
+        // 3D tiles: lane a + 8 g(c), t = i + a + c, band = K*NJ + J
+        const long long band = q / th;
+        tp = q - band * th;
+        const int J = (int)(band % m.NJ), K = (int)(band / m.NJ);
+        const int a = lane & 7, g = lane >> 3, c = g ^ (g >> 1) ^ (g >> 2);
+        j = 8 * J + a;
+        k = 8 * K + c;
+        lo = a + c;
+    }
+    if (j >= m.ny || k >= m.nz) return false;
+    const long long t0 = 2 * tp;
+    return t0 + 1 >= lo && t0 < lo + m.nx;
+}
+
 __device__ __forceinline__ double2 ld2(const double *p, long long u)
 {
     return reinterpret_cast<const double2 *>(p)[u];
@@ -114,6 +149,10 @@ __device__ __forceinline__ void st2(double *p, long long u, double2 v)
 
 // ---- relaxed agent-scope loads/stores for the band hand-off --------------------
 constexpr int kSpinLimit = 1 << 20;
+// a wait this long (~10 ms of polls) only happens when a workgroup it waits on
+// was never dispatched: persistent grids that were sized to be co-resident
+// treat it as "not resident" and fall back (gather_first, k_trsv_tile3d)
+constexpr int kResidSpin = 1 << 13;
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1652,7 +1691,7 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     Gate g, int T, int NJ, int NK, const int *__restrict__ order, const double *__restrict__ b,
     const double *__restrict__ c1, const double *__restrict__ c2, const double *__restrict__ dv,
     const double *__restrict__ rv, const double *__restrict__ c0, double *__restrict__ x,
-    unsigned long long *gran, int *err, long long *trace)
+    unsigned long long *gran, int *err, long long *trace, int dyn)
 {
     using C = TileCfg<DIV>;
     constexpr int PB = C::PBN * 64;             // double2 per array per slot
@@ -1677,16 +1716,23 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     // hot spot on one memory channel
     unsigned long long *dummy_ld = gran + (long long)ntask * tgran + (long long)blockIdx.x * 128 + lane;
     unsigned long long *dummy_st = dummy_ld + 64;
-    // Tiles are CLAIMED in dependency order from a queue (one agent-scope
-    // atomic per tile, issued one tile ahead by the compute wave), not dealt
-    // statically: a workgroup claims a tile only while it runs, and the
-    // smallest unfinished tile's owner has finished every tile it claimed
-    // before it, whose sources all precede it -- so any grid drains, resident
-    // or not (the occupancy API is not trusted).  q[0] = next tile,
-    // q[8] = workgroups finished; the last one re-arms both for the next launch.
+    // Tiles are dealt statically (dyn = 0: workgroup w takes every
+    // gridDim.x-th tile of the dependency order), which needs the whole grid
+    // co-resident -- the grid is sized from the occupancy API, which this pool
+    // has seen over-promise.  So the boundary wave's waits are
+    // bounded by kResidSpin in that mode: a longer wait sets err bit 3 (8) and
+    // the workgroup finishes without waiting (garbage, but the grid drains);
+    // the host then reruns with dyn = 1 for the triangle's life: tiles CLAIMED
+    // in dependency order from a queue (one agent-scope atomic per tile, issued
+    // one tile ahead by the compute wave), where a workgroup claims a tile only
+    // while it runs and the smallest unfinished tile's owner has finished every
+    // tile it claimed before it -- any grid drains, resident or not.  (The
+    // queue is the fallback, not the default: C4 L / U 221.6 / 230.1 us static
+    // against 242.7 / 257.3 us claimed, profiles/r04_tile_queue_ab.txt.)
+    // q[0] = next tile, q[16] = workgroups finished; the last one re-arms both.
     unsigned long long *q = gran + (long long)ntask * tgran + 128LL * kTileDummyBlocks;
     __shared__ int tq[2];                       // the current and the next claimed tile
-    if (threadIdx.x == 0) tq[0] = (int)atomicAdd(q, 1ull);
+    if (threadIdx.x == 0) tq[0] = dyn ? (int)atomicAdd(q, 1ull) : (int)blockIdx.x;
     __syncthreads();
     int kq = 0;                                 // tiles this workgroup has run
     for (int task = tq[0]; task < ntask; task = tq[++kq & 1]) {
@@ -1863,9 +1909,9 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
                         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
                         for (int m = 0; m < GL; m++) v[u][m] = ld_agent(paddr(bi, m));
-                        if (++spins > kSpinLimit) {
+                        if (++spins > (dyn ? kSpinLimit : kResidSpin)) {
                             dead = true;
-                            if (lane == 0) atomicOr(err, 1);
+                            if (lane == 0) atomicOr(err, dyn ? 1 : 8);   // 8: static grid not resident
                         }
                         __builtin_amdgcn_s_waitcnt(vm_wait(0));
                     }
@@ -1921,7 +1967,7 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     // the next tile, claimed now (its latency hides in this tile's batches)
     // and handed to every wave through LDS before the task's final barrier
     int next_task = 0;
-    if (lane == 0) next_task = (int)atomicAdd(q, 1ull);
+    if (lane == 0) next_task = dyn ? (int)atomicAdd(q, 1ull) : task + (int)gridDim.x;
     if (TRACE && lane == 0) {
         trace[(long long)band * TS + 0] = (long long)__builtin_amdgcn_s_memrealtime();
         trace[(long long)band * TS + 2] = blockIdx.x;
@@ -2037,10 +2083,10 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     }   // task loop
     // every claim of this workgroup has returned: count it out; the last
     // workgroup re-arms the queue (the next launch follows a kernel boundary)
-    if (threadIdx.x == 0) {
-        if (atomicAdd(q + 8, 1ull) == (unsigned long long)gridDim.x - 1) {
+    if (dyn && threadIdx.x == 0) {
+        if (atomicAdd(q + 16, 1ull) == (unsigned long long)gridDim.x - 1) {
             st_agent(q, 0ull);
-            st_agent(q + 8, 0ull);
+            st_agent(q + 16, 0ull);
         }
     }
 }
@@ -2741,7 +2787,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
 // checks the flag every 256 retries, so the grid drains either way.
 // DONE_ABORT gates the rest of the enqueued cycle off; the host restores the
 // control block and reruns the cycle on the per-step kernels (same bits).
-constexpr int kResidSpin = 1 << 13;         // ~10 ms: far beyond any resident grid's first gather
+
 __device__ __forceinline__ int ld_agent_int(const int *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2865,26 +2911,120 @@ __device__ __forceinline__ bool gather_h_first(const unsigned long long *row, un
     return true;
 }
 
-template <int J>
+// XCD-local form (GG_MGS_GATHER=2): ONE block per XCD (the first to arrive,
+// elected per launch) gathers the step's G partials -- gather_sum, the same
+// order, the same bits -- and stores the sum with a PLAIN store into its
+// XCD's slot; the XCD's other blocks poll that slot (thread 0, sc1 loads).
+// A plain store keeps the line in the XCD's L2, where the sc1 (L1-bypassing)
+// polls of the same XCD find it: 234 / 677 ns a hop idle / streaming against
+// 470 / 740 for sc1 stores (profiles/r04_xcd_handoff.txt).  Correct by
+// construction, not by placement: a block polls only the slot of the XCD it
+// runs on (HW_REG_XCC_ID), which only a reducer ON that XCD writes.  8 pollers
+// of the G-granule row instead of G.
+constexpr int kXcdSlot = 16;                 // words per XCD slot (own 128-B line)
+constexpr int kXcds = 8;
+__device__ __forceinline__ unsigned xcc_id()
+{
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v & (kXcds - 1);
+}
+__device__ __forceinline__ void st_plain(unsigned long long *p, unsigned long long v)
+{
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+// this block's role for the launch: the first block of its XCD to raise the
+// XCD's election word to `seq` (strictly increasing per launch) reduces
+__device__ __forceinline__ void xcd_elect(unsigned long long *elect, unsigned long long seq, bool &red,
+                                          unsigned &xcc)
+{
+    __shared__ unsigned sx;
+    __shared__ int sr;
+    if (threadIdx.x == 0) {
+        const unsigned x = xcc_id();
+        sx = x;
+        sr = atomicMax(elect + x * kXcdSlot, seq) < seq;
+    }
+    __syncthreads();
+    red = sr != 0;
+    xcc = sx;
+}
+// step k's sum: slot = this XCD's word of step k
+__device__ __forceinline__ double gather_xcd(const unsigned long long *row, unsigned long long *slot, int k, int G,
+                                            bool red, int *err, int &par, const int *abortw)
+{
+    if (red) {
+        const double h = gather_sum(row, G, err, par, abortw);
+        if (threadIdx.x == 0) st_plain(slot, (unsigned long long)__double_as_longlong(h));
+        return h;
+    }
+    __shared__ double hb[2];                    // alternating: steps k and k+2 are a barrier apart
+    if (threadIdx.x == 0) hb[k & 1] = __longlong_as_double((long long)poll_granule(slot, err, abortw));
+    __syncthreads();
+    return hb[k & 1];
+}
+__device__ __forceinline__ bool gather_xcd_first(const unsigned long long *row, unsigned long long *slot, int G,
+                                                 bool red, DevState *ds, int &par, double &h)
+{
+    if (red) {
+        if (!gather_first(row, G, ds, par, h)) return false;
+        if (threadIdx.x == 0) st_plain(slot, (unsigned long long)__double_as_longlong(h));
+        return true;
+    }
+    __shared__ double hb0;
+    int miss = 0;
+    if (threadIdx.x == 0) {
+        unsigned long long a = ld_agent(slot);
+        int spins = 0;
+        while (a == kSentinel && !miss) {
+            __builtin_amdgcn_s_sleep(1);
+            a = ld_agent(slot);
+            if (++spins > kResidSpin) miss = 1;
+        }
+        hb0 = __longlong_as_double((long long)a);
+    }
+    if (__syncthreads_or(miss)) {
+        if (threadIdx.x == 0) set_abort(ds);
+        return false;
+    }
+    h = hb0;
+    return true;
+}
+
+// XG: the all-gather's form -- 0 every block gathers, 2 XCD-local reducers
+// (gather_xcd; xb = per step kXcds slots of kXcdSlot words, elect / seq the
+// per-launch election)
+// PF: v_{k+1} streamed while step k's sum is gathered (1), or after it (0):
+// polls issued behind a wave's own in-flight basis loads wait for them (the
+// memory returns in order) and the gather then also pays the stream's latency
+template <int J, int XG, int PF>
 __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m, DevState *ds,
                                                             const double *__restrict__ w_in,
                                                             double *__restrict__ V, long long ldv,
                                                             double *H, double *cs, double *sn,
                                                             double *s, double *hist,
                                                             unsigned long long *gran, unsigned long long *hg,
-                                                            long long units, int *err)
+                                                            long long units, int *err, unsigned long long *xb,
+                                                            unsigned long long *elect, unsigned long long seq,
+                                                            UnitMap um)
 {
     if (gated(g)) return;
     if (block_aborted(ds)) return;                            // co-residency (gather_first)
+    bool red = true;
+    unsigned xcc = 0;
+    if constexpr (XG == 2) xcd_elect(elect, seq, red, xcc);
+    auto xslot = [&](int k) { return xb + ((long long)k * kXcds + xcc) * kXcdSlot; };
     const int G = gridDim.x;
     const long long stride = (long long)G * kBlock;
     const long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x;
     const int *abortw = &ds->done;
     double2 w[J], vk[J], vn[J];
+    bool val[J];                                              // unit holds a real row (UnitMap)
 #pragma unroll
     for (int j = 0; j < J; j++) {
         const long long u = u0 + j * stride;
-        if (u < units) {
+        val[j] = u < units && unit_real(um, u);
+        if (val[j]) {
             w[j] = ld2(w_in, u);
             vk[j] = ld2(V, u);
         }
@@ -2897,30 +3037,41 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < J; j++)
-        if (u0 + j * stride < units) {
+        if (val[j]) {
             acc += w[j].x * vk[j].x;
             acc += w[j].y * vk[j].y;
         }
     publish(0, acc);                                          // <w, v_0>
     for (int k = 0; k <= i; k++) {
-        if (k < i) {                                          // v_{k+1}, in flight during the sum
-            const double *vnp = V + (long long)(k + 1) * ldv;
+        auto load_next = [&]() {
+            if (k < i) {
+                const double *vnp = V + (long long)(k + 1) * ldv;
 #pragma unroll
-            for (int j = 0; j < J; j++)
-                if (u0 + j * stride < units) vn[j] = ld2_nt(vnp, u0 + j * stride);   // streamed
-        }
+                for (int j = 0; j < J; j++)
+                    if (val[j]) vn[j] = ld2_nt(vnp, u0 + j * stride);   // streamed
+            }
+        };
+        if constexpr (PF) load_next();                        // v_{k+1}, in flight during the sum
         double h;
         if (k == 0) {
-            if (!gather_h_first<false>(gran, hg, G, ds, par, h)) return;
+            if (XG == 2 ? !gather_xcd_first(gran, xslot(0), G, red, ds, par, h)
+                        : !gather_h_first<false>(gran, hg, G, ds, par, h))
+                return;
+        } else if constexpr (XG == 2) {
+            h = gather_xcd(gran + (long long)k * G, xslot(k), k, G, red, err, par, abortw);
         } else {
             h = gather_h<false>(gran + (long long)k * G, hg + k, k, G, err, par, abortw);
+        }
+        if constexpr (!PF) {
+            __builtin_amdgcn_sched_barrier(0);
+            load_next();                                      // v_{k+1} after the sum
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         acc = 0.0;
 #pragma unroll
         for (int j = 0; j < J; j++) {
-            if (u0 + j * stride < units) {
+            if (val[j]) {
                 w[j].x = a * vk[j].x + w[j].x;
                 w[j].y = a * vk[j].y + w[j].y;
                 const double2 o = (k < i) ? vn[j] : w[j];     // next dot: v_{k+1}, or the norm
@@ -2931,7 +3082,10 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(gather_h<false>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par, abortw));
+    const double hn = sqrt(XG == 2 ? gather_xcd(gran + (long long)(i + 1) * G, xslot(i + 1), i + 1, G, red, err, par,
+                                                abortw)
+                                   : gather_h<false>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par,
+                                                     abortw));
     if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
@@ -2956,7 +3110,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
 #pragma unroll
     for (int j = 0; j < J; j++) {
         const long long u = u0 + j * stride;
-        if (u < units) {
+        if (val[j]) {
             double2 a = w[j];
             a.x = inv * a.x;
             a.y = inv * a.y;
@@ -2991,7 +3145,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
                                                             double *H, double *cs, double *sn,
                                                             double *s, double *hist,
                                                             unsigned long long *gran, unsigned long long *hg,
-                                                            long long units, int *err)
+                                                            long long units, int *err, UnitMap um)
 {
     constexpr int J = kWideJR + kWideJL;
     if (gated(g)) return;
@@ -3004,6 +3158,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
     const int u0 = blockIdx.x * kBlock + threadIdx.x;
     // this thread's units u0 + j stride, j < nval
     const int nval = units > u0 ? (int)((units - u0 + stride - 1) / stride) : 0;
+    // (no padding skip here: the validity mask costs this kernel its registers
+    // -- 148 VGPRs spilled -- at 256 VGPRs; um is unused)
+    (void)um;
+    auto ok = [&](int j) { return j < nval; };
     double2 wr[kWideJR];
     auto wget = [&](int j) -> double2 { return j < kWideJR ? wr[j] : wl[(j - kWideJR) * kBlock + threadIdx.x]; };
     auto wset = [&](int j, double2 v) {
@@ -3024,7 +3182,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
     // second read), 1 streams it non-temporally like v_k's last read
     // stash: v_k's units j < kWideJS come from LDS (written one step earlier)
     auto fetch = [&](int j, int ub, const double2 *vkp, const double2 *vnp, bool stash) {
-        if (j < J && j < nval) {
+        if (j < J && ok(j)) {
             if (stash && j < kWideJS) {
                 pk[j % kWideD] = vst[j * kBlock + threadIdx.x];
             } else {
@@ -3050,7 +3208,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         for (int j = 0; j < kWideD; j++) fetch(j, ub, vec(V), nullptr, false);
 #pragma unroll
         for (int j = 0; j < J; j++) {
-            if (j < nval) {
+            if (ok(j)) {
                 const double2 wv = vec(w_in)[ub + j * stride];
                 wset(j, wv);
                 const double2 v0 = pk[j % kWideD];
@@ -3080,7 +3238,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
         acc = 0.0;
 #pragma unroll
         for (int j = 0; j < J; j++) {
-            if (j < nval) {
+            if (ok(j)) {
                 double2 wv = wget(j);
                 const double2 vk = pk[j % kWideD];
                 wv.x = a * vk.x + wv.x;
@@ -3119,7 +3277,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
     double2 *vout = reinterpret_cast<double2 *>(V + (long long)(i + 1) * ldv);
 #pragma unroll
     for (int j = 0; j < J; j++) {
-        if (j < nval) {
+        if (ok(j)) {
             double2 a = wget(j);
             a.x = inv * a.x;
             a.y = inv * a.y;
@@ -3174,12 +3332,13 @@ __global__ void k_update_y_serial(Gate g, int m, DevState *ds, const double *H, 
 // acc += sum_{j<=k} V_j y_j   (ascending j, as the reference's x[i] += v*y loop)
 __global__ __launch_bounds__(kBlock) void k_update_x(Gate g, const DevState *ds, const double *y,
                                                      const double *V, long long ldv, double *acc,
-                                                     long long units)
+                                                     long long units, UnitMap um)
 {
     if (gated(g)) return;
     const int k = ds->upd_k;
     for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units;
          u += (long long)gridDim.x * kBlock) {
+        if (!unit_real(um, u)) continue;                      // padding: +0 stays +0
         double2 a = ld2(acc, u);
         // eight basis vectors' loads in flight at a time, added in ascending j
         for (int j0 = 0; j0 <= k; j0 += 8) {
@@ -3459,6 +3618,13 @@ int tile_batch_steps() { return GG_TILE_BATCH; }
 
 // tests: GG_TILE_GRID = workgroups of the tile solve (beyond what can be
 // resident: the task queue must still drain it)
+// the tile solve's mode: static (0) unless the triangle fell back to the
+// queue (1); GG_TILE_QUEUE=1 forces the queue (tests, A/B)
+static int tile_dyn(const DevTri &T)
+{
+    const char *e = std::getenv("GG_TILE_QUEUE");
+    return (T.tile_queue || (e && e[0] == '1')) ? 1 : 0;
+}
 static int tile_grid_override(int g)
 {
     const char *e = std::getenv("GG_TILE_GRID");
@@ -3615,11 +3781,11 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         if (T.trace)                                                                               \
             k_trsv_tile3d<FWD, DIV, true><<<grid, TileCfg<DIV>::THREADS, 0, st>>>(                 \
                 g, w.T, w.NJ, w.NK, T.order.p, b, k1, k2, dv, rv, k0, x, T.bnd.p, err,              \
-                T.trace);                                                                          \
+                T.trace, tile_dyn(T));                                                             \
         else                                                                                       \
             k_trsv_tile3d<FWD, DIV><<<grid, TileCfg<DIV>::THREADS, 0, st>>>(                       \
                 g, w.T, w.NJ, w.NK, T.order.p, b, k1, k2, dv, rv, k0, x, T.bnd.p, err,              \
-                nullptr);                                                                          \
+                nullptr, tile_dyn(T));                                                             \
     } while (0)
             if (div == WD_UFMA || div == WD_SFMA) {
                 // GG_DIV_FMA (build_tri admits the unit L and a non-unit U)
@@ -3767,6 +3933,11 @@ void launch_arnoldi_finalize_r(Gate g, int i, int m, DevState *ds, const double 
     k_arnoldi_finalize<<<G, kBlock, 0, st>>>(g, i, m, ds, part, nparts_in, w, vnext, H, cs, sn, s,
                                               hist, Ppad / 2);
 }
+#ifndef GG_MGS_GATHER_DEFAULT
+#define GG_MGS_GATHER_DEFAULT 2
+#endif
+constexpr int kMgsGatherDefault = GG_MGS_GATHER_DEFAULT;
+
 int arnoldi_persist_units(int G, long long Ppad)
 {
     const long long units = Ppad / 2, per = (long long)G * kBlock;
@@ -3781,10 +3952,10 @@ int arnoldi_persist_max_blocks(int J)
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     auto occ = [&](const void *f) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) == hipSuccess; };
-    const bool ok = J == 1   ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<1>))
-                    : J == 2 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<2>))
-                    : J == 4 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<4>))
-                    : J == 8 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<8>))
+    const bool ok = J == 1   ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<1, 2, 1>))
+                    : J == 2 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<2, 2, 1>))
+                    : J == 4 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<4, 2, 1>))
+                    : J == 8 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<8, 2, 1>))
                              : false;
     return ok ? cus * per : 0;
 }
@@ -3809,34 +3980,63 @@ bool arnoldi_wide_ok(int G, long long Ppad)
 void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, double *V, long long ldv,
                          double *H, double *cs, double *sn, double *s, double *hist,
                          unsigned long long *gran, unsigned long long *hg, int G, long long Ppad, int *err,
-                         hipStream_t st)
+                         const UnitMap &um, hipStream_t st)
 {
     k_arnoldi_wide<<<G, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg,
-                                                          Ppad / 2, err);
+                                                          Ppad / 2, err, um);
+}
+
+#ifndef GG_MGS_PREFETCH_DEFAULT
+#define GG_MGS_PREFETCH_DEFAULT 1
+#endif
+int mgs_prefetch()
+{
+    const char *e = std::getenv("GG_MGS_PREFETCH");    // 1: v_{k+1} streamed during the gather, 0: after it
+    return e ? (atoi(e) != 0) : GG_MGS_PREFETCH_DEFAULT;
+}
+int mgs_gather_form()
+{
+    const char *e = std::getenv("GG_MGS_GATHER");      // 0: every block gathers, 2: XCD-local reducers
+    return e ? (atoi(e) == 2 ? 2 : 0) : kMgsGatherDefault;
 }
 
 void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
                             long long ldv, double *H, double *cs, double *sn, double *s,
                             double *hist, unsigned long long *gran, unsigned long long *hg, int G, long long Ppad,
-                            int *err, hipStream_t st)
+                            int *err, unsigned long long *xb, unsigned long long *elect, unsigned long long seq,
+                            const UnitMap &um, hipStream_t st)
 {
     const int J = arnoldi_persist_units(G, Ppad);
-#define GG_PERSIST(JJ)                                                                       \
-    k_arnoldi_persist<JJ><<<G, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, \
-                                                 hg, Ppad / 2, err)
-    if (J == 1) GG_PERSIST(1);
-    else if (J == 2) GG_PERSIST(2);
-    else if (J == 4) GG_PERSIST(4);
-    else GG_PERSIST(8);
+    const int xg = mgs_gather_form();
+    const int pf = mgs_prefetch();
+#define GG_PERSIST(JJ, XG, PF)                                                                       \
+    k_arnoldi_persist<JJ, XG, PF><<<G, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, \
+                                                                         hist, gran, hg, Ppad / 2, err, xb, elect, seq, um)
+#define GG_PERSIST_J(XG, PF)                                                                       \
+    do {                                                                                           \
+        if (J == 1) GG_PERSIST(1, XG, PF);                                                         \
+        else if (J == 2) GG_PERSIST(2, XG, PF);                                                    \
+        else if (J == 4) GG_PERSIST(4, XG, PF);                                                    \
+        else GG_PERSIST(8, XG, PF);                                                                \
+    } while (0)
+    if (xg == 2) {
+        if (pf) GG_PERSIST_J(2, 1);
+        else GG_PERSIST_J(2, 0);
+    } else {
+        if (pf) GG_PERSIST_J(0, 1);
+        else GG_PERSIST_J(0, 0);
+    }
+#undef GG_PERSIST_J
 #undef GG_PERSIST
 }
 
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
-                   const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st)
+                   const double *V, long long ldv, double *acc, int G, long long Ppad, hipStream_t st,
+                   const UnitMap &um)
 {
     if (m <= kMaxRestart) k_update_y<<<1, 64, 0, st>>>(g, m, ds, H, s, ysmall);
     else k_update_y_serial<<<1, 64, 0, st>>>(g, m, ds, H, s, ysmall);
-    k_update_x<<<G, kBlock, 0, st>>>(g, ds, ysmall, V, ldv, acc, Ppad / 2);
+    k_update_x<<<G, kBlock, 0, st>>>(g, ds, ysmall, V, ldv, acc, Ppad / 2, um);
 }
 void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st)
 {

@@ -323,6 +323,9 @@ struct gg_solver {
     std::vector<double> tap_max, tap_min, tap_avg;
     DBuf<unsigned long long> gran;      // m * (m+2) * G hand-off granules, then m * (m+2) sums
                                         // (gather_h), re-armed per cycle
+    DBuf<unsigned long long> xgran;     // m * (m+2) * kMgsXcdWords: the XCD-local gather's slots (re-armed per cycle)
+    DBuf<unsigned long long> elect;     // per XCD: the last launch that elected its reducer
+    unsigned long long mgs_seq = 0;     // persistent orthogonalization launches so far (election)
     DBuf<double> hist;
     long long hist_cap = 0;
     DBuf<DevState> ds;
@@ -464,6 +467,13 @@ void ensure_workspace(gg_solver *s, int m)
         s->persist = !off && !force_wide && pj != 0 && s->G <= arnoldi_persist_max_blocks(pj);
         s->wide = !off && !s->persist && arnoldi_wide_ok(s->G, s->Ppad);   // long vectors: w on chip
         if (s->persist || s->wide) s->gran.alloc((size_t)m * (m + 2) * (s->G + 1));
+        if (s->persist) {
+            s->xgran.alloc((size_t)m * (m + 2) * kMgsXcdWords);
+            if (!s->elect.p) {
+                s->elect.alloc(kMgsElectWords);
+                GG_HIP(hipMemsetAsync(s->elect.p, 0, kMgsElectWords * sizeof(unsigned long long), s->st));
+            }
+        }
     }
     s->H.alloc((size_t)(m + 1) * m);
     GG_HIP(hipMemsetAsync(s->H.p, 0, (size_t)(m + 1) * m * sizeof(double), s->st));
@@ -669,8 +679,33 @@ bool fuse_spmv_active(gg_solver *s)
     return fused_spmv_ok(s->L, s->dA);
 }
 
+// the padding map of the solver's vector space (kernels.h UnitMap)
+UnitMap unit_map(const gg_solver *s)
+{
+    UnitMap um;
+    const char *e = std::getenv("GG_NO_PADSKIP");           // A/B: every unit
+    if (e && e[0] == '1') return um;
+    if (!s->wave) {
+        um.kind = 0;
+        um.n = s->A.n;
+        return um;
+    }
+    const Wave2D &w = s->wl;
+    um.kind = w.tile ? 2 : 1;
+    um.nx = w.nx;
+    um.ny = w.ny;
+    um.nz = w.nz;
+    um.T = w.T;
+    um.skew = w.skew;
+    um.NJ = w.NJ;
+    um.nbands = w.nbands;
+    um.n = s->A.n;
+    return um;
+}
+
 void enqueue_cycle(gg_solver *s, int m)
 {
+    const UnitMap um = unit_map(s);
     DevState *ds = s->ds.p;
     const long long P = s->Ppad;
     const bool split = s->pkind == GG_PRECOND_SPLIT;
@@ -680,6 +715,7 @@ void enqueue_cycle(gg_solver *s, int m)
     const bool persist = s->persist && !s->shared;
     const bool wide = s->wide && !s->shared;
     if (persist || wide) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
+    if (persist) launch_fill_u64(s->xgran.p, (long long)s->xgran.n, kSentinel, s->st);
     const bool fuse = fuse_spmv_active(s);
     for (int i = 0; i < m; i++) {
         Gate gi;
@@ -722,11 +758,12 @@ void enqueue_cycle(gg_solver *s, int m)
         if (persist) {
             launch_arnoldi_persist(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                    s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
-                                   P, s->err.p, s->st);
+                                   P, s->err.p, s->xgran.p + (size_t)i * (m + 2) * kMgsXcdWords, s->elect.p,
+                                   ++s->mgs_seq, um, s->st);
         } else if (wide) {
             launch_arnoldi_wide(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                 s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
-                                P, s->err.p, s->st);
+                                P, s->err.p, um, s->st);
         } else {
             double *pin = s->partA.p, *pout = s->partB.p;
             launch_dot(gi, s->w.p, s->V.p, pin, s->G, P, s->st);               // <w, v_0>
@@ -746,7 +783,7 @@ void enqueue_cycle(gg_solver *s, int m)
     gu.done = &ds->done;
     gu.mask = DONE_RESTART | DONE_INIT | DONE_ABORT;
     launch_update(gu, m, ds, s->H.p, s->s.p, s->ysm.p, s->V.p, P, split || usplit ? s->y.p : s->xv.p, s->G, P,
-                  s->st);
+                  s->st, um);
     if (split) apply_right(s, gu, s->y.p, s->xv.p);                            // x = Mr y
     if (usplit) apply_user(s, gu, GG_APPLY_RIGHT, s->y.p, s->xv.p);
     Gate gr;
@@ -774,16 +811,22 @@ void reset_wave(DevTri *T, hipStream_t st)
 }
 
 // Device error word: bit 0 = wavefront boundary wait timed out, bit 1 = a
-// WD_RCP step saw a numerator outside its safe range (repeat with WD_HW).
-struct RcpFallback {};
+// WD_RCP step saw a numerator outside its safe range (repeat with WD_HW), bit
+// 3 = a statically dealt tile grid was not co-resident (repeat with the tile
+// queue, k_trsv_tile3d).  Bits 1 and 3 throw Fallback: the caller applies it
+// (apply_fallback) and repeats the solve / apply.
+struct Fallback {
+    int bits;
+};
 void check_err(gg_solver *s)
 {
     // on the solver's stream: a plain hipMemcpy would not wait for its kernels
     int err = 0;
     GG_HIP(hipMemcpyAsync(&err, s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
     GG_HIP(hipStreamSynchronize(s->st));
+    if (err & 8) throw Fallback{err};              // (the residency timeout also left garbage)
     GG_REQUIRE((err & 1) == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
-    if (err & 2) throw RcpFallback{};
+    if (err & 2) throw Fallback{err};
 }
 // the control block and the error word in one round trip (after a cycle)
 DevState read_state_checked(gg_solver *s)
@@ -796,15 +839,19 @@ DevState read_state_checked(gg_solver *s)
     GG_HIP(hipMemcpyAsync(s->h_err, s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
     GG_HIP(hipStreamSynchronize(s->st));
     const int err = *s->h_err;
+    if (err & 8) throw Fallback{err};
     GG_REQUIRE((err & 1) == 0, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
-    if (err & 2) throw RcpFallback{};
+    if (err & 2) throw Fallback{err};
     return *s->h_state;
 }
-// switch every WD_RCP triangle to IEEE division for the rest of the solver's life
-void demote_rcp(gg_solver *s)
+// for the rest of the solver's life: every WD_RCP triangle divides (bit 1),
+// every 3D tile triangle claims its tiles from the queue (bit 3)
+void apply_fallback(gg_solver *s, const Fallback &f)
 {
-    for (DevTri *T : {&s->L, &s->U})
-        if (T->kind == DevTri::WAVE2D && T->div == WD_RCP) T->div = WD_HW;
+    for (DevTri *T : {&s->L, &s->U}) {
+        if ((f.bits & 2) && T->kind == DevTri::WAVE2D && T->div == WD_RCP) T->div = WD_HW;
+        if ((f.bits & 8) && T->kind == DevTri::WAVE2D && T->wl.tile) T->tile_queue = true;
+    }
 }
 
 // A persistent orthogonalization grid that was not co-resident aborted the
@@ -961,11 +1008,15 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
 int solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
                  gg_result *res)
 {
-    try {
-        return solve_device_once(s, d_b, d_x, opt, res);
-    } catch (RcpFallback &) {
-        demote_rcp(s);      // d_x is written only at the very end, so simply start over
-        return solve_device_once(s, d_b, d_x, opt, res);
+    // d_x is written only at the very end, so a fallback simply starts over
+    // (each fallback at most once: the bits it applies do not come back)
+    for (int attempt = 0;; attempt++) {
+        try {
+            return solve_device_once(s, d_b, d_x, opt, res);
+        } catch (Fallback &f) {
+            if (attempt >= 2) throw Error{GG_EHIP, "gg_solve: fallbacks exhausted"};
+            apply_fallback(s, f);
+        }
     }
 }
 
@@ -1457,7 +1508,9 @@ int gg_mgs_kernel(gg_solver *s, char *name, int cap)
     if (!s || !name || cap <= 0) return GG_EINVAL;
     std::string k;
     if (s->m_alloc > 0 && !s->shared) {
-        if (s->persist) k = "k_arnoldi_persist<" + std::to_string(arnoldi_persist_units(s->G, s->Ppad)) + ">";
+        if (s->persist)
+            k = "k_arnoldi_persist<" + std::to_string(arnoldi_persist_units(s->G, s->Ppad)) + ", " +
+                std::to_string(mgs_gather_form()) + ">";
         else if (s->wide) k = "k_arnoldi_wide";
     }
     std::snprintf(name, (size_t)cap, "%s", k.c_str());
@@ -1836,11 +1889,16 @@ int gg_precond_apply(gg_solver *s, int op, const double *in, double *out)
         }
         check_err(s);
     };
-    try {
-        run();
-    } catch (RcpFallback &) {
-        demote_rcp(s);
-        run();
+    for (int attempt = 0;; attempt++) {
+        try {
+            run();
+            break;
+        } catch (Fallback &f) {
+            if (attempt >= 2) throw Error{GG_EHIP, "gg_precond_apply: fallbacks exhausted"};
+            apply_fallback(s, f);
+            for (DevTri *T : {&s->L, &s->U})
+                if (T->kind == DevTri::WAVE2D) reset_wave(T, s->st);   // a drained grid left granules set
+        }
     }
     if (s->nat_out.n < (size_t)std::max(s->A.n, 1)) s->nat_out.alloc(std::max(s->A.n, 1));
     launch_gather(s->ww.p, split && op == GG_APPLY_RIGHT ? s->sx_out.p : s->nat2lay.p, s->nat_out.p,

@@ -27,7 +27,11 @@ EXPORTS = ["gg_dd_unique_id", "gg_dd_create", "gg_dd_destroy", "gg_dd_comm_ranks
            "gg_dd_set_system", "gg_dd_info",
            "gg_dd_perm", "gg_dd_dot_layout", "gg_dd_solve", "gg_dd_solve_device",
            "gg_dd_get_history", "gg_dd_spmv", "gg_dd_precond_apply", "gg_dd_set_division",
-           "gg_dd_time_exchange"]
+           "gg_dd_time_exchange", "gg_dd_profile_enable", "gg_dd_profile_reset", "gg_dd_profile_get",
+           "gg_dd_bytes"]
+# gg_dd_prof_kind (ggmres_dd.h)
+PROF_SPMV, PROF_TRSV_L, PROF_SEP, PROF_TRSV_U, PROF_ORTH = range(5)
+PROF_NAMES = ("spmv", "trsv_L", "separator", "trsv_U", "orthogonalization")
 
 
 def _lib():
@@ -54,6 +58,11 @@ def _lib():
         L.gg_dd_precond_apply.argtypes = [_VP, _D, _D]
         L.gg_dd_set_division.argtypes = [_VP, ctypes.c_int]
         L.gg_dd_time_exchange.argtypes = [_VP, ctypes.c_longlong, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        L.gg_dd_profile_enable.argtypes = [_VP, ctypes.c_int]
+        L.gg_dd_profile_reset.argtypes = [_VP]
+        L.gg_dd_profile_get.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                        ctypes.POINTER(ctypes.c_double)]
+        L.gg_dd_bytes.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         _done = True
     return L
 
@@ -166,6 +175,25 @@ class DD:
     def set_division(self, mode):
         """ggmres.DIV_EXACT / DIV_RCP / DIV_FMA for the shards' wavefront triangular solves"""
         _check(_lib().gg_dd_set_division(self.h, int(mode)))
+
+    def profile(self, on=True, kinds=None):
+        """in-solve timing of the families (PROF_*) of every inner iteration"""
+        mask = 0
+        if on:
+            mask = (1 << len(PROF_NAMES)) - 1 if kinds is None else sum(1 << k for k in kinds)
+        _check(_lib().gg_dd_profile_reset(self.h))
+        _check(_lib().gg_dd_profile_enable(self.h, mask))
+
+    def profile_get(self, kind):
+        n, ms = ctypes.c_int(), ctypes.c_double()
+        _check(_lib().gg_dd_profile_get(self.h, int(kind), ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+    def bytes(self, kind):
+        """algorithmic bytes of one launch of family kind (PROF_SPMV / _TRSV_L / _TRSV_U), this process's shards"""
+        b = ctypes.c_double()
+        _check(_lib().gg_dd_bytes(self.h, int(kind), ctypes.byref(b)))
+        return b.value
 
     def time_exchange(self, cnt, reps=200):
         """average microseconds of one all-gather of cnt doubles per shard"""

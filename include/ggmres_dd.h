@@ -113,6 +113,22 @@ int gg_dd_set_division(gg_dd *d, int mode);
  * all-gather of cnt doubles per shard over this communicator -- the exchange
  * every sharded operator and dot pays (cnt <= (m+1) * G of the last solve) */
 int gg_dd_time_exchange(gg_dd *d, long long cnt, int reps, double *avg_us);
+/* In-solve timing of the sharded solve's families per inner iteration
+ * (hipEvent pairs on the solver's stream, accounted for the iterations that
+ * really ran): the interior rows' + separator rows' SpMV with its halo
+ * exchange, the interior L solve, the separator step (interface exchange and
+ * separator solves), the interior U solve, the orthogonalization (its
+ * exchanges included).  kinds: a mask of (1 << GG_DD_PROF_*). */
+enum gg_dd_prof_kind {
+    GG_DD_PROF_SPMV = 0, GG_DD_PROF_TRSV_L = 1, GG_DD_PROF_SEP = 2, GG_DD_PROF_TRSV_U = 3,
+    GG_DD_PROF_ORTH = 4, GG_DD_PROF_NKINDS = 5
+};
+int gg_dd_profile_enable(gg_dd *d, int kinds);
+int gg_dd_profile_reset(gg_dd *d);
+int gg_dd_profile_get(gg_dd *d, int kind, int *launches, double *total_ms);
+/* algorithmic bytes of one launch of family `kind`
+ * (GG_DD_PROF_SPMV / _TRSV_L / _TRSV_U) over the shards of this process */
+int gg_dd_bytes(gg_dd *d, int kind, double *bytes);
 
 #ifdef __cplusplus
 }

@@ -7,8 +7,10 @@ occupancy API"; ADVICE r3 on the fused SpMV's block order).
   forced here with dynamic LDS (GG_PERSIST_TEST_LDS) so that fewer blocks fit
   than the grid has.  Results bit-identical to the per-step kernels and to the
   order-matched oracle.
-* k_trsv_tile3d: tiles claimed from a queue (no co-residency needed) -- forced
-  with more workgroups than can be resident (GG_TILE_GRID).
+* k_trsv_tile3d: tiles dealt statically; a grid that is not co-resident times
+  out (err bit 3) and the solve / apply repeats with tiles claimed from a queue
+  (no co-residency needed) -- forced with more workgroups than can be resident
+  (GG_TILE_GRID); GG_TILE_QUEUE=1 runs the queue from the start.
 * k_trsv_wave2d_spmv: the SpMV blocks take the low block indices, so a grid with
   more bands than CUs still drains.
 """
@@ -83,16 +85,20 @@ def test_wide_grid_not_coresident_reruns_per_step(monkeypatch):
     same(g, ot)
 
 
+@pytest.mark.parametrize("queue", [False, True])
 @pytest.mark.parametrize("dims, grid", [((4, 200, 200), 625), ((3, 300, 300), 1444)])
-def test_tile_queue_drains_oversized_grid(monkeypatch, dims, grid):
+def test_tile_queue_drains_oversized_grid(monkeypatch, dims, grid, queue):
     """3D tile solve with one workgroup per tile (625 / 1,444 > the 512 that can
-    be resident): the task queue drains it; every apply bit-exact vs the
-    oracle, the queue re-armed launch after launch"""
+    be resident): dealt statically it times out and falls back to the queue
+    (queue False), or runs the queue from the start (True); every apply
+    bit-exact vs the oracle, the queue re-armed launch after launch"""
     nx, ny, nz = dims
     A = M.grid_7pt(nx, ny, nz, upwind=0.1)
     n = A.shape[0]
     L, U = O.ilu0(A)
     monkeypatch.setenv("GG_TILE_GRID", str(grid))
+    if queue:
+        monkeypatch.setenv("GG_TILE_QUEUE", "1")
     s = ggmres.Solver(0)
     try:
         s.set_matrix(A)
