@@ -170,3 +170,69 @@ def rhs_ones(A):
 def rhs_uniform(n, seed=20261015):
     """b ~ U[0,1) from PCG64(seed)."""
     return np.random.Generator(np.random.PCG64(seed)).random(n)
+
+
+def pg_netlist(path, nx, ny, pad_stride=50, isrc_frac=0.01, seed=20261015):
+    """Write a synthetic IBM-power-grid-style flat SPICE netlist (the reference
+    driver's input, src/parser.cpp:69-272, 1904-2886; read back by
+    ggmres.host.Netlist = gg_host_read_netlist): an nx x ny resistor mesh (one
+    metal layer, 0.05-0.5 ohm segments), a 10-90 fF decoupling capacitor from
+    every node to ground (listed FIRST, so the MNA numbers the grid nodes in
+    row-major order), load currents (PULSE, 0 -> 1-5 mA) at a seeded
+    `isrc_frac` of the nodes, and a VDD pad every `pad_stride` nodes in both
+    directions: a 10 mOhm package resistor to a pad node held at 1.8 V by a
+    voltage source (MNA: one branch-current row each, zero diagonal).
+    Returns (n_grid, n_pads)."""
+    rng = np.random.default_rng(seed)
+    nm = lambda j, i: f"n{j}_{i}"
+    out = ["* synthetic IBM-PG-style power grid", ".tran 10p 1n"]
+    cap = rng.integers(10, 91, (ny, nx))
+    for j in range(ny):
+        out.extend(f"C{j}_{i} {nm(j, i)} 0 {cap[j, i]}f" for i in range(nx))
+    rh = rng.uniform(0.05, 0.5, (ny, nx))
+    rv = rng.uniform(0.05, 0.5, (ny, nx))
+    for j in range(ny):
+        for i in range(nx):
+            if i + 1 < nx:
+                out.append(f"R{j}_{i}h {nm(j, i)} {nm(j, i + 1)} {rh[j, i]:.5f}")
+            if j + 1 < ny:
+                out.append(f"R{j}_{i}v {nm(j, i)} {nm(j + 1, i)} {rv[j, i]:.5f}")
+    n = nx * ny
+    loads = np.sort(rng.choice(n, size=max(1, int(round(isrc_frac * n))), replace=False))
+    amp = rng.uniform(1.0, 5.0, loads.size)
+    for k, (r, a) in enumerate(zip(loads, amp)):
+        out.append(f"I{k} {nm(r // nx, r % nx)} 0 0 PULSE(0, {a:.3f}m, 50p, 20p, 20p, 200p, 500p)")
+    npad = 0
+    for j in range(pad_stride // 2, ny, pad_stride):
+        for i in range(pad_stride // 2, nx, pad_stride):
+            out.append(f"Rp{npad} {nm(j, i)} X{npad} 10m")
+            out.append(f"V{npad} X{npad} 0 1.8")
+            npad += 1
+    out.append(f".print tran v({nm(0, 0)}) v({nm(ny // 2, nx // 2)})")
+    out.append(".end")
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+    return n, npad
+
+
+def mna_pivot_order(n_grid, n_pads, n):
+    """Row / column permutations that give an MNA system with voltage-source
+    branch rows (zero diagonal) a nonzero diagonal for ILU(0) -- the pivoting
+    ILU++'s factorization does for the reference's PG path
+    (src/mna_solve_gpu_gmres.cpp:316-474).  Unknowns (gg_host_read_netlist):
+    [grid nodes | pad nodes X_k | branch currents I_k]; the branch row I_k
+    (V_{X_k} = V) has its only entry in column X_k, X_k's KCL row has +1 in
+    column I_k.  Returned as (prow, pcol) in the split engine's convention
+    (B = P_r A P_c: B row i = A row prow[i], B column pcol[c] = A column c):
+    the tail (pad and branch unknowns) FIRST -- B rows [I_k ..., X_k ..., grid],
+    B columns [X_k ..., I_k ..., grid] -- so the grid block keeps its 5-point
+    pattern, its rows referencing the tail only in columns left of the grid."""
+    assert n == n_grid + 2 * n_pads
+    X = np.arange(n_grid, n_grid + n_pads)
+    I = np.arange(n_grid + n_pads, n)
+    grid = np.arange(n_grid)
+    prow = np.concatenate([I, X, grid]).astype(np.int32)
+    colorder = np.concatenate([X, I, grid])          # B column c = A column colorder[c]
+    pcol = np.empty(n, np.int32)
+    pcol[colorder] = np.arange(n, dtype=np.int32)
+    return prow, pcol
