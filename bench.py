@@ -93,7 +93,10 @@ def parse():
                         "(1000^2 5-pt, the default sharded system at --gpus N > 1)")
     p.add_argument("--pg-perm", choices=["identity", "random"], default="identity",
                    help="pg: the split's row / column permutations")
-    p.add_argument("--workload", choices=["c2", "c3", "c3s", "c4", "c5", "dd", "replicas", "pg"], default=None,
+    p.add_argument("--pad-stride", type=int, default=50,
+                   help="netlist: a VDD pad (package R + voltage source) every this many nodes per direction")
+    p.add_argument("--workload", choices=["c2", "c3", "c3s", "c4", "c5", "dd", "replicas", "pg", "netlist"],
+                   default=None,
                    help="default: c2 at N = 1 (one C2 solve per step, the headline), the sharded C2 "
                         "solve at N > 1; dd: the sharded solve (C4 unless --dd-grid c2); replicas: "
                         "one independent C2 solve per rank; c5: a backward-Euler transient (A = G + C/h, "
@@ -203,6 +206,74 @@ def pg_split(A, device, seed=20261015, identity=True):
     L.sort_indices()
     U.sort_indices()
     return L, U, middle, prow, pcol, lscale, rscale
+
+
+def pulse_at(q, t):
+    """PULSE(v1, v2, td, tr, tf, pw, per) at time t (gen_PULSEut_kernel semantics,
+    src/kernels.cu:223-245)"""
+    v1, v2, td, tr, tf, pw, per = q
+    if t < td:
+        return v1
+    tt = (t - td) % per if per > 0 else t - td
+    if tt < tr:
+        return v1 + (v2 - v1) * tt / tr
+    if tt < tr + pw:
+        return v2
+    if tt < tr + pw + tf:
+        return v2 + (v1 - v2) * (tt - tr - pw) / tf
+    return v1
+
+
+def netlist_system(a, device):
+    """The reference's PG workload (src/mna_solve_gpu_gmres.cpp:190-647): a
+    synthetic IBM-PG-style netlist (ggmres.matrices.pg_netlist: R mesh, decap
+    to ground at every node, PULSE load currents, VDD pads = package R +
+    voltage source) read by the library's SPICE front end (gg_host_read_netlist)
+    into MNA G, C, B; A = G + C/h at the netlist's .tran step; the split
+    preconditioner of the PG engine with non-identity permutations: the
+    pivoting ordering that puts the voltage-source branch rows' zero diagonals
+    off the diagonal (mna_pivot_order: tail of pad / branch unknowns first),
+    (L, U) = the device ILU(0) of B = P_r A P_c (leftILU semantics), unit
+    scales; b = B u(t) + (C/h) x0 at t = 10 steps (loads switched on), x0 = 0.
+    ILU++ itself is not built here: its multilevel factors are
+    replaced by this ILU(0) with the same kind of row / column permutations."""
+    import tempfile
+    import scipy.sparse as sp
+    import ggmres
+    from ggmres import host as H, matrices as M
+    t0 = time.perf_counter()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "pg.sp")
+        ng, npad = M.pg_netlist(path, a.grid, a.grid, pad_stride=a.pad_stride)
+        t1 = time.perf_counter()
+        nl = H.Netlist(path)
+    t_parse = time.perf_counter() - t1
+    h = nl.tstep
+    A = (nl.G + nl.C / h).tocsr()
+    A.sort_indices()
+    n = A.shape[0]
+    prow, pcol = M.mna_pivot_order(ng, npad, n)
+    Pr = sp.csr_matrix((np.ones(n), (np.arange(n), prow)), shape=(n, n))
+    Pc = sp.csr_matrix((np.ones(n), (np.arange(n), pcol)), shape=(n, n))
+    B = (Pr @ A @ Pc).tocsr()
+    B.sort_indices()
+    f = ggmres.Solver(device)
+    f.set_matrix(B)
+    vals, _ = f.ilu0_device_values()
+    f.close()
+    F = sp.csr_matrix((vals, B.indices, B.indptr), shape=(n, n))
+    L = (sp.tril(F, -1) + sp.identity(n)).tocsr()
+    U = sp.triu(F).tocsr()
+    L.sort_indices()
+    U.sort_indices()
+    ones = np.ones(n)
+    t = 10 * h
+    u = np.array([par[0] if kind == 0 else pulse_at(par, t) if kind == 1 else np.interp(t, par[0::2], par[1::2])
+                  for kind, par in nl.sources])
+    b = np.asarray(nl.B @ u).ravel()
+    info = {"n_grid": ng, "pads": npad, "n": n, "nnz": int(A.nnz), "h": h, "t": t,
+            "parse_s": round(t_parse, 3), "setup_s": round(time.perf_counter() - t0, 3)}
+    return A, b, (L, U, ones, prow, pcol, ones, ones), info
 
 
 def cpu_model():
@@ -572,18 +643,23 @@ def main():
     c4 = a.workload == "c4"
     c3s = a.workload == "c3s"           # GMRES + ILU(0) on the C3 stand-in (general sparsity)
     pg = a.workload == "pg"             # the split (PG) engine on the C2 grid
+    netlist = a.workload == "netlist"   # the split engine on an MNA system from a PG netlist
     h5 = 1e-2
-    A = M.grid_7pt(a.c4_grid) if c4 else M.power_law() if c3s else M.laplacian_5pt(a.grid)
-    if c5:
-        A = M.transient(A, c=1e-3, h=h5)
-    n = A.shape[0]
-    b = M.rhs_ones(A)
-    s = ggmres.Solver(local)
     t_setup = time.perf_counter()
+    if netlist:
+        A, b, split, net_info = netlist_system(a, local)
+    else:
+        A = M.grid_7pt(a.c4_grid) if c4 else M.power_law() if c3s else M.laplacian_5pt(a.grid)
+        if c5:
+            A = M.transient(A, c=1e-3, h=h5)
+        b = M.rhs_ones(A)
+    n = A.shape[0]
+    s = ggmres.Solver(local)
     s.set_matrix(A)
     kilu = a.ilu_level if a.workload in ("c2", "c3s") else 0
-    if pg:
-        split = pg_split(A, local, identity=a.pg_perm == "identity")
+    if pg or netlist:
+        if pg:
+            split = pg_split(A, local, identity=a.pg_perm == "identity")
         s.set_precond_split(*split)
     elif kilu:
         s.set_precond_iluk_device(kilu)
@@ -748,7 +824,7 @@ def main():
                      if os.environ.get("GG_TRSV_LEVELS") == "1" else "k_trsv_flow")
         else:
             kname = KERNEL_NAMES[dom]
-        pmc_wl = "c4" if c4 else "c3s" if c3s else "pg" if pg else None
+        pmc_wl = "c4" if c4 else "c3s" if c3s else "pg" if pg else "netlist" if netlist else None
         roof = {"kernel": kname, "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
@@ -767,7 +843,7 @@ def main():
         mul = u_mul if dom == "trsv_U" else l_mul
         fm = u_fma if dom == "trsv_U" else l_fma
         cyc = CHAIN_CYCLES[(dom + "_fma") if fm else
-                           "trsv_L" if dom == "trsv_L" and not pg else "trsv_U_mul" if mul else "trsv_U"]
+                           "trsv_L" if dom == "trsv_L" and not (pg or netlist) else "trsv_U_mul" if mul else "trsv_U"]
         # the DAG's longest path (ILU(k): skew k+1; 3D: nx + ny + nz - 2, whose
         # per-step chain is the 2D one: the tile kernel's plane term is off it)
         steps = 3 * a.c4_grid - 2 if c4 else a.grid + (kilu + 1) * (a.grid - 1)
@@ -775,6 +851,15 @@ def main():
         lat = {"kernel": roof["kernel"], "bound": "dependency chain", "critical_steps": steps,
                "cycles_per_step": cyc, "clock_ghz": SHADER_GHZ, "floor_us": round(floor_us, 2),
                "achieved_us": roof["avg_us"], "frac": round(floor_us / roof["avg_us"], 4)}
+    elif roof and dom in ("trsv_L", "trsv_U") and not s.uses_wavefront:
+        # the dataflow solve (k_trsv_flow): its chain is the triangle's level
+        # count, each level one cross-workgroup hand-off (idle sc1 store -> sc1
+        # poll: 0.47 us same XCD, profiles/r04_xcd_handoff.txt)
+        lv = s.trsv_levels(0 if dom == "trsv_L" else 1)
+        floor_us = lv * 0.47
+        lat = {"kernel": roof["kernel"], "bound": "dependency chain (levels x hand-off)", "critical_steps": lv,
+               "us_per_step": 0.47, "floor_us": round(floor_us, 2), "achieved_us": roof["avg_us"],
+               "frac": round(floor_us / roof["avg_us"], 4)}
     spmv_bytes = s.bytes_spmv()
     # isolated SpMV (4 rotating copies of A, x, y: > 256 MiB, not Infinity-Cache served)
     spmv_iso_ms = s.time_spmv(reps=100, nrot=4)
@@ -786,7 +871,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and a.cpu_iters > 0 and not c5 and not c4 and not c3s:
         import oracle as O
-        if pg:
+        if pg or netlist:
             Ls, Us, mid, pr, pc, lsc, rsc = split
             osplit = O.Split(O.csr(Ls), O.csr(Us), mid, pr, pc, lsc, rsc)
         else:
@@ -797,7 +882,7 @@ def main():
         os.sched_setaffinity(0, {core})
         try:
             t1 = time.perf_counter()
-            if pg:
+            if pg or netlist:
                 o = O.gmres_split(A, osplit, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
             else:
                 o = O.gmres_left(A, L, U, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
@@ -807,7 +892,7 @@ def main():
         cpu = {"value": round(o["inner"] / ct, 3), "unit": "iterations/s", "cores": 1,
                "kind": "port", "pinned_core": core, "nproc": os.cpu_count(),
                "affinity_cores": len(aff), "cpu_model": cpu_model(),
-               "sample": f"oracle/ fp64 serial C restatement of {'GMRESilu (split)' if pg else 'GMRES_leftILU0'} on the same C2 "
+               "sample": f"oracle/ fp64 serial C restatement of {'GMRESilu (split)' if pg or netlist else 'GMRES_leftILU0'} on the same "
                          f"system, first {o['inner']} inner iterations ({ct:.1f} s), one thread "
                          f"pinned to core {core}"}
 
@@ -828,12 +913,20 @@ def main():
                                 f"(no parity claim at this size), ILU({kilu}) left (device-factored; "
                                 f"C3 names ILU(1)), GMRES({a.restart}), tol {a.tol:g}, "
                                 f"b=A*1, x0=0, one solve per step") if c3s else
+                               (f"PG netlist (the reference's mna_solve_gpu_gmres workload): synthetic "
+                                f"IBM-PG-style {a.grid}x{a.grid} R mesh + decaps + PULSE loads + {net_info['pads']} VDD "
+                                f"pads (package R + V source) -> gg_host_read_netlist -> MNA A = G + C/h "
+                                f"(h {net_info['h']:g}); PG engine (GMRESilu_GPU) with the split of the device ILU(0) "
+                                f"of P_r A P_c (pivoting order: pad / branch unknowns first), unit scales, "
+                                f"GMRES({a.restart}), tol {a.tol:g}, b = B u(t = {net_info['t']:g}), x0=0, "
+                                f"one solve per step") if netlist else
                                (f"PG engine (GMRESilu_GPU) on the C2 grid: {a.grid}x{a.grid} 5-pt Laplacian, "
                                 f"synthetic ILU++-style split (device ILU(0) of P_r D_l^-1 A D_r^-1 P_c, "
                                 f"{a.pg_perm} permutations, seeded scales), GMRES({a.restart}), tol {a.tol:g}, "
                                 f"b=A*1, x0=0, one solve per step") if pg else
                                (f"C2: {a.grid}x{a.grid} 5-pt Laplacian CSR, ILU({kilu}) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, one solve per step"),
+                   **({"netlist": net_info} if netlist else {}),
                    "n": n, "nnz": int(A.nnz), "restart": a.restart, "tol": a.tol,
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
                    "wavefront_sptrsv": s.uses_wavefront,

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -115,7 +116,9 @@ struct Levels {
     std::vector<int> ptr;    // nlev+1
     std::vector<int> rows;   // n
 };
-Levels level_sets(const CanonTri &T);
+// ext_cols: columns >= n (an upper tail's references into the bordered grid,
+// solved before it) are ignored rather than rejected
+Levels level_sets(const CanonTri &T, bool ext_cols = false);
 
 // 2D structured-grid wavefront layout (SURVEY.md 7 hard parts)
 //   natural row r = j*nx + i, band = j/64, lane l = j%64, step t = i + l:
@@ -154,9 +157,19 @@ struct Wave2D {
     // stays the grid's plane count).
     bool tile = false;
     int NJ = 0, NK = 0;           // tiles along the line / plane directions
+    // bordered grid (detect_border2d; 2D, skew 1): the first `bnt` rows are a
+    // tail of non-grid rows (an MNA system's pad nodes and voltage-source
+    // branch currents, pivoted ahead of the mesh) at slots [0, bnt); grid row
+    // r >= bnt at bofs + its 2D slot.  P covers both.
+    int bnt = 0;
+    long long bofs = 0;
     static constexpr int kTileGran = 16;   // hand-off values per step: 8 plane-edge + 8 line-edge
     long long ngran() const { return tile ? (long long)nbands * T * kTileGran : (long long)nz * nbands * T; }
     long long slot(long long r) const {
+        if (r < bnt) return r;
+        return bofs + grid_slot(r - bnt);
+    }
+    long long grid_slot(long long r) const {
         const long long nxy = (long long)nx * ny;
         const long long k = r / nxy, q = r % nxy;
         if (tile) {
@@ -179,6 +192,14 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U, bool split_u = false)
 // 3D: offsets {nx*ny, nx, 1} in this order in L and in U (canonical orders),
 // no wrap-around; nz >= 2 planes of the 2D layout
 Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U);
+// Bordered 2D grid: rows [0, nt) a small tail (any pattern), rows [nt, n) an
+// unskewed 5-point grid block that detect_wave2d accepts once the tail columns
+// are stripped from its L rows (they must lead each row's canonical order: the
+// tail is solved first, and b - sum(tail terms) is the head of the row's own
+// sum).  U rows of the grid reference the grid only (U rows of the tail may
+// reference anything).  gl / gu: the grid block's triangles (indices - nt, tail
+// terms of L stripped).  ok=false otherwise.
+Wave2D detect_border2d(const CanonTri &L, const CanonTri &U, bool split_u, CanonTri &gl, CanonTri &gu);
 
 // rows with more off-diagonal terms than this are solved by a whole wave in the
 // sync-free triangular solve (kernels.hip k_trsv_flow)
@@ -287,13 +308,33 @@ struct DevTri {
     long long *trace = nullptr;  // diagnostics: per band, nbatch+1 timestamps (gg_trace_precond)
     double bytes = 0;            // algorithmic bytes per solve
     double bytes_mul = 0;        // the same with WD_MUL (y streamed in place of d (, y))
-    double alg_bytes() const { const int e = eff_div(); return (e == WD_MUL || e == WD_SFMA) ? bytes_mul : bytes; }
+    double alg_bytes() const
+    {
+        const int e = eff_div();
+        return ((e == WD_MUL || e == WD_SFMA) ? bytes_mul : bytes) + (tail ? tail->bytes + cbytes : 0.0);
+    }
+    // Bordered grid (Wave2D::bnt; this triangle = the grid block's wavefront,
+    // its arrays and pointers relative to slot bofs): the tail rows as a LEVEL
+    // triangle over the whole layout (columns are slots), solved by the flow
+    // kernel before the grid (lower) or after it (upper); the lower grid rows'
+    // tail terms as a coupling CSR (absolute row slots, tail columns) applied to
+    // b in place between the two (b must be scratch: the split engine's t1)
+    std::unique_ptr<DevTri> tail;
+    long long bofs = 0;
+    int ncoup = 0;
+    DBuf<long long> cslot;
+    DBuf<int> crp, cci;
+    DBuf<double> cv;
+    double cbytes = 0;
 };
 
 // device triangle from a canonical one: WAVE2D when `wl` is an active grid
 // layout (nat2lay: row -> slot, arrays of length Ppad), else LEVEL (solver.hip)
 void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector<long long> *nat2lay,
                long long Ppad, hipStream_t st);
+// bordered grid (wl.bnt > 0): C the whole canonical triangle, Cg its grid
+// block (detect_border2d); exact division only (the tail's flow kernel divides)
+void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const Wave2D &wl, hipStream_t st);
 long long round_up(long long a, long long b);
 
 struct DevState;   // device-side GMRES control block (kernels.h)

@@ -87,7 +87,7 @@ CanonTri canon_upper_firstdiag(const Csr &U)
     return C;
 }
 
-Levels level_sets(const CanonTri &T)
+Levels level_sets(const CanonTri &T, bool ext_cols)
 {
     const int n = T.off.n;
     std::vector<int> lev(n, 0);
@@ -99,6 +99,7 @@ Levels level_sets(const CanonTri &T)
             GG_REQUIRE(T.lower ? c < r : c > r, GG_EINVAL,
                        std::string(T.lower ? "lower" : "upper") + " factor has an entry on the wrong side of the diagonal at row " +
                            std::to_string(r));
+            if (ext_cols && c >= n) continue;
             l = std::max(l, lev[c] + 1);
         }
         lev[r] = l;
@@ -168,6 +169,80 @@ Wave2D detect_wave2d(const CanonTri &L, const CanonTri &U, bool split_u)
     w.T = (nx + 63 * w.skew + 2 * (w.skew - 1) + kWaveTAlign - 1) / kWaveTAlign * kWaveTAlign;
     w.P2 = (long long)w.nbands * w.T * 64;
     w.P = w.P2;
+    return w;
+}
+
+Wave2D detect_border2d(const CanonTri &L, const CanonTri &U, bool split_u, CanonTri &gl, CanonTri &gu)
+{
+    Wave2D w;
+    const int n = L.off.n;
+    if (n < 256 || U.off.n != n) return w;
+    // the line length: the most frequent L offset above 1
+    std::vector<int> cnt;
+    for (int r = 0; r < n; r++)
+        for (int k = L.off.rp[r]; k < L.off.rp[r + 1]; k++) {
+            const int o = r - L.off.ci[k];
+            if (o > 1 && o <= 65536) {
+                if ((int)cnt.size() <= o) cnt.resize(o + 1, 0);
+                cnt[o]++;
+            }
+        }
+    int nx = 0;
+    for (int o = 2; o < (int)cnt.size(); o++)
+        if (cnt[o] > (nx ? cnt[nx] : 0)) nx = o;
+    if (nx < 3 || cnt[nx] < n / 4) return w;
+    // the tail: every row with a U term off the grid pattern, and every row
+    // with an off-pattern L term into the grid block, lies in it (a fixed point:
+    // the tail grows until the grid rows' odd L terms all point into it)
+    int nt = 0;
+    for (int r = 0; r < n; r++)
+        for (int k = U.off.rp[r]; k < U.off.rp[r + 1]; k++) {
+            const int o = U.off.ci[k] - r;
+            if (o != 1 && o != nx) nt = std::max(nt, r + 1);
+        }
+    for (bool grew = true; grew;) {
+        grew = false;
+        for (int r = nt; r < n; r++)
+            for (int k = L.off.rp[r]; k < L.off.rp[r + 1]; k++) {
+                const int c = L.off.ci[k], o = r - c;
+                if (o != 1 && o != nx && c >= nt) {
+                    nt = r + 1;
+                    grew = true;
+                    break;
+                }
+            }
+    }
+    const int ng = n - nt;
+    if (nt == 0 || nt > n / 8 || ng % nx != 0 || ng / nx < 2) return w;
+    // the grid block; the tail terms of its L rows must lead the row
+    auto block = [&](const CanonTri &T, CanonTri &B) -> bool {
+        B = CanonTri{};
+        B.lower = T.lower;
+        B.off.n = ng;
+        B.off.rp.assign(ng + 1, 0);
+        B.d.assign(T.d.begin() + nt, T.d.end());
+        for (int r = nt; r < n; r++) {
+            bool grid = false;
+            for (int k = T.off.rp[r]; k < T.off.rp[r + 1]; k++) {
+                const int c = T.off.ci[k];
+                if (c < nt) {
+                    if (grid) return false;
+                    continue;
+                }
+                grid = true;
+                B.off.ci.push_back(c - nt);
+                B.off.v.push_back(T.off.v[k]);
+            }
+            B.off.rp[r - nt + 1] = (int)B.off.ci.size();
+        }
+        return true;
+    };
+    if (!block(L, gl) || !block(U, gu)) return w;
+    w = detect_wave2d(gl, gu, split_u);
+    if (!w.ok || w.skew != 1) return Wave2D{};
+    w.bnt = nt;
+    w.bofs = (nt + 63LL) / 64 * 64;      // the grid's arrays stay 512-B aligned
+    w.P = w.bofs + w.P2;
     return w;
 }
 

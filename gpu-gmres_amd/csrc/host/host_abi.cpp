@@ -119,6 +119,39 @@ int gg_host_wave3d(int n, const int *l_rp, const int *l_ci, const double *l_v, c
     }
 }
 
+int gg_host_split_layout(int n, const int *l_rp, const int *l_ci, const double *l_v, const int *u_rp,
+                         const int *u_ci, const double *u_v, long long *slot, int *info)
+{
+    if (n < 0 || !info) return GG_EINVAL;
+    try {
+        const CanonTri cl = canon_lower_lastdiag(wrap(n, l_rp, l_ci, l_v));
+        const CanonTri cu = canon_upper_firstdiag(wrap(n, u_rp, u_ci, u_v));
+        // the solver's choice (solver.hip gg_set_precond_split)
+        Wave2D w = detect_wave2d(cl, cu, true);
+        if (!w.ok) {
+            CanonTri gl, gu;
+            w = detect_border2d(cl, cu, true, gl, gu);
+        }
+        if (w.ok && w.nbands > 512) w.ok = false;
+        for (int k = 0; k < 9; k++) info[k] = 0;
+        if (!w.ok) return 0;
+        info[0] = w.bnt ? 5 : 2;
+        info[1] = w.nx;
+        info[2] = w.ny;
+        info[3] = w.nz;
+        info[4] = w.nbands;
+        info[5] = w.T;
+        info[6] = w.bnt;
+        info[7] = (int)w.bofs;
+        info[8] = w.skew;
+        if (slot)
+            for (int r = 0; r < n; r++) slot[r] = w.slot(r);
+        return 1;
+    } catch (...) {
+        return GG_EINVAL;
+    }
+}
+
 int gg_host_wave_layout(int n, const int *l_rp, const int *l_ci, const double *l_v, const int *u_rp,
                         const int *u_ci, const double *u_v, long long *slot, int *info)
 {

@@ -692,6 +692,23 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
     }
 }
 
+// Bordered grid, forward solve (DevTri::tail): a grid row's tail terms lead
+// its canonical order, so b[row] - (its tail terms, in order) is exactly the
+// head of the row's own sum; it is formed here, in place, once the tail is
+// solved, and the wavefront continues the sum from it.  One row per thread.
+__global__ void k_border_sub(Gate g, int nrow, const long long *__restrict__ slot, const int *__restrict__ rp,
+                             const int *__restrict__ ci, const double *__restrict__ v,
+                             const double *__restrict__ x, double *b)
+{
+    if (gated(g)) return;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nrow) return;
+    const long long p = slot[q];
+    double acc = b[p];
+    for (int k = rp[q]; k < rp[q + 1]; k++) acc = acc - v[k] * x[ci[k]];
+    b[p] = acc;
+}
+
 // The sharded solve's separator step in ONE launch (dd.hip apply_minv): the
 // three row phases of SepFlow -- separator L rows (b_S - L_SI y_I, then the
 // separator triangle's terms, / d), separator U rows (y_S, then the triangle's
@@ -3659,7 +3676,7 @@ int wave_batch_steps(int div, bool d3, int skew)
 bool fused_spmv_ok(const DevTri &T, const DevCsr &A)
 {
     const Wave2D &w = T.wl;
-    return T.kind == DevTri::WAVE2D && T.lower && w.ok && !w.tile && w.nz == 1 && w.skew == 1 && !T.trace &&
+    return T.kind == DevTri::WAVE2D && T.lower && !T.tail && w.ok && !w.tile && w.nz == 1 && w.skew == 1 && !T.trace &&
            (T.eff_div() == WD_UFMA || T.eff_div() == WD_SFMA) && A.sell && w.T % kFsGroup == 0 &&
            (long long)A.nslice >= (long long)w.nbands * w.T && (long long)A.n >= (long long)w.nbands * w.T * 64;
 }
@@ -3699,7 +3716,30 @@ void launch_trsv_spmv(Gate g, DevTri &T, const DevCsr &A, const double *v, doubl
             g, wl.T, wl.nbands, T.c1s.p, T.c2s.p, T.rw.p, nullptr, x, T.bnd.p, err, wl.P2, fs);
 }
 
+static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st);
+
 void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st)
+{
+    if (!T.tail) {
+        launch_trsv_one(g, T, b, x, err, st);
+        return;
+    }
+    // bordered grid: tail, coupling, grid (forward); grid, tail (backward)
+    DevTri &tl = *T.tail;
+    tl.fast = 0;
+    if (T.lower) {
+        launch_trsv_one(g, tl, b, x, err, st);
+        if (T.ncoup)
+            k_border_sub<<<(T.ncoup + kBlock - 1) / kBlock, kBlock, 0, st>>>(
+                g, T.ncoup, T.cslot.p, T.crp.p, T.cci.p, T.cv.p, x, const_cast<double *>(b));
+        launch_trsv_one(g, T, b + T.bofs, x + T.bofs, err, st);
+    } else {
+        launch_trsv_one(g, T, b + T.bofs, x + T.bofs, err, st);
+        launch_trsv_one(g, tl, b, x, err, st);
+    }
+}
+
+static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st)
 {
     if (T.kind == DevTri::LEVEL) {
         const int nlev = (int)T.lev_ptr.size() - 1;

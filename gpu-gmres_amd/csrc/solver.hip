@@ -133,9 +133,15 @@ std::vector<int> tile_order(const Wave2D &w)
 
 // Build a device triangular solve from a canonical triangle.  WAVE2D when a
 // grid layout is active, else LEVEL (one launch per dependency level).
+void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st);
+
 void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector<long long> *nat2lay,
                long long Ppad, hipStream_t st)
 {
+    T.tail.reset();
+    T.bofs = 0;
+    T.ncoup = 0;
+    T.cbytes = 0;
     T.lower = C.lower;
     T.n = C.off.n;
     T.il = !C.lower && wl && wl->ok && wl->u_inline_first;
@@ -227,10 +233,18 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
         T.bytes_mul = (double)n * (8.0 * ((unit ? 4 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
     } else {
+        build_level(T, C, level_sets(C), st);
+    }
+}
+
+// LEVEL triangle: the flow kernel's tasks over the level sets `lv` of C
+void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st)
+{
+    const int n = C.off.n;
+    {
         T.kind = DevTri::LEVEL;
         T.off.upload(C.off, st);
         T.d.upload(C.d, st);
-        Levels lv = level_sets(C);
         T.lev_ptr = lv.ptr;
         T.lev_rows.upload(lv.rows, st);
         // flow tasks in level order: runs of up to 64 short rows, long rows alone
@@ -257,6 +271,68 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         T.tasks.upload(tasks, st);
         T.bytes = 12.0 * C.off.nnz() + 4.0 * (n + 1) + 24.0 * n;
     }
+}
+
+void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const Wave2D &wl, hipStream_t st)
+{
+    const int nt = wl.bnt;
+    // the grid block: a plain 2D wavefront in its own slot space
+    Wave2D wg = wl;
+    wg.bnt = 0;
+    wg.bofs = 0;
+    wg.P = wg.P2;
+    std::vector<long long> gslot(Cg.off.n);
+    for (int r = 0; r < Cg.off.n; r++) gslot[r] = wg.slot(r);
+    build_tri(T, Cg, &wg, &gslot, round_up(wg.P2, 512), st);
+    // exact division only: the tail rows divide in the flow kernel, so the
+    // grid must too for the reference's bits (no WD_MUL / fused forms)
+    T.mul_ok = false;
+    T.fma_ok = false;
+    T.bofs = wl.bofs;
+    // the tail over the whole layout (its columns are slots); level sets over
+    // the tail's own rows only (an upper tail's grid columns are final before it runs)
+    CanonTri Ct;
+    Ct.lower = C.lower;
+    Ct.off.n = nt;
+    Ct.off.rp.assign(nt + 1, 0);
+    Ct.d.assign(C.d.begin(), C.d.begin() + nt);
+    for (int r = 0; r < nt; r++) {
+        for (int k = C.off.rp[r]; k < C.off.rp[r + 1]; k++) {
+            Ct.off.ci.push_back((int)wl.slot(C.off.ci[k]));
+            Ct.off.v.push_back(C.off.v[k]);
+        }
+        Ct.off.rp[r + 1] = (int)Ct.off.ci.size();
+    }
+    T.tail = std::make_unique<DevTri>();
+    T.tail->lower = C.lower;
+    T.tail->n = nt;
+    build_level(*T.tail, Ct, level_sets(Ct, true), st);
+    // the grid rows' tail terms (lower: the leading terms of the row, detect_border2d)
+    std::vector<long long> cs;
+    std::vector<int> crp(1, 0), cci;
+    std::vector<double> cv;
+    for (int r = nt; r < C.off.n; r++) {
+        const int k0 = C.off.rp[r];
+        int k = k0;
+        while (k < C.off.rp[r + 1] && C.off.ci[k] < nt) k++;
+        if (k == k0) continue;
+        GG_REQUIRE(C.lower, GG_EINVAL, "bordered grid: an upper grid row references the tail");
+        cs.push_back(wl.slot(r));
+        for (int q = k0; q < k; q++) {
+            cci.push_back(C.off.ci[q]);
+            cv.push_back(C.off.v[q]);
+        }
+        crp.push_back((int)cci.size());
+    }
+    T.ncoup = (int)cs.size();
+    if (T.ncoup) {
+        T.cslot.upload(cs, st);
+        T.crp.upload(crp, st);
+        T.cci.upload(cci, st);
+        T.cv.upload(cv, st);
+    }
+    // coupling: per row its slot, b read + written; per term column, value, x
+    T.cbytes = 24.0 * T.ncoup + 4.0 * (T.ncoup + 1) + 20.0 * cci.size();
 }
 
 }  // namespace gg
@@ -493,6 +569,8 @@ void prof_end(gg_solver *s, int mark);
 void trsv(gg_solver *s, Gate g, DevTri &T, int kind, int i, const double *in, double *out)
 {
     const int mk = i >= 0 ? prof_begin(s, kind, i) : -1;
+    // a bordered forward solve forms its grid rows' heads in b (DevTri::tail)
+    GG_REQUIRE(!T.tail || !T.lower || in == s->t1.p, GG_EINVAL, "bordered forward solve: input must be scratch");
     T.fast = s->div_mode;
     launch_trsv(g, T, in, out, s->err.p, s->st);
     prof_end(s, mk);
@@ -691,6 +769,7 @@ UnitMap unit_map(const gg_solver *s)
         return um;
     }
     const Wave2D &w = s->wl;
+    if (w.bnt) return um;                                   // bordered grid: every unit
     um.kind = w.tile ? 2 : 1;
     um.nx = w.nx;
     um.ny = w.ny;
@@ -1414,15 +1493,29 @@ int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const d
     // grid-shaped factors (the split of a 5-point grid in natural order) take
     // the 2D wavefront: L rows ascending = the kernel's order, U rows ascending
     // = in-line term first (u_inline_first)
+    // A power grid's MNA system pivoted with its pads and voltage-source
+    // branches first (ggmres.matrices.mna_pivot_order) is a bordered grid:
+    // the tail by the flow kernel, the mesh by the wavefront (GG_NO_BORDER=1:
+    // the flow kernel for everything)
     Wave2D wl;
+    CanonTri gl, gu;
     const char *env = std::getenv("GG_NO_WAVEFRONT");
     if (!(env && env[0] == '1')) {
         wl = detect_wave2d(cl, cu, true);
+        if (!wl.ok) {
+            const char *nb = std::getenv("GG_NO_BORDER");
+            if (!(nb && nb[0] == '1')) wl = detect_border2d(cl, cu, true, gl, gu);
+        }
         if (wl.ok && wl.nbands > 512) wl.ok = false;
     }
     setup_space(s, &wl, perm_row, perm_col);
-    build_tri(s->L, cl, &wl, &s->nat2lay_h, s->Ppad, s->st);
-    build_tri(s->U, cu, &wl, &s->nat2lay_h, s->Ppad, s->st);
+    if (wl.ok && wl.bnt) {
+        build_tri_bordered(s->L, cl, gl, wl, s->st);
+        build_tri_bordered(s->U, cu, gu, wl, s->st);
+    } else {
+        build_tri(s->L, cl, &wl, &s->nat2lay_h, s->Ppad, s->st);
+        build_tri(s->U, cu, &wl, &s->nat2lay_h, s->Ppad, s->st);
+    }
     const long long Pp = s->Ppad;
     const std::vector<long long> &lay = s->nat2lay_h;
     // padding slots: every divisor and multiplier 1.0 (apply_start divides by
@@ -1502,6 +1595,20 @@ int gg_set_division(gg_solver *s, int mode)
     }
     s->div_mode = mode;
     return GG_OK;
+}
+int gg_trsv_levels(gg_solver *s, int which)
+{
+    if (!s || (which != 0 && which != 1)) return GG_EINVAL;
+    const DevTri &T = which ? s->U : s->L;
+    if (T.kind == DevTri::LEVEL) return (int)T.lev_ptr.size() - 1;
+    if (T.kind == DevTri::WAVE2D) {
+        const Wave2D &w = T.wl;
+        // (bordered: the tail's levels run before / after the grid's)
+        const int tail = T.tail ? (int)T.tail->lev_ptr.size() - 1 : 0;
+        if (w.nz > 1) return w.nx + w.ny + w.nz - 2 + tail;
+        return w.nx + w.skew * (w.ny - 1) + tail;
+    }
+    return 0;
 }
 int gg_mgs_kernel(gg_solver *s, char *name, int cap)
 {
@@ -1998,8 +2105,8 @@ int gg_trace_precond(gg_solver *s, int which, long long *out, long long cap, int
     GG_REQUIRE(s && out && nbands && nbatch && (which == 0 || which == 1), GG_EINVAL, "bad argument");
     GG_REQUIRE(s->pkind >= 0, GG_ESTATE, "no preconditioner");
     DevTri &T = which == 0 ? s->L : s->U;
-    GG_REQUIRE(T.kind == DevTri::WAVE2D && ((T.wl.nz == 1 && T.wl.skew == 1) || T.wl.tile), GG_ESTATE,
-               "unskewed 2D or 3D tile wavefront path not active");
+    GG_REQUIRE(T.kind == DevTri::WAVE2D && !T.tail && ((T.wl.nz == 1 && T.wl.skew == 1) || T.wl.tile), GG_ESTATE,
+               "unskewed 2D or 3D tile wavefront path not active (bordered grids are not traced)");
     set_device(s);
     ensure_workspace(s, std::max(s->m_alloc, 1));
     // per band (2D) 3 nbatch + 8 words, per tile (3D tiles, k_trsv_tile3d) 5 nbatch + 8

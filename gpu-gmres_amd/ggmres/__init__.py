@@ -33,7 +33,7 @@ EXPORTS = [
     "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced",
     "gg_transient_mna", "gg_set_division", "gg_division_active",
     "gg_trsv_kernel", "gg_mgs_kernel", "gg_set_precond_user", "gg_solve_device_f32",
-    "gg_device_fingerprint", "gg_set_matrix_count",
+    "gg_device_fingerprint", "gg_set_matrix_count", "gg_trsv_levels",
 ]
 # gg_precond_fn: int (*)(void *ctx, int op, const float *in, float *out, int n), device arrays
 PRECOND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -100,6 +100,7 @@ def lib():
         L.gg_device_fingerprint.argtypes = [ctypes.POINTER(_VP), ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_ulonglong)]
         L.gg_set_matrix_count.restype = ctypes.c_longlong
+        L.gg_trsv_levels.argtypes = [_VP, ctypes.c_int]
         L.gg_solve.argtypes = [_VP, _D, _D, ctypes.POINTER(Options), ctypes.POINTER(Result)]
         L.gg_solve_device.argtypes = [_VP, _VP, _VP, ctypes.POINTER(Options),
                                       ctypes.POINTER(Result)]
@@ -267,6 +268,10 @@ class Solver:
     def division_active(self, which):
         """the division triangle `which` (0 = L / Ml, 1 = U / Mr) runs with"""
         return _check(lib().gg_division_active(self.h, int(which)), allow_nc=True)
+
+    def trsv_levels(self, which):
+        """dependency chain of triangle `which`: levels (dataflow solve) or wavefront steps"""
+        return _check(lib().gg_trsv_levels(self.h, int(which)), allow_nc=True)
 
     def trsv_kernel(self, which):
         """rocprofv3 name of the kernel running triangle `which` (0 = L, 1 = U)"""

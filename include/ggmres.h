@@ -213,6 +213,10 @@ int gg_trsv_kernel(gg_solver *s, int which, char *name, int cap);
  * iterations (k_arnoldi_persist<J> / k_arnoldi_wide), "" when the per-step
  * kernels ran (or before the first solve); returns its length */
 int gg_mgs_kernel(gg_solver *s, char *name, int cap);
+/* the dependency chain of triangle `which` (0 = L / Ml, 1 = U / Mr): its
+ * level count (the dataflow solve), or the wavefront's critical steps
+ * (nx + skew (ny - 1) for a 2D band layout, nx + ny + nz - 2 for 3D) */
+int gg_trsv_levels(gg_solver *s, int which);
 /* 1 if the structured-grid wavefront triangular solve is active, else 0 */
 int gg_uses_wavefront(gg_solver *s);
 /* the SpMV kernel the solver's matrix takes: 1 sliced ELL (k_spmv_sell: short,

@@ -89,6 +89,15 @@ int gg_host_wave3d(int n, const int *l_row_ptr, const int *l_col_idx, const doub
 int gg_host_wave_layout(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,
                         const int *u_row_ptr, const int *u_col_idx, const double *u_val,
                         long long *slot, int *info);
+/* The same for the split (ILU++) factors of gg_set_precond_split (L diagonal
+ * last, U diagonal first; the PG path's MyILUPP::HostPrecond_left/_right,
+ * src/preconditioner.cu:1094-1137): info[0] = 2 (2D bands) or 5 (bordered
+ * grid: the first info[6] rows -- an MNA system's pads and voltage-source
+ * branches -- at slots [0, info[6]), the grid rows at info[7] + their 2D
+ * slot), info[1..5] = nx, ny, nz, bands, T.  0 when the layout is natural. */
+int gg_host_split_layout(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,
+                         const int *u_row_ptr, const int *u_col_idx, const double *u_val,
+                         long long *slot, int *info);
 /* coo2csrDouble_in (src/formatConvert.cpp:165-216): COO -> CSR in place;
  * on return row_idx[0..nrows] holds the row pointers (row_idx needs
  * max(nz, nrows + 1) slots), entries of a row bubble-sorted by column.

@@ -300,3 +300,44 @@ def test_wave_layout_matches_restatement(ggmres_lib, dims):
     assert len(np.unique(slot)) == n
     lay2nat, _ = device_layout(n, nx, ny if nz > 1 else None)
     assert np.array_equal(lay2nat[slot], np.arange(n))
+
+
+def split_layout(lib, L, U):
+    n = L.n
+    slot = np.zeros(max(n, 1), np.int64)
+    info = np.zeros(9, np.int32)
+    ok = lib.gg_host_split_layout(ctypes.c_int(n), L.rp.ctypes.data_as(PI), L.ci.ctypes.data_as(PI),
+                                  L.v.ctypes.data_as(PD), U.rp.ctypes.data_as(PI), U.ci.ctypes.data_as(PI),
+                                  U.v.ctypes.data_as(PD), slot.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)),
+                                  info.ctypes.data_as(PI))
+    return ok, slot[:n], info
+
+
+@pytest.mark.parametrize("grid, stride", [(60, 20), (150, 50), (64, 30)])
+def test_split_layout_bordered_netlist(ggmres_lib, tmp_path, grid, stride):
+    """An MNA power grid pivoted with its pads and branch rows first
+    (mna_pivot_order) is a bordered grid for the split engine: the tail of
+    2 x pads rows at slots [0, tail), the mesh as a 2D wavefront after them --
+    the layout the order-matched oracle restates (device_layout border=)."""
+    from helpers import device_layout, make_split, netlist_system
+    A, prow, pcol, nt = netlist_system(str(tmp_path / "pg.sp"), grid, stride)
+    n = A.shape[0]
+    P = make_split(A, seed=3, perm=(prow, pcol))
+    ok, slot, info = split_layout(ggmres_lib, P.L, P.U)
+    assert ok == 1 and info[0] == 5 and tuple(info[1:3]) == (grid, grid)
+    assert info[6] == nt and info[7] == (nt + 63) // 64 * 64
+    assert len(np.unique(slot)) == n
+    lay2nat, _ = device_layout(n, grid, border=nt)
+    assert np.array_equal(lay2nat[slot], np.arange(n))
+
+
+def test_split_layout_plain_and_natural(ggmres_lib):
+    """grid-shaped split factors: the plain 2D layout; a random symmetric
+    permutation of the grid: natural order"""
+    from helpers import make_split
+    A = M.laplacian_5pt(48, 40)
+    P = make_split(A, seed=9, identity_perm=True)
+    ok, slot, info = split_layout(ggmres_lib, P.L, P.U)
+    assert ok == 1 and info[0] == 2 and info[6] == 0 and tuple(info[1:3]) == (48, 40)
+    P = make_split(A, seed=9)
+    assert split_layout(ggmres_lib, P.L, P.U)[0] == 0
