@@ -101,6 +101,9 @@ def parse():
                         "solve at N > 1; dd: the sharded solve (C4 unless --dd-grid c2); replicas: "
                         "one independent C2 solve per rank; c5: a backward-Euler transient (A = G + C/h, "
                         "1%% PULSE sources) of --c5-steps time steps per step")
+    p.add_argument("--dd-part", choices=["slabs", "grid"], default="slabs",
+                   help="dd: base partition -- slabs = contiguous index ranges (GG_PART_BLOCKS) or grid = "
+                        "px x py rectangles of the 2D grid (GG_PART_GRID: interior chains nx/px + ny/py)")
     p.add_argument("--dd-sep", choices=["color", "natural"], default="color",
                    help="dd: separator order -- a greedy colouring of its graph (GG_PART_COLOR_SEP, "
                         "default: a few-level separator solve) or partition4's ascending index")
@@ -423,7 +426,8 @@ def bench_dd(a, torch, dist, world, rank, local):
     elif world == 1:
         d = DD(a.dd_parts, device=local)
         ranks = 1
-    d.set_system(A, host.PART_BLOCKS | (host.PART_COLOR_SEP if a.dd_sep == "color" else 0))
+    part = host.PART_GRID if a.dd_part == "grid" else host.PART_BLOCKS
+    d.set_system(A, part | (host.PART_COLOR_SEP if a.dd_sep == "color" else 0))
     import ggmres
     dd_div = a.division
     d.set_division(DIV_MODES[dd_div])
@@ -527,7 +531,7 @@ def bench_dd(a, torch, dist, world, rank, local):
         "ms_per_step": round(el_max * 1e3 / a.steps, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": (f"sharded solve: {'C4 %d^3 7-pt' % a.c4_grid if a.dd_grid == 'c4' else 'C2 %dx%d 5-pt' % (a.grid, a.grid)}"
-                                f", {parts}-way partition4 (contiguous slabs) arrow ordering"
+                                f", {parts}-way partition4 ({'px x py grid rectangles' if a.dd_part == 'grid' else 'contiguous slabs'}) arrow ordering"
                                 f"{', separator by colour' if a.dd_sep == 'color' else ''}, ILU(0) of "
                                 f"the permuted matrix, GMRES({a.restart}), tol {a.tol:g}, b=A*1, x0=0, "
                                 f"one solve per step"),

@@ -1038,8 +1038,8 @@ int gg_dd_set_system(gg_dd *d, int n, const int *rp, const int *ci, const double
     GG_API_BEGIN
     GG_REQUIRE(d && rp && (n == 0 || (ci && val)), GG_EINVAL, "null argument");
     GG_REQUIRE(n >= 1 && rp[0] == 0, GG_EINVAL, "dd: bad CSR");
-    GG_REQUIRE((method & ~GG_PART_COLOR_SEP) == GG_PART_BISECT || (method & ~GG_PART_COLOR_SEP) == GG_PART_BLOCKS,
-               GG_EINVAL, "dd: method must be GG_PART_BISECT or GG_PART_BLOCKS (| GG_PART_COLOR_SEP)");
+    GG_REQUIRE((method & ~(GG_PART_COLOR_SEP | 3)) == 0 && (method & 3) != 3, GG_EINVAL,
+               "dd: method must be GG_PART_BISECT, GG_PART_BLOCKS or GG_PART_GRID (| GG_PART_COLOR_SEP)");
     for (int r = 0; r < n; r++) {
         GG_REQUIRE(rp[r + 1] >= rp[r], GG_EINVAL, "dd: row_ptr not monotone");
         for (int k = rp[r]; k < rp[r + 1]; k++)

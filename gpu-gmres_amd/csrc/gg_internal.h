@@ -57,6 +57,10 @@ void ilu0_left(const Csr &A, Csr &L, Csr &U);                 // leftILU semanti
 void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &node_part,
                      std::vector<int> &part_size, std::vector<int> &pinv, std::vector<int> &q);
 Csr arrow_permute(const Csr &A, const std::vector<int> &pinv, const std::vector<int> &q);
+// GG_PART_GRID's shape: line length nx (the pattern's most frequent |offset| > 1)
+// and px x py = nparts blocks (px the largest divisor <= sqrt); nx = 0 if A is not
+// a natural-order grid of whole lines with room for the blocks
+void grid_blocks(const Csr &A, int nparts, int &nx, int &px, int &py);
 Csr csr_block(const Csr &A, int r0, int r1, int c0, int c1);
 // Matrix Market reader (host/mtx.cpp; readSparseMatrix semantics, fp64)
 bool read_mtx(const char *path, bool expand_symmetric, int &nrows, int &ncols, Csr &A);

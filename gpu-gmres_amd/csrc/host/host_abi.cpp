@@ -186,7 +186,7 @@ int gg_host_partition(int n, const int *rp, const int *ci, int nparts, int metho
                       int *part_size, int *pinv, int *q)
 {
     if (n < 1 || !rp || !ci || nparts < 1 || nparts > n || !node_part || !part_size || !pinv || !q ||
-        ((method & ~GG_PART_COLOR_SEP) != GG_PART_BISECT && (method & ~GG_PART_COLOR_SEP) != GG_PART_BLOCKS))
+        (method & ~(GG_PART_COLOR_SEP | 3)) != 0 || (method & 3) == 3)
         return GG_EINVAL;
     try {
         std::vector<double> none(rp[n], 0.0);

@@ -106,6 +106,34 @@ void bisect(const std::vector<int> &xadj, const std::vector<int> &adj, std::vect
 
 }  // namespace
 
+void grid_blocks(const Csr &A, int nparts, int &nx, int &px, int &py)
+{
+    // line length: the most frequent |offset| above 1 of the pattern
+    const int n = A.n;
+    std::vector<int> cnt;
+    for (int r = 0; r < n; r++)
+        for (int k = A.rp[r]; k < A.rp[r + 1]; k++) {
+            const int o = std::abs(A.ci[k] - r);
+            if (o > 1 && o <= (1 << 20)) {
+                if ((int)cnt.size() <= o) cnt.resize(o + 1, 0);
+                cnt[o]++;
+            }
+        }
+    nx = 0;
+    for (int o = 2; o < (int)cnt.size(); o++)
+        if (cnt[o] > (nx ? cnt[nx] : 0)) nx = o;
+    if (nx == 0 || n % nx != 0) {
+        nx = px = py = 0;
+        return;
+    }
+    // px the largest divisor of nparts not above sqrt(nparts), py = nparts / px
+    px = 1;
+    for (int d = 1; (long long)d * d <= nparts; d++)
+        if (nparts % d == 0) px = d;
+    py = nparts / px;
+    if (px > nx || py > n / nx) nx = px = py = 0;
+}
+
 void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &node_part,
                      std::vector<int> &part_size, std::vector<int> &pinv, std::vector<int> &q)
 {
@@ -116,6 +144,18 @@ void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &nod
     if ((method & 3) == GG_PART_BLOCKS) {
         // contiguous index ranges: strips / slabs of a natural-order grid
         for (int j = 0; j < n; j++) node_part[j] = (int)((long long)j * nparts / n);
+    } else if ((method & 3) == GG_PART_GRID) {
+        // px x py rectangles of a natural-order grid (grid_blocks): each
+        // interior stays a rectangle in row-major order, a sub-grid whose
+        // wavefront chain is nx/px + ny/py rather than a slab's nx + ny/N
+        int nx = 0, px = 0, py = 0;
+        grid_blocks(A, nparts, nx, px, py);
+        GG_REQUIRE(nx > 0, GG_EINVAL, "GG_PART_GRID: the matrix is not a natural-order grid");
+        const int ny = n / nx;
+        for (int j = 0; j < n; j++) {
+            const int bx = (int)((long long)(j % nx) * px / nx), by = (int)((long long)(j / nx) * py / ny);
+            node_part[j] = by * px + bx;
+        }
     } else {
         std::vector<int> all(n), mark(n, 0), seen(n, 0);
         std::iota(all.begin(), all.end(), 0);

@@ -7,7 +7,7 @@ import scipy.sparse as sp
 
 from . import _check, _csr_arrays, lib
 
-PART_BISECT, PART_BLOCKS, PART_COLOR_SEP = 0, 1, 4
+PART_BISECT, PART_BLOCKS, PART_GRID, PART_COLOR_SEP = 0, 1, 2, 4
 _PI = ctypes.POINTER(ctypes.c_int)
 _PD = ctypes.POINTER(ctypes.c_double)
 

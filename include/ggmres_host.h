@@ -47,6 +47,9 @@ int gg_host_wave2d(int n, const int *l_row_ptr, const int *l_col_idx, const doub
 enum gg_part_method {
     GG_PART_BISECT = 0,    /* recursive BFS bisection of the node graph (METIS stand-in) */
     GG_PART_BLOCKS = 1,    /* contiguous index ranges (strips / slabs of a natural-order grid) */
+    GG_PART_GRID = 2,      /* px x py rectangles of a natural-order 2D grid (px the largest divisor
+                              of nparts <= sqrt(nparts); line length = the pattern's most frequent
+                              |offset| > 1): rectangular interiors, shorter wavefront chains */
     GG_PART_COLOR_SEP = 4  /* flag (extension): separator ordered by a greedy colouring of its
                               graph, then by index, instead of by index alone */
 };

@@ -79,6 +79,31 @@ def blocks_base(n, nparts):
     return [j * nparts // n for j in range(n)]
 
 
+def grid_base(rp, ci, n, nparts):
+    """GG_PART_GRID (an extension, not in the reference): px x py rectangles
+    of a natural-order grid.  Line length nx = the most frequent |offset| > 1
+    of the pattern (ties: the smallest), px = the largest divisor of nparts not
+    above sqrt(nparts), py = nparts / px; node j = (i, y) = (j % nx, j // nx)
+    goes to part (y * py // ny) * px + i * px // nx.  None if not a grid."""
+    off = {}
+    for r in range(n):
+        for k in range(rp[r], rp[r + 1]):
+            o = abs(int(ci[k]) - r)
+            if 1 < o <= (1 << 20):
+                off[o] = off.get(o, 0) + 1
+    if not off:
+        return None
+    nx = min(off, key=lambda o: (-off[o], o))
+    if n % nx:
+        return None
+    ny = n // nx
+    px = max(d for d in range(1, nparts + 1) if d * d <= nparts and nparts % d == 0)
+    py = nparts // px
+    if px > nx or py > ny:
+        return None
+    return [((j // nx) * py // ny) * px + (j % nx) * px // nx for j in range(n)]
+
+
 def permute_dense(A, pinv):
     """P A P^T as a dense array (small test sizes)"""
     D = np.asarray(A.todense())

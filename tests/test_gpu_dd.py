@@ -35,6 +35,10 @@ CASES = {
     "5pt_200x160_P4_color": (lambda: M.laplacian_5pt(200, 160), 4, host.PART_BLOCKS | host.PART_COLOR_SEP, 2, 1),
     "7pt_16x16x32_P8_upwind_color": (lambda: M.grid_7pt(16, 16, 32, upwind=0.1), 8,
                                      host.PART_BLOCKS | host.PART_COLOR_SEP, 3, 1),
+    # px x py rectangles (GG_PART_GRID): rectangular interiors on the 2D
+    # wavefront with chains of nx/px + ny/py steps, a cross-shaped separator
+    "5pt_200x160_P4_grid": (lambda: M.laplacian_5pt(200, 160), 4, host.PART_GRID | host.PART_COLOR_SEP, 2, 1),
+    "5pt_160x200_P8_grid": (lambda: M.laplacian_5pt(160, 200), 8, host.PART_GRID | host.PART_COLOR_SEP, 2, 1),
 }
 
 _cache = {}

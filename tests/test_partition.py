@@ -61,6 +61,39 @@ def test_partition4_color_separator_exact(name, nparts):
             assert max(lev.values()) + 1 <= 2
 
 
+@pytest.mark.parametrize("dims", [(40, 30), (64, 64), (37, 50)])
+@pytest.mark.parametrize("nparts", [2, 4, 6, 8])
+def test_partition4_grid_blocks_exact(dims, nparts):
+    """GG_PART_GRID: px x py rectangles of a 2D grid, then partition4's
+    adjustment -- exact vs the restatement; every interior is a full rectangle
+    (a row-major sub-grid: the sharded solve's wavefront applies to it) whose
+    sides are about nx/px and ny/py"""
+    nx, ny = dims
+    A = M.laplacian_5pt(nx, ny)
+    n = A.shape[0]
+    got = H.partition(A, nparts, H.PART_GRID)
+    ref = OP.partition4_adjust(A.indptr, A.indices, n, nparts, OP.grid_base(A.indptr, A.indices, n, nparts))
+    for k, r in zip(("node_part", "part_size", "pinv", "q"), ref):
+        assert np.array_equal(got[k], r), k
+    px = max(d for d in range(1, nparts + 1) if d * d <= nparts and nparts % d == 0)
+    py = nparts // px
+    for p in range(nparts):
+        nodes = np.flatnonzero(got["node_part"] == p)
+        i, y = nodes % nx, nodes // nx
+        w, h = i.max() - i.min() + 1, y.max() - y.min() + 1
+        assert w * h == nodes.size                       # a full rectangle
+        assert abs(w - nx / px) <= 3 and abs(h - ny / py) <= 3   # two separator layers, rounding
+        assert np.all(np.diff(nodes) > 0)                # row-major in the permuted order
+        b0 = got["begin"][p]
+        assert np.array_equal(got["q"][b0:b0 + nodes.size], nodes)
+
+
+def test_partition_grid_rejects_non_grid():
+    A = M.power_law(800, 6000, seed=9)
+    with pytest.raises(Exception):
+        H.partition(A, 4, H.PART_GRID)
+
+
 @pytest.mark.parametrize("name", sorted(GRIDS))
 @pytest.mark.parametrize("method", [H.PART_BLOCKS, H.PART_BISECT, H.PART_BLOCKS | H.PART_COLOR_SEP])
 @pytest.mark.parametrize("nparts", [2, 4, 8])
