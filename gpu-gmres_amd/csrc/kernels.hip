@@ -2840,31 +2840,88 @@ __device__ __forceinline__ unsigned long long poll_granule(const unsigned long l
     return a;
 }
 
+// A thread's granules of a G-partial row (q = threadIdx.x + r*kBlock, G <=
+// 1024): all of them loaded at once, then only the pending ones polled again --
+// one memory round trip for the row instead of one per granule (a poll loop
+// per granule serializes them: G = 544 put three sc1 round trips on every
+// all-gather).  The sum is taken afterwards in q order, as before: same bits.
+constexpr int kGatherPer = 4;
+template <int NP>
+__device__ __forceinline__ bool gather_row(const unsigned long long *row, int G, unsigned long long (&a)[NP],
+                                           int limit, const int *abortw)
+{
+#pragma unroll
+    for (int r = 0; r < NP; r++) {
+        const int q = threadIdx.x + r * kBlock;
+        a[r] = q < G ? ld_agent(row + q) : 0ull;
+    }
+    int spins = 0;
+    while (true) {
+        bool pend = false;
+#pragma unroll
+        for (int r = 0; r < NP; r++) pend |= a[r] == kSentinel;
+        if (!pend) return true;
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int r = 0; r < NP; r++)
+            if (a[r] == kSentinel) a[r] = ld_agent(row + threadIdx.x + r * kBlock);
+        if (abortw && (spins & 255) == 255 && (ld_agent_int(abortw) & DONE_ABORT)) return false;
+        if (++spins > limit) return false;
+    }
+}
+template <int NP>
+__device__ __forceinline__ double gather_row_sum(const unsigned long long (&a)[NP], int G)
+{
+    double v = 0.0;
+#pragma unroll
+    for (int r = 0; r < NP; r++)
+        if (threadIdx.x + r * kBlock < G) v += __longlong_as_double((long long)a[r]);
+    return v;
+}
+
+// NP: granules per thread the row may have (G <= NP * kBlock); NP = 0: one
+// poll loop per granule (k_arnoldi_wide, whose 256 VGPRs are taken by w and
+// the stream: the parallel form spills there)
+template <int NP = kGatherPer>
 __device__ __forceinline__ double gather_sum(const unsigned long long *row, int G, int *err, int &par,
                                              const int *abortw = nullptr)
 {
-    double v = 0.0;
-    for (int q = threadIdx.x; q < G; q += kBlock)
-        v += __longlong_as_double((long long)poll_granule(row + q, err, abortw));
-    return block_sum_pp(v, par);
+    if constexpr (NP == 0) {
+        double v = 0.0;
+        for (int q = threadIdx.x; q < G; q += kBlock)
+            v += __longlong_as_double((long long)poll_granule(row + q, err, abortw));
+        return block_sum_pp(v, par);
+    } else {
+        unsigned long long a[NP];
+        if (!gather_row<NP>(row, G, a, kSpinLimit, abortw) && !(abortw && (ld_agent_int(abortw) & DONE_ABORT)))
+            atomicOr(err, 1);
+        return block_sum_pp(gather_row_sum<NP>(a, G), par);
+    }
 }
 
 // The launch's first all-gather with the co-residency bound: false = this
 // block timed out (DONE_ABORT set) and must return (block-uniform)
+template <int NP = kGatherPer>
 __device__ __forceinline__ bool gather_first(const unsigned long long *row, int G, DevState *ds, int &par,
                                              double &h)
 {
     double v = 0.0;
     int miss = 0;
-    for (int q = threadIdx.x; q < G; q += kBlock) {
-        unsigned long long a = ld_agent(row + q);
-        int spins = 0;
-        while (a == kSentinel && !miss) {
-            __builtin_amdgcn_s_sleep(1);
-            a = ld_agent(row + q);
-            if (++spins > kResidSpin) miss = 1;
+    if constexpr (NP == 0) {
+        for (int q = threadIdx.x; q < G; q += kBlock) {
+            unsigned long long a = ld_agent(row + q);
+            int spins = 0;
+            while (a == kSentinel && !miss) {
+                __builtin_amdgcn_s_sleep(1);
+                a = ld_agent(row + q);
+                if (++spins > kResidSpin) miss = 1;
+            }
+            v += __longlong_as_double((long long)a);
         }
-        v += __longlong_as_double((long long)a);
+    } else {
+        unsigned long long a[NP];
+        miss = gather_row<NP>(row, G, a, kResidSpin, nullptr) ? 0 : 1;
+        v = gather_row_sum<NP>(a, G);
     }
     if (__syncthreads_or(miss)) {
         if (threadIdx.x == 0) set_abort(ds);
@@ -2882,12 +2939,12 @@ __device__ __forceinline__ bool gather_first(const unsigned long long *row, int 
 // more hop.  Measured (C2 / C4, profiles/r03_gather_ab.txt): k_arnoldi_wide
 // (C4, streaming the basis beside the polls) 472.5 -> 456.6 us, so it leads;
 // k_arnoldi_persist (C2) 73.2 -> 77.5 us, so every block gathers there.
-template <bool LEADER>
+template <bool LEADER, int NP = kGatherPer>
 __device__ __forceinline__ double gather_h(const unsigned long long *row, unsigned long long *hg, int k, int G,
                                            int *err, int &par, const int *abortw)
 {
     if (!LEADER || blockIdx.x == 0) {
-        const double h = gather_sum(row, G, err, par, abortw);
+        const double h = gather_sum<LEADER ? 0 : NP>(row, G, err, par, abortw);
         if (LEADER && threadIdx.x == 0) st_agent(hg, (unsigned long long)__double_as_longlong(h));
         return h;
     }
@@ -2899,12 +2956,12 @@ __device__ __forceinline__ double gather_h(const unsigned long long *row, unsign
 // step 0 of a launch: gather_h with the co-residency bound on every wait
 // (LEADER: block 0 gathers with the bound, the others' poll of its sum granule
 // is bounded alike -- whichever block is missing, every waiting block times out)
-template <bool LEADER>
+template <bool LEADER, int NP = kGatherPer>
 __device__ __forceinline__ bool gather_h_first(const unsigned long long *row, unsigned long long *hg, int G,
                                                DevState *ds, int &par, double &h)
 {
     if (!LEADER || blockIdx.x == 0) {
-        if (!gather_first(row, G, ds, par, h)) return false;
+        if (!gather_first<LEADER ? 0 : NP>(row, G, ds, par, h)) return false;
         if (LEADER && threadIdx.x == 0) st_agent(hg, (unsigned long long)__double_as_longlong(h));
         return true;
     }
@@ -2967,11 +3024,12 @@ __device__ __forceinline__ void xcd_elect(unsigned long long *elect, unsigned lo
     xcc = sx;
 }
 // step k's sum: slot = this XCD's word of step k
+template <int NP>
 __device__ __forceinline__ double gather_xcd(const unsigned long long *row, unsigned long long *slot, int k, int G,
                                             bool red, int *err, int &par, const int *abortw)
 {
     if (red) {
-        const double h = gather_sum(row, G, err, par, abortw);
+        const double h = gather_sum<NP>(row, G, err, par, abortw);
         if (threadIdx.x == 0) st_plain(slot, (unsigned long long)__double_as_longlong(h));
         return h;
     }
@@ -2980,11 +3038,12 @@ __device__ __forceinline__ double gather_xcd(const unsigned long long *row, unsi
     __syncthreads();
     return hb[k & 1];
 }
+template <int NP>
 __device__ __forceinline__ bool gather_xcd_first(const unsigned long long *row, unsigned long long *slot, int G,
                                                  bool red, DevState *ds, int &par, double &h)
 {
     if (red) {
-        if (!gather_first(row, G, ds, par, h)) return false;
+        if (!gather_first<NP>(row, G, ds, par, h)) return false;
         if (threadIdx.x == 0) st_plain(slot, (unsigned long long)__double_as_longlong(h));
         return true;
     }
@@ -3014,6 +3073,7 @@ __device__ __forceinline__ bool gather_xcd_first(const unsigned long long *row, 
 // PF: v_{k+1} streamed while step k's sum is gathered (1), or after it (0):
 // polls issued behind a wave's own in-flight basis loads wait for them (the
 // memory returns in order) and the gather then also pays the stream's latency
+constexpr int persist_np(int J) { return J >= 8 ? 0 : kGatherPer; }
 template <int J, int XG, int PF>
 __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m, DevState *ds,
                                                             const double *__restrict__ w_in,
@@ -3025,6 +3085,9 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
                                                             unsigned long long *elect, unsigned long long seq,
                                                             UnitMap um)
 {
+    // granules per thread loaded at once in the all-gathers (persist_np; J =
+    // 8 polls them one by one: the parallel form would cost it an occupancy step)
+    constexpr int kNP = persist_np(J);
     if (gated(g)) return;
     if (block_aborted(ds)) return;                            // co-residency (gather_first)
     bool red = true;
@@ -3071,13 +3134,13 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         if constexpr (PF) load_next();                        // v_{k+1}, in flight during the sum
         double h;
         if (k == 0) {
-            if (XG == 2 ? !gather_xcd_first(gran, xslot(0), G, red, ds, par, h)
-                        : !gather_h_first<false>(gran, hg, G, ds, par, h))
+            if (XG == 2 ? !gather_xcd_first<kNP>(gran, xslot(0), G, red, ds, par, h)
+                        : !gather_h_first<false, kNP>(gran, hg, G, ds, par, h))
                 return;
         } else if constexpr (XG == 2) {
-            h = gather_xcd(gran + (long long)k * G, xslot(k), k, G, red, err, par, abortw);
+            h = gather_xcd<kNP>(gran + (long long)k * G, xslot(k), k, G, red, err, par, abortw);
         } else {
-            h = gather_h<false>(gran + (long long)k * G, hg + k, k, G, err, par, abortw);
+            h = gather_h<false, kNP>(gran + (long long)k * G, hg + k, k, G, err, par, abortw);
         }
         if constexpr (!PF) {
             __builtin_amdgcn_sched_barrier(0);
@@ -3099,9 +3162,9 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(XG == 2 ? gather_xcd(gran + (long long)(i + 1) * G, xslot(i + 1), i + 1, G, red, err, par,
+    const double hn = sqrt(XG == 2 ? gather_xcd<kNP>(gran + (long long)(i + 1) * G, xslot(i + 1), i + 1, G, red, err, par,
                                                 abortw)
-                                   : gather_h<false>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par,
+                                   : gather_h<false, kNP>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par,
                                                      abortw));
     if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
         const int ld = m + 1;
@@ -4047,6 +4110,8 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             const UnitMap &um, hipStream_t st)
 {
     const int J = arnoldi_persist_units(G, Ppad);
+    GG_REQUIRE(persist_np(J) == 0 || G <= persist_np(J) * kBlock, GG_EINVAL,
+               "k_arnoldi_persist: grid beyond the all-gather's reach");
     const int xg = mgs_gather_form();
     const int pf = mgs_prefetch();
 #define GG_PERSIST(JJ, XG, PF)                                                                       \

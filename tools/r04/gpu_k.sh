@@ -16,3 +16,15 @@ import json; d=json.loads(open('gpurun_out/r04k_netlist_${g}_nb$nb.json').read()
 k=d['kernels']; c=d['config']; print('netlist $g nb=$nb', d['value'], c['iters_per_solve'], c['relres'], c['netlist'], {n:k[n]['avg_us'] for n in k}); print(d['roofline']); print(d.get('latency_roofline')); print(d['cpu_baseline'])"
   done
 done
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_dd.py -k "grid" \
+  > gpurun_out/r04k_dd_grid_tests.log 2>&1 || { tail -40 gpurun_out/r04k_dd_grid_tests.log; exit 1; }
+tail -4 gpurun_out/r04k_dd_grid_tests.log
+for P in 4 8; do
+  for part in slabs grid; do
+    timeout -k 10 300 python -u bench.py --workload dd --dd-grid c2 --dd-parts $P --dd-part $part --steps 2 --warmup 1 \
+      > gpurun_out/r04k_dd_${P}_$part.json 2> gpurun_out/r04k_dd_${P}_$part.err || { tail -20 gpurun_out/r04k_dd_${P}_$part.err; exit 1; }
+    python3 -c "
+import json; d=json.loads(open('gpurun_out/r04k_dd_${P}_$part.json').read().strip().splitlines()[-1])
+print('dd P=$P $part', d['value'], d['config'].get('iters_per_solve'), d.get('roofline'), d.get('kernels'))"
+  done
+done

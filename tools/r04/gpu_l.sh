@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 4: parallel all-gather polls in the persistent MGS -- parity + C2 bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_residency.py tests/test_gpu_c2_history.py \
+  "tests/test_gpu_parity.py::test_gmres_left_c1_parity" tests/test_gpu_fastdiv.py \
+  > gpurun_out/r04l_tests.log 2>&1 || { tail -40 gpurun_out/r04l_tests.log; exit 1; }
+tail -3 gpurun_out/r04l_tests.log
+timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 > gpurun_out/r04l_c2.json 2> gpurun_out/r04l_c2.err || { tail -20 gpurun_out/r04l_c2.err; exit 1; }
+python3 -c "
+import json; d=json.loads(open('gpurun_out/r04l_c2.json').read().strip().splitlines()[-1])
+k=d['kernels']; print('c2', d['value'], {n:k[n]['avg_us'] for n in k}); print(d['roofline'])"
