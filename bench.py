@@ -101,9 +101,10 @@ def parse():
                         "solve at N > 1; dd: the sharded solve (C4 unless --dd-grid c2); replicas: "
                         "one independent C2 solve per rank; c5: a backward-Euler transient (A = G + C/h, "
                         "1%% PULSE sources) of --c5-steps time steps per step")
-    p.add_argument("--dd-part", choices=["slabs", "grid"], default="slabs",
+    p.add_argument("--dd-part", choices=["slabs", "grid"], default=None,
                    help="dd: base partition -- slabs = contiguous index ranges (GG_PART_BLOCKS) or grid = "
-                        "px x py rectangles of the 2D grid (GG_PART_GRID: interior chains nx/px + ny/py)")
+                        "px x py rectangles of the 2D grid (GG_PART_GRID: interior chains nx/px + ny/py); "
+                        "default grid on the C2 system, slabs on C4")
     p.add_argument("--dd-sep", choices=["color", "natural"], default="color",
                    help="dd: separator order -- a greedy colouring of its graph (GG_PART_COLOR_SEP, "
                         "default: a few-level separator solve) or partition4's ascending index")
@@ -623,6 +624,10 @@ def main():
         a.workload = "c2" if world == 1 else "dd"
         a.dd_grid = a.dd_grid or "c2"
     a.dd_grid = a.dd_grid or "c4"
+    # rectangles on the 2D grid (GG_PART_GRID: chains nx/px + ny/py, and the
+    # C2 solve converges in fewer iterations: 3,910 vs 6,369 at 4 shards,
+    # profiles/r04k_dd_4_*.json), slabs on the 3D one
+    a.dd_part = a.dd_part or ("grid" if a.dd_grid == "c2" else "slabs")
     replicas = a.workload == "replicas"
     if replicas:
         a.workload = "c2"
