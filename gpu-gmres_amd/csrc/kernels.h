@@ -178,7 +178,8 @@ int arnoldi_persist_max_blocks(int J);
 // gather_xcd; re-armed with the granules), elect: kMgsElectWords words (zeroed
 // once), seq: strictly increasing per launch
 constexpr int kMgsXcdWords = 8 * 16, kMgsElectWords = 8 * 16;
-int mgs_gather_form();   // GG_MGS_GATHER: 0 every block gathers, 2 XCD-local reducers
+constexpr int kMgsXcds = 8;          // XCDs (GG_MGS_GATHER 3: one reducer-only block each)
+int mgs_gather_form();   // GG_MGS_GATHER: 0 every block gathers, 2 XCD-local reducers, 3 reducer-only blocks
 int mgs_prefetch();      // GG_MGS_PREFETCH: 1 v_{k+1} streamed during the gather, 0 after it
 void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
                             long long ldv, double *H, double *cs, double *sn, double *s,

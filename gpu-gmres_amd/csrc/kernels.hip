@@ -3023,6 +3023,32 @@ __device__ __forceinline__ void xcd_elect(unsigned long long *elect, unsigned lo
     red = sr != 0;
     xcc = sx;
 }
+// XG 3: a unit-holding block reduces for its XCD only when no reducer-only
+// block has claimed the XCD for this launch (word 1 of the XCD's election
+// slot).  The reducer-only blocks are blocks 0..kXcds-1, dispatched first and
+// (round-robin) one per XCD, so the claim is normally there already; a short
+// bounded wait covers its landing, and an XCD left without one (placement is
+// not guaranteed) elects a unit-holding block as in XG 2.  Two reducers on one
+// XCD store the same bits into its slot: harmless.
+__device__ __forceinline__ void xcd_elect3(unsigned long long *elect, unsigned long long seq, bool &red,
+                                           unsigned &xcc)
+{
+    __shared__ unsigned sx;
+    __shared__ int sr;
+    if (threadIdx.x == 0) {
+        const unsigned x = xcc_id();
+        sx = x;
+        bool claimed = false;
+        for (int t = 0; t < 16 && !claimed; t++) {
+            claimed = ld_agent(elect + x * kXcdSlot + 1) == seq;
+            if (!claimed) __builtin_amdgcn_s_sleep(8);
+        }
+        sr = !claimed && atomicMax(elect + x * kXcdSlot, seq) < seq;
+    }
+    __syncthreads();
+    red = sr != 0;
+    xcc = sx;
+}
 // step k's sum: slot = this XCD's word of step k
 template <int NP>
 __device__ __forceinline__ double gather_xcd(const unsigned long long *row, unsigned long long *slot, int k, int G,
@@ -3090,14 +3116,41 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     constexpr int kNP = persist_np(J);
     if (gated(g)) return;
     if (block_aborted(ds)) return;                            // co-residency (gather_first)
+    // XG 3: the first kXcds blocks hold no units; they only reduce (below)
+    constexpr int XR = XG == 3 ? kXcds : 0;
+    const int G = gridDim.x - XR;                             // the blocks holding units
+    const int ub = (int)blockIdx.x - XR;                      // this block's unit-block index
+    const int *abortw = &ds->done;
     bool red = true;
     unsigned xcc = 0;
-    if constexpr (XG == 2) xcd_elect(elect, seq, red, xcc);
     auto xslot = [&](int k) { return xb + ((long long)k * kXcds + xcc) * kXcdSlot; };
-    const int G = gridDim.x;
+    if constexpr (XG == 3) {
+        if (ub < 0) {
+            // reducer-only block: claim this XCD for the launch, then gather
+            // every step's row (no basis loads in front of its polls) and
+            // store the sum into the XCD's slot -- gather_xcd's reducer half
+            int par = 0;
+            __shared__ unsigned sxr;
+            if (threadIdx.x == 0) {
+                sxr = xcc_id();
+                atomicMax(elect + sxr * kXcdSlot + 1, seq);
+            }
+            __syncthreads();
+            xcc = sxr;
+            double h;
+            if (!gather_first<kNP>(gran, G, ds, par, h)) return;
+            if (threadIdx.x == 0) st_plain(xslot(0), (unsigned long long)__double_as_longlong(h));
+            for (int k = 1; k <= i + 1; k++) {
+                h = gather_sum<kNP>(gran + (long long)k * G, G, err, par, abortw);
+                if (threadIdx.x == 0) st_plain(xslot(k), (unsigned long long)__double_as_longlong(h));
+            }
+            return;
+        }
+        xcd_elect3(elect, seq, red, xcc);
+    }
+    if constexpr (XG == 2) xcd_elect(elect, seq, red, xcc);
     const long long stride = (long long)G * kBlock;
-    const long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x;
-    const int *abortw = &ds->done;
+    const long long u0 = ub * (long long)kBlock + threadIdx.x;
     double2 w[J], vk[J], vn[J];
     bool val[J];                                              // unit holds a real row (UnitMap)
 #pragma unroll
@@ -3112,7 +3165,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     int par = 0;                                              // block_sum_pp's LDS row
     auto publish = [&](int k, double acc) {
         acc = block_sum_pp(acc, par);
-        if (threadIdx.x == 0) st_agent(gran + (long long)k * G + blockIdx.x, (unsigned long long)__double_as_longlong(acc));
+        if (threadIdx.x == 0) st_agent(gran + (long long)k * G + ub, (unsigned long long)__double_as_longlong(acc));
     };
     double acc = 0.0;
 #pragma unroll
@@ -3134,10 +3187,10 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         if constexpr (PF) load_next();                        // v_{k+1}, in flight during the sum
         double h;
         if (k == 0) {
-            if (XG == 2 ? !gather_xcd_first<kNP>(gran, xslot(0), G, red, ds, par, h)
+            if (XG >= 2 ? !gather_xcd_first<kNP>(gran, xslot(0), G, red, ds, par, h)
                         : !gather_h_first<false, kNP>(gran, hg, G, ds, par, h))
                 return;
-        } else if constexpr (XG == 2) {
+        } else if constexpr (XG >= 2) {
             h = gather_xcd<kNP>(gran + (long long)k * G, xslot(k), k, G, red, err, par, abortw);
         } else {
             h = gather_h<false, kNP>(gran + (long long)k * G, hg + k, k, G, err, par, abortw);
@@ -3146,7 +3199,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             __builtin_amdgcn_sched_barrier(0);
             load_next();                                      // v_{k+1} after the sum
         }
-        if (blockIdx.x == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
+        if (ub == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         acc = 0.0;
 #pragma unroll
@@ -3162,11 +3215,11 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         }
         publish(k + 1, acc);
     }
-    const double hn = sqrt(XG == 2 ? gather_xcd<kNP>(gran + (long long)(i + 1) * G, xslot(i + 1), i + 1, G, red, err, par,
+    const double hn = sqrt(XG >= 2 ? gather_xcd<kNP>(gran + (long long)(i + 1) * G, xslot(i + 1), i + 1, G, red, err, par,
                                                 abortw)
                                    : gather_h<false, kNP>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par,
                                                      abortw));
-    if (blockIdx.x == 0 && threadIdx.x == 0) {               // as k_arnoldi_finalize
+    if (ub == 0 && threadIdx.x == 0) {                       // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
         Hc[i + 1] = hn;
@@ -4037,7 +4090,7 @@ void launch_arnoldi_finalize_r(Gate g, int i, int m, DevState *ds, const double 
                                               hist, Ppad / 2);
 }
 #ifndef GG_MGS_GATHER_DEFAULT
-#define GG_MGS_GATHER_DEFAULT 2
+#define GG_MGS_GATHER_DEFAULT 3
 #endif
 constexpr int kMgsGatherDefault = GG_MGS_GATHER_DEFAULT;
 
@@ -4099,8 +4152,10 @@ int mgs_prefetch()
 }
 int mgs_gather_form()
 {
-    const char *e = std::getenv("GG_MGS_GATHER");      // 0: every block gathers, 2: XCD-local reducers
-    return e ? (atoi(e) == 2 ? 2 : 0) : kMgsGatherDefault;
+    // 0: every block gathers, 2: XCD-local reducers elected among the blocks,
+    // 3: XCD-local reducer-only blocks (kXcds extra blocks)
+    const char *e = std::getenv("GG_MGS_GATHER");
+    return e ? (atoi(e) == 2 ? 2 : atoi(e) == 3 ? 3 : 0) : kMgsGatherDefault;
 }
 
 void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w, double *V,
@@ -4115,8 +4170,8 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
     const int xg = mgs_gather_form();
     const int pf = mgs_prefetch();
 #define GG_PERSIST(JJ, XG, PF)                                                                       \
-    k_arnoldi_persist<JJ, XG, PF><<<G, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, \
-                                                                         hist, gran, hg, Ppad / 2, err, xb, elect, seq, um)
+    k_arnoldi_persist<JJ, XG, PF><<<G + (XG == 3 ? kXcds : 0), kBlock, persist_test_lds(), st>>>(          \
+        g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2, err, xb, elect, seq, um)
 #define GG_PERSIST_J(XG, PF)                                                                       \
     do {                                                                                           \
         if (J == 1) GG_PERSIST(1, XG, PF);                                                         \
@@ -4124,7 +4179,9 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
         else if (J == 4) GG_PERSIST(4, XG, PF);                                                    \
         else GG_PERSIST(8, XG, PF);                                                                \
     } while (0)
-    if (xg == 2) {
+    if (xg == 3 && pf) {
+        GG_PERSIST_J(3, 1);
+    } else if (xg >= 2) {
         if (pf) GG_PERSIST_J(2, 1);
         else GG_PERSIST_J(2, 0);
     } else {

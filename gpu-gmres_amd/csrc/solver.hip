@@ -540,7 +540,9 @@ void ensure_workspace(gg_solver *s, int m)
         const char *wf = std::getenv("GG_WIDE_FORCE");
         const bool force_wide = wf && wf[0] == '1';
         const int pj = arnoldi_persist_units(s->G, s->Ppad);
-        s->persist = !off && !force_wide && pj != 0 && s->G <= arnoldi_persist_max_blocks(pj);
+        // (GG_MGS_GATHER 3: kXcds reducer-only blocks beside the G)
+        const int xr = (mgs_gather_form() == 3 && mgs_prefetch()) ? kMgsXcds : 0;
+        s->persist = !off && !force_wide && pj != 0 && s->G + xr <= arnoldi_persist_max_blocks(pj);
         s->wide = !off && !s->persist && arnoldi_wide_ok(s->G, s->Ppad);   // long vectors: w on chip
         if (s->persist || s->wide) s->gran.alloc((size_t)m * (m + 2) * (s->G + 1));
         if (s->persist) {
