@@ -3152,6 +3152,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     const long long stride = (long long)G * kBlock;
     const long long u0 = ub * (long long)kBlock + threadIdx.x;
     double2 w[J], vk[J], vn[J];
+    [[maybe_unused]] double2 vn2[PF == 2 ? J : 1];            // PF 2: v_{k+2} landing during step k
     bool val[J];                                              // unit holds a real row (UnitMap)
 #pragma unroll
     for (int j = 0; j < J; j++) {
@@ -3161,6 +3162,15 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             w[j] = ld2(w_in, u);
             vk[j] = ld2(V, u);
         }
+    }
+    auto load_v = [&](int q, double2 (&dst)[J]) {            // basis vector q, streamed
+        const double *vp = V + (long long)q * ldv;
+#pragma unroll
+        for (int j = 0; j < J; j++)
+            if (val[j]) dst[j] = ld2_nt(vp, u0 + j * stride);
+    };
+    if constexpr (PF == 2) {
+        if (i >= 1) load_v(1, vn);                            // v_1, behind w and v_0
     }
     int par = 0;                                              // block_sum_pp's LDS row
     auto publish = [&](int k, double acc) {
@@ -3176,15 +3186,9 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         }
     publish(0, acc);                                          // <w, v_0>
     for (int k = 0; k <= i; k++) {
-        auto load_next = [&]() {
-            if (k < i) {
-                const double *vnp = V + (long long)(k + 1) * ldv;
-#pragma unroll
-                for (int j = 0; j < J; j++)
-                    if (val[j]) vn[j] = ld2_nt(vnp, u0 + j * stride);   // streamed
-            }
-        };
-        if constexpr (PF) load_next();                        // v_{k+1}, in flight during the sum
+        if constexpr (PF == 1) {
+            if (k < i) load_v(k + 1, vn);                     // v_{k+1}, in flight during the sum
+        }
         double h;
         if (k == 0) {
             if (XG >= 2 ? !gather_xcd_first<kNP>(gran, xslot(0), G, red, ds, par, h)
@@ -3195,9 +3199,15 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         } else {
             h = gather_h<false, kNP>(gran + (long long)k * G, hg + k, k, G, err, par, abortw);
         }
-        if constexpr (!PF) {
+        if constexpr (PF == 0) {
             __builtin_amdgcn_sched_barrier(0);
-            load_next();                                      // v_{k+1} after the sum
+            if (k < i) load_v(k + 1, vn);                     // v_{k+1} after the sum
+        }
+        if constexpr (PF == 2) {
+            // v_{k+2} issued after this step's polls (which so find no basis
+            // loads of their own in front of them: v_{k+1} was issued a step ago)
+            __builtin_amdgcn_sched_barrier(0);
+            if (k + 2 <= i) load_v(k + 2, vn2);
         }
         if (ub == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
@@ -3211,6 +3221,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
                 acc += w[j].x * o.x;
                 acc += w[j].y * o.y;
                 vk[j] = vn[j];
+                if constexpr (PF == 2) vn[j] = vn2[j];
             }
         }
         publish(k + 1, acc);
@@ -4090,7 +4101,7 @@ void launch_arnoldi_finalize_r(Gate g, int i, int m, DevState *ds, const double 
                                               hist, Ppad / 2);
 }
 #ifndef GG_MGS_GATHER_DEFAULT
-#define GG_MGS_GATHER_DEFAULT 3
+#define GG_MGS_GATHER_DEFAULT 2
 #endif
 constexpr int kMgsGatherDefault = GG_MGS_GATHER_DEFAULT;
 
@@ -4108,9 +4119,14 @@ int arnoldi_persist_max_blocks(int J)
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     auto occ = [&](const void *f) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) == hipSuccess; };
-    const bool ok = J == 1   ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<1, 2, 1>))
-                    : J == 2 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<2, 2, 1>))
-                    : J == 4 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<4, 2, 1>))
+    // the instantiation launch_arnoldi_persist picks (PF 2 holds v_{k+2} too)
+    const bool pf2 = mgs_gather_form() == 2 && mgs_prefetch() == 2;
+    const bool ok = J == 1   ? occ(pf2 ? reinterpret_cast<const void *>(k_arnoldi_persist<1, 2, 2>)
+                                       : reinterpret_cast<const void *>(k_arnoldi_persist<1, 2, 1>))
+                    : J == 2 ? occ(pf2 ? reinterpret_cast<const void *>(k_arnoldi_persist<2, 2, 2>)
+                                       : reinterpret_cast<const void *>(k_arnoldi_persist<2, 2, 1>))
+                    : J == 4 ? occ(pf2 ? reinterpret_cast<const void *>(k_arnoldi_persist<4, 2, 2>)
+                                       : reinterpret_cast<const void *>(k_arnoldi_persist<4, 2, 1>))
                     : J == 8 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<8, 2, 1>))
                              : false;
     return ok ? cus * per : 0;
@@ -4143,12 +4159,14 @@ void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, do
 }
 
 #ifndef GG_MGS_PREFETCH_DEFAULT
-#define GG_MGS_PREFETCH_DEFAULT 1
+#define GG_MGS_PREFETCH_DEFAULT 2
 #endif
 int mgs_prefetch()
 {
-    const char *e = std::getenv("GG_MGS_PREFETCH");    // 1: v_{k+1} streamed during the gather, 0: after it
-    return e ? (atoi(e) != 0) : GG_MGS_PREFETCH_DEFAULT;
+    // 1: v_{k+1} streamed during step k's gather, 0: after it, 2: v_{k+2}
+    // issued after step k's gather (prefetch distance 2, J <= 4)
+    const char *e = std::getenv("GG_MGS_PREFETCH");
+    return e ? std::min(std::max(atoi(e), 0), 2) : GG_MGS_PREFETCH_DEFAULT;
 }
 int mgs_gather_form()
 {
@@ -4179,7 +4197,11 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
         else if (J == 4) GG_PERSIST(4, XG, PF);                                                    \
         else GG_PERSIST(8, XG, PF);                                                                \
     } while (0)
-    if (xg == 3 && pf) {
+    if (xg == 2 && pf == 2 && J <= 4) {
+        if (J == 1) GG_PERSIST(1, 2, 2);
+        else if (J == 2) GG_PERSIST(2, 2, 2);
+        else GG_PERSIST(4, 2, 2);
+    } else if (xg == 3 && pf) {
         GG_PERSIST_J(3, 1);
     } else if (xg >= 2) {
         if (pf) GG_PERSIST_J(2, 1);

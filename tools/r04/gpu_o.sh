@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 4: reducer-only blocks for the persistent MGS all-gathers (GG_MGS_PREFETCH 2) -- parity + A/B
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_residency.py tests/test_gpu_c2_history.py \
+  "tests/test_gpu_parity.py::test_gmres_left_c1_parity" tests/test_gpu_fastdiv.py tests/test_gpu_border.py \
+  > gpurun_out/r04o_tests.log 2>&1 || { tail -40 gpurun_out/r04o_tests.log; exit 1; }
+tail -3 gpurun_out/r04o_tests.log
+for pf in 2 1; do
+  GG_MGS_PREFETCH=$pf timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --cpu-iters 0 > gpurun_out/r04o_c2_pf$pf.json 2> gpurun_out/r04o_c2_pf$pf.err || { tail -20 gpurun_out/r04o_c2_pf$pf.err; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/r04o_c2_pf$pf.json').read().strip().splitlines()[-1])
+k=d['kernels']; print('c2 pf=$pf', d['value'], {n:k[n]['avg_us'] for n in k})"
+done
