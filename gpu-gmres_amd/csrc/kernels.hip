@@ -3152,7 +3152,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     const long long stride = (long long)G * kBlock;
     const long long u0 = ub * (long long)kBlock + threadIdx.x;
     double2 w[J], vk[J], vn[J];
-    [[maybe_unused]] double2 vn2[PF == 2 ? J : 1];            // PF 2: v_{k+2} landing during step k
+    [[maybe_unused]] double2 vl[PF == 2 ? J : 1];             // PF 2: the third basis buffer
     bool val[J];                                              // unit holds a real row (UnitMap)
 #pragma unroll
     for (int j = 0; j < J; j++) {
@@ -3163,7 +3163,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             vk[j] = ld2(V, u);
         }
     }
-    auto load_v = [&](int q, double2 (&dst)[J]) {            // basis vector q, streamed
+    auto load_v = [&](int q, double2 *dst) {                  // basis vector q, streamed
         const double *vp = V + (long long)q * ldv;
 #pragma unroll
         for (int j = 0; j < J; j++)
@@ -3185,15 +3185,19 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             acc += w[j].y * vk[j].y;
         }
     publish(0, acc);                                          // <w, v_0>
-    for (int k = 0; k <= i; k++) {
+    // step k: h_k, w -= h_k v_k, the partial of the next dot (v_{k+1}, or the
+    // norm), published.  cur = v_k, nxt = v_{k+1} (loaded), lnd = the buffer
+    // v_{k+2} lands in (PF 2; the three rotate, no register copies -- a copy of
+    // a landing buffer would wait for its loads)
+    auto step = [&](int k, double2 *cur, double2 *nxt, double2 *lnd) -> bool {
         if constexpr (PF == 1) {
-            if (k < i) load_v(k + 1, vn);                     // v_{k+1}, in flight during the sum
+            if (k < i) load_v(k + 1, nxt);                    // v_{k+1}, in flight during the sum
         }
         double h;
         if (k == 0) {
             if (XG >= 2 ? !gather_xcd_first<kNP>(gran, xslot(0), G, red, ds, par, h)
                         : !gather_h_first<false, kNP>(gran, hg, G, ds, par, h))
-                return;
+                return false;
         } else if constexpr (XG >= 2) {
             h = gather_xcd<kNP>(gran + (long long)k * G, xslot(k), k, G, red, err, par, abortw);
         } else {
@@ -3201,30 +3205,44 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
         }
         if constexpr (PF == 0) {
             __builtin_amdgcn_sched_barrier(0);
-            if (k < i) load_v(k + 1, vn);                     // v_{k+1} after the sum
+            if (k < i) load_v(k + 1, nxt);                    // v_{k+1} after the sum
         }
         if constexpr (PF == 2) {
-            // v_{k+2} issued after this step's polls (which so find no basis
-            // loads of their own in front of them: v_{k+1} was issued a step ago)
+            // v_{k+2} issued after this step's polls, which so find no basis
+            // loads of their own in front of them (v_{k+1} went out a step ago)
             __builtin_amdgcn_sched_barrier(0);
-            if (k + 2 <= i) load_v(k + 2, vn2);
+            if (k + 2 <= i) load_v(k + 2, lnd);
         }
         if (ub == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
-        acc = 0.0;
+        double acc = 0.0;
 #pragma unroll
         for (int j = 0; j < J; j++) {
             if (val[j]) {
-                w[j].x = a * vk[j].x + w[j].x;
-                w[j].y = a * vk[j].y + w[j].y;
-                const double2 o = (k < i) ? vn[j] : w[j];     // next dot: v_{k+1}, or the norm
+                w[j].x = a * cur[j].x + w[j].x;
+                w[j].y = a * cur[j].y + w[j].y;
+                const double2 o = (k < i) ? nxt[j] : w[j];    // next dot: v_{k+1}, or the norm
                 acc += w[j].x * o.x;
                 acc += w[j].y * o.y;
-                vk[j] = vn[j];
-                if constexpr (PF == 2) vn[j] = vn2[j];
             }
         }
         publish(k + 1, acc);
+        return true;
+    };
+    if constexpr (PF == 2) {
+        for (int k = 0; k <= i; k += 3) {
+            if (!step(k, vk, vn, vl)) return;
+            if (k + 1 > i) break;
+            step(k + 1, vn, vl, vk);
+            if (k + 2 > i) break;
+            step(k + 2, vl, vk, vn);
+        }
+    } else {
+        for (int k = 0; k <= i; k += 2) {
+            if (!step(k, vk, vn, nullptr)) return;
+            if (k + 1 > i) break;
+            step(k + 1, vn, vk, nullptr);
+        }
     }
     const double hn = sqrt(XG >= 2 ? gather_xcd<kNP>(gran + (long long)(i + 1) * G, xslot(i + 1), i + 1, G, red, err, par,
                                                 abortw)
