@@ -14,3 +14,14 @@ for pf in 2 1; do
 import json; d=json.loads(open('gpurun_out/r04o_c2_pf$pf.json').read().strip().splitlines()[-1])
 k=d['kernels']; print('c2 pf=$pf', d['value'], {n:k[n]['avg_us'] for n in k})"
 done
+# sharded solve, local shards: per-shard kernel families for the N = 2/4/8 projections
+for wl in "c2 grid" "c4 slabs"; do
+  set -- $wl
+  for P in 2 4 8; do
+    timeout -k 10 300 python -u bench.py --workload dd --dd-grid $1 --dd-part $2 --dd-parts $P --steps 1 --warmup 1 \
+      > gpurun_out/r04o_dd_$1_$P.json 2> gpurun_out/r04o_dd_$1_$P.err || { tail -20 gpurun_out/r04o_dd_$1_$P.err; exit 1; }
+    python3 -c "
+import json; d=json.loads(open('gpurun_out/r04o_dd_$1_$P.json').read().strip().splitlines()[-1])
+print('dd $1 P=$P', d['value'], d['config'].get('iters_per_solve'), d.get('families') or d.get('kernels'))"
+  done
+done
