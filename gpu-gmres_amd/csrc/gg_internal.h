@@ -301,6 +301,7 @@ struct DevTri {
     bool fma_ok = false;         // unskewed 2D grid / 3D tiles, canonical order, unit L or mul_ok U (c*s uploaded)
     int fast = 0;                // the owner's gg_set_division mode (GG_DIV_RCP: WD_MUL, GG_DIV_FMA: WD_*FMA)
     bool prefilled = false;      // LEVEL, per launch: x already holds the sentinel (flow kernel)
+    bool mul = false;            // LEVEL, per launch: x = RN(acc * rw) (a bordered grid's tail under WD_MUL)
     bool tile_queue = false;     // 3D tiles: claim tiles from a queue (after a non-resident static grid)
     int eff_div() const
     {

@@ -516,10 +516,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
 // ======================================================= triangular solves
 // Level-scheduled row solve (one launch per dependency level):
 //   x[r] = (b[r] - sum_k off[k] * x[col[k]]) / d[r]   in canonical order
+// y (optional): RN(1/d) -- x = RN(acc * y), WD_MUL's row (a bordered grid's
+// tail under gg_set_division(GG_DIV_RCP / _FMA), DevTri::tail)
 __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const int *rows,
                                                        const int *rp, const int *ci,
                                                        const double *v, const double *d,
-                                                       const double *b, double *x)
+                                                       const double *b, double *x, const double *y)
 {
     if (gated(g)) return;
     int t = blockIdx.x * kBlock + threadIdx.x;
@@ -527,7 +529,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const in
     int r = rows[t];
     double acc = b[r];
     for (int k = rp[r]; k < rp[r + 1]; k++) acc = acc - v[k] * x[ci[k]];
-    x[r] = acc / d[r];
+    x[r] = y ? acc * y[r] : acc / d[r];
 }
 
 // Sync-free (dataflow) form of the same solve, one launch per triangle: x is
@@ -557,7 +559,8 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                                                       const int *__restrict__ rp, const int *__restrict__ ci,
                                                       const double *__restrict__ v,
                                                       const double *__restrict__ d,
-                                                      const double *__restrict__ b, double *x, int *err)
+                                                      const double *__restrict__ b, double *x, int *err,
+                                                      const double *__restrict__ y)
 {
     if (gated(g)) return;
     __shared__ double prod[kBlock];            // a long row's products, one 64-slot area per wave
@@ -647,7 +650,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 }
             }
-            if (lane == 0) st_agent(xu + r, (unsigned long long)__double_as_longlong(acc / d[r]));
+            if (lane == 0) st_agent(xu + r, (unsigned long long)__double_as_longlong(y ? acc * y[r] : acc / d[r]));
             continue;
         }
         // up to 64 short rows, one per lane
@@ -656,7 +659,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
         int k = pending ? rp[r] : 0;
         const int k1 = pending ? rp[r + 1] : 0;
         double acc = pending ? b[r] : 0.0;
-        const double dr = pending ? d[r] : 1.0;
+        const double dr = pending ? (y ? y[r] : d[r]) : 1.0;   // y: the reciprocal (WD_MUL's row)
         int spins = 0;
         while (__any(pending)) {
             if (pending) {
@@ -677,7 +680,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                     }
                 }
                 if (k == k1) {
-                    st_agent(xu + r, (unsigned long long)__double_as_longlong(acc / dr));
+                    st_agent(xu + r, (unsigned long long)__double_as_longlong(y ? acc * dr : acc / dr));
                     pending = false;
                 }
             }
@@ -3872,6 +3875,7 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
     // bordered grid: tail, coupling, grid (forward); grid, tail (backward)
     DevTri &tl = *T.tail;
     tl.fast = 0;
+    tl.mul = T.eff_div() == WD_MUL;          // the tail rows divide as the grid's do
     if (T.lower) {
         launch_trsv_one(g, tl, b, x, err, st);
         if (T.ncoup)
@@ -3917,14 +3921,15 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
                 k_fill_gated<<<blocks_for(nrows, kBlock, 8192), kBlock, 0, st>>>(
                     g, reinterpret_cast<unsigned long long *>(x), nrows, kSentinel);
             k_trsv_flow<<<blocks, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p, T.off.ci.p,
-                                                   T.off.v.p, T.d.p, b, x, err);
+                                                   T.off.v.p, T.d.p, b, x, err, T.mul ? T.rw.p : nullptr);
             return;
         }
         for (int l = 0; l < nlev; l++) {
             const int cnt = T.lev_ptr[l + 1] - T.lev_ptr[l];
             if (cnt == 0) continue;
             k_trsv_level<<<(cnt + kBlock - 1) / kBlock, kBlock, 0, st>>>(
-                g, cnt, T.lev_rows.p + T.lev_ptr[l], T.off.rp.p, T.off.ci.p, T.off.v.p, T.d.p, b, x);
+                g, cnt, T.lev_rows.p + T.lev_ptr[l], T.off.rp.p, T.off.ci.p, T.off.v.p, T.d.p, b, x,
+                T.mul ? T.rw.p : nullptr);
         }
     } else if (T.kind == DevTri::WAVE2D) {
         const Wave2D &w = T.wl;

@@ -284,9 +284,10 @@ void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const 
     std::vector<long long> gslot(Cg.off.n);
     for (int r = 0; r < Cg.off.n; r++) gslot[r] = wg.slot(r);
     build_tri(T, Cg, &wg, &gslot, round_up(wg.P2, 512), st);
-    // exact division only: the tail rows divide in the flow kernel, so the
-    // grid must too for the reference's bits (no WD_MUL / fused forms)
-    T.mul_ok = false;
+    // no fused rows: GG_DIV_FMA's order (nearest term first) would put a grid
+    // row's tail terms LAST, inside the wavefront's recurrence -- under
+    // GG_DIV_FMA a bordered grid takes WD_MUL (eff_div), whose rows keep the
+    // canonical order (tail terms first), the tail rows multiplying too
     T.fma_ok = false;
     T.bofs = wl.bofs;
     // the tail over the whole layout (its columns are slots); level sets over
@@ -307,6 +308,16 @@ void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const 
     T.tail->lower = C.lower;
     T.tail->n = nt;
     build_level(*T.tail, Ct, level_sets(Ct, true), st);
+    // WD_MUL on the whole triangle needs every tail 1/d finite and normal too
+    bool tail_mul = true;
+    std::vector<double> ry(nt);
+    for (int r = 0; r < nt; r++) {
+        const double d = Ct.d[r];
+        if (!(std::fabs(d) >= 0x1p-1020 && std::fabs(d) <= 0x1p1020)) tail_mul = false;
+        ry[r] = 1.0 / d;
+    }
+    T.mul_ok = T.mul_ok && tail_mul;
+    if (T.mul_ok) T.tail->rw.upload(ry, st);
     // the grid rows' tail terms (lower: the leading terms of the row, detect_border2d)
     std::vector<long long> cs;
     std::vector<int> crp(1, 0), cci;

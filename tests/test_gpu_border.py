@@ -59,7 +59,7 @@ def test_border_operators_bitexact(systems, grid):
 @pytest.mark.parametrize("grid", [60, 150])
 def test_border_gmres_parity(systems, grid):
     """serial oracle within tolerance; order-matched oracle in the bordered
-    layout bit for bit; the fast division modes stay exact on a bordered grid"""
+    layout bit for bit"""
     A, P, nt = systems[grid]
     n = A.shape[0]
     b = np.random.default_rng(1).random(n)
@@ -79,11 +79,46 @@ def test_border_gmres_parity(systems, grid):
         assert g["ret"] == ot["ret"] and g["iters"] == ot["iters"] and g["inner"] == ot["inner"]
         assert np.array_equal(g["hist"], ot["hist"])
         assert np.array_equal(g["x"], ot["x"])
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("grid", [60, 150])
+def test_border_mul_division(systems, grid):
+    """gg_set_division(GG_DIV_RCP or GG_DIV_FMA) on a bordered grid: x =
+    RN(acc * RN(1/d)) on every row -- the mesh's wavefront (WD_MUL) and the
+    tail's flow kernel alike; FMA's fused rows would put a mesh row's tail terms
+    inside the recurrence, so FMA falls back to the multiply.  Bit-exact vs the
+    order-matched oracle in its multiply mode, within 1e-10 of the serial
+    reference arithmetic."""
+    A, P, nt = systems[grid]
+    n = A.shape[0]
+    b = np.random.default_rng(1).random(n)
+    o = O.gmres_split(A, P, b, m=32, max_iter=600, tol=1e-10)
+    lay, G = device_layout(n, grid, border=nt)
+    O.set_dot_order(lay, G)
+    O.set_div_mode(1, 1)
+    try:
+        ot = O.gmres_split(A, P, b, m=32, max_iter=600, tol=1e-10)
+        rng = np.random.default_rng(7)
+        vs = [rng.standard_normal(n) for _ in range(2)]
+        ref_ops = [(P.left(v), P.right(v)) for v in vs]
+    finally:
+        O.set_dot_order(None)
+        O.set_div_mode()
+    s = split_solver(A, P)
+    try:
         for mode in (ggmres.DIV_RCP, ggmres.DIV_FMA):
             s.set_division(mode)
-            assert s.division_active(0) == s.division_active(1) == ggmres.DIV_EXACT
-            g2 = s.solve(b, restart=32, max_iter=600, tol=1e-10)
-            assert np.array_equal(g2["x"], ot["x"])
+            assert s.division_active(0) == s.division_active(1) == ggmres.DIV_RCP
+            for v, (l, r) in zip(vs, ref_ops):
+                assert np.array_equal(s.precond_apply(ggmres.APPLY_LEFT, v), l)
+                assert np.array_equal(s.precond_apply(ggmres.APPLY_RIGHT, v), r)
+            g = s.solve(b, restart=32, max_iter=600, tol=1e-10)
+            assert g["iters"] == ot["iters"] and np.array_equal(g["hist"], ot["hist"])
+            assert np.array_equal(g["x"], ot["x"])
+            # (the serial engine divides: the convergence test may fire one iteration apart)
+            assert abs(g["iters"] - o["iters"]) <= 1 and rel_err(g["x"], o["x"]) <= 1e-8
     finally:
         s.close()
 
