@@ -4182,7 +4182,7 @@ void launch_arnoldi_wide(Gate g, int i, int m, DevState *ds, const double *w, do
 }
 
 #ifndef GG_MGS_PREFETCH_DEFAULT
-#define GG_MGS_PREFETCH_DEFAULT 2
+#define GG_MGS_PREFETCH_DEFAULT 1
 #endif
 int mgs_prefetch()
 {
