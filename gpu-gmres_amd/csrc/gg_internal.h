@@ -57,10 +57,15 @@ void ilu0_left(const Csr &A, Csr &L, Csr &U);                 // leftILU semanti
 void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &node_part,
                      std::vector<int> &part_size, std::vector<int> &pinv, std::vector<int> &q);
 Csr arrow_permute(const Csr &A, const std::vector<int> &pinv, const std::vector<int> &q);
-// GG_PART_GRID's shape: line length nx (the pattern's most frequent |offset| > 1)
-// and px x py = nparts blocks (px the largest divisor <= sqrt); nx = 0 if A is not
-// a natural-order grid of whole lines with room for the blocks
-void grid_blocks(const Csr &A, int nparts, int &nx, int &px, int &py);
+// GG_PART_GRID's shape: line length nx (the pattern's most frequent |offset| > 1),
+// for a 3D grid the plane nx*ny (the most frequent multiple of nx above it, if
+// >= n/8 entries), and px x py (x pz) = nparts blocks -- 2D: px the largest
+// divisor <= sqrt; 3D: px <= py <= pz, the most cube-like; nx = 0 if A is not a
+// natural-order grid of whole lines (planes) with room for the blocks
+struct GridBlocks {
+    int nx = 0, ny = 0, nz = 1, px = 0, py = 0, pz = 1;
+};
+void grid_blocks(const Csr &A, int nparts, GridBlocks &gb);
 Csr csr_block(const Csr &A, int r0, int r1, int c0, int c1);
 // Matrix Market reader (host/mtx.cpp; readSparseMatrix semantics, fp64)
 bool read_mtx(const char *path, bool expand_symmetric, int &nrows, int &ncols, Csr &A);

@@ -106,32 +106,61 @@ void bisect(const std::vector<int> &xadj, const std::vector<int> &adj, std::vect
 
 }  // namespace
 
-void grid_blocks(const Csr &A, int nparts, int &nx, int &px, int &py)
+void grid_blocks(const Csr &A, int nparts, GridBlocks &gb)
 {
-    // line length: the most frequent |offset| above 1 of the pattern
+    // line length: the most frequent |offset| above 1 of the pattern (ties: the
+    // smallest); plane size: the most frequent larger offset that is a multiple
+    // of it, if it is frequent (>= n/8 entries: a 7-point 3D grid)
     const int n = A.n;
+    gb = GridBlocks{};
     std::vector<int> cnt;
     for (int r = 0; r < n; r++)
         for (int k = A.rp[r]; k < A.rp[r + 1]; k++) {
             const int o = std::abs(A.ci[k] - r);
-            if (o > 1 && o <= (1 << 20)) {
+            if (o > 1 && o <= (1 << 24)) {
                 if ((int)cnt.size() <= o) cnt.resize(o + 1, 0);
                 cnt[o]++;
             }
         }
-    nx = 0;
+    int nx = 0;
     for (int o = 2; o < (int)cnt.size(); o++)
         if (cnt[o] > (nx ? cnt[nx] : 0)) nx = o;
-    if (nx == 0 || n % nx != 0) {
-        nx = px = py = 0;
-        return;
+    if (nx == 0 || n % nx != 0) return;
+    long long nxy = 0;
+    for (long long o = 2LL * nx; o < (long long)cnt.size(); o += nx)
+        if (cnt[o] >= n / 8 && cnt[o] > (nxy ? cnt[nxy] : 0)) nxy = o;
+    if (nxy && n % nxy == 0 && n / nxy >= 2) {
+        gb.nx = nx;
+        gb.ny = (int)(nxy / nx);
+        gb.nz = (int)(n / nxy);
+        // px <= py <= pz, the most cube-like factorization
+        int best = -1;
+        for (int a = 1; a <= nparts; a++) {
+            if (nparts % a) continue;
+            for (int b = a; b <= nparts / a; b++) {
+                if ((nparts / a) % b) continue;
+                const int c = nparts / a / b;
+                if (c < b) continue;
+                if (best < 0 || c - a < best) {
+                    best = c - a;
+                    gb.px = a;
+                    gb.py = b;
+                    gb.pz = c;
+                }
+            }
+        }
+    } else {
+        gb.nx = nx;
+        gb.ny = n / nx;
+        gb.nz = 1;
+        // px the largest divisor of nparts not above sqrt(nparts), py = nparts / px
+        gb.px = 1;
+        for (int d = 1; (long long)d * d <= nparts; d++)
+            if (nparts % d == 0) gb.px = d;
+        gb.py = nparts / gb.px;
+        gb.pz = 1;
     }
-    // px the largest divisor of nparts not above sqrt(nparts), py = nparts / px
-    px = 1;
-    for (int d = 1; (long long)d * d <= nparts; d++)
-        if (nparts % d == 0) px = d;
-    py = nparts / px;
-    if (px > nx || py > n / nx) nx = px = py = 0;
+    if (gb.px > gb.nx || gb.py > gb.ny || gb.pz > gb.nz) gb = GridBlocks{};
 }
 
 void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &node_part,
@@ -145,16 +174,18 @@ void partition_arrow(const Csr &A, int nparts, int method, std::vector<int> &nod
         // contiguous index ranges: strips / slabs of a natural-order grid
         for (int j = 0; j < n; j++) node_part[j] = (int)((long long)j * nparts / n);
     } else if ((method & 3) == GG_PART_GRID) {
-        // px x py rectangles of a natural-order grid (grid_blocks): each
-        // interior stays a rectangle in row-major order, a sub-grid whose
-        // wavefront chain is nx/px + ny/py rather than a slab's nx + ny/N
-        int nx = 0, px = 0, py = 0;
-        grid_blocks(A, nparts, nx, px, py);
-        GG_REQUIRE(nx > 0, GG_EINVAL, "GG_PART_GRID: the matrix is not a natural-order grid");
-        const int ny = n / nx;
+        // px x py rectangles of a natural-order 2D grid, px x py x pz boxes
+        // of a 3D one (grid_blocks): each interior stays a rectangle / box in
+        // row-major order, a sub-grid whose wavefront chain is nx/px + ny/py
+        // (+ nz/pz) rather than a slab's nx + ny/N (nx + ny + nz/N)
+        GridBlocks gb;
+        grid_blocks(A, nparts, gb);
+        GG_REQUIRE(gb.nx > 0, GG_EINVAL, "GG_PART_GRID: the matrix is not a natural-order grid");
+        const long long nxy = (long long)gb.nx * gb.ny;
         for (int j = 0; j < n; j++) {
-            const int bx = (int)((long long)(j % nx) * px / nx), by = (int)((long long)(j / nx) * py / ny);
-            node_part[j] = by * px + bx;
+            const long long i = j % gb.nx, y = (j / gb.nx) % gb.ny, z = j / nxy;
+            const int bx = (int)(i * gb.px / gb.nx), by = (int)(y * gb.py / gb.ny), bz = (int)(z * gb.pz / gb.nz);
+            node_part[j] = (bz * gb.py + by) * gb.px + bx;
         }
     } else {
         std::vector<int> all(n), mark(n, 0), seen(n, 0);

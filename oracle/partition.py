@@ -80,28 +80,50 @@ def blocks_base(n, nparts):
 
 
 def grid_base(rp, ci, n, nparts):
-    """GG_PART_GRID (an extension, not in the reference): px x py rectangles
-    of a natural-order grid.  Line length nx = the most frequent |offset| > 1
-    of the pattern (ties: the smallest), px = the largest divisor of nparts not
-    above sqrt(nparts), py = nparts / px; node j = (i, y) = (j % nx, j // nx)
-    goes to part (y * py // ny) * px + i * px // nx.  None if not a grid."""
+    """GG_PART_GRID (an extension, not in the reference): rectangles of a
+    natural-order 2D grid, boxes of a 3D one.  Line length nx = the most
+    frequent |offset| > 1 of the pattern (ties: the smallest); plane size nxy =
+    the most frequent larger multiple of nx with at least n/8 entries (3D).
+    2D: px = the largest divisor of nparts not above sqrt(nparts), py = nparts
+    / px, node j = (i, y) -> part (y * py // ny) * px + i * px // nx.  3D: px <=
+    py <= pz with pz - px smallest, node (i, y, z) -> part ((z * pz // nz) * py
+    + y * py // ny) * px + i * px // nx.  None if not a grid."""
     off = {}
     for r in range(n):
         for k in range(rp[r], rp[r + 1]):
             o = abs(int(ci[k]) - r)
-            if 1 < o <= (1 << 20):
+            if 1 < o <= (1 << 24):
                 off[o] = off.get(o, 0) + 1
     if not off:
         return None
     nx = min(off, key=lambda o: (-off[o], o))
     if n % nx:
         return None
-    ny = n // nx
-    px = max(d for d in range(1, nparts + 1) if d * d <= nparts and nparts % d == 0)
-    py = nparts // px
-    if px > nx or py > ny:
+    planes = [o for o in off if o > nx and o % nx == 0 and off[o] >= n // 8]
+    nxy = min(planes, key=lambda o: (-off[o], o)) if planes else None
+    if nxy and n % nxy == 0 and n // nxy >= 2:
+        ny, nz = nxy // nx, n // nxy
+        best = None
+        for a in range(1, nparts + 1):
+            if nparts % a:
+                continue
+            for b in range(a, nparts // a + 1):
+                if (nparts // a) % b:
+                    continue
+                c = nparts // a // b
+                if c < b:
+                    continue
+                if best is None or c - a < best[0]:
+                    best = (c - a, a, b, c)
+        _, px, py, pz = best
+    else:
+        ny, nz = n // nx, 1
+        px = max(d for d in range(1, nparts + 1) if d * d <= nparts and nparts % d == 0)
+        py, pz = nparts // px, 1
+    if px > nx or py > ny or pz > nz:
         return None
-    return [((j // nx) * py // ny) * px + (j % nx) * px // nx for j in range(n)]
+    return [(((j // (nx * ny)) * pz // nz) * py + ((j // nx) % ny) * py // ny) * px + (j % nx) * px // nx
+            for j in range(n)]
 
 
 def permute_dense(A, pinv):

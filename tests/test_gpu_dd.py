@@ -39,6 +39,8 @@ CASES = {
     # wavefront with chains of nx/px + ny/py steps, a cross-shaped separator
     "5pt_200x160_P4_grid": (lambda: M.laplacian_5pt(200, 160), 4, host.PART_GRID | host.PART_COLOR_SEP, 2, 1),
     "5pt_160x200_P8_grid": (lambda: M.laplacian_5pt(160, 200), 8, host.PART_GRID | host.PART_COLOR_SEP, 2, 1),
+    # 2 x 2 x 2 boxes of a 3D grid: box interiors on the 3D tile wavefront
+    "7pt_24_P8_grid": (lambda: M.grid_7pt(24), 8, host.PART_GRID | host.PART_COLOR_SEP, 3, 1),
 }
 
 _cache = {}

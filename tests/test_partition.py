@@ -88,6 +88,30 @@ def test_partition4_grid_blocks_exact(dims, nparts):
         assert np.array_equal(got["q"][b0:b0 + nodes.size], nodes)
 
 
+@pytest.mark.parametrize("dims, nparts, pdims", [((12, 12, 12), 8, (2, 2, 2)), ((16, 10, 12), 4, (1, 2, 2)),
+                                                 ((20, 12, 9), 2, (1, 1, 2)), ((10, 12, 14), 6, (1, 2, 3))])
+def test_partition4_grid_boxes_3d_exact(dims, nparts, pdims):
+    """GG_PART_GRID on a 3D 7-point grid: px x py x pz boxes (the most
+    cube-like factorization), exact vs the restatement; every interior a full
+    box in row-major order (the tile wavefront applies to it)"""
+    nx, ny, nz = dims
+    A = M.grid_7pt(nx, ny, nz)
+    n = A.shape[0]
+    got = H.partition(A, nparts, H.PART_GRID)
+    ref = OP.partition4_adjust(A.indptr, A.indices, n, nparts, OP.grid_base(A.indptr, A.indices, n, nparts))
+    for k, r in zip(("node_part", "part_size", "pinv", "q"), ref):
+        assert np.array_equal(got[k], r), k
+    px, py, pz = pdims
+    for p in range(nparts):
+        nodes = np.flatnonzero(got["node_part"] == p)
+        i, y, z = nodes % nx, (nodes // nx) % ny, nodes // (nx * ny)
+        w, h, d = (v.max() - v.min() + 1 for v in (i, y, z))
+        assert w * h * d == nodes.size                    # a full box
+        assert abs(w - nx / px) <= 3 and abs(h - ny / py) <= 3 and abs(d - nz / pz) <= 3
+        b0 = got["begin"][p]
+        assert np.array_equal(got["q"][b0:b0 + nodes.size], nodes)
+
+
 def test_partition_grid_rejects_non_grid():
     A = M.power_law(800, 6000, seed=9)
     with pytest.raises(Exception):

@@ -18,3 +18,10 @@ import json; d=json.loads(open('gpurun_out/r04r_${f}_fx$fx.json').read().strip()
 k=d['kernels']; print('$f fx=$fx', d['value'], {n:k[n]['avg_us'] for n in k}, d.get('latency_roofline'))"
   done
 done
+for P in 4 8; do
+  timeout -k 10 300 python -u bench.py --workload dd --dd-grid c4 --dd-part grid --dd-parts $P --steps 1 --warmup 1 \
+    > gpurun_out/r04r_dd_c4grid_$P.json 2> gpurun_out/r04r_dd_c4grid_$P.err || { tail -20 gpurun_out/r04r_dd_c4grid_$P.err; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/r04r_dd_c4grid_$P.json').read().strip().splitlines()[-1])
+print('dd c4 grid P=$P', d['value'], d['config'].get('iters_per_solve'), json.dumps(d.get('kernels_per_rank'))[:900])"
+done
