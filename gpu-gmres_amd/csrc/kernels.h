@@ -41,6 +41,9 @@ struct UnitMap {
     int kind = -1;        // -1 every unit, 0 natural order (n rows), 1 2D band wavefront, 2 3D tiles
     int nx = 0, ny = 0, nz = 1, T = 0, skew = 1, NJ = 0, nbands = 0;
     long long n = 0;
+    // bordered grid (Wave2D::bnt): units [0, tbase) hold the tail (real while
+    // slot < tn), the wavefront layout starts at unit tbase
+    long long tbase = 0, tn = 0;
 };
 
 constexpr int kBlock = 256;

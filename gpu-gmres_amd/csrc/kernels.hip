@@ -101,6 +101,10 @@ __device__ __forceinline__ bool unit_real(const UnitMap &m, long long u)
 {
     if (m.kind < 0) return true;
     if (m.kind == 0) return 2 * u < m.n;
+    if (m.tbase) {
+        if (u < m.tbase) return 2 * u < m.tn;
+        u -= m.tbase;
+    }
     const int lane = (int)(u & 63);
     const long long q = u >> 6;
     const int th = m.T >> 1;

@@ -782,8 +782,9 @@ UnitMap unit_map(const gg_solver *s)
         return um;
     }
     const Wave2D &w = s->wl;
-    if (w.bnt) return um;                                   // bordered grid: every unit
     um.kind = w.tile ? 2 : 1;
+    um.tbase = w.bofs / 2;                                  // bordered grid: the tail's units first
+    um.tn = w.bnt;
     um.nx = w.nx;
     um.ny = w.ny;
     um.nz = w.nz;

@@ -25,3 +25,7 @@ for P in 4 8; do
 import json; d=json.loads(open('gpurun_out/r04r_dd_c4grid_$P.json').read().strip().splitlines()[-1])
 print('dd c4 grid P=$P', d['value'], d['config'].get('iters_per_solve'), json.dumps(d.get('kernels_per_rank'))[:900])"
 done
+timeout -k 10 300 python -u bench.py --workload netlist --steps 3 --warmup 1 --cpu-iters 0 > gpurun_out/r04r_netlist.json 2> gpurun_out/r04r_netlist.err || { tail -20 gpurun_out/r04r_netlist.err; exit 1; }
+python3 -c "
+import json; d=json.loads(open('gpurun_out/r04r_netlist.json').read().strip().splitlines()[-1])
+k=d['kernels']; print('netlist', d['value'], {n:k[n]['avg_us'] for n in k})"
