@@ -104,7 +104,7 @@ def parse():
     p.add_argument("--dd-part", choices=["slabs", "grid"], default=None,
                    help="dd: base partition -- slabs = contiguous index ranges (GG_PART_BLOCKS) or grid = "
                         "px x py rectangles of the 2D grid (GG_PART_GRID: interior chains nx/px + ny/py); "
-                        "default grid on the C2 system, slabs on C4")
+                        "default grid")
     p.add_argument("--dd-sep", choices=["color", "natural"], default="color",
                    help="dd: separator order -- a greedy colouring of its graph (GG_PART_COLOR_SEP, "
                         "default: a few-level separator solve) or partition4's ascending index")
@@ -624,10 +624,11 @@ def main():
         a.workload = "c2" if world == 1 else "dd"
         a.dd_grid = a.dd_grid or "c2"
     a.dd_grid = a.dd_grid or "c4"
-    # rectangles on the 2D grid (GG_PART_GRID: chains nx/px + ny/py, and the
-    # C2 solve converges in fewer iterations: 3,910 vs 6,369 at 4 shards,
-    # profiles/r04k_dd_4_*.json), slabs on the 3D one
-    a.dd_part = a.dd_part or ("grid" if a.dd_grid == "c2" else "slabs")
+    # rectangles / boxes (GG_PART_GRID: chains nx/px + ny/py (+ nz/pz)): C2
+    # converges in 3,910 iterations vs the slabs' 6,369 at 4 shards
+    # (profiles/r04k_dd_4_*.json); C4 at 8 shards 230 vs 175 it/s
+    # (profiles/r04r_dd_c4grid_8.json vs r04q_dd_c4_8.json)
+    a.dd_part = a.dd_part or "grid"
     replicas = a.workload == "replicas"
     if replicas:
         a.workload = "c2"

@@ -553,7 +553,6 @@ __global__ void k_fill_gated(Gate g, unsigned long long *p, long long n, unsigne
         p[i] = v;
 }
 
-constexpr int kFlowXcds = 8;                // launch_trsv's one-XCD placement of narrow-level solves
 // long rows: issue the next round's loads before this round's serial sum (1;
 // 92 VGPRs, 5 waves per SIMD) or after it (0; 62 VGPRs, 8 waves per SIMD)
 #ifndef GG_FLOW_PREFETCH
@@ -565,16 +564,14 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                                                       const double *__restrict__ v,
                                                       const double *__restrict__ d,
                                                       const double *__restrict__ b, double *x, int *err,
-                                                      const double *__restrict__ y, int xs)
+                                                      const double *__restrict__ y)
 {
     if (gated(g)) return;
-    // xs > 1: only every xs-th workgroup works (launch_trsv: one XCD)
-    if (xs > 1 && blockIdx.x % xs) return;
     __shared__ double prod[kBlock];            // a long row's products, one 64-slot area per wave
     const int lane = threadIdx.x & 63;
     double *wprod = prod + (threadIdx.x & ~63);
-    const long long wid = ((blockIdx.x / xs) * (long long)blockDim.x + threadIdx.x) >> 6;
-    const long long nw = ((gridDim.x / xs) * (long long)blockDim.x) >> 6;
+    const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
     unsigned long long *xu = reinterpret_cast<unsigned long long *>(x);
     for (long long t = wid; t < ntask; t += nw) {
         const int2 tk = tasks[t];
@@ -3923,27 +3920,12 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
                                   : per_level <= wave_slots ? 1
                                   : (int)std::min<long long>(8, 2 * ((per_level + wave_slots - 1) / wave_slots));
             const long long need = ((long long)T.ntask + kBlock / 64 - 1) / (kBlock / 64);   // a wave per task
-            int blocks = (int)std::min<long long>(std::min<long long>(flow_blocks, (long long)bpc * std::max(cus, 1)), need);
-            // narrow levels (a few tasks each): the working blocks on ONE XCD --
-            // the launch has 8 workgroups per working one and only every 8th
-            // works (workgroups are dealt round-robin over the XCDs), so a
-            // level's hand-off to the next is an L2-local store -> poll instead
-            // of a cross-XCD one (placement is for speed only; at most one
-            // working block per CU of an XCD, so they stay co-resident)
-            // GG_FLOW_XCD: 0 off, 1 on, unset = when a level holds <= 2 waves per CU of one XCD
-            const char *fx = getenv("GG_FLOW_XCD");
-            const int xcus = std::max(cus / kFlowXcds, 1);
-            const bool xcd = fx ? atoi(fx) != 0 : (per_level <= 2LL * xcus && bpc_s == nullptr);
-            int xs = 1;
-            if (xcd) {
-                blocks = (int)std::min<long long>(std::min<long long>(blocks, xcus), need);
-                xs = kFlowXcds;
-            }
+            const int blocks = (int)std::min<long long>(std::min<long long>(flow_blocks, (long long)bpc * std::max(cus, 1)), need);
             if (!T.prefilled)
                 k_fill_gated<<<blocks_for(nrows, kBlock, 8192), kBlock, 0, st>>>(
                     g, reinterpret_cast<unsigned long long *>(x), nrows, kSentinel);
-            k_trsv_flow<<<blocks * xs, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p, T.off.ci.p,
-                                                        T.off.v.p, T.d.p, b, x, err, T.mul ? T.rw.p : nullptr, xs);
+            k_trsv_flow<<<blocks, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p, T.off.ci.p,
+                                                   T.off.v.p, T.d.p, b, x, err, T.mul ? T.rw.p : nullptr);
             return;
         }
         for (int l = 0; l < nlev; l++) {

@@ -5,8 +5,8 @@
 #   tests           the whole GPU suite (pytest -m gpu), log -> gpurun_out/TAG_tests.log
 #   c2 | c4 | netlist | pg
 #                   bench.py on that workload -> gpurun_out/TAG_bench_WL.json
-#   dd              the sharded solve with local shards: C2 on px x py rectangles and
-#                   C4 on slabs, P = 2 / 4 / 8 -> gpurun_out/TAG_dd_{c2,c4}_P.json
+#   dd              the sharded solve with local shards: C2 on px x py rectangles, C4 on
+#                   px x py x pz boxes, P = 2 / 4 / 8 -> gpurun_out/TAG_dd_{c2,c4}_P.json
 #   prof:WL         tools/profile_round.sh TAG WL (rocprofv3 stats + PMC traffic)
 #   smoke           __graft_entry__.smoke()
 # Every step has its own time limit and the script stops at the first failure.
@@ -40,7 +40,7 @@ for st in "$@"; do
             || { tail -20 gpurun_out/${TAG}_bench_$st.err; exit 1; }
         summary gpurun_out/${TAG}_bench_$st.json ;;
     dd)
-        for wl in "c2 grid" "c4 slabs"; do
+        for wl in "c2 grid" "c4 grid"; do
             set -- $wl
             for P in 2 4 8; do
                 f=gpurun_out/${TAG}_dd_$1_$P
