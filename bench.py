@@ -146,6 +146,18 @@ CHAIN_CYCLES = {"trsv_L": 38.89, "trsv_U": 62.66, "trsv_U_mul": 43.72,
 SHADER_GHZ = 2.399
 
 
+def chain_key(kernel, dom, fma, mul):
+    """CHAIN_CYCLES entry of a wavefront solve: from the kernel's division
+    template argument (kernels.hip WaveDiv: 0 unit, 1 IEEE division, 2
+    reciprocal + FMA corrections, 3 multiply by RN(1/d), 4 / 5 fused rows)
+    when the name carries it, else from the solver's division mode"""
+    import re
+    m = re.match(r"k_trsv_wave2d_spmv<(\d+)>", kernel) or re.match(r"k_trsv_(?:wave2d|tile3d)<\w+, (\d+)", kernel)
+    if m:
+        return {0: "trsv_L", 1: "trsv_U", 2: "trsv_U", 3: "trsv_U_mul", 4: "trsv_L_fma", 5: "trsv_U_fma"}[int(m.group(1))]
+    return (dom + "_fma") if fma else "trsv_U_mul" if mul else dom
+
+
 def pmc_traffic(kernel, workload=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, or profiles/pmc_traffic_<workload>.json; written
@@ -852,8 +864,7 @@ def main():
         # a non-unit L (the split engine's) divides like U
         mul = u_mul if dom == "trsv_U" else l_mul
         fm = u_fma if dom == "trsv_U" else l_fma
-        cyc = CHAIN_CYCLES[(dom + "_fma") if fm else
-                           "trsv_L" if dom == "trsv_L" and not (pg or netlist) else "trsv_U_mul" if mul else "trsv_U"]
+        cyc = CHAIN_CYCLES[chain_key(roof["kernel"], dom, fm, mul)]
         # the DAG's longest path (ILU(k): skew k+1; 3D: nx + ny + nz - 2, whose
         # per-step chain is the 2D one: the tile kernel's plane term is off it)
         steps = 3 * a.c4_grid - 2 if c4 else a.grid + (kilu + 1) * (a.grid - 1)
