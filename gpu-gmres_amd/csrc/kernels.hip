@@ -3916,9 +3916,14 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
             const char *bpc_s = getenv("GG_FLOW_BPC");
             const long long per_level = (T.ntask + nlev - 1) / std::max(nlev, 1);
             const long long wave_slots = 4LL * std::max(cus, 1);          // 4 waves per block, 1 block per CU
+            // (the randomly permuted PG split, 1,100 tasks per level: 2 blocks per
+            // CU 84 / 102 us for L / U against 95 / 127 at 4 and 102 / 131 at 8,
+            // profiles/r04s_pgr_bpc*.json -- so the extra factor 2 only beyond
+            // two waves per slot)
+            const long long wpl = (per_level + wave_slots - 1) / wave_slots;
             const int bpc = bpc_s ? std::max(1, atoi(bpc_s))
                                   : per_level <= wave_slots ? 1
-                                  : (int)std::min<long long>(8, 2 * ((per_level + wave_slots - 1) / wave_slots));
+                                  : (int)std::min<long long>(8, per_level > 2 * wave_slots ? 2 * wpl : wpl);
             const long long need = ((long long)T.ntask + kBlock / 64 - 1) / (kBlock / 64);   // a wave per task
             const int blocks = (int)std::min<long long>(std::min<long long>(flow_blocks, (long long)bpc * std::max(cus, 1)), need);
             if (!T.prefilled)
