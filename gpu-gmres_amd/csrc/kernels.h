@@ -188,7 +188,8 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             long long ldv, double *H, double *cs, double *sn, double *s,
                             double *hist, unsigned long long *gran, unsigned long long *hg, int G,
                             long long Ppad, int *err, unsigned long long *xb, unsigned long long *elect,
-                            unsigned long long seq, const UnitMap &um, hipStream_t st);
+                            unsigned long long seq, const UnitMap &um, hipStream_t st,
+                            long long *trace = nullptr);   // diagnostics: GG_MGS_TRACE (solver.hip)
 // the same for long vectors (w on chip, the basis streamed): kWideG blocks
 constexpr int kWideG = 512;
 bool arnoldi_wide_ok(int G, long long Ppad);

@@ -3116,7 +3116,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
                                                             unsigned long long *gran, unsigned long long *hg,
                                                             long long units, int *err, unsigned long long *xb,
                                                             unsigned long long *elect, unsigned long long seq,
-                                                            UnitMap um)
+                                                            UnitMap um, long long *trace)
 {
     // granules per thread loaded at once in the all-gathers (persist_np; J =
     // 8 polls them one by one: the parallel form would cost it an occupancy step)
@@ -3158,6 +3158,13 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     if constexpr (XG == 2) xcd_elect(elect, seq, red, xcc);
     const long long stride = (long long)G * kBlock;
     const long long u0 = ub * (long long)kBlock + threadIdx.x;
+    // diagnostics (GG_MGS_TRACE): per step the start, h known, partial formed,
+    // partial published -- row 0 unit-block 0, row 1 the reducer of XCD 0
+    const int trow = !trace ? -1 : ub == 0 ? 0 : (red && xcc == 0 && XG == 2) ? 1 : -1;
+    auto stamp = [&](int k, int ph) {
+        if (trow >= 0 && threadIdx.x == 0)
+            trace[((long long)trow * (i + 2) + k) * 4 + ph] = (long long)__builtin_amdgcn_s_memrealtime();
+    };
     double2 w[J], vk[J], vn[J];
     [[maybe_unused]] double2 vl[PF == 2 ? J : 1];             // PF 2: the third basis buffer
     bool val[J];                                              // unit holds a real row (UnitMap)
@@ -3197,6 +3204,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     // v_{k+2} lands in (PF 2; the three rotate, no register copies -- a copy of
     // a landing buffer would wait for its loads)
     auto step = [&](int k, double2 *cur, double2 *nxt, double2 *lnd) -> bool {
+        stamp(k, 0);
         if constexpr (PF == 1) {
             if (k < i) load_v(k + 1, nxt);                    // v_{k+1}, in flight during the sum
         }
@@ -3220,6 +3228,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             __builtin_amdgcn_sched_barrier(0);
             if (k + 2 <= i) load_v(k + 2, lnd);
         }
+        stamp(k, 1);
         if (ub == 0 && threadIdx.x == 0) H[k + i * (m + 1)] = h;
         const double a = -h;
         double acc = 0.0;
@@ -3233,7 +3242,9 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
                 acc += w[j].y * o.y;
             }
         }
+        stamp(k, 2);
         publish(k + 1, acc);
+        stamp(k, 3);
         return true;
     };
     if constexpr (PF == 2) {
@@ -3251,10 +3262,12 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             step(k + 1, vn, vk, nullptr);
         }
     }
+    stamp(i + 1, 0);
     const double hn = sqrt(XG >= 2 ? gather_xcd<kNP>(gran + (long long)(i + 1) * G, xslot(i + 1), i + 1, G, red, err, par,
                                                 abortw)
                                    : gather_h<false, kNP>(gran + (long long)(i + 1) * G, hg + i + 1, i + 1, G, err, par,
                                                      abortw));
+    stamp(i + 1, 1);
     if (ub == 0 && threadIdx.x == 0) {                       // as k_arnoldi_finalize
         const int ld = m + 1;
         double *Hc = H + i * ld;
@@ -4212,7 +4225,7 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             long long ldv, double *H, double *cs, double *sn, double *s,
                             double *hist, unsigned long long *gran, unsigned long long *hg, int G, long long Ppad,
                             int *err, unsigned long long *xb, unsigned long long *elect, unsigned long long seq,
-                            const UnitMap &um, hipStream_t st)
+                            const UnitMap &um, hipStream_t st, long long *trace)
 {
     const int J = arnoldi_persist_units(G, Ppad);
     GG_REQUIRE(persist_np(J) == 0 || G <= persist_np(J) * kBlock, GG_EINVAL,
@@ -4221,7 +4234,7 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
     const int pf = mgs_prefetch();
 #define GG_PERSIST(JJ, XG, PF)                                                                       \
     k_arnoldi_persist<JJ, XG, PF><<<G + (XG == 3 ? kXcds : 0), kBlock, persist_test_lds(), st>>>(          \
-        g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2, err, xb, elect, seq, um)
+        g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2, err, xb, elect, seq, um, trace)
 #define GG_PERSIST_J(XG, PF)                                                                       \
     do {                                                                                           \
         if (J == 1) GG_PERSIST(1, XG, PF);                                                         \

@@ -413,6 +413,8 @@ struct gg_solver {
     DBuf<unsigned long long> xgran;     // m * (m+2) * kMgsXcdWords: the XCD-local gather's slots (re-armed per cycle)
     DBuf<unsigned long long> elect;     // per XCD: the last launch that elected its reducer
     unsigned long long mgs_seq = 0;     // persistent orthogonalization launches so far (election)
+    DBuf<long long> mgs_trace;          // diagnostics: GG_MGS_TRACE=N stamps the N-th persistent launch
+    int mgs_trace_i = -1;               // (its inner index; printed to stderr after the solve)
     DBuf<double> hist;
     long long hist_cap = 0;
     DBuf<DevState> ds;
@@ -796,6 +798,35 @@ UnitMap unit_map(const gg_solver *s)
     return um;
 }
 
+// diagnostics: GG_MGS_TRACE=N -- device time stamps of the N-th persistent
+// orthogonalization launch (k_arnoldi_persist: per step start / h known /
+// partial formed / published, for unit-block 0 and XCD 0's reducer)
+long long *mgs_trace_for(gg_solver *s, int i, int m)
+{
+    static const long long at = [] {
+        const char *e = std::getenv("GG_MGS_TRACE");
+        return e ? atoll(e) : -1LL;
+    }();
+    if (at < 0 || (long long)s->mgs_seq + 1 != at) return nullptr;
+    s->mgs_trace.alloc((size_t)2 * (m + 2) * 4);
+    GG_HIP(hipMemsetAsync(s->mgs_trace.p, 0, s->mgs_trace.n * sizeof(long long), s->st));
+    s->mgs_trace_i = i;
+    return s->mgs_trace.p;
+}
+void mgs_trace_print(gg_solver *s)
+{
+    if (s->mgs_trace_i < 0) return;
+    const int i = s->mgs_trace_i;
+    std::vector<long long> h((size_t)2 * (i + 2) * 4);
+    GG_HIP(hipMemcpy(h.data(), s->mgs_trace.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    for (int row = 0; row < 2; row++)
+        for (int k = 0; k <= i + 1; k++) {
+            const long long *t = &h[((size_t)row * (i + 2) + k) * 4];
+            std::fprintf(stderr, "mgs_trace i=%d row=%d k=%d %lld %lld %lld %lld\n", i, row, k, t[0], t[1], t[2], t[3]);
+        }
+    s->mgs_trace_i = -1;
+}
+
 void enqueue_cycle(gg_solver *s, int m)
 {
     const UnitMap um = unit_map(s);
@@ -852,7 +883,7 @@ void enqueue_cycle(gg_solver *s, int m)
             launch_arnoldi_persist(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                    s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
                                    P, s->err.p, s->xgran.p + (size_t)i * (m + 2) * kMgsXcdWords, s->elect.p,
-                                   ++s->mgs_seq, um, s->st);
+                                   ++s->mgs_seq, um, s->st, mgs_trace_for(s, i, m));
         } else if (wide) {
             launch_arnoldi_wide(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                 s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
@@ -1079,6 +1110,7 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
     }
     GG_HIP(hipEventRecord(s->ev1, s->st));
     check_err(s);
+    mgs_trace_print(s);
     launch_gather(s->xv.p, split ? s->sx_out.p : s->nat2lay.p, d_x, n, s->st);
     GG_HIP(hipStreamSynchronize(s->st));
     float ms = 0.f;
