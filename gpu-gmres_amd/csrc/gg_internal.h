@@ -307,6 +307,7 @@ struct DevTri {
     int fast = 0;                // the owner's gg_set_division mode (GG_DIV_RCP: WD_MUL, GG_DIV_FMA: WD_*FMA)
     bool prefilled = false;      // LEVEL, per launch: x already holds the sentinel (flow kernel)
     bool mul = false;            // LEVEL, per launch: x = RN(acc * rw) (a bordered grid's tail under WD_MUL)
+    bool fmrow = false;          // LEVEL: GG_DIV_FMA's rows (terms pre-scaled, fused order; rw = RN(1/d) or none)
     bool tile_queue = false;     // 3D tiles: claim tiles from a queue (after a non-resident static grid)
     int eff_div() const
     {
@@ -330,6 +331,7 @@ struct DevTri {
     // tail terms as a coupling CSR (absolute row slots, tail columns) applied to
     // b in place between the two (b must be scratch: the split engine's t1)
     std::unique_ptr<DevTri> tail;
+    std::unique_ptr<DevTri> tail_fma;   // the same rows as GG_DIV_FMA forms them (when fma_ok)
     long long bofs = 0;
     int ncoup = 0;
     DBuf<long long> cslot;

@@ -521,16 +521,25 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
 // Level-scheduled row solve (one launch per dependency level):
 //   x[r] = (b[r] - sum_k off[k] * x[col[k]]) / d[r]   in canonical order
 // y (optional): RN(1/d) -- x = RN(acc * y), WD_MUL's row (a bordered grid's
-// tail under gg_set_division(GG_DIV_RCP / _FMA), DevTri::tail)
+// tail under gg_set_division(GG_DIV_RCP), DevTri::tail).  fm: GG_DIV_FMA's row
+// (a bordered grid's tail, DevTri::tail_fma): acc = RN(b * y) (b when y is null),
+// then acc = fma(-v, x, acc) over the terms as stored -- pre-scaled by y and in
+// the fused order (nearest first) -- and no division
 __global__ __launch_bounds__(kBlock) void k_trsv_level(Gate g, int cnt, const int *rows,
                                                        const int *rp, const int *ci,
                                                        const double *v, const double *d,
-                                                       const double *b, double *x, const double *y)
+                                                       const double *b, double *x, const double *y, int fm)
 {
     if (gated(g)) return;
     int t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= cnt) return;
     int r = rows[t];
+    if (fm) {                       // GG_DIV_FMA's rows (the terms pre-scaled and in fused order)
+        double acc = y ? b[r] * y[r] : b[r];
+        for (int k = rp[r]; k < rp[r + 1]; k++) acc = __builtin_fma(-v[k], x[ci[k]], acc);
+        x[r] = acc;
+        return;
+    }
     double acc = b[r];
     for (int k = rp[r]; k < rp[r + 1]; k++) acc = acc - v[k] * x[ci[k]];
     x[r] = y ? acc * y[r] : acc / d[r];
@@ -564,7 +573,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                                                       const double *__restrict__ v,
                                                       const double *__restrict__ d,
                                                       const double *__restrict__ b, double *x, int *err,
-                                                      const double *__restrict__ y)
+                                                      const double *__restrict__ y, int fm)
 {
     if (gated(g)) return;
     __shared__ double prod[kBlock];            // a long row's products, one 64-slot area per wave
@@ -576,6 +585,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
     for (long long t = wid; t < ntask; t += nw) {
         const int2 tk = tasks[t];
         if (tk.y < 0) {
+            // (fm triangles are built without long rows: build_tri_bordered)
             // one long row, the whole wave: each round 256 of its terms (4 per
             // lane) are loaded and polled together, their products v*x formed
             // in parallel, then lane 0 subtracts them from acc one by one in
@@ -662,8 +672,9 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
         bool pending = r >= 0;
         int k = pending ? rp[r] : 0;
         const int k1 = pending ? rp[r + 1] : 0;
-        double acc = pending ? b[r] : 0.0;
-        const double dr = pending ? (y ? y[r] : d[r]) : 1.0;   // y: the reciprocal (WD_MUL's row)
+        // y: the reciprocal (WD_MUL's row; fm: b's pre-scale, GG_DIV_FMA's row)
+        double acc = pending ? ((fm && y) ? b[r] * y[r] : b[r]) : 0.0;
+        const double dr = pending ? (y ? y[r] : d[r]) : 1.0;
         int spins = 0;
         while (__any(pending)) {
             if (pending) {
@@ -679,12 +690,13 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                     for (int j = 0; j < 4; j++) {
                         if (stop || k >= k1) break;
                         if (u[j] == kSentinel) { stop = true; break; }
-                        acc = acc - v[k] * __longlong_as_double((long long)u[j]);
+                        const double xj = __longlong_as_double((long long)u[j]);
+                        acc = fm ? __builtin_fma(-v[k], xj, acc) : acc - v[k] * xj;
                         k++;
                     }
                 }
                 if (k == k1) {
-                    st_agent(xu + r, (unsigned long long)__double_as_longlong(y ? acc * dr : acc / dr));
+                    st_agent(xu + r, (unsigned long long)__double_as_longlong(fm ? acc : y ? acc * dr : acc / dr));
                     pending = false;
                 }
             }
@@ -705,14 +717,15 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
 // solved, and the wavefront continues the sum from it.  One row per thread.
 __global__ void k_border_sub(Gate g, int nrow, const long long *__restrict__ slot, const int *__restrict__ rp,
                              const int *__restrict__ ci, const double *__restrict__ v,
-                             const double *__restrict__ x, double *b)
+                             const double *__restrict__ x, double *b, int fm)
 {
     if (gated(g)) return;
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nrow) return;
     const long long p = slot[q];
     double acc = b[p];
-    for (int k = rp[q]; k < rp[q + 1]; k++) acc = acc - v[k] * x[ci[k]];
+    // fm: GG_DIV_FMA's unit L rows (the tail terms lead the fused row too)
+    for (int k = rp[q]; k < rp[q + 1]; k++) acc = fm ? __builtin_fma(-v[k], x[ci[k]], acc) : acc - v[k] * x[ci[k]];
     b[p] = acc;
 }
 
@@ -3890,14 +3903,17 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
         return;
     }
     // bordered grid: tail, coupling, grid (forward); grid, tail (backward)
-    DevTri &tl = *T.tail;
+    const int e = T.eff_div();
+    const bool fm = e == WD_UFMA || e == WD_SFMA;
+    // the tail rows divide as the grid's do (GG_DIV_FMA: the fused-order copy)
+    DevTri &tl = fm ? *T.tail_fma : *T.tail;
     tl.fast = 0;
-    tl.mul = T.eff_div() == WD_MUL;          // the tail rows divide as the grid's do
+    tl.mul = e == WD_MUL;
     if (T.lower) {
         launch_trsv_one(g, tl, b, x, err, st);
         if (T.ncoup)
             k_border_sub<<<(T.ncoup + kBlock - 1) / kBlock, kBlock, 0, st>>>(
-                g, T.ncoup, T.cslot.p, T.crp.p, T.cci.p, T.cv.p, x, const_cast<double *>(b));
+                g, T.ncoup, T.cslot.p, T.crp.p, T.cci.p, T.cv.p, x, const_cast<double *>(b), fm ? 1 : 0);
         launch_trsv_one(g, T, b + T.bofs, x + T.bofs, err, st);
     } else {
         launch_trsv_one(g, T, b + T.bofs, x + T.bofs, err, st);
@@ -3943,7 +3959,8 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
                 k_fill_gated<<<blocks_for(nrows, kBlock, 8192), kBlock, 0, st>>>(
                     g, reinterpret_cast<unsigned long long *>(x), nrows, kSentinel);
             k_trsv_flow<<<blocks, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p, T.off.ci.p,
-                                                   T.off.v.p, T.d.p, b, x, err, T.mul ? T.rw.p : nullptr);
+                                                   T.off.v.p, T.d.p, b, x, err,
+                                                   (T.mul || T.fmrow) ? T.rw.p : nullptr, T.fmrow ? 1 : 0);
             return;
         }
         for (int l = 0; l < nlev; l++) {
@@ -3951,7 +3968,7 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
             if (cnt == 0) continue;
             k_trsv_level<<<(cnt + kBlock - 1) / kBlock, kBlock, 0, st>>>(
                 g, cnt, T.lev_rows.p + T.lev_ptr[l], T.off.rp.p, T.off.ci.p, T.off.v.p, T.d.p, b, x,
-                T.mul ? T.rw.p : nullptr);
+                (T.mul || T.fmrow) ? T.rw.p : nullptr, T.fmrow ? 1 : 0);
         }
     } else if (T.kind == DevTri::WAVE2D) {
         const Wave2D &w = T.wl;

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <atomic>
 #include <thread>
 #include <cmath>
@@ -133,12 +134,13 @@ std::vector<int> tile_order(const Wave2D &w)
 
 // Build a device triangular solve from a canonical triangle.  WAVE2D when a
 // grid layout is active, else LEVEL (one launch per dependency level).
-void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st);
+void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st, bool no_long = false);
 
 void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector<long long> *nat2lay,
                long long Ppad, hipStream_t st)
 {
     T.tail.reset();
+    T.tail_fma.reset();
     T.bofs = 0;
     T.ncoup = 0;
     T.cbytes = 0;
@@ -238,7 +240,8 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
 }
 
 // LEVEL triangle: the flow kernel's tasks over the level sets `lv` of C
-void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st)
+// (no_long: every row one lane's -- GG_DIV_FMA's rows have no long-row form)
+void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st, bool no_long)
 {
     const int n = C.off.n;
     {
@@ -249,7 +252,7 @@ void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st)
         T.lev_rows.upload(lv.rows, st);
         // flow tasks in level order: runs of up to 64 short rows, long rows alone
         const char *fl = std::getenv("GG_FLOW_LONG");       // tuning: terms above which a row is long
-        const int flow_long = fl ? std::max(0, atoi(fl)) : kFlowLong;
+        const int flow_long = no_long ? INT_MAX : fl ? std::max(0, atoi(fl)) : kFlowLong;
         std::vector<int2> tasks;
         int run0 = 0, runn = 0;
         auto flush = [&]() {
@@ -284,11 +287,7 @@ void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const 
     std::vector<long long> gslot(Cg.off.n);
     for (int r = 0; r < Cg.off.n; r++) gslot[r] = wg.slot(r);
     build_tri(T, Cg, &wg, &gslot, round_up(wg.P2, 512), st);
-    // no fused rows: GG_DIV_FMA's order (nearest term first) would put a grid
-    // row's tail terms LAST, inside the wavefront's recurrence -- under
-    // GG_DIV_FMA a bordered grid takes WD_MUL (eff_div), whose rows keep the
-    // canonical order (tail terms first), the tail rows multiplying too
-    T.fma_ok = false;
+    const bool grid_fma = T.fma_ok, grid_unit = T.div == WD_UNIT;
     T.bofs = wl.bofs;
     // the tail over the whole layout (its columns are slots); level sets over
     // the tail's own rows only (an upper tail's grid columns are final before it runs)
@@ -318,6 +317,38 @@ void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const 
     }
     T.mul_ok = T.mul_ok && tail_mul;
     if (T.mul_ok) T.tail->rw.upload(ry, st);
+    // GG_DIV_FMA: the mesh rows' tail terms lead the fused row (oracle
+    // orc_set_fma_tail), so the forward solve forms them before the wavefront
+    // as fused multiply-adds on the unit L (a non-unit L would need them
+    // inside RN(b * y): that triangle takes WD_MUL instead); the tail rows as
+    // their own fused rows -- pre-scaled by y = RN(1/d), nearest term first
+    bool tail_unit = true;
+    for (int r = 0; r < nt; r++) tail_unit = tail_unit && Ct.d[r] == 1.0;
+    T.fma_ok = grid_fma && (C.lower ? (grid_unit && tail_unit) : tail_mul);
+    if (T.fma_ok) {
+        CanonTri Cf;
+        Cf.lower = C.lower;
+        Cf.off.n = nt;
+        Cf.off.rp = Ct.off.rp;
+        Cf.off.ci.resize(Ct.off.ci.size());
+        Cf.off.v.resize(Ct.off.v.size());
+        Cf.d.assign(nt, 1.0);
+        for (int r = 0; r < nt; r++) {
+            const int k0 = Ct.off.rp[r], k1 = Ct.off.rp[r + 1];
+            for (int q = 0; q < k1 - k0; q++) {
+                // lower: nearest first = descending columns; upper: ascending (canonical)
+                const int k = C.lower ? k1 - 1 - q : k0 + q;
+                Cf.off.ci[k0 + q] = Ct.off.ci[k];
+                Cf.off.v[k0 + q] = Ct.off.v[k] * ry[r];
+            }
+        }
+        T.tail_fma = std::make_unique<DevTri>();
+        T.tail_fma->lower = C.lower;
+        T.tail_fma->n = nt;
+        build_level(*T.tail_fma, Cf, level_sets(Ct, true), st, true);
+        T.tail_fma->fmrow = true;
+        T.tail_fma->rw.upload(ry, st);
+    }
     // the grid rows' tail terms (lower: the leading terms of the row, detect_border2d)
     std::vector<long long> cs;
     std::vector<int> crp(1, 0), cci;

@@ -69,6 +69,7 @@ def lib():
         L.orc_sub_seq.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
         L.orc_gen_rot.argtypes = [ctypes.c_double, ctypes.c_double, _PD, _PD]
         L.orc_set_div_mode.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_set_fma_tail.argtypes = [ctypes.c_int]
         L.orc_set_orth.argtypes = [ctypes.c_int]
         L.orc_apply_rot.argtypes = [_PD, _PD, ctypes.c_double, ctypes.c_double]
         common = [_f64p, _f64p, ctypes.c_int, _PI, _PD, _f64p, ctypes.c_int, _PI, _PI]
@@ -224,6 +225,14 @@ def set_div_mode(mul_l=False, mul_u=False):
     pre-scaled by 1.0 / d, the nearest term first, fused multiply-adds); for
     order-matched checks only -- reset with set_div_mode()."""
     lib().orc_set_div_mode(int(mul_l), int(mul_u))
+
+
+def set_fma_tail(tail=0):
+    """GG_DIV_FMA on a bordered grid (split engine): the Ml rows below the
+    first `tail` rows take their tail-column terms first (canonical order),
+    then the rest nearest first -- as the device forms them (k_border_sub
+    before the mesh wavefront).  0 (default) = every row nearest first."""
+    lib().orc_set_fma_tail(int(tail))
 
 
 def set_orth(cgs2=False):

@@ -340,6 +340,13 @@ void orc_set_div_mode(int mul_l, int mul_u)
     g_mul_l = mul_l < 0 ? 0 : mul_l > 2 ? 2 : mul_l;
     g_mul_u = mul_u < 0 ? 0 : mul_u > 2 ? 2 : mul_u;
 }
+/* GG_DIV_FMA on a bordered grid (the device's Wave2D::bnt, split engine): in
+ * the Ml rows below the first `tail` rows the terms of columns < tail (the
+ * tail, pads and branch currents) come first, in canonical order, then the
+ * rest nearest first -- the tail's contribution is formed before the mesh's
+ * wavefront starts the row.  0 = no tail (every row nearest first). */
+static int g_fma_tail = 0;
+void orc_set_fma_tail(int tail) { g_fma_tail = tail > 0 ? tail : 0; }
 static double divide(double a, double d, int mul) { return mul ? a * (1.0 / d) : a / d; }
 
 void orc_lusolve(int n, const int *l_rp, const int *l_ci, const double *l_v,
@@ -399,7 +406,11 @@ void orc_split_left(const orc_split_t *p, const double *in, double *out)
         int lb = p->l_rp[i], ub = p->l_rp[i + 1];
         if (g_mul_l == 2) {         /* GG_DIV_FMA: pre-scaled, nearest term first */
             double yd = 1.0 / p->l_v[ub - 1], acc = out[i] * yd;
-            for (int j = ub - 2; j >= lb; j--) acc = fma(-(p->l_v[j] * yd), out[p->l_ci[j]], acc);
+            int j0 = lb;            /* (a bordered grid's mesh row: its tail terms first) */
+            if (i >= g_fma_tail)
+                for (; j0 < ub - 1 && p->l_ci[j0] < g_fma_tail; j0++)
+                    acc = fma(-(p->l_v[j0] * yd), out[p->l_ci[j0]], acc);
+            for (int j = ub - 2; j >= j0; j--) acc = fma(-(p->l_v[j] * yd), out[p->l_ci[j]], acc);
             out[i] = acc;
             continue;
         }

@@ -53,6 +53,7 @@ void orc_free(void *p);
 
 /* x = (LU)^-1 y  (LUSolve_ignoreZero, src/SpMV_compute.cpp:92-136) */
 void orc_set_div_mode(int mul_l, int mul_u);
+void orc_set_fma_tail(int tail);
 void orc_set_orth(int cgs2);
 void orc_lusolve(int n, const int *l_rp, const int *l_ci, const double *l_v,
                  const int *u_rp, const int *u_ci, const double *u_v,

@@ -83,34 +83,41 @@ def test_border_gmres_parity(systems, grid):
         s.close()
 
 
+def order_matched(A, P, b, n, grid, nt, mode_l, mode_u, tail, vs=()):
+    lay, G = device_layout(n, grid, border=nt)
+    O.set_dot_order(lay, G)
+    O.set_div_mode(mode_l, mode_u)
+    O.set_fma_tail(tail)
+    try:
+        ot = O.gmres_split(A, P, b, m=32, max_iter=600, tol=1e-10)
+        ops = [(P.left(v), P.right(v)) for v in vs]
+    finally:
+        O.set_dot_order(None)
+        O.set_div_mode()
+        O.set_fma_tail(0)
+    return ot, ops
+
+
 @pytest.mark.parametrize("grid", [60, 150])
 def test_border_mul_division(systems, grid):
-    """gg_set_division(GG_DIV_RCP or GG_DIV_FMA) on a bordered grid: x =
-    RN(acc * RN(1/d)) on every row -- the mesh's wavefront (WD_MUL) and the
-    tail's flow kernel alike; FMA's fused rows would put a mesh row's tail terms
-    inside the recurrence, so FMA falls back to the multiply.  Bit-exact vs the
-    order-matched oracle in its multiply mode, within 1e-10 of the serial
+    """gg_set_division(GG_DIV_RCP) on a bordered grid: x = RN(acc * RN(1/d)) on
+    every row -- the mesh's wavefront (WD_MUL) and the tail's flow kernel alike.
+    Under GG_DIV_FMA the non-unit L (whose fused rows would need the tail terms
+    inside RN(b * y)) takes the multiply too, the U the fused rows.  Bit-exact
+    vs the order-matched oracle in those modes, within 1e-10 of the serial
     reference arithmetic."""
     A, P, nt = systems[grid]
     n = A.shape[0]
     b = np.random.default_rng(1).random(n)
     o = O.gmres_split(A, P, b, m=32, max_iter=600, tol=1e-10)
-    lay, G = device_layout(n, grid, border=nt)
-    O.set_dot_order(lay, G)
-    O.set_div_mode(1, 1)
-    try:
-        ot = O.gmres_split(A, P, b, m=32, max_iter=600, tol=1e-10)
-        rng = np.random.default_rng(7)
-        vs = [rng.standard_normal(n) for _ in range(2)]
-        ref_ops = [(P.left(v), P.right(v)) for v in vs]
-    finally:
-        O.set_dot_order(None)
-        O.set_div_mode()
+    rng = np.random.default_rng(7)
+    vs = [rng.standard_normal(n) for _ in range(2)]
     s = split_solver(A, P)
     try:
-        for mode in (ggmres.DIV_RCP, ggmres.DIV_FMA):
+        for mode, want_u, mode_u in ((ggmres.DIV_RCP, ggmres.DIV_RCP, 1), (ggmres.DIV_FMA, ggmres.DIV_FMA, 2)):
+            ot, ref_ops = order_matched(A, P, b, n, grid, nt, 1, mode_u, nt, vs)
             s.set_division(mode)
-            assert s.division_active(0) == s.division_active(1) == ggmres.DIV_RCP
+            assert s.division_active(0) == ggmres.DIV_RCP and s.division_active(1) == want_u
             for v, (l, r) in zip(vs, ref_ops):
                 assert np.array_equal(s.precond_apply(ggmres.APPLY_LEFT, v), l)
                 assert np.array_equal(s.precond_apply(ggmres.APPLY_RIGHT, v), r)
@@ -119,6 +126,45 @@ def test_border_mul_division(systems, grid):
             assert np.array_equal(g["x"], ot["x"])
             # (the serial engine divides: the convergence test may fire one iteration apart)
             assert abs(g["iters"] - o["iters"]) <= 1 and rel_err(g["x"], o["x"]) <= 1e-8
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("grid", [60, 150])
+def test_border_fma_unit_l(systems, grid, tmp_path):
+    """The bench's netlist split (ILU(0) of the pivoted B: unit L, unit scales)
+    under GG_DIV_FMA: both triangles fused -- the mesh rows' tail terms first
+    (k_border_sub, fused), then the wavefront's rows; the tail rows fused in
+    the flow kernel (pre-scaled, nearest term first).  Bit-exact vs the
+    order-matched oracle in FMA mode with orc_set_fma_tail, within 1e-10 of
+    the serial reference arithmetic."""
+    A, P0, nt = systems[grid]
+    n = A.shape[0]
+    import scipy.sparse as sp
+    prow, pcol = P0.perm_row, P0.perm_col
+    Pr = sp.csr_matrix((np.ones(n), (np.arange(n), prow)), shape=(n, n))
+    Pc = sp.csr_matrix((np.ones(n), (np.arange(n), pcol)), shape=(n, n))
+    B = (Pr @ A @ Pc).tocsr()
+    B.sort_indices()
+    Lt, Ut = O.ilu0(B)
+    ones = np.ones(n)
+    P = O.Split(Lt, Ut, ones, prow, pcol, ones, ones)
+    b = np.random.default_rng(2).random(n)
+    o = O.gmres_split(A, P, b, m=32, max_iter=600, tol=1e-10)
+    rng = np.random.default_rng(9)
+    vs = [rng.standard_normal(n) for _ in range(2)]
+    ot, ref_ops = order_matched(A, P, b, n, grid, nt, 2, 2, nt, vs)
+    s = split_solver(A, P)
+    try:
+        s.set_division(ggmres.DIV_FMA)
+        assert s.division_active(0) == s.division_active(1) == ggmres.DIV_FMA
+        for v, (l, r) in zip(vs, ref_ops):
+            assert np.array_equal(s.precond_apply(ggmres.APPLY_LEFT, v), l)
+            assert np.array_equal(s.precond_apply(ggmres.APPLY_RIGHT, v), r)
+        g = s.solve(b, restart=32, max_iter=600, tol=1e-10)
+        assert g["iters"] == ot["iters"] and np.array_equal(g["hist"], ot["hist"])
+        assert np.array_equal(g["x"], ot["x"])
+        assert abs(g["iters"] - o["iters"]) <= 1 and rel_err(g["x"], o["x"]) <= 1e-8
     finally:
         s.close()
 
