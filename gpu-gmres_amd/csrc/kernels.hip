@@ -1118,6 +1118,11 @@ __device__ __forceinline__ void trsv_wave2d_body(
     const double *__restrict__ ce1, const double *__restrict__ ce2, const FusedSpmv &fs)
 {
     using C = WaveCfg<DIV, D3, S>;
+    // LDS work in the lane shift's shadow -- not for the unit L's fused rows,
+    // whose step is one FMA after the shift: there the pair's reads and staging
+    // write go after the pair (C2 fused L 86.7 -> 84.5 us, netlist L 91.5 ->
+    // 90.4; the other forms keep it: the exact unit L 88.9 -> 90.3 without)
+    constexpr bool SH = kWaveShadow && DIV != WD_UFMA;
     static_assert(!FS || (FWD && !D3 && S == 1 && !TRACE && C::LOADERS == 1), "fused SpMV: forward 2D, one loader");
     static_assert(!IL || (S == 1 && !D3), "in-line-first rows: unskewed 2D grids");
     constexpr bool FM = DIV == WD_UFMA || DIV == WD_SFMA;     // GG_DIV_FMA rows
@@ -1479,7 +1484,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
                     bz = bb - e0 * xz;
                 }
                 const double xs = dpp_shift_old<ctrl>(xp, old);
-                if constexpr (kWaveShadow) {
+                if constexpr (SH) {
                     // LDS work of the pair in the cross-lane shift's latency:
                     // the look-ahead reads at the first step, the previous
                     // pair's x staging at the second
@@ -1546,11 +1551,11 @@ __device__ __forceinline__ void trsv_wave2d_body(
             // and publishes the edge values), then the pair kWaveLook ahead is
             // read; the scheduling fence keeps it all inside this pair, in the
             // recurrence's latency bubbles
-            if (!kWaveShadow || kk == C::PBN - 1)
+            if (!SH || kk == C::PBN - 1)
                 xbuf[(bi & 1) * PB + kk * 64 + lane] =
                     FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
 
-            if (!kWaveShadow && kk + kWaveLook < C::PBN) {
+            if (!SH && kk + kWaveLook < C::PBN) {
 #pragma unroll
                 for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
             }
