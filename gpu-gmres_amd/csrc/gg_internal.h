@@ -213,6 +213,8 @@ Wave2D detect_border2d(const CanonTri &L, const CanonTri &U, bool split_u, Canon
 // rows with more off-diagonal terms than this are solved by a whole wave in the
 // sync-free triangular solve (kernels.hip k_trsv_flow)
 constexpr int kFlowLong = 32;
+// bordered-grid tails this small run in one workgroup (kernels.hip k_tail_small)
+constexpr int kTailSmallRows = 16384, kTailSmallLevels = 256;
 
 // SpMV row blocks: each block <= 256 rows and <= kSpmvCap nnz (CSR-stream)
 constexpr int kSpmvCap = 2048;
@@ -286,6 +288,7 @@ struct DevTri {
     DBuf<double> d;
     std::vector<int> lev_ptr;    // host
     DBuf<int> lev_rows;
+    DBuf<int> lev_ptr_d;         // a small bordered tail (k_tail_small): lev_ptr on the device
     // the flow kernel's tasks over lev_rows (level order): {first, count} = up
     // to 64 rows of at most kFlowLong terms, one per lane; count = -1: one row
     // with more terms, taken by a whole wave

@@ -729,6 +729,48 @@ __global__ void k_border_sub(Gate g, int nrow, const long long *__restrict__ slo
     b[p] = acc;
 }
 
+// A small bordered-grid tail (DevTri::tail_small) in ONE workgroup: its level
+// sets one after the other with a barrier between (no sentinel pre-fill, no
+// polls), each row with k_trsv_level's operations (fm: GG_DIV_FMA's rows, y:
+// the multiply); then, for the forward solve, the mesh rows' tail terms
+// (k_border_sub's operations) -- the three or four launches of the general
+// path (fill, flow, coupling) in one: 4-5 us each for an 800-row tail
+__global__ __launch_bounds__(1024) void k_tail_small(Gate g, int nlev, const int *__restrict__ lev_ptr,
+                                                     const int *__restrict__ rows, const int *__restrict__ rp,
+                                                     const int *__restrict__ ci, const double *__restrict__ v,
+                                                     const double *__restrict__ d, const double *__restrict__ y,
+                                                     int fm, const double *b, double *x, int ncoup,
+                                                     const long long *__restrict__ cslot, const int *__restrict__ crp,
+                                                     const int *__restrict__ cci, const double *__restrict__ cv,
+                                                     double *bmut, int cfm)
+{
+    if (gated(g)) return;
+    for (int l = 0; l < nlev; l++) {
+        const int q1 = lev_ptr[l + 1];
+        for (int q = lev_ptr[l] + (int)threadIdx.x; q < q1; q += (int)blockDim.x) {
+            const int r = rows[q];
+            double acc;
+            if (fm) {
+                acc = y ? b[r] * y[r] : b[r];
+                for (int k = rp[r]; k < rp[r + 1]; k++) acc = __builtin_fma(-v[k], x[ci[k]], acc);
+            } else {
+                acc = b[r];
+                for (int k = rp[r]; k < rp[r + 1]; k++) acc = acc - v[k] * x[ci[k]];
+                acc = y ? acc * y[r] : acc / d[r];
+            }
+            x[r] = acc;
+        }
+        __syncthreads();
+    }
+    for (int q = threadIdx.x; q < ncoup; q += blockDim.x) {
+        const long long p = cslot[q];
+        double acc = bmut[p];
+        for (int k = crp[q]; k < crp[q + 1]; k++)
+            acc = cfm ? __builtin_fma(-cv[k], x[cci[k]], acc) : acc - cv[k] * x[cci[k]];
+        bmut[p] = acc;
+    }
+}
+
 // The sharded solve's separator step in ONE launch (dd.hip apply_minv): the
 // three row phases of SepFlow -- separator L rows (b_S - L_SI y_I, then the
 // separator triangle's terms, / d), separator U rows (y_S, then the triangle's
@@ -3914,6 +3956,24 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
     DevTri &tl = fm ? *T.tail_fma : *T.tail;
     tl.fast = 0;
     tl.mul = e == WD_MUL;
+    if (tl.lev_ptr_d.p) {
+        // a small tail: one workgroup for the tail and the coupling
+        auto tail_small = [&](bool coup) {
+            k_tail_small<<<1, 1024, 0, st>>>(g, (int)tl.lev_ptr.size() - 1, tl.lev_ptr_d.p, tl.lev_rows.p,
+                                             tl.off.rp.p, tl.off.ci.p, tl.off.v.p, tl.d.p,
+                                             (tl.mul || tl.fmrow) ? tl.rw.p : nullptr, tl.fmrow ? 1 : 0, b, x,
+                                             coup ? T.ncoup : 0, T.cslot.p, T.crp.p, T.cci.p, T.cv.p,
+                                             const_cast<double *>(b), fm ? 1 : 0);
+        };
+        if (T.lower) {
+            tail_small(true);
+            launch_trsv_one(g, T, b + T.bofs, x + T.bofs, err, st);
+        } else {
+            launch_trsv_one(g, T, b + T.bofs, x + T.bofs, err, st);
+            tail_small(false);
+        }
+        return;
+    }
     if (T.lower) {
         launch_trsv_one(g, tl, b, x, err, st);
         if (T.ncoup)

@@ -306,7 +306,14 @@ void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const 
     T.tail = std::make_unique<DevTri>();
     T.tail->lower = C.lower;
     T.tail->n = nt;
-    build_level(*T.tail, Ct, level_sets(Ct, true), st);
+    const Levels tlv = level_sets(Ct, true);
+    build_level(*T.tail, Ct, tlv, st);
+    // a small tail (an MNA system's pads and branches: hundreds of rows in a
+    // few levels) runs in one workgroup, levels separated by barriers
+    // (kernels.hip k_tail_small); GG_TAIL_SMALL=0 keeps the flow kernel
+    const char *ts = std::getenv("GG_TAIL_SMALL");
+    const bool small = !(ts && ts[0] == '0') && nt <= kTailSmallRows && (int)tlv.ptr.size() - 1 <= kTailSmallLevels;
+    if (small) T.tail->lev_ptr_d.upload(tlv.ptr, st);
     // WD_MUL on the whole triangle needs every tail 1/d finite and normal too
     bool tail_mul = true;
     std::vector<double> ry(nt);
@@ -345,9 +352,10 @@ void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const 
         T.tail_fma = std::make_unique<DevTri>();
         T.tail_fma->lower = C.lower;
         T.tail_fma->n = nt;
-        build_level(*T.tail_fma, Cf, level_sets(Ct, true), st, true);
+        build_level(*T.tail_fma, Cf, tlv, st, true);
         T.tail_fma->fmrow = true;
         T.tail_fma->rw.upload(ry, st);
+        if (small) T.tail_fma->lev_ptr_d.upload(tlv.ptr, st);
     }
     // the grid rows' tail terms (lower: the leading terms of the row, detect_border2d)
     std::vector<long long> cs;
