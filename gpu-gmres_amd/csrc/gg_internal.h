@@ -291,9 +291,17 @@ struct DevTri {
     DBuf<int> lev_ptr_d;         // a small bordered tail (k_tail_small): lev_ptr on the device
     // the flow kernel's tasks over lev_rows (level order): {first, count} = up
     // to 64 rows of at most kFlowLong terms, one per lane; count = -1: one row
-    // with more terms, taken by a whole wave
+    // with more terms, taken by a whole wave; {.z, .w} = the run's first
+    // 64-entry group and width in the sliced copy (ell)
     int ntask = 0;
-    DBuf<int2> tasks;
+    DBuf<int4> tasks;
+    // sliced (ELL) copy of the short rows' terms, per task w groups of 64
+    // entries, group k = every lane's k-th term (canonical order; column -1
+    // past a row's end): the kernel reads a lane's terms without rp and with
+    // one coalesced load per term index (k_trsv_flow<true>)
+    bool ell = false;
+    DBuf<int> eci;
+    DBuf<double> ev;
     // WAVE2D (layout arrays, length P)
     Wave2D wl;
     DBuf<double> c1, c2, dw, rw; // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor, rw: RN(1/dw)

@@ -567,13 +567,105 @@ __global__ void k_fill_gated(Gate g, unsigned long long *p, long long n, unsigne
 #ifndef GG_FLOW_PREFETCH
 #define GG_FLOW_PREFETCH 1
 #endif
-__global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const int2 *__restrict__ tasks,
+// one long row (more than kFlowLong terms), the whole wave: each round 256 of
+// its terms (4 per lane) are loaded and polled together, their products v*x
+// formed in parallel, then lane 0 subtracts them from acc one by one in
+// canonical order -- the reference's serial arithmetic
+__device__ __forceinline__ void flow_long_row(int r, const int *__restrict__ rp, const int *__restrict__ ci,
+                                              const double *__restrict__ v, const double *__restrict__ d,
+                                              const double *__restrict__ b, unsigned long long *xu, int *err,
+                                              const double *__restrict__ y, double *wprod, int lane)
+{
+    const int k0 = rp[r], k1 = rp[r + 1];
+    double acc = b[r];
+    int spins = 0;
+    // round kc's columns, coefficients and x polls; the next round's
+    // are issued before this round's serial sum (their latency hidden)
+    int c[4];
+    double vv[4];
+    unsigned long long u[4];
+    auto fetch = [&](int kc, int *cc, double *vc, unsigned long long *uc) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int k = kc + q * 64 + lane;
+            cc[q] = k < k1 ? ci[k] : -1;
+            vc[q] = k < k1 ? v[k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) uc[q] = cc[q] >= 0 ? ld_agent(xu + cc[q]) : 0ull;
+    };
+    fetch(k0, c, vv, u);
+    for (int kc = k0; kc < k1; kc += 256) {
+        if (!GG_FLOW_PREFETCH && kc > k0) fetch(kc, c, vv, u);
+        while (true) {
+            bool miss = false;
+#pragma unroll
+            for (int q = 0; q < 4; q++) miss |= c[q] >= 0 && u[q] == kSentinel;
+            if (!__any(miss)) break;
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > kSpinLimit) {
+                if (lane == 0) atomicOr(err, 1);
+                break;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (c[q] >= 0 && u[q] == kSentinel) u[q] = ld_agent(xu + c[q]);
+        }
+        double pq[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) pq[q] = vv[q] * __longlong_as_double((long long)u[q]);
+        if (GG_FLOW_PREFETCH && kc + 256 < k1) fetch(kc + 256, c, vv, u);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            wprod[lane] = pq[q];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            const int cnt = k1 - (kc + q * 64);
+            if (lane == 0) {
+                // the 64 products in canonical order, read 8 at a time one
+                // chunk ahead (a read-then-subtract loop waits an LDS round
+                // trip per term)
+                const double2 *wp2 = reinterpret_cast<const double2 *>(wprod);
+                double2 cur[4], nxt[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) cur[e] = wp2[e];
+#pragma unroll
+                for (int c8 = 0; c8 < 8; c8++) {
+                    if (c8 + 1 < 8) {
+#pragma unroll
+                        for (int e = 0; e < 4; e++) nxt[e] = wp2[(c8 + 1) * 4 + e];
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int j = c8 * 8 + 2 * e;
+                        if (j < cnt) acc = acc - cur[e].x;
+                        if (j + 1 < cnt) acc = acc - cur[e].y;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; e++) cur[e] = nxt[e];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+    }
+    if (lane == 0) st_agent(xu + r, (unsigned long long)__double_as_longlong(y ? acc * y[r] : acc / d[r]));
+}
+
+// ELL: short rows read their terms from the sliced copy (DevTri::eci / ev,
+// task {.z, .w}) instead of rp / ci / v: no rp -> ci -> poll chain of dependent
+// loads, one coalesced load per term index, and the next task's loads issued
+// behind this task's polls; the operations are the same (pgr: L 84.0 -> 62.8,
+// U 103.0 -> 68.9 us without the pipelining, profiles/r04y_pgr_e*.json).
+template <bool ELL>
+__global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const int4 *__restrict__ tasks,
                                                       const int *__restrict__ rows,
                                                       const int *__restrict__ rp, const int *__restrict__ ci,
                                                       const double *__restrict__ v,
                                                       const double *__restrict__ d,
                                                       const double *__restrict__ b, double *x, int *err,
-                                                      const double *__restrict__ y, int fm)
+                                                      const double *__restrict__ y, int fm,
+                                                      const int *__restrict__ eci, const double *__restrict__ ev)
 {
     if (gated(g)) return;
     __shared__ double prod[kBlock];            // a long row's products, one 64-slot area per wave
@@ -582,89 +674,119 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
     const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
     const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
     unsigned long long *xu = reinterpret_cast<unsigned long long *>(x);
-    for (long long t = wid; t < ntask; t += nw) {
-        const int2 tk = tasks[t];
-        if (tk.y < 0) {
-            // (fm triangles are built without long rows: build_tri_bordered)
-            // one long row, the whole wave: each round 256 of its terms (4 per
-            // lane) are loaded and polled together, their products v*x formed
-            // in parallel, then lane 0 subtracts them from acc one by one in
-            // canonical order -- the reference's serial arithmetic
-            const int r = rows[tk.x];
-            const int k0 = rp[r], k1 = rp[r + 1];
-            double acc = b[r];
-            int spins = 0;
-            // round kc's columns, coefficients and x polls; the next round's
-            // are issued before this round's serial sum (their latency hidden)
-            int c[4];
-            double vv[4];
-            unsigned long long u[4];
-            auto fetch = [&](int kc, int *cc, double *vc, unsigned long long *uc) {
+    if constexpr (ELL) {
+        // Short rows one per lane, terms from the sliced copy four at a time
+        // (cc / vv: terms kb .. kb+3, column -1 past the row's end).  Software
+        // pipelined over the wave's tasks: the next task's header is loaded two
+        // tasks ahead, its row indices and first four terms one task ahead
+        // (issued behind this task's polls), so a row waits on one memory
+        // latency -- its polls -- after the previous task's.
+        auto head = [&](const int4 &q, int &rq, int (&cq)[4], double (&vq)[4]) {
+            rq = (q.y > 0 && lane < q.y) ? rows[q.x + lane] : -1;
+            const long long eb = (long long)q.z * 64 + lane;
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int k = kc + q * 64 + lane;
-                    cc[q] = k < k1 ? ci[k] : -1;
-                    vc[q] = k < k1 ? v[k] : 0.0;
-                }
+            for (int j = 0; j < 4; j++) {
+                const bool in = q.y > 0 && j < q.w;
+                cq[j] = in ? eci[eb + (long long)j * 64] : -1;
+                vq[j] = in ? ev[eb + (long long)j * 64] : 0.0;
+            }
+        };
+        // (past the end: zeros by a value select -- a select between pointers
+        // to the task and to a local would make the load a flat one)
+        auto task_at = [&](long long i) {
+            const bool ok = i < ntask;
+            const int4 q = tasks[ok ? i : 0];
+            return make_int4(ok ? q.x : 0, ok ? q.y : 0, ok ? q.z : 0, ok ? q.w : 0);
+        };
+        int4 tk = task_at(wid);
+        int4 tkn = task_at(wid + nw);
+        int r, cc[4];
+        double vv[4];
+        head(tk, r, cc, vv);
+        for (long long t = wid; t < ntask; t += nw) {
+            int rn, ccn[4];
+            double vvn[4];
+            const int4 tk2 = task_at(t + 2 * nw);
+            if (tk.y < 0) {
+                head(tkn, rn, ccn, vvn);
+                flow_long_row(rows[tk.x], rp, ci, v, d, b, xu, err, y, wprod, lane);
+            } else {
+                bool pending = r >= 0;
+                // y: the reciprocal (WD_MUL's row; fm: b's pre-scale, GG_DIV_FMA's row)
+                double acc = pending ? ((fm && y) ? b[r] * y[r] : b[r]) : 0.0;
+                const double dr = pending ? (y ? y[r] : d[r]) : 1.0;
+                unsigned long long u[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++) uc[q] = cc[q] >= 0 ? ld_agent(xu + cc[q]) : 0ull;
-            };
-            fetch(k0, c, vv, u);
-            for (int kc = k0; kc < k1; kc += 256) {
-                if (!GG_FLOW_PREFETCH && kc > k0) fetch(kc, c, vv, u);
-                while (true) {
-                    bool miss = false;
+                for (int j = 0; j < 4; j++) u[j] = cc[j] >= 0 ? ld_agent(xu + cc[j]) : 0ull;
+                head(tkn, rn, ccn, vvn);
+                const int w = tk.w;
+                const long long eb = (long long)tk.z * 64 + lane;
+                int kb = 0, k = 0, spins = 0;   // chunk base, terms consumed
+                bool polled = true;             // u holds this round's polls
+                while (__any(pending)) {
+                    if (pending) {
+                        // consume the sources in canonical order as far as
+                        // they are ready (a source once seen stays final)
+                        while (true) {
+                            if (!polled) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) miss |= c[q] >= 0 && u[q] == kSentinel;
-                    if (!__any(miss)) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > kSpinLimit) {
-                        if (lane == 0) atomicOr(err, 1);
-                        break;
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        if (c[q] >= 0 && u[q] == kSentinel) u[q] = ld_agent(xu + c[q]);
-                }
-                double pq[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) pq[q] = vv[q] * __longlong_as_double((long long)u[q]);
-                if (GG_FLOW_PREFETCH && kc + 256 < k1) fetch(kc + 256, c, vv, u);
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    wprod[lane] = pq[q];
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    const int cnt = k1 - (kc + q * 64);
-                    if (lane == 0) {
-                        // the 64 products in canonical order, read 8 at a time one
-                        // chunk ahead (a read-then-subtract loop waits an LDS round
-                        // trip per term)
-                        const double2 *wp2 = reinterpret_cast<const double2 *>(wprod);
-                        double2 cur[4], nxt[4];
-#pragma unroll
-                        for (int e = 0; e < 4; e++) cur[e] = wp2[e];
-#pragma unroll
-                        for (int c8 = 0; c8 < 8; c8++) {
-                            if (c8 + 1 < 8) {
-#pragma unroll
-                                for (int e = 0; e < 4; e++) nxt[e] = wp2[(c8 + 1) * 4 + e];
+                                for (int j = 0; j < 4; j++)
+                                    u[j] = (kb + j >= k && cc[j] >= 0) ? ld_agent(xu + cc[j]) : 0ull;
                             }
+                            polled = false;
+                            bool stop = false;
 #pragma unroll
-                            for (int e = 0; e < 4; e++) {
-                                const int j = c8 * 8 + 2 * e;
-                                if (j < cnt) acc = acc - cur[e].x;
-                                if (j + 1 < cnt) acc = acc - cur[e].y;
+                            for (int j = 0; j < 4; j++) {
+                                if (!stop && kb + j >= k && cc[j] >= 0) {
+                                    if (u[j] == kSentinel) {
+                                        stop = true;
+                                    } else {
+                                        const double xj = __longlong_as_double((long long)u[j]);
+                                        acc = fm ? __builtin_fma(-vv[j], xj, acc) : acc - vv[j] * xj;
+                                        k++;
+                                    }
+                                }
                             }
+                            if (stop) break;
+                            if (cc[3] < 0 || kb + 4 >= w) {
+                                st_agent(xu + r, (unsigned long long)__double_as_longlong(fm ? acc : y ? acc * dr
+                                                                                                  : acc / dr));
+                                pending = false;
+                                break;
+                            }
+                            kb += 4;
 #pragma unroll
-                            for (int e = 0; e < 4; e++) cur[e] = nxt[e];
+                            for (int j = 0; j < 4; j++) {
+                                cc[j] = kb + j < w ? eci[eb + (long long)(kb + j) * 64] : -1;
+                                vv[j] = kb + j < w ? ev[eb + (long long)(kb + j) * 64] : 0.0;
+                            }
                         }
                     }
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    if (__any(pending)) {
+                        __builtin_amdgcn_s_sleep(4);
+                        if (++spins > kSpinLimit) {
+                            if (pending) atomicOr(err, 1);
+                            pending = false;
+                        }
+                    }
                 }
             }
-            if (lane == 0) st_agent(xu + r, (unsigned long long)__double_as_longlong(y ? acc * y[r] : acc / d[r]));
+            tk = tkn;
+            tkn = tk2;
+            r = rn;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                cc[j] = ccn[j];
+                vv[j] = vvn[j];
+            }
+        }
+        return;
+    }
+    for (long long t = wid; t < ntask; t += nw) {
+        const int4 tk = tasks[t];
+        if (tk.y < 0) {
+            // (fm triangles are built without long rows: build_tri_bordered)
+            flow_long_row(rows[tk.x], rp, ci, v, d, b, xu, err, y, wprod, lane);
             continue;
         }
         // up to 64 short rows, one per lane
@@ -3679,9 +3801,11 @@ int trsv_flow_max_blocks()
 {
     int dev = 0, per = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_trsv_flow, kBlock, 0) != hipSuccess) return 0;
+    int per2 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_trsv_flow<false>, kBlock, 0) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_trsv_flow<true>, kBlock, 0) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    return per * cus;
+    return std::min(per, per2) * cus;
 }
 int ilu0_columns_max_blocks()
 {
@@ -4023,9 +4147,16 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
             if (!T.prefilled)
                 k_fill_gated<<<blocks_for(nrows, kBlock, 8192), kBlock, 0, st>>>(
                     g, reinterpret_cast<unsigned long long *>(x), nrows, kSentinel);
-            k_trsv_flow<<<blocks, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p, T.off.ci.p,
-                                                   T.off.v.p, T.d.p, b, x, err,
-                                                   (T.mul || T.fmrow) ? T.rw.p : nullptr, T.fmrow ? 1 : 0);
+            if (T.ell)
+                k_trsv_flow<true><<<blocks, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p,
+                                                             T.off.ci.p, T.off.v.p, T.d.p, b, x, err,
+                                                             (T.mul || T.fmrow) ? T.rw.p : nullptr, T.fmrow ? 1 : 0,
+                                                             T.eci.p, T.ev.p);
+            else
+                k_trsv_flow<false><<<blocks, kBlock, 0, st>>>(g, T.ntask, T.tasks.p, T.lev_rows.p, T.off.rp.p,
+                                                              T.off.ci.p, T.off.v.p, T.d.p, b, x, err,
+                                                              (T.mul || T.fmrow) ? T.rw.p : nullptr, T.fmrow ? 1 : 0,
+                                                              nullptr, nullptr);
             return;
         }
         for (int l = 0; l < nlev; l++) {

@@ -253,23 +253,60 @@ void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st,
         // flow tasks in level order: runs of up to 64 short rows, long rows alone
         const char *fl = std::getenv("GG_FLOW_LONG");       // tuning: terms above which a row is long
         const int flow_long = no_long ? INT_MAX : fl ? std::max(0, atoi(fl)) : kFlowLong;
-        std::vector<int2> tasks;
+        std::vector<int4> tasks;
         int run0 = 0, runn = 0;
         auto flush = [&]() {
-            if (runn) tasks.push_back(make_int2(run0, runn));
+            if (runn) tasks.push_back(make_int4(run0, runn, 0, 0));
             runn = 0;
         };
         for (int q = 0; q < (int)lv.rows.size(); q++) {
             const int r = lv.rows[q];
             if (C.off.rp[r + 1] - C.off.rp[r] > flow_long) {
                 flush();
-                tasks.push_back(make_int2(q, -1));
+                tasks.push_back(make_int4(q, -1, 0, 0));
             } else {
                 if (runn == 0) run0 = q;
                 if (++runn == 64) flush();
             }
         }
         flush();
+        // the sliced copy, where its padding stays within 2x the short rows'
+        // terms (GG_FLOW_ELL=0: the CSR form only)
+        long long groups = 0, terms = 0;
+        for (int4 &tk : tasks) {
+            if (tk.y < 0) continue;
+            int w = 0;
+            for (int j = 0; j < tk.y; j++) {
+                const int r = lv.rows[tk.x + j];
+                w = std::max(w, C.off.rp[r + 1] - C.off.rp[r]);
+                terms += C.off.rp[r + 1] - C.off.rp[r];
+            }
+            tk.z = (int)groups;
+            tk.w = w;
+            groups += w;
+        }
+        const char *fe = std::getenv("GG_FLOW_ELL");
+        T.ell = !(fe && fe[0] == '0') && groups * 64 <= 2 * terms + 64LL * (long long)tasks.size() &&
+                groups * 64 < INT_MAX;
+        T.eci.release();
+        T.ev.release();
+        if (T.ell) {
+            std::vector<int> eci((size_t)std::max<long long>(groups, 1) * 64, -1);
+            std::vector<double> ev(eci.size(), 0.0);
+            for (const int4 &tk : tasks) {
+                if (tk.y < 0) continue;
+                for (int j = 0; j < tk.y; j++) {
+                    const int r = lv.rows[tk.x + j];
+                    for (int k = C.off.rp[r]; k < C.off.rp[r + 1]; k++) {
+                        const size_t e = ((size_t)tk.z + (k - C.off.rp[r])) * 64 + j;
+                        eci[e] = C.off.ci[k];
+                        ev[e] = C.off.v[k];
+                    }
+                }
+            }
+            T.eci.upload(eci, st);
+            T.ev.upload(ev, st);
+        }
         T.ntask = (int)tasks.size();
         T.tasks.upload(tasks, st);
         T.bytes = 12.0 * C.off.nnz() + 4.0 * (n + 1) + 24.0 * n;

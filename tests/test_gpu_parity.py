@@ -129,12 +129,15 @@ def test_spmv_c3_standin_full_size(solver):
 
 
 @pytest.mark.parametrize("name", sorted(MATS))
-@pytest.mark.parametrize("force_level", [False, True, "per_level"])
+@pytest.mark.parametrize("force_level", [False, True, "csr", "per_level"])
 def test_ilu0_apply_bitexact(solver, name, force_level, monkeypatch):
     """wavefront kernel where it applies; force_level: the dataflow level kernel
-    (k_trsv_flow); "per_level": one k_trsv_level launch per level"""
+    (k_trsv_flow, short rows from its sliced term copy where built; "csr": from
+    the CSR arrays, GG_FLOW_ELL=0); "per_level": one k_trsv_level launch per level"""
     if force_level:
         monkeypatch.setenv("GG_NO_WAVEFRONT", "1")
+    if force_level == "csr":
+        monkeypatch.setenv("GG_FLOW_ELL", "0")
     if force_level == "per_level":
         monkeypatch.setenv("GG_TRSV_LEVELS", "1")
     A = MATS[name]()
@@ -407,7 +410,10 @@ def test_iluk_device_zero_pivot(solver):
         solver.set_precond_iluk_device(1)
 
 
-def test_gmres_split_parity(solver):
+@pytest.mark.parametrize("ell", ["1", "0"])
+def test_gmres_split_parity(solver, ell, monkeypatch):
+    """randomly permuted split factors (the flow kernel; ell "0": its CSR form)"""
+    monkeypatch.setenv("GG_FLOW_ELL", ell)
     A = M.laplacian_5pt(40)
     P = make_split(A, seed=9)
     b = M.rhs_uniform(A.shape[0])
