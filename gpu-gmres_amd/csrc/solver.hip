@@ -290,9 +290,11 @@ void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st,
                 groups * 64 < INT_MAX;
         T.eci.release();
         T.ev.release();
+        std::vector<int> eci;
+        std::vector<double> ev;
         if (T.ell) {
-            std::vector<int> eci((size_t)std::max<long long>(groups, 1) * 64, -1);
-            std::vector<double> ev(eci.size(), 0.0);
+            eci.assign((size_t)std::max<long long>(groups, 1) * 64, -1);
+            ev.assign(eci.size(), 0.0);
             for (const int4 &tk : tasks) {
                 if (tk.y < 0) continue;
                 for (int j = 0; j < tk.y; j++) {
@@ -309,6 +311,7 @@ void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st,
         }
         T.ntask = (int)tasks.size();
         T.tasks.upload(tasks, st);
+        GG_HIP(hipStreamSynchronize(st));       // the host vectors end here
         T.bytes = 12.0 * C.off.nnz() + 4.0 * (n + 1) + 24.0 * n;
     }
 }
