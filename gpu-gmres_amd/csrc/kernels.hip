@@ -654,9 +654,10 @@ __device__ __forceinline__ void flow_long_row(int r, const int *__restrict__ rp,
 
 // ELL: short rows read their terms from the sliced copy (DevTri::eci / ev,
 // task {.z, .w}) instead of rp / ci / v: no rp -> ci -> poll chain of dependent
-// loads, one coalesced load per term index, and the next task's loads issued
-// behind this task's polls; the operations are the same (pgr: L 84.0 -> 62.8,
-// U 103.0 -> 68.9 us without the pipelining, profiles/r04y_pgr_e*.json).
+// loads, one coalesced load per term index; the operations are the same (pgr:
+// L 84.0 -> 62.8, U 103.0 -> 68.9 us, profiles/r04y_pgr_e*.json; a software-
+// pipelined task loop -- the next task's loads behind this one's polls --
+// measured 67.1 / 73.1 us, r04z_pgr_e1.json, not kept).
 template <bool ELL>
 __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const int4 *__restrict__ tasks,
                                                       const int *__restrict__ rows,
@@ -674,119 +675,74 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
     const long long wid = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
     const long long nw = (gridDim.x * (long long)blockDim.x) >> 6;
     unsigned long long *xu = reinterpret_cast<unsigned long long *>(x);
-    if constexpr (ELL) {
-        // Short rows one per lane, terms from the sliced copy four at a time
-        // (cc / vv: terms kb .. kb+3, column -1 past the row's end).  Software
-        // pipelined over the wave's tasks: the next task's header is loaded two
-        // tasks ahead, its row indices and first four terms one task ahead
-        // (issued behind this task's polls), so a row waits on one memory
-        // latency -- its polls -- after the previous task's.
-        auto head = [&](const int4 &q, int &rq, int (&cq)[4], double (&vq)[4]) {
-            rq = (q.y > 0 && lane < q.y) ? rows[q.x + lane] : -1;
-            const long long eb = (long long)q.z * 64 + lane;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const bool in = q.y > 0 && j < q.w;
-                cq[j] = in ? eci[eb + (long long)j * 64] : -1;
-                vq[j] = in ? ev[eb + (long long)j * 64] : 0.0;
-            }
-        };
-        // (past the end: zeros by a value select -- a select between pointers
-        // to the task and to a local would make the load a flat one)
-        auto task_at = [&](long long i) {
-            const bool ok = i < ntask;
-            const int4 q = tasks[ok ? i : 0];
-            return make_int4(ok ? q.x : 0, ok ? q.y : 0, ok ? q.z : 0, ok ? q.w : 0);
-        };
-        int4 tk = task_at(wid);
-        int4 tkn = task_at(wid + nw);
-        int r, cc[4];
-        double vv[4];
-        head(tk, r, cc, vv);
-        for (long long t = wid; t < ntask; t += nw) {
-            int rn, ccn[4];
-            double vvn[4];
-            const int4 tk2 = task_at(t + 2 * nw);
-            if (tk.y < 0) {
-                head(tkn, rn, ccn, vvn);
-                flow_long_row(rows[tk.x], rp, ci, v, d, b, xu, err, y, wprod, lane);
-            } else {
-                bool pending = r >= 0;
-                // y: the reciprocal (WD_MUL's row; fm: b's pre-scale, GG_DIV_FMA's row)
-                double acc = pending ? ((fm && y) ? b[r] * y[r] : b[r]) : 0.0;
-                const double dr = pending ? (y ? y[r] : d[r]) : 1.0;
-                unsigned long long u[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) u[j] = cc[j] >= 0 ? ld_agent(xu + cc[j]) : 0ull;
-                head(tkn, rn, ccn, vvn);
-                const int w = tk.w;
-                const long long eb = (long long)tk.z * 64 + lane;
-                int kb = 0, k = 0, spins = 0;   // chunk base, terms consumed
-                bool polled = true;             // u holds this round's polls
-                while (__any(pending)) {
-                    if (pending) {
-                        // consume the sources in canonical order as far as
-                        // they are ready (a source once seen stays final)
-                        while (true) {
-                            if (!polled) {
-#pragma unroll
-                                for (int j = 0; j < 4; j++)
-                                    u[j] = (kb + j >= k && cc[j] >= 0) ? ld_agent(xu + cc[j]) : 0ull;
-                            }
-                            polled = false;
-                            bool stop = false;
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                if (!stop && kb + j >= k && cc[j] >= 0) {
-                                    if (u[j] == kSentinel) {
-                                        stop = true;
-                                    } else {
-                                        const double xj = __longlong_as_double((long long)u[j]);
-                                        acc = fm ? __builtin_fma(-vv[j], xj, acc) : acc - vv[j] * xj;
-                                        k++;
-                                    }
-                                }
-                            }
-                            if (stop) break;
-                            if (cc[3] < 0 || kb + 4 >= w) {
-                                st_agent(xu + r, (unsigned long long)__double_as_longlong(fm ? acc : y ? acc * dr
-                                                                                                  : acc / dr));
-                                pending = false;
-                                break;
-                            }
-                            kb += 4;
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                cc[j] = kb + j < w ? eci[eb + (long long)(kb + j) * 64] : -1;
-                                vv[j] = kb + j < w ? ev[eb + (long long)(kb + j) * 64] : 0.0;
-                            }
-                        }
-                    }
-                    if (__any(pending)) {
-                        __builtin_amdgcn_s_sleep(4);
-                        if (++spins > kSpinLimit) {
-                            if (pending) atomicOr(err, 1);
-                            pending = false;
-                        }
-                    }
-                }
-            }
-            tk = tkn;
-            tkn = tk2;
-            r = rn;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                cc[j] = ccn[j];
-                vv[j] = vvn[j];
-            }
-        }
-        return;
-    }
     for (long long t = wid; t < ntask; t += nw) {
         const int4 tk = tasks[t];
         if (tk.y < 0) {
             // (fm triangles are built without long rows: build_tri_bordered)
             flow_long_row(rows[tk.x], rp, ci, v, d, b, xu, err, y, wprod, lane);
+            continue;
+        }
+        if constexpr (ELL) {
+            // up to 64 short rows, one per lane, terms from the sliced copy four
+            // at a time (cc / vv: terms kb .. kb+3; column -1 past the row's end)
+            const int r = lane < tk.y ? rows[tk.x + lane] : -1;
+            const int w = tk.w;
+            const long long eb = (long long)tk.z * 64 + lane;
+            int cc[4];
+            double vv[4];
+            auto chunk = [&](int kb) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    cc[j] = kb + j < w ? eci[eb + (long long)(kb + j) * 64] : -1;
+                    vv[j] = kb + j < w ? ev[eb + (long long)(kb + j) * 64] : 0.0;
+                }
+            };
+            chunk(0);
+            bool pending = r >= 0;
+            // y: the reciprocal (WD_MUL's row; fm: b's pre-scale, GG_DIV_FMA's row)
+            double acc = pending ? ((fm && y) ? b[r] * y[r] : b[r]) : 0.0;
+            const double dr = pending ? (y ? y[r] : d[r]) : 1.0;
+            int kb = 0, k = 0;                  // chunk base, terms consumed
+            int spins = 0;
+            while (__any(pending)) {
+                if (pending) {
+                    // consume the sources in canonical order as far as they
+                    // are ready (a source once seen stays final)
+                    while (true) {
+                        unsigned long long u[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) u[j] = (kb + j >= k && cc[j] >= 0) ? ld_agent(xu + cc[j]) : 0ull;
+                        bool stop = false;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            if (!stop && kb + j >= k && cc[j] >= 0) {
+                                if (u[j] == kSentinel) {
+                                    stop = true;
+                                } else {
+                                    const double xj = __longlong_as_double((long long)u[j]);
+                                    acc = fm ? __builtin_fma(-vv[j], xj, acc) : acc - vv[j] * xj;
+                                    k++;
+                                }
+                            }
+                        }
+                        if (stop) break;
+                        if (cc[3] < 0 || kb + 4 >= w) {
+                            st_agent(xu + r, (unsigned long long)__double_as_longlong(fm ? acc : y ? acc * dr : acc / dr));
+                            pending = false;
+                            break;
+                        }
+                        kb += 4;
+                        chunk(kb);
+                    }
+                }
+                if (__any(pending)) {
+                    __builtin_amdgcn_s_sleep(4);
+                    if (++spins > kSpinLimit) {
+                        if (pending) atomicOr(err, 1);
+                        pending = false;
+                    }
+                }
+            }
             continue;
         }
         // up to 64 short rows, one per lane
