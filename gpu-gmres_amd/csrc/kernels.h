@@ -128,6 +128,10 @@ void launch_div(Gate g, const double *in, const double *s, double *out, int n, h
 // y = A x (resid: y = b - A x); ydiv: y[r] /= ydiv[r] (the split engine's folded row scaling)
 void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, double *y, bool resid,
                  hipStream_t st, const double *ydiv = nullptr);
+// y[r] = (sum_k a_k RN(x[c_k] / xdiv[c_k])) / ydiv[r] on the sliced copy (false, nothing
+// launched, when A has none): the split engine's D_r^-1 in the SpMV's gathers
+bool launch_spmv_xdiv(Gate g, const DevCsr &A, const double *x, const double *xdiv, double *y, hipStream_t st,
+                      const double *ydiv);
 
 // ---- triangular solves ---------------------------------------------------------
 void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st);

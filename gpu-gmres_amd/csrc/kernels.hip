@@ -477,14 +477,17 @@ __device__ __forceinline__ int xcd_block()
     return x * q + (x < rem ? x : rem) + (blockIdx.x >> 3);
 }
 
-template <bool RESID, bool YDIV = false>
+// XDIV: x[c] = RN(x[c] / xdiv[c]) formed per gathered term -- the split
+// engine's D_r^-1 pass (k_div) folded into the gathers, the same division
+template <bool RESID, bool YDIV = false, bool XDIV = false>
 __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice, const int *sptr,
                                                       const int *__restrict__ ci,
                                                       const double *__restrict__ v,
                                                       const double *__restrict__ x,
                                                       const double *__restrict__ b,
                                                       double *__restrict__ y,
-                                                      const double *__restrict__ ydiv)
+                                                      const double *__restrict__ ydiv,
+                                                      const double *__restrict__ xdiv)
 {
     if (gated(g)) return;
     const int s = xcd_block() * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -506,6 +509,15 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
 #pragma unroll
         for (int k = 0; k < 8; k++)
             if (k0 + k < w && c[k] >= 0) xv[k] = x[c[k]];
+        if constexpr (XDIV) {
+            double dv[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (k0 + k < w && c[k] >= 0) dv[k] = xdiv[c[k]];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (k0 + k < w && c[k] >= 0) xv[k] = xv[k] / dv[k];
+        }
 #pragma unroll
         for (int k = 0; k < 8; k++)
             if (k0 + k < w && c[k] >= 0) acc += a[k] * xv[k];
@@ -3889,7 +3901,7 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
     do {                                                                                               \
         if (A.sell)                                                                                    \
             k_spmv_sell<R, D><<<(A.nslice + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st>>>(        \
-                g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, b, y, ydiv);                           \
+                g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, b, y, ydiv, nullptr);                  \
         else                                                                                           \
             k_spmv_stream<R, D><<<A.nblk, kBlock, 0, st>>>(g, A.blk.p, A.rp.p, A.ci.p, A.v.p, x, b, y, \
                                                           ydiv);                                       \
@@ -3902,6 +3914,16 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
         else GG_SPMV(false, false);
     }
 #undef GG_SPMV
+}
+
+bool launch_spmv_xdiv(Gate g, const DevCsr &A, const double *x, const double *xdiv, double *y, hipStream_t st,
+                      const double *ydiv)
+{
+    if (!A.sell || !ydiv) return false;
+    if (A.nblk == 0) return true;
+    k_spmv_sell<false, true, true><<<(A.nslice + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st>>>(
+        g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, nullptr, y, ydiv, xdiv);
+    return true;
 }
 
 template <bool FWD, int DIV>

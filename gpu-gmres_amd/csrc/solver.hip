@@ -736,6 +736,16 @@ void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1
     trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
     launch_div(g, s->t2.p, s->rs_l.p, out, (int)s->P, s->st);
 }
+// the split engine's inner iteration folds Mr's D_r^-1 into the SpMV when A'
+// has its sliced copy (GG_SPMV_XDIV=0: the separate pass, apply_right)
+static bool xdiv_fold()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("GG_SPMV_XDIV");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 // Ml(A' z) with Ml's row gather and D_l^-1 in the SpMV (resid: Ml(b - A x))
 void spmv_left(gg_solver *s, Gate g, const double *z, const double *b, double *out, int i = -1,
                bool fuse = false)
@@ -952,6 +962,20 @@ void enqueue_cycle(gg_solver *s, int m)
             prof_end(s, mk);
             mk = prof_begin(s, GG_PROF_PRECOND, i);
             apply_minv(s, gi, s->ww.p, s->w.p, i);                             // w = M^-1 ww
+            prof_end(s, mk);
+        } else if (!fuse && s->dA.sell && s->U.kind == DevTri::WAVE2D && xdiv_fold()) {
+            // z = Mr v_i without its last pass: D_r^-1 goes into the SpMV's
+            // gathers (the same division per term, k_spmv_sell<.., XDIV>) --
+            // on grid-ordered factors, whose gathers are local (netlist 3,595
+            // -> 3,635 it/s; on the randomly permuted split the second gather
+            // doubles the SpMV's misses, 49.8 -> 112.7 us: profiles/r04p_*_x*.json)
+            launch_mul(gi, vi, s->mid_l.p, s->t1.p, (int)s->P, s->st);
+            trsv(s, gi, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
+            mk = prof_begin(s, GG_PROF_SPMV, i);
+            launch_spmv_xdiv(gi, s->dA, s->t2.p, s->rs_l.p, s->t1.p, s->st, s->ls_l.p);
+            prof_end(s, mk);
+            mk = prof_begin(s, GG_PROF_PRECOND, i);
+            trsv(s, gi, s->L, GG_PROF_TRSV_L, i, s->t1.p, s->w.p);              // w = Ml A z
             prof_end(s, mk);
         } else {
             apply_right(s, gi, vi, s->z.p, i);                                 // z = Mr v_i
