@@ -7,10 +7,12 @@ tol 1e-8, b = A*1, x0 = 0.  One step = one full solve (device-resident b, x;
 the ILU factorization and H2D copies are setup, outside the timed region).
 
 value = inner (Arnoldi) iterations of all ranks / max-over-ranks wall time.
-roofline: the single kernel with the most time in the step (found in a
-profiled warmup step that brackets every kernel family), timed live inside the
-timed region with hipEvent pairs around its launches only, on the solver's
-stream (gg_profile_*); algorithmic bytes from SURVEY.md 8(d) (DESIGN.md
+roofline: the single kernel with the most time over the timed region: the
+candidates (single-kernel families within 2x of the largest in a profiled
+warmup step) are each bracketed with hipEvent pairs in a rotating share of the
+timed solves, on the solver's stream (gg_profile_*), and every candidate's
+entry is reported under "rooflines" (the triangular solves with their
+dependency-chain fraction too); algorithmic bytes from SURVEY.md 8(d) (DESIGN.md
 "Kernels"); traffic: HBM bytes per launch from the committed rocprofv3 PMC
 passes (profiles/pmc_traffic.json), null when those counters were taken on
 other kernel sources (src_sha).  cpu_baseline: the fp64 oracle restatement
@@ -800,29 +802,41 @@ def main():
             fam = profiled_pass()
         else:
             step()
-    # the roofline entry is for ONE kernel: the single-kernel family with the most
-    # time (ilu0_apply = trsv_L + trsv_U and mgs_givens are families of launches);
-    # inside the timed region only its launches are bracketed with events
-    dom = None
+    # roofline candidates: the single-kernel families (the SpMV when it has its
+    # own launch, each triangular solve, the orthogonalization when one launch
+    # per inner iteration does it: k_arnoldi_persist / k_arnoldi_wide) that the
+    # breakdown pass finds within 2x of the largest.  Inside the timed region
+    # ONE candidate is bracketed with events per solve, rotating, so every
+    # candidate is timed live on the solver's stream at the perturbation of a
+    # single family, and the roofline kernel is the one with the most time over
+    # the timed region (not chosen from one warm-up step)
+    kind_of = dict((f[0], f[1]) for f in FAMS)
+    cands = []
     if not a.no_profile:
-        if not fam:
-            dom = "trsv_U"
-        else:
-            # single-kernel families: SpMV, each triangular solve, and the
-            # orthogonalization when one launch per inner iteration does it
-            # (k_arnoldi_persist / k_arnoldi_wide)
-            if not c5 and s.mgs_kernel():
-                KERNEL_NAMES["mgs_givens"] = s.mgs_kernel()
-            single = {k: v for k, v in fam.items() if k in KERNEL_NAMES}
-            dom = max(single, key=lambda k: single[k]["share_of_step"]) if single else None
-        if dom:
-            s.profile(True, kinds=[dict((f[0], f[1]) for f in FAMS)[dom]])
+        if not c5 and s.mgs_kernel():
+            KERNEL_NAMES["mgs_givens"] = s.mgs_kernel()
+        fused_l = s.trsv_kernel(0).startswith("k_trsv_wave2d_spmv")
+        single = {k: v for k, v in fam.items() if k in KERNEL_NAMES and not (k == "spmv" and fused_l)}
+        if single:
+            top = max(v["share_of_step"] for v in single.values())
+            cands = [k for k in ("spmv", "trsv_L", "trsv_U", "mgs_givens")
+                     if k in single and single[k]["share_of_step"] >= 0.5 * top]
+        elif not fam:
+            cands = ["trsv_U"]
+        s.profile(True, kinds=[kind_of[cands[0]]] if cands else [])
+    bracketed = {k: 0 for k in cands}
     barrier()
     t0 = time.perf_counter()
-    res = [step() for _ in range(a.steps)]
+    res = []
+    for k in range(a.steps):
+        if cands:
+            c = cands[k % len(cands)]
+            s.profile_select([kind_of[c]])
+            bracketed[c] += 1
+        res.append(step())
     barrier()
     el = time.perf_counter() - t0
-    timed = families(res, el) if dom else {}
+    timed = families(res, el) if cands else {}
     s.profile(False)
 
     inner = sum(r["inner"] for r in res)
@@ -836,51 +850,71 @@ def main():
     if not a.no_profile and not fam:
         fam = profiled_pass()
 
-    roof = None
-    if dom and dom in timed:
-        f = timed[dom]
-        if dom == "spmv":
+    # time of each candidate over the whole timed region: its event-timed
+    # average x its launches per solve x the solves
+    for k in list(timed):
+        if k not in bracketed or not bracketed[k]:
+            timed.pop(k)
+            continue
+        f = timed[k]
+        f["solves_bracketed"] = bracketed[k]
+        f["est_ms_timed_region"] = round(f["avg_us"] * 1e-3 * f["launches"] / bracketed[k] * a.steps, 3)
+        f["share_of_step"] = round(f["est_ms_timed_region"] / (el * 1e3), 4)
+    dom = max(timed, key=lambda k: timed[k]["est_ms_timed_region"]) if timed else None
+
+    pmc_wl = "c4" if c4 else "c3s" if c3s else "pg" if pg else "netlist" if netlist else None
+
+    def roof_of(name):
+        """(roofline, latency_roofline) of one timed family"""
+        f = timed[name]
+        if name == "spmv":
             KERNEL_NAMES["spmv"] = "k_spmv_sell<false>" if s.spmv_sliced else "k_spmv_stream<false>"
-        if dom in ("trsv_L", "trsv_U") and not s.uses_wavefront:
+        if name in ("trsv_L", "trsv_U") and not s.uses_wavefront:
             kname = ("k_trsv_level (one launch per dependency level; one 'launch' here = one triangle)"
                      if os.environ.get("GG_TRSV_LEVELS") == "1" else "k_trsv_flow")
         else:
-            kname = KERNEL_NAMES[dom]
-        pmc_wl = "c4" if c4 else "c3s" if c3s else "pg" if pg else "netlist" if netlist else None
+            kname = KERNEL_NAMES[name]
         roof = {"kernel": kname, "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(kname, pmc_wl) if not kilu else None,
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
-                "launches_timed": f["launches"]}
-        if dom == "mgs_givens":
+                "launches_timed": f["launches"], "solves_bracketed": f["solves_bracketed"],
+                "share_of_timed_region": f["share_of_step"]}
+        if name == "mgs_givens":
             roof["alg_bytes_note"] = ("v_0..v_i and w read once, v_{i+1} written: 8 n (i+3) bytes at "
                                       "cycle index i, averaged over the launches timed")
-    # the triangular solves are latency-bound: their other roofline is the
-    # dependency chain, nx + ny - 1 wavefront steps at the bare per-step chain
-    # latency (tools/lat_probe.hip on MI355X, profiles/r01_lat_probe.txt)
-    lat = None
-    if roof and dom in ("trsv_L", "trsv_U") and s.uses_wavefront and not c5:
-        # a non-unit L (the split engine's) divides like U
-        mul = u_mul if dom == "trsv_U" else l_mul
-        fm = u_fma if dom == "trsv_U" else l_fma
-        cyc = CHAIN_CYCLES[chain_key(roof["kernel"], dom, fm, mul)]
-        # the DAG's longest path (ILU(k): skew k+1; 3D: nx + ny + nz - 2, whose
-        # per-step chain is the 2D one: the tile kernel's plane term is off it)
-        steps = 3 * a.c4_grid - 2 if c4 else a.grid + (kilu + 1) * (a.grid - 1)
-        floor_us = steps * cyc / (SHADER_GHZ * 1e3)
-        lat = {"kernel": roof["kernel"], "bound": "dependency chain", "critical_steps": steps,
-               "cycles_per_step": cyc, "clock_ghz": SHADER_GHZ, "floor_us": round(floor_us, 2),
-               "achieved_us": roof["avg_us"], "frac": round(floor_us / roof["avg_us"], 4)}
-    elif roof and dom in ("trsv_L", "trsv_U") and not s.uses_wavefront:
-        # the dataflow solve (k_trsv_flow): its chain is the triangle's level
-        # count, each level one cross-workgroup hand-off (idle sc1 store -> sc1
-        # poll: 0.47 us same XCD, profiles/r04_xcd_handoff.txt)
-        lv = s.trsv_levels(0 if dom == "trsv_L" else 1)
-        floor_us = lv * 0.47
-        lat = {"kernel": roof["kernel"], "bound": "dependency chain (levels x hand-off)", "critical_steps": lv,
-               "us_per_step": 0.47, "floor_us": round(floor_us, 2), "achieved_us": roof["avg_us"],
-               "frac": round(floor_us / roof["avg_us"], 4)}
+        # the triangular solves are latency-bound: their other roofline is the
+        # dependency chain, nx + ny - 1 wavefront steps at the bare per-step chain
+        # latency (tools/lat_probe.hip on MI355X, profiles/r01_lat_probe.txt)
+        lat = None
+        if name in ("trsv_L", "trsv_U") and s.uses_wavefront and not c5:
+            # a non-unit L (the split engine's) divides like U
+            mul = u_mul if name == "trsv_U" else l_mul
+            fm = u_fma if name == "trsv_U" else l_fma
+            cyc = CHAIN_CYCLES[chain_key(roof["kernel"], name, fm, mul)]
+            # the DAG's longest path (ILU(k): skew k+1; 3D: nx + ny + nz - 2, whose
+            # per-step chain is the 2D one: the tile kernel's plane term is off it)
+            steps = 3 * a.c4_grid - 2 if c4 else a.grid + (kilu + 1) * (a.grid - 1)
+            floor_us = steps * cyc / (SHADER_GHZ * 1e3)
+            lat = {"kernel": roof["kernel"], "bound": "dependency chain", "critical_steps": steps,
+                   "cycles_per_step": cyc, "clock_ghz": SHADER_GHZ, "floor_us": round(floor_us, 2),
+                   "achieved_us": roof["avg_us"], "frac": round(floor_us / roof["avg_us"], 4)}
+        elif name in ("trsv_L", "trsv_U") and not s.uses_wavefront:
+            # the dataflow solve (k_trsv_flow): its chain is the triangle's level
+            # count, each level one cross-workgroup hand-off (idle sc1 store -> sc1
+            # poll: 0.47 us same XCD, profiles/r04_xcd_handoff.txt)
+            lv = s.trsv_levels(0 if name == "trsv_L" else 1)
+            floor_us = lv * 0.47
+            lat = {"kernel": roof["kernel"], "bound": "dependency chain (levels x hand-off)", "critical_steps": lv,
+                   "us_per_step": 0.47, "floor_us": round(floor_us, 2), "achieved_us": roof["avg_us"],
+                   "frac": round(floor_us / roof["avg_us"], 4)}
+        return roof, lat
+
+    roofs = {k: roof_of(k) for k in timed}
+    roof, lat = roofs[dom] if dom else (None, None)
+    rooflines = {k: dict(r, **({"latency_frac": l["frac"], "latency_floor_us": l["floor_us"]} if l else {}))
+                 for k, (r, l) in roofs.items()}
     spmv_bytes = s.bytes_spmv()
     # isolated SpMV (4 rotating copies of A, x, y: > 256 MiB, not Infinity-Cache served)
     spmv_iso_ms = s.time_spmv(reps=100, nrot=4)
@@ -889,7 +923,7 @@ def main():
                 "frac": round(spmv_bytes / (spmv_iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
     # ---- CPU baseline (rank 0, N=1): the oracle restatement -----------------------
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and a.cpu_iters > 0 and not c5 and not c4 and not c3s:
         import oracle as O
         if pg or netlist:
@@ -916,6 +950,25 @@ def main():
                "sample": f"oracle/ fp64 serial C restatement of {'GMRESilu (split)' if pg or netlist else 'GMRES_leftILU0'} on the same "
                          f"system, first {o['inner']} inner iterations ({ct:.1f} s), one thread "
                          f"pinned to core {core}"}
+        # the same restatement on this process's cores (OpenMP build: SpMV,
+        # BLAS-1 and update loops parallel, triangular solves serial as in the
+        # reference's host engine; OMP_NUM_THREADS as the box sets it)
+        try:
+            O.use_mt(True)
+            thr = O.threads()
+            t1 = time.perf_counter()
+            if pg or netlist:
+                o = O.gmres_split(A, osplit, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
+            else:
+                o = O.gmres_left(A, L, U, b, m=a.restart, max_iter=a.cpu_iters, tol=a.tol)
+            ct = time.perf_counter() - t1
+            cpu_mt = {"value": round(o["inner"] / ct, 3), "unit": "iterations/s", "cores": thr,
+                      "kind": "port", "affinity_cores": len(aff),
+                      "sample": f"the same restatement built with OpenMP (liboracle_mt.so: SpMV, dots, AXPYs "
+                                f"and the update on {thr} threads, the ILU triangular solves serial), "
+                                f"first {o['inner']} inner iterations ({ct:.1f} s)"}
+        finally:
+            O.use_mt(False)
 
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,
@@ -962,10 +1015,14 @@ def main():
                    "parallelism": "single" if world == 1 else f"replicas{world}",
                    "setup_s": round(t_setup, 3)},
         "roofline": roof, "latency_roofline": lat,
+        "rooflines": rooflines,
+        "rooflines_from": ("one candidate family bracketed with hipEvents per timed solve, rotating; "
+                           "roofline = the candidate with the most time over the timed region"),
         "kernels": fam,
         "kernels_from": "one profiled warmup step, every family bracketed by hipEvents",
         "spmv_isolated": spmv_iso,
         "cpu_baseline": cpu,
+        "cpu_baseline_mt": cpu_mt,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

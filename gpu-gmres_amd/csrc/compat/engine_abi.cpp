@@ -116,7 +116,10 @@ struct Ctx {
 };
 constexpr size_t kCacheCap = 8;
 std::mutex g_mu;
-std::vector<std::unique_ptr<Ctx>> g_cache;
+// leaked on purpose: a static vector's destructor would run
+// gg_destroy (stream sync, hipFree) during static destruction, possibly after
+// the HIP runtime has been torn down; the OS reclaims the memory at exit
+std::vector<std::unique_ptr<Ctx>> &g_cache = *new std::vector<std::unique_ptr<Ctx>>;
 unsigned long long g_tick = 0;
 
 unsigned long long host_fingerprint(const void *p, size_t bytes)

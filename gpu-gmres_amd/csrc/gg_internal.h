@@ -209,6 +209,10 @@ Wave2D detect_wave3d(const CanonTri &L, const CanonTri &U);
 // reference anything).  gl / gu: the grid block's triangles (indices - nt, tail
 // terms of L stripped).  ok=false otherwise.
 Wave2D detect_border2d(const CanonTri &L, const CanonTri &U, bool split_u, CanonTri &gl, CanonTri &gu);
+// the split engine's layout choice (gg_set_precond_split, gg_host_split_layout):
+// the 2D wavefront, else the bordered grid, honouring GG_NO_WAVEFRONT=1 (flow
+// kernel for everything) and GG_NO_BORDER=1 (no bordered grid); at most 512 bands
+Wave2D select_split_layout(const CanonTri &L, const CanonTri &U, CanonTri &gl, CanonTri &gu);
 
 // rows with more off-diagonal terms than this are solved by a whole wave in the
 // sync-free triangular solve (kernels.hip k_trsv_flow)

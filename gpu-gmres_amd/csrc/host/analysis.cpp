@@ -329,4 +329,19 @@ std::vector<int> spmv_blocks(const Csr &A, std::vector<int> &long_rows)
     return b;
 }
 
+
+Wave2D select_split_layout(const CanonTri &L, const CanonTri &U, CanonTri &gl, CanonTri &gu)
+{
+    Wave2D w;
+    const char *env = std::getenv("GG_NO_WAVEFRONT");
+    if (env && env[0] == '1') return w;
+    w = detect_wave2d(L, U, true);
+    if (!w.ok) {
+        const char *nb = std::getenv("GG_NO_BORDER");
+        if (!(nb && nb[0] == '1')) w = detect_border2d(L, U, true, gl, gu);
+    }
+    if (w.ok && w.nbands > 512) w.ok = false;
+    return w;
+}
+
 }  // namespace gg

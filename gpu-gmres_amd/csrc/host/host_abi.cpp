@@ -126,13 +126,10 @@ int gg_host_split_layout(int n, const int *l_rp, const int *l_ci, const double *
     try {
         const CanonTri cl = canon_lower_lastdiag(wrap(n, l_rp, l_ci, l_v));
         const CanonTri cu = canon_upper_firstdiag(wrap(n, u_rp, u_ci, u_v));
-        // the solver's choice (solver.hip gg_set_precond_split)
-        Wave2D w = detect_wave2d(cl, cu, true);
-        if (!w.ok) {
-            CanonTri gl, gu;
-            w = detect_border2d(cl, cu, true, gl, gu);
-        }
-        if (w.ok && w.nbands > 512) w.ok = false;
+        // the solver's choice (solver.hip gg_set_precond_split), environment
+        // overrides included
+        CanonTri gl, gu;
+        const Wave2D w = select_split_layout(cl, cu, gl, gu);
         for (int k = 0; k < 9; k++) info[k] = 0;
         if (!w.ok) return 0;
         info[0] = w.bnt ? 5 : 2;

@@ -24,11 +24,51 @@ __device__ __forceinline__ bool gated(const Gate &g)
 }
 
 // ---- reductions -------------------------------------------------------------
+// The xor butterfly v += v[lane ^ o], o = 32, 16, .., 1 (every lane ends with
+// the same sum).  After the steps above o, v depends only on the lane bits
+// below 2o, so any lane that agrees with lane ^ o on the bits below o and
+// differs in bit o holds v[lane ^ o]: in-place v_permlane32 / 16 swaps (o =
+// 32, 16) and DPP row_ror:o within rows of 16 (o = 8 .. 1; adding o mod 16
+// flips bit o and keeps the lower bits).  The same operands in the same order
+// as the ds_bpermute form (__shfl_xor), so the same bits, at VALU latency
+// instead of six LDS round trips.  GG_WAVE_SUM_SHFL=1 keeps __shfl_xor.
+#ifndef GG_WAVE_SUM_SHFL
+#define GG_WAVE_SUM_SHFL 0
+#endif
+__device__ __forceinline__ unsigned perm32_self(unsigned v)
+{
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %0" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ unsigned perm16_self(unsigned v)
+{
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %0" : "+v"(v));
+    return v;
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_sum(double v)
 {
+    if constexpr (GG_WAVE_SUM_SHFL) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        return v;
+    } else {
+        v += __hiloint2double((int)perm32_self((unsigned)__double2hiint(v)),
+                              (int)perm32_self((unsigned)__double2loint(v)));
+        v += __hiloint2double((int)perm16_self((unsigned)__double2hiint(v)),
+                              (int)perm16_self((unsigned)__double2loint(v)));
+        v += dpp64<0x128>(v);       // row_ror:8
+        v += dpp64<0x124>(v);       // row_ror:4
+        v += dpp64<0x122>(v);       // row_ror:2
+        v += dpp64<0x121>(v);       // row_ror:1
+        return v;
+    }
 }
 
 // 256-thread block sum, result broadcast to every thread.
@@ -1033,6 +1073,26 @@ constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 #ifndef GG_WAVE_XCD
 #define GG_WAVE_XCD 8
 #endif
+// Redundant compute waves: GG_WAVE_NC waves (on distinct SIMDs) run the same
+// recurrence on the same operands -- bit-identical values -- and wave c stages
+// only the step pairs kk with kk % NC == c for the writer wave.  A single
+// wave's LDS store path runs at half rate (MI355X_MICROARCH.md LDS table:
+// stores from one wave), so the pair's ds_write_b128 (~26 cycles) sat on the
+// recurrence: C2 trace 44 cycles per step with it, 33 with no staging at all
+// (timing bound, GG_WAVE_NOSTAGE; C2 4,123 -> 4,350 it/s on one box).
+// Measured on one box (round 5, profiles/r05/stage_ab.txt): NC = 1 / 2 / 3 / 4
+// 3,723 / 3,787 / 3,700 / 3,689 it/s (more waves: more LDS reads and a later
+// barrier), so 2.  Not kept: four ds_write_addtid_b32 per pair instead of the
+// b128 (one data dword, no address): 53 cycles per step -- a single wave's
+// addtid stores run at a fraction of their rate.
+#ifndef GG_WAVE_NC
+#define GG_WAVE_NC 2
+#endif
+constexpr int kWaveNC = GG_WAVE_NC;
+// diagnostics only (timing bound, wrong results): no x staging at all
+#ifndef GG_WAVE_NOSTAGE
+#define GG_WAVE_NOSTAGE 0
+#endif
 // the same placement for the forward solve (1: one workgroup per band)
 #ifndef GG_WAVE_XCD_L
 #define GG_WAVE_XCD_L 1
@@ -1060,7 +1120,8 @@ struct WaveCfg {
     static constexpr int RFIT = (150 * 1024 / 16 - 64 - 2 * PBN * 64) / SLOT;
     static constexpr int RVM = 2 + 63 / NPER;
     static constexpr int R = kWaveRing < RFIT ? (kWaveRing < RVM ? kWaveRing : RVM) : (RFIT < RVM ? RFIT : RVM);
-    static constexpr int THREADS = (3 + LOADERS) * 64;                  // compute, boundary, writer, loaders
+    static constexpr int NC = kWaveNC;                                  // redundant compute waves
+    static constexpr int THREADS = (2 + NC + LOADERS) * 64;             // compute(s), boundary, writer, loaders
     static constexpr int LDS2 = R * SLOT + 64 + 2 * PBN * 64;            // ring, boundary, x staging
     static_assert(R >= 3 && (R - 2) * NPER <= 63, "ring depth vs vmcnt range");
     static_assert(B == 8 || B == 16, "batch");
@@ -1275,6 +1336,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // (lanes 0..C::B-1 of each half are used), x staging [2][C::PBN][64]
     __shared__ double2 lds[C::LDS2];
     __shared__ int xdone;                       // batches the compute wave has staged (GG_WAVE_DECOUPLE)
+    double2 *ring = lds;                        // ring | boundary | x staging
     double *bring = reinterpret_cast<double *>(lds + C::R * C::SLOT);
     double2 *xbuf = lds + C::R * C::SLOT + 64;
     if (threadIdx.x == 0) xdone = 0;            // read only after the first barrier
@@ -1311,7 +1373,9 @@ __device__ __forceinline__ void trsv_wave2d_body(
     unsigned long long *pub = bnd + ((long long)kp * nbands + band) * T;
     unsigned long long *prog_mine = D3 ? prog + (long long)kp * nbands + band : nullptr;
     unsigned long long *prog_prev = has_prev ? prog + (long long)(FWD ? kp - 1 : kp + 1) * nbands + band : nullptr;
-    if (wave >= 3) {
+    constexpr int NC = C::NC;                   // waves [0, NC) compute, NC boundary, NC + 1 writer, loaders
+    static_assert(NC >= 1 && NC <= 4 && (NC == 1 || !GG_WAVE_DECOUPLE), "redundant compute waves");
+    if (wave >= NC + 2) {
         // ------------------------------------------------ loader wave(s)
         const double2 *src[7] = {reinterpret_cast<const double2 *>(b) + boff,
                                  reinterpret_cast<const double2 *>(c1) + boff,
@@ -1365,9 +1429,9 @@ __device__ __forceinline__ void trsv_wave2d_body(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         if constexpr (C::LOADERS == 1) {
-            wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN, D3 ? C::A2 + 1 : FS ? 0 : -1>(src, lds, np, nbatch);
+            wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN, D3 ? C::A2 + 1 : FS ? 0 : -1>(src, ring, np, nbatch);
         } else {
-            wave_loader<FWD, C::R, C::SLOT, 1, C::PBN>(src + (wave - 3), lds + (wave - 3) * PB, np, nbatch);
+            wave_loader<FWD, C::R, C::SLOT, 1, C::PBN>(src + (wave - NC - 2), ring + (wave - NC - 2) * PB, np, nbatch);
         }
         if constexpr (FS) {
             const int gpb = T / kFsGroup;
@@ -1376,7 +1440,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
         raw_barrier();                      // final barrier (the writer drains the last batch)
         continue;
     }
-    if (wave == 2) {
+    if (wave == NC + 1) {
         // ------------------------------------------------ writer wave
         // After barrier bi+1 the compute wave's x of batch bi sits in xbuf[bi & 1]:
         // store it to HBM and publish the edge lane's values of the batch as
@@ -1442,7 +1506,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
         }
         continue;
     }
-    if (wave == 1) {
+    if (wave == NC) {
         // ------------------------------------------------ boundary wave
         // Before barrier bi it places batch bi's values in bring[bi & 1].  Step
         // t of this band's edge lane needs the source band's step t -+ 63.  Polls
@@ -1540,9 +1604,10 @@ __device__ __forceinline__ void trsv_wave2d_body(
         continue;
     }
 
-    // ---------------------------------------------------- compute wave
+    // ---------------------------------------------------- compute wave(s)
+    const int cw = wave;                        // this compute wave's share of the staging
     constexpr int ctrl = FWD ? 0x138 : 0x130;   // wave_shr:1 / wave_shl:1
-    long long *tr = TRACE ? trace + (long long)band * (3 * nbatch + 8) : nullptr;
+    long long *tr = TRACE && cw == 0 ? trace + (long long)band * (3 * nbatch + 8) : nullptr;
     long long ph[4] = {0, 0, 0, 0};     // TRACE: barrier wait, top->step0, step0->last, last->end
     long long t_top = 0;
     double xp = 0.0;                        // this lane's previous step value
@@ -1551,6 +1616,13 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // ahead of their use; the boundary values are read first (LDS returns in
     // order and they are needed at the batch's first step).
     double2 rg[C::PBN][C::A];
+    // one step pair's x into staging half h, pair kk (.x = the value at the
+    // lower memory address)
+    auto stage = [&](int h, int kk, double vx, double vy) {
+        if constexpr (!GG_WAVE_NOSTAGE) {
+            if (kk % NC == cw) xbuf[h * PB + kk * 64 + lane] = make_double2(vx, vy);
+        }
+    };
     raw_barrier();                          // barrier 0: batch 0 is in LDS
     for (int bi = 0; bi < nbatch; bi++) {
         if (bi > 0) {
@@ -1566,14 +1638,14 @@ __device__ __forceinline__ void trsv_wave2d_body(
             }
         }
         if constexpr (TRACE) {
-            if (lane == 0) tr[bi] = (long long)__builtin_amdgcn_s_memrealtime();
+            if (lane == 0 && tr) tr[bi] = (long long)__builtin_amdgcn_s_memrealtime();
         }
         const double2 *br = reinterpret_cast<const double2 *>(bring + (bi & 1) * 64);
         // issue order = need order: the first pair's boundary values and
         // operands, then the look-ahead pairs, then the remaining boundary
         // values (LDS returns in order, so the first step waits on ~A+1 reads)
         double2 bv[C::PBN];
-        const double2 *sc = lds + (bi % C::R) * C::SLOT + lane;
+        const double2 *sc = ring + (bi % C::R) * C::SLOT + lane;
         bv[0] = br[0];
 #pragma unroll
         for (int a = 0; a < C::A; a++) rg[0][a] = sc[a * PB];
@@ -1626,9 +1698,8 @@ __device__ __forceinline__ void trsv_wave2d_body(
                         for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
                     }
                     if (h == 1 && kk > 0) {
-                        xbuf[(bi & 1) * PB + (kk - 1) * 64 + lane] =
-                            FWD ? make_double2(xv[2 * kk - 2], xv[2 * kk - 1])
-                                : make_double2(xv[2 * kk - 1], xv[2 * kk - 2]);
+                        if (FWD) stage(bi & 1, kk - 1, xv[2 * kk - 2], xv[2 * kk - 1]);
+                        else stage(bi & 1, kk - 1, xv[2 * kk - 1], xv[2 * kk - 2]);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -1683,9 +1754,10 @@ __device__ __forceinline__ void trsv_wave2d_body(
             // and publishes the edge values), then the pair kWaveLook ahead is
             // read; the scheduling fence keeps it all inside this pair, in the
             // recurrence's latency bubbles
-            if (!SH || kk == C::PBN - 1)
-                xbuf[(bi & 1) * PB + kk * 64 + lane] =
-                    FWD ? make_double2(xv[2 * kk], xv[2 * kk + 1]) : make_double2(xv[2 * kk + 1], xv[2 * kk]);
+            if (!SH || kk == C::PBN - 1) {
+                if (FWD) stage(bi & 1, kk, xv[2 * kk], xv[2 * kk + 1]);
+                else stage(bi & 1, kk, xv[2 * kk + 1], xv[2 * kk]);
+            }
 
             if (!SH && kk + kWaveLook < C::PBN) {
 #pragma unroll
@@ -1701,7 +1773,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
     seq += nbatch;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();                          // final barrier: the writer drains the last batch
-    if (TRACE && lane == 0) {
+    if (TRACE && lane == 0 && tr) {
         tr[nbatch] = (long long)__builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int k = 0; k < 4; k++) tr[nbatch + 1 + k] = ph[k];
@@ -4348,24 +4420,46 @@ int arnoldi_persist_units(int G, long long Ppad)
     return J <= 1 ? 1 : J <= 2 ? 2 : J <= 4 ? 4 : J <= 8 ? 8 : 0;
 }
 
+// the k_arnoldi_persist instantiation for J units per thread under the
+// current GG_MGS_GATHER / GG_MGS_PREFETCH (one choice for the occupancy query
+// and the launch: ADVICE r4)
+using PersistFn = void (*)(Gate, int, int, DevState *, const double *, double *, long long, double *, double *,
+                           double *, double *, double *, unsigned long long *, unsigned long long *, long long, int *,
+                           unsigned long long *, unsigned long long *, unsigned long long, UnitMap, long long *);
+template <int XG, int PF>
+PersistFn persist_fn_j(int J)
+{
+    if constexpr (PF == 2) {
+        return J == 1 ? k_arnoldi_persist<1, XG, PF> : J == 2 ? k_arnoldi_persist<2, XG, PF>
+                                                               : k_arnoldi_persist<4, XG, PF>;
+    } else {
+        return J == 1   ? k_arnoldi_persist<1, XG, PF>
+               : J == 2 ? k_arnoldi_persist<2, XG, PF>
+               : J == 4 ? k_arnoldi_persist<4, XG, PF>
+                        : k_arnoldi_persist<8, XG, PF>;
+    }
+}
+PersistFn persist_fn(int J)
+{
+    const int xg = mgs_gather_form();
+    const int pf = mgs_prefetch();
+    if (xg == 2 && pf == 2 && J <= 4) return persist_fn_j<2, 2>(J);
+    if (xg == 3 && pf) return persist_fn_j<3, 1>(J);
+    if (xg >= 2) return pf ? persist_fn_j<2, 1>(J) : persist_fn_j<2, 0>(J);
+    return pf ? persist_fn_j<0, 1>(J) : persist_fn_j<0, 0>(J);
+}
+
 // blocks of the J-unit instantiation that can be resident at once
 int arnoldi_persist_max_blocks(int J)
 {
     int dev = 0, cus = 0, per = 0;
+    if (J != 1 && J != 2 && J != 4 && J != 8) return 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    auto occ = [&](const void *f) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) == hipSuccess; };
-    // the instantiation launch_arnoldi_persist picks (PF 2 holds v_{k+2} too)
-    const bool pf2 = mgs_gather_form() == 2 && mgs_prefetch() == 2;
-    const bool ok = J == 1   ? occ(pf2 ? reinterpret_cast<const void *>(k_arnoldi_persist<1, 2, 2>)
-                                       : reinterpret_cast<const void *>(k_arnoldi_persist<1, 2, 1>))
-                    : J == 2 ? occ(pf2 ? reinterpret_cast<const void *>(k_arnoldi_persist<2, 2, 2>)
-                                       : reinterpret_cast<const void *>(k_arnoldi_persist<2, 2, 1>))
-                    : J == 4 ? occ(pf2 ? reinterpret_cast<const void *>(k_arnoldi_persist<4, 2, 2>)
-                                       : reinterpret_cast<const void *>(k_arnoldi_persist<4, 2, 1>))
-                    : J == 8 ? occ(reinterpret_cast<const void *>(k_arnoldi_persist<8, 2, 1>))
-                             : false;
-    return ok ? cus * per : 0;
+    // the instantiation launch_arnoldi_persist launches
+    const void *f = reinterpret_cast<const void *>(persist_fn(J));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) != hipSuccess) return 0;
+    return cus * per;
 }
 
 // k_arnoldi_wide: usable when G = kWideG blocks of kWideJR + kWideJL units per
@@ -4421,33 +4515,10 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
     const int J = arnoldi_persist_units(G, Ppad);
     GG_REQUIRE(persist_np(J) == 0 || G <= persist_np(J) * kBlock, GG_EINVAL,
                "k_arnoldi_persist: grid beyond the all-gather's reach");
-    const int xg = mgs_gather_form();
-    const int pf = mgs_prefetch();
-#define GG_PERSIST(JJ, XG, PF)                                                                       \
-    k_arnoldi_persist<JJ, XG, PF><<<G + (XG == 3 ? kXcds : 0), kBlock, persist_test_lds(), st>>>(          \
-        g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2, err, xb, elect, seq, um, trace)
-#define GG_PERSIST_J(XG, PF)                                                                       \
-    do {                                                                                           \
-        if (J == 1) GG_PERSIST(1, XG, PF);                                                         \
-        else if (J == 2) GG_PERSIST(2, XG, PF);                                                    \
-        else if (J == 4) GG_PERSIST(4, XG, PF);                                                    \
-        else GG_PERSIST(8, XG, PF);                                                                \
-    } while (0)
-    if (xg == 2 && pf == 2 && J <= 4) {
-        if (J == 1) GG_PERSIST(1, 2, 2);
-        else if (J == 2) GG_PERSIST(2, 2, 2);
-        else GG_PERSIST(4, 2, 2);
-    } else if (xg == 3 && pf) {
-        GG_PERSIST_J(3, 1);
-    } else if (xg >= 2) {
-        if (pf) GG_PERSIST_J(2, 1);
-        else GG_PERSIST_J(2, 0);
-    } else {
-        if (pf) GG_PERSIST_J(0, 1);
-        else GG_PERSIST_J(0, 0);
-    }
-#undef GG_PERSIST_J
-#undef GG_PERSIST
+    const PersistFn f = persist_fn(J);
+    const int extra = (mgs_gather_form() == 3 && mgs_prefetch()) ? kXcds : 0;   // reducer-only blocks
+    f<<<G + extra, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2,
+                                                     err, xb, elect, seq, um, trace);
 }
 
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,

@@ -423,6 +423,10 @@ void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const 
     }
     // coupling: per row its slot, b read + written; per term column, value, x
     T.cbytes = 24.0 * T.ncoup + 4.0 * (T.ncoup + 1) + 20.0 * cci.size();
+    // the uploads above (ry, tlv.ptr, cs / crp / cci / cv) are asynchronous
+    // copies from these local vectors: they must have been taken before the
+    // vectors go out of scope (as build_level)
+    GG_HIP(hipStreamSynchronize(st));
 }
 
 }  // namespace gg
@@ -1646,17 +1650,8 @@ int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const d
     // branches first (ggmres.matrices.mna_pivot_order) is a bordered grid:
     // the tail by the flow kernel, the mesh by the wavefront (GG_NO_BORDER=1:
     // the flow kernel for everything)
-    Wave2D wl;
     CanonTri gl, gu;
-    const char *env = std::getenv("GG_NO_WAVEFRONT");
-    if (!(env && env[0] == '1')) {
-        wl = detect_wave2d(cl, cu, true);
-        if (!wl.ok) {
-            const char *nb = std::getenv("GG_NO_BORDER");
-            if (!(nb && nb[0] == '1')) wl = detect_border2d(cl, cu, true, gl, gu);
-        }
-        if (wl.ok && wl.nbands > 512) wl.ok = false;
-    }
+    Wave2D wl = select_split_layout(cl, cu, gl, gu);
     setup_space(s, &wl, perm_row, perm_col);
     if (wl.ok && wl.bnt) {
         build_tri_bordered(s->L, cl, gl, wl, s->st);
@@ -2074,9 +2069,16 @@ int gg_device_fingerprint(const void *const *d_p, const unsigned long long *byte
     for (int i = 0; i < count; i++)
         GG_REQUIRE((d_p[i] || bytes[i] == 0) && bytes[i] % 4 == 0, GG_EINVAL, "gg_device_fingerprint: bad buffer");
     if (count == 0) return GG_OK;
-    // kMax accumulators per host thread, never freed (a thread_local destructor
-    // would run after the HIP runtime's own teardown)
-    static thread_local unsigned long long *acc = nullptr;
+    // kMax accumulators per host thread and DEVICE (the kernel runs
+    // on the current device, so its accumulator must live there too), never
+    // freed (a thread_local destructor would run after the HIP runtime's own
+    // teardown)
+    constexpr int kDevs = 64;
+    static thread_local unsigned long long *accs[kDevs] = {};
+    int dev = 0;
+    GG_HIP(hipGetDevice(&dev));
+    GG_REQUIRE(dev >= 0 && dev < kDevs, GG_EINVAL, "gg_device_fingerprint: device index out of range");
+    unsigned long long *&acc = accs[dev];
     if (!acc) GG_HIP(hipMalloc(reinterpret_cast<void **>(&acc), kMax * sizeof(unsigned long long)));
     GG_HIP(hipMemsetAsync(acc, 0, count * sizeof(unsigned long long), nullptr));
     for (int i = 0; i < count; i++) launch_fingerprint(d_p[i], (long long)(bytes[i] / 4), acc + i, nullptr);

@@ -472,6 +472,12 @@ class Solver:
         _check(lib().gg_profile_enable(self.h, mask))
         _check(lib().gg_profile_reset(self.h))
 
+    def profile_select(self, kinds):
+        """Switch the timed families to `kinds` WITHOUT clearing what was
+        accumulated (bench.py rotates one bracketed family per timed solve)."""
+        mask = sum(1 << int(k) for k in set(kinds))
+        _check(lib().gg_profile_enable(self.h, mask))
+
     def profile_get(self, kind):
         """(launches, total_ms) of one kernel family over the profiled solves."""
         n, ms = ctypes.c_int(), ctypes.c_double()

@@ -12,7 +12,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "liboracle.so")
+_LIB_MT = os.path.join(_HERE, "liboracle_mt.so")   # bench.py cpu_baseline_mt only (OpenMP loops)
 _lib = None
+_libs = {}
 
 CSR = namedtuple("CSR", "n rp ci v")
 
@@ -36,51 +38,73 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
-def lib():
+def use_mt(on):
+    """Route the oracle calls to liboracle_mt.so (OpenMP SpMV / BLAS-1 / update
+    loops, serial triangular solves; another reduction order -- a timing
+    baseline, never a checker) or back to the serial checker."""
     global _lib
+    _lib = None
+    _load(_LIB_MT if on else _LIB)
+
+
+def threads():
+    """threads the loaded oracle library runs its loops on (1 = the serial checker)"""
+    return int(lib().orc_threads())
+
+
+def lib():
     if _lib is None:
-        if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(
-                os.path.join(_HERE, "oracle.c")):
-            build()
-        L = ctypes.CDLL(_LIB)
-        L.orc_spmv.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p]
-        L.orc_residual.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
-        for f in (L.orc_ilu0,):
-            f.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p,
-                          _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
-                          _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD)]
-            f.restype = ctypes.c_int
-        L.orc_ilu0_values.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p]
-        L.orc_iluk.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p,
-                               _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
-                               _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD)]
-        L.orc_iluk.restype = ctypes.c_int
-        L.orc_free.argtypes = [ctypes.c_void_p]
-        L.orc_lusolve.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _i32p, _i32p, _f64p,
-                                  _f64p, _f64p]
-        for f in (L.orc_split_left, L.orc_split_right, L.orc_split_start):
-            f.argtypes = [ctypes.POINTER(SplitT), _f64p, _f64p]
-        L.orc_set_dot_order.argtypes = [ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
-                                        ctypes.c_void_p]
-        L.orc_set_dot_order_shards.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-                                               ctypes.c_void_p]
-        L.orc_canon_trsv.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, _f64p,
-                                     _f64p, _f64p]
-        L.orc_sub_seq.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
-        L.orc_gen_rot.argtypes = [ctypes.c_double, ctypes.c_double, _PD, _PD]
-        L.orc_set_div_mode.argtypes = [ctypes.c_int, ctypes.c_int]
-        L.orc_set_fma_tail.argtypes = [ctypes.c_int]
-        L.orc_set_orth.argtypes = [ctypes.c_int]
-        L.orc_apply_rot.argtypes = [_PD, _PD, ctypes.c_double, ctypes.c_double]
-        common = [_f64p, _f64p, ctypes.c_int, _PI, _PD, _f64p, ctypes.c_int, _PI, _PI]
-        L.orc_gmres_left.argtypes = ([ctypes.c_int, _i32p, _i32p, _f64p,
-                                      _i32p, _i32p, _f64p, _i32p, _i32p, _f64p] + common)
-        L.orc_gmres_left.restype = ctypes.c_int
-        L.orc_gmres_split.argtypes = ([ctypes.c_int, _i32p, _i32p, _f64p,
-                                       ctypes.POINTER(SplitT)] + common)
-        L.orc_gmres_split.restype = ctypes.c_int
-        _lib = L
+        _load(_LIB)
     return _lib
+
+
+def _load(path):
+    global _lib
+    if path in _libs:
+        _lib = _libs[path]
+        return
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(
+            os.path.join(_HERE, "oracle.c")):
+        build()
+    L = ctypes.CDLL(path)
+    L.orc_spmv.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p]
+    L.orc_residual.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
+    for f in (L.orc_ilu0,):
+        f.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p,
+                      _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
+                      _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD)]
+        f.restype = ctypes.c_int
+    L.orc_ilu0_values.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p]
+    L.orc_iluk.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p,
+                           _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD),
+                           _i32p, ctypes.POINTER(_PI), ctypes.POINTER(_PD)]
+    L.orc_iluk.restype = ctypes.c_int
+    L.orc_free.argtypes = [ctypes.c_void_p]
+    L.orc_lusolve.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _i32p, _i32p, _f64p,
+                              _f64p, _f64p]
+    for f in (L.orc_split_left, L.orc_split_right, L.orc_split_start):
+        f.argtypes = [ctypes.POINTER(SplitT), _f64p, _f64p]
+    L.orc_set_dot_order.argtypes = [ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
+                                    ctypes.c_void_p]
+    L.orc_set_dot_order_shards.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.c_void_p]
+    L.orc_canon_trsv.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, _f64p,
+                                 _f64p, _f64p]
+    L.orc_sub_seq.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
+    L.orc_gen_rot.argtypes = [ctypes.c_double, ctypes.c_double, _PD, _PD]
+    L.orc_set_div_mode.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.orc_set_fma_tail.argtypes = [ctypes.c_int]
+    L.orc_set_orth.argtypes = [ctypes.c_int]
+    L.orc_apply_rot.argtypes = [_PD, _PD, ctypes.c_double, ctypes.c_double]
+    common = [_f64p, _f64p, ctypes.c_int, _PI, _PD, _f64p, ctypes.c_int, _PI, _PI]
+    L.orc_gmres_left.argtypes = ([ctypes.c_int, _i32p, _i32p, _f64p,
+                                  _i32p, _i32p, _f64p, _i32p, _i32p, _f64p] + common)
+    L.orc_gmres_left.restype = ctypes.c_int
+    L.orc_gmres_split.argtypes = ([ctypes.c_int, _i32p, _i32p, _f64p,
+                                   ctypes.POINTER(SplitT)] + common)
+    L.orc_gmres_split.restype = ctypes.c_int
+    _libs[path] = L
+    _lib = L
 
 
 def csr(A):

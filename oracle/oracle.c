@@ -12,6 +12,22 @@
 #include <string.h>
 
 /* Equal(a, 0) with eps = 1e-9 (src/defs.h:45-47), evaluated with fabs. */
+/* cpu_baseline_mt (bench.py): the same restatement built with -fopenmp
+ * (liboracle_mt.so) runs the SpMV, BLAS-1 and update loops on every host core;
+ * the triangular solves stay serial, as in the reference's host engine.  The
+ * reductions then sum in another order: a timing baseline only, never a checker.
+ * Without -fopenmp (liboracle.so, the checker) these expand to nothing. */
+#ifdef _OPENMP
+#include <omp.h>
+int orc_threads(void) { return omp_get_max_threads(); }
+#define ORC_PAR_FOR _Pragma("omp parallel for schedule(static)")
+#define ORC_PAR_SUM(t) _Pragma("omp parallel for schedule(static) reduction(+:t)")
+#else
+int orc_threads(void) { return 1; }
+#define ORC_PAR_FOR
+#define ORC_PAR_SUM(t)
+#endif
+
 static int is_zero(double a) { return fabs(a) < 1e-9; }
 
 void orc_free(void *p) { free(p); }
@@ -21,6 +37,7 @@ void orc_spmv(int n, const int *rp, const int *ci, const double *v,
               const double *x, double *y)
 {
     /* computeSpMV (src/SpMV_compute.cpp:19-36): serial per-row sum in CSR order */
+    ORC_PAR_FOR
     for (int i = 0; i < n; i++) {
         double t = 0.0;
         for (int j = rp[i]; j < rp[i + 1]; j++) t += v[j] * x[ci[j]];
@@ -34,6 +51,7 @@ void orc_residual(int n, const int *rp, const int *ci, const double *v,
     /* sgemv(v, A, alpha=-1, x, beta=1, y=b) (src/gmres.cu:77-88) */
     double *t = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
     orc_spmv(n, rp, ci, v, x, t);
+    ORC_PAR_FOR
     for (int i = 0; i < n; i++) r[i] = -1.0 * t[i] + 1.0 * b[i];
     free(t);
 }
@@ -572,6 +590,7 @@ static double dot(const double *x, const double *y, int n)
 {
     if (g_blocked) return dot_blocked(x, y);
     double t = 0.0;                 /* dot (src/gmres.cu:68-74) */
+    ORC_PAR_SUM(t)
     for (int i = 0; i < n; i++) t += x[i] * y[i];
     return t;
 }
@@ -579,6 +598,7 @@ static double norm2(const double *v, int n)
 {
     if (g_blocked) return sqrt(dot_blocked(v, v));
     double t = 0.0;                 /* norm2 (src/gmres.cu:60-66) */
+    ORC_PAR_SUM(t)
     for (int i = 0; i < n; i++) t += v[i] * v[i];
     return sqrt(t);
 }
@@ -601,8 +621,10 @@ static void update(double *x, int k, const double *H, int m, const double *s,
         y[i] /= H[i + i * (m + 1)];
         for (int j = i - 1; j >= 0; j--) y[j] -= H[j + i * (m + 1)] * y[i];
     }
-    for (int j = 0; j <= k; j++)
+    for (int j = 0; j <= k; j++) {
+        ORC_PAR_FOR
         for (int i = 0; i < n; i++) x[i] += V[(size_t)j * n + i] * y[j];
+    }
     free(y);
 }
 
@@ -680,6 +702,7 @@ static int gmres_core(const op_t *op, const double *b, double *x, int m,
 
     while (j <= *max_iter) {
         double inv = 1.0 / beta;
+        ORC_PAR_FOR
         for (int t = 0; t < n; t++) V[t] = inv * r[t];
         for (int t = 0; t <= m; t++) s[t] = 0.0;
         s[0] = beta;
@@ -713,6 +736,7 @@ static int gmres_core(const op_t *op, const double *b, double *x, int m,
                     double h = dot(w, vk, n);
                     H[k + i * (m + 1)] = h;
                     double a = -h;
+                    ORC_PAR_FOR
                     for (int t = 0; t < n; t++) w[t] = a * vk[t] + w[t];
                 }
             }
@@ -722,6 +746,7 @@ static int gmres_core(const op_t *op, const double *b, double *x, int m,
             double *vn = V + (size_t)(i + 1) * nn;
             if (hn != 0.0) {
                 double hinv = 1.0 / hn;
+                ORC_PAR_FOR
                 for (int t = 0; t < n; t++) vn[t] = hinv * w[t];
             } else {
                 for (int t = 0; t < n; t++) vn[t] = 0.0;

@@ -50,6 +50,8 @@ int orc_iluk(int lofM, int n, const int *rp, const int *ci, const double *v,
              int *u_rp, int **u_ci, double **u_v);
 
 void orc_free(void *p);
+/* threads the OpenMP build (liboracle_mt.so) runs its loops on; 1 for the checker */
+int orc_threads(void);
 
 /* x = (LU)^-1 y  (LUSolve_ignoreZero, src/SpMV_compute.cpp:92-136) */
 void orc_set_div_mode(int mul_l, int mul_u);

@@ -2,7 +2,7 @@
 (tests/golden/c2_history.npz) from the fp64 oracle restatement (oracle/, test
 infrastructure).
 
-    python tests/golden/make_c2_history.py        # ~4 CPU minutes per run, 2 runs in parallel
+    python tests/golden/make_c2_history.py        # ~4 CPU minutes per run, 3 runs in parallel
 
 C2 of BASELINE.json: 1000 x 1000 5-point Laplacian, ILU(0) left
 (GMRES_leftILU0, src/gmres.cu:566-717; leftILU src/leftILU.cu:27-336),
@@ -12,10 +12,16 @@ solve.  Two runs of the same restatement:
   serial  the reference's arithmetic: serial dot/norm sums (src/gmres.cu:45-74)
           and the reference's row division x = acc / d
           (LUSolve_ignoreZero, src/SpMV_compute.cpp:118-133);
+  tree    the reference's row arithmetic (x = acc / d) with the device's
+          fixed reduction tree (oracle.set_dot_order over the wavefront
+          layout): what the GPU's GG_DIV_EXACT mode must reproduce bit for
+          bit; against "serial" it isolates the summation order's share of
+          the per-entry deviation;
   fma     the device's default arithmetic restated (bench.py's GG_DIV_FMA):
           the device's fixed reduction tree (oracle.set_dot_order over the
           wavefront layout) and the fused rows (oracle.set_div_mode(2, 2)) --
-          the GPU must reproduce this one bit for bit.
+          the GPU must reproduce this one bit for bit; against "tree" it
+          isolates the fused rows' share.
 
 Per run: return code, iteration count, inner index, the full residual history
 (|s[i+1]|/normb per inner iteration, beta/normb per restart), ||x||_2, sum(x),
@@ -45,8 +51,9 @@ def run(mode):
     A = M.laplacian_5pt(NX)
     b = M.rhs_ones(A)
     L, U = O.ilu0(A)
-    if mode == "fma":
+    if mode in ("tree", "fma"):
         O.set_dot_order(*device_layout(A.shape[0], nx=NX))
+    if mode == "fma":
         O.set_div_mode(2, 2)
     try:
         o = O.gmres_left(A, L, U, b, m=RESTART, max_iter=MAX_ITER, tol=TOL)
@@ -64,8 +71,8 @@ def run(mode):
 
 
 def main():
-    with Pool(2) as pool:
-        res = pool.map(run, ["serial", "fma"])
+    with Pool(3) as pool:
+        res = pool.map(run, ["serial", "tree", "fma"])
     out = {f"{mode}/{k}": v for mode, d in res for k, v in d.items()}
     out["config"] = np.array([NX, RESTART, MAX_ITER, X_STRIDE], np.int64)
     out["tol"] = np.array([TOL])

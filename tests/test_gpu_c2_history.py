@@ -21,6 +21,19 @@ src/gmres.cu:566-717):
                       fall eight decades while the rounding of any other
                       summation order stays near the first entries' ulp;
     and the solution within 1e-10 relative (measured 2.7e-14 on the sample).
+
+The same solve in the reference's row arithmetic (gg_set_division(GG_DIV_EXACT):
+x = RN(acc / d), the device's reduction tree) against the fixture's "tree" run
+(the oracle with the device's summation order and the reference's division):
+bit for bit, and the same two bars against "serial".  Where the per-entry
+deviation comes from (tests/golden/make_c2_history.py, all
+three runs 6,699 iterations):
+    tree vs serial  (summation order only)   per-entry 4.43e-9, scale 2.5e-13
+    fma  vs tree    (fused rows only)         per-entry 2.76e-9, scale 9.2e-17
+    fma  vs serial  (both)                    per-entry 2.50e-9, scale 2.5e-13
+so the per-entry figure is the parallel summation order's (the exact division
+alone does not bring it near 1e-10), and the fused rows add nothing at the
+history's scale.
 """
 import os
 
@@ -43,15 +56,14 @@ def fix():
         return {k: z[k] for k in z.files}
 
 
-@pytest.fixture(scope="module")
-def c2_fma(fix):
+def c2_solve(fix, div):
     nx, m, max_iter, stride = (int(v) for v in fix["config"])
     tol = float(fix["tol"][0])
     A = M.laplacian_5pt(nx)
     b = M.rhs_ones(A)
     s = ggmres.Solver(0)
     try:
-        s.set_division(ggmres.DIV_FMA)
+        s.set_division(div)
         s.set_matrix(A)
         s.set_precond_ilu0()
         kernels = (s.trsv_kernel(0), s.trsv_kernel(1))
@@ -62,6 +74,16 @@ def c2_fma(fix):
     g["kernels"] = kernels
     g["stride"] = stride
     return g
+
+
+@pytest.fixture(scope="module")
+def c2_fma(fix):
+    return c2_solve(fix, ggmres.DIV_FMA)
+
+
+@pytest.fixture(scope="module")
+def c2_exact(fix):
+    return c2_solve(fix, ggmres.DIV_EXACT)
 
 
 def test_c2_runs_the_bench_path(c2_fma):
@@ -81,8 +103,7 @@ def test_c2_full_history_bitexact_vs_order_matched_oracle(c2_fma, fix):
     assert abs(np.linalg.norm(x) - fix["fma/x_norm_sum"][0]) <= 1e-14 * fix["fma/x_norm_sum"][0]
 
 
-def test_c2_full_history_tolerance_vs_reference_arithmetic(c2_fma, fix):
-    g = c2_fma
+def check_vs_serial(g, fix, label):
     ret, iters, inner = (int(v) for v in fix["serial/ret_iters_inner"])
     assert (g["ret"], g["iters"], g["inner"]) == (ret, iters, inner)
     h, hs = np.asarray(g["hist"]), fix["serial/hist"]
@@ -90,7 +111,7 @@ def test_c2_full_history_tolerance_vs_reference_arithmetic(c2_fma, fix):
     scale = np.max(np.abs(h - hs)) / np.max(np.abs(hs))
     ok, msg = hist_close(h, hs, ENTRY_RTOL)
     per_entry = np.max(np.abs(h - hs) / np.abs(hs))
-    print(f"C2 full history vs the reference's arithmetic: scale-relative {scale:.3e}, "
+    print(f"C2 full history ({label}) vs the reference's arithmetic: scale-relative {scale:.3e}, "
           f"per-entry max {per_entry:.3e} ({msg}), first 3000 entries "
           f"{np.max(np.abs(h[:3000] - hs[:3000]) / np.abs(hs[:3000])):.3e}")
     assert scale <= SCALE_RTOL
@@ -98,3 +119,26 @@ def test_c2_full_history_tolerance_vs_reference_arithmetic(c2_fma, fix):
     x = np.asarray(g["x"])
     assert rel_err(x[::g["stride"]], fix["serial/x_sample"]) <= SCALE_RTOL
     assert abs(np.linalg.norm(x) - fix["serial/x_norm_sum"][0]) <= SCALE_RTOL * fix["serial/x_norm_sum"][0]
+
+
+def test_c2_full_history_tolerance_vs_reference_arithmetic(c2_fma, fix):
+    check_vs_serial(c2_fma, fix, "GG_DIV_FMA")
+
+
+def test_c2_exact_division_runs_the_reference_rows(c2_exact):
+    assert c2_exact["kernels"][0].startswith("k_trsv_wave2d<true, 0,")     # unit L, no division
+    assert c2_exact["kernels"][1].startswith("k_trsv_wave2d<false, 2,")    # WD_RCP: RN(acc / d) exactly
+    assert c2_exact["mgs_kernel"].startswith("k_arnoldi_persist")
+
+
+def test_c2_exact_division_history_bitexact_vs_tree_order_oracle(c2_exact, fix):
+    g = c2_exact
+    ret, iters, inner = (int(v) for v in fix["tree/ret_iters_inner"])
+    assert (g["ret"], g["iters"], g["inner"]) == (ret, iters, inner) == (0, 6699, 6699)
+    assert np.array_equal(np.asarray(g["hist"]), fix["tree/hist"])
+    x = np.asarray(g["x"])
+    assert np.array_equal(x[::g["stride"]], fix["tree/x_sample"])
+
+
+def test_c2_exact_division_tolerance_vs_reference_arithmetic(c2_exact, fix):
+    check_vs_serial(c2_exact, fix, "GG_DIV_EXACT")
