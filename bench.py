@@ -116,9 +116,12 @@ def parse():
                         "GG_DIV_FMA, default); rcp = x = acc * RN(1/d) on the wavefront solves "
                         "(GG_DIV_RCP); both tolerance parity 1e-10 (tests/test_gpu_fastdiv.py); "
                         "exact = the reference's row arithmetic bit for bit")
-    p.add_argument("--dd-comm", choices=["ipc", "rccl"], default="ipc",
+    p.add_argument("--dd-comm", choices=["ipc", "rccl", "loopback"], default="ipc",
                    help="sharded solve at N > 1: ipc = device-initiated all-gathers through hipIpc-mapped "
-                        "exchange areas over xGMI (GG_DD_IPC, default), rccl = RCCL collectives (GG_DD_RCCL)")
+                        "exchange areas over xGMI (GG_DD_IPC, default), rccl = RCCL collectives (GG_DD_RCCL); "
+                        "loopback (one process, timing only): shard --dd-rank of --dd-parts alone on this GPU, "
+                        "every exchange the in-process all-gather over its own buffer, --max-iter iterations")
+    p.add_argument("--dd-rank", type=int, default=0, help="dd loopback: the shard this process times")
     p.add_argument("--dd-orth", choices=["cgs2", "mgs"], default="cgs2",
                    help="sharded solve: cgs2 = three all-gathers per inner iteration (GG_SOLVE_CGS2, tolerance "
                         "parity; default), mgs = the reference's modified Gram-Schmidt (i + 2 all-gathers)")
@@ -438,6 +441,9 @@ def bench_dd(a, torch, dist, world, rank, local):
         if ranks != world or myrank != rank:
             raise SystemExit(f"bench.py: RCCL communicator has {ranks} ranks (rank {myrank}), "
                              f"expected {world} (rank {rank})")
+    elif world == 1 and comm == "loopback":
+        d = DD(a.dd_parts, device=local, rank=a.dd_rank, comm="loopback")
+        ranks = 1
     elif world == 1:
         d = DD(a.dd_parts, device=local)
         ranks = 1
@@ -453,11 +459,15 @@ def bench_dd(a, torch, dist, world, rank, local):
 
     flags = ggmres.SOLVE_CGS2 if a.dd_orth == "cgs2" else 0
 
+    loop = comm == "loopback"
+    # loopback: a fixed iteration count (the values are not the system's)
+    tol = 1e-300 if loop else a.tol
+
     def step():
         dx.zero_()
         torch.cuda.synchronize()
         return d.solve_device(db.data_ptr(), dx.data_ptr(), restart=a.restart,
-                              max_iter=a.max_iter, tol=a.tol, flags=flags)
+                              max_iter=a.max_iter, tol=tol, flags=flags)
 
     def barrier():
         torch.cuda.synchronize()
@@ -466,6 +476,10 @@ def bench_dd(a, torch, dist, world, rank, local):
         torch.cuda.synchronize()
 
     from ggmres import dd as DDM
+
+    # shards whose launches one event bracket covers: every shard of a local
+    # (in-process) run, one per rank otherwise
+    per_bracket = a.dd_parts if (world == 1 and not loop) else 1
 
     def families(inner_run, el):
         """this rank's per-family event timing (every inner iteration's families
@@ -476,6 +490,8 @@ def bench_dd(a, torch, dist, world, rank, local):
             if cnt == 0:
                 continue
             fam[name] = {"launches": cnt, "avg_us": round(ms * 1e3 / cnt, 3),
+                         "shards_per_launch": per_bracket,
+                         "avg_us_per_shard": round(ms * 1e3 / cnt / per_bracket, 3),
                          "share_of_step": round(ms / (el * 1e3), 4)}
             if k in (DDM.PROF_SPMV, DDM.PROF_TRSV_L, DDM.PROF_TRSV_U):
                 byt = d.bytes(k)
@@ -527,8 +543,11 @@ def bench_dd(a, torch, dist, world, rank, local):
         roof = {"kernel": kname[dom], "bound": "hbm", "achieved": f["achieved_gbs"], "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
+                "avg_us_per_shard": f["avg_us_per_shard"], "shards_per_launch": per_bracket,
                 "launches_timed": f["launches"], "rank": rank,
-                "note": "per rank (its own shard), event-timed inside the timed region on the solver's stream"}
+                "note": ("event-timed inside the timed region on the solver's stream; one bracket covers "
+                         + ("every local shard (bytes and time of all of them: the rate is theirs together)"
+                            if per_bracket > 1 else "this rank's own shard"))}
     # every rank's breakdown next to the exchange latency (rank 0 prints them)
     per_rank = [{"rank": rank, "kernels": fam}]
     if dist:
@@ -538,12 +557,15 @@ def bench_dd(a, torch, dist, world, rank, local):
     parts = world if world > 1 else a.dd_parts
     # the exchange every sharded operator and dot pays, timed after the timed
     # region: one dot's G partials, and CGS2's (i+1) G at i = 15
-    info_g = d.dot_layout(rank if world > 1 else 0)[1]
+    info_g = d.dot_layout(rank if world > 1 else a.dd_rank if loop else 0)[1]
     xch = {f"{c}_doubles_us": round(d.time_exchange(c, reps=200), 2) for c in (info_g, 16 * info_g)}
     out = {
         "metric": METRIC, "value": round(inner / el_max, 3), "unit": "iterations/s",
         "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(el_max * 1e3 / a.steps, 3), "higher_is_better": True,
+        # one step = one solve: the time to solution next to the rate (the
+        # sharded preconditioner converges in its own iteration count)
+        "ms_per_solve": round(el_max * 1e3 / a.steps, 3), "iters_per_solve": res[0]["inner"],
         "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": (f"sharded solve: {'C4 %d^3 7-pt' % a.c4_grid if a.dd_grid == 'c4' else 'C2 %dx%d 5-pt' % (a.grid, a.grid)}"
                                 f", {parts}-way partition4 ({'px x py grid rectangles' if a.dd_part == 'grid' else 'contiguous slabs'}) arrow ordering"
@@ -555,7 +577,9 @@ def bench_dd(a, torch, dist, world, rank, local):
                                 "(GG_DD_IPC)" if comm == "ipc" else
                                 "RCCL all-gather over xGMI" + (" (IPC unavailable: fallback)"
                                                                if a.dd_comm == "ipc" else ""))
-                               if world > 1 else f"in-process ({parts} shards on one GPU)",
+                               if world > 1 else ("loopback: the in-process all-gather kernel over this "
+                                                  "shard's own buffer (timing only)") if loop
+                               else f"in-process ({parts} shards on one GPU)",
                    "exchange_ranks": ranks if world > 1 else None,
                    "exchange_latency": xch,
                    "division": dd_div,
@@ -570,7 +594,9 @@ def bench_dd(a, torch, dist, world, rank, local):
                    "separator_step": {0: "level launches", 1: "fused dataflow launch (k_sep_flow)",
                                       2: "2D wavefront", 3: "3D tile wavefront"}.get(info["wave_separator"]),
                    "iters_per_solve": res[0]["inner"], "relres": res[0]["relres"],
-                   "parallelism": f"dd{parts}", "setup_s": round(t_setup, 3)},
+                   "parallelism": (f"rank {a.dd_rank} of dd{parts} alone (loopback exchanges, timing only: "
+                                   f"{a.max_iter} iterations, values not the system's)") if loop else f"dd{parts}",
+                   "setup_s": round(t_setup, 3)},
         "roofline": roof,
         "kernels_per_rank": per_rank,
         "kernels_from": "one profiled warmup step per rank, every family bracketed by hipEvents",

@@ -211,6 +211,12 @@ void exchange(gg_dd *d, const Get &buf, long long off, long long cnt, hipStream_
         GG_NCCL(ncclAllGather(b + (long long)s.p * cnt, b, (size_t)cnt, ncclDouble, d->comm, st));
     } else if (d->kind == GG_DD_IPC) {
         ipc_allgather(d, buf(*d->sh[0]) + off, cnt, st);
+    } else if (d->kind == GG_DD_LOOPBACK) {
+        // the one shard's buffer as every shard's: the all-gather kernel's
+        // traffic and launch, no peer values (timing only)
+        ShardPtrs ptr{};
+        for (int q = 0; q < d->P; q++) ptr.p[q] = buf(*d->sh[0]);
+        launch_allgather_local(ptr, d->P, off, cnt, st);
     } else {
         ShardPtrs ptr{};
         for (int q = 0; q < d->P; q++) ptr.p[q] = buf(*d->sh[q]);
@@ -905,8 +911,10 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
     GG_API_BEGIN
     GG_REQUIRE(out, GG_EINVAL, "null out");
     GG_REQUIRE(nparts >= 1 && nparts <= kMaxShards, GG_EINVAL, "dd: nparts must be in [1, 16]");
-    GG_REQUIRE(comm == GG_DD_LOCAL || comm == GG_DD_RCCL || comm == GG_DD_IPC, GG_EINVAL,
-               "dd: unknown communicator");
+    GG_REQUIRE(comm == GG_DD_LOCAL || comm == GG_DD_RCCL || comm == GG_DD_IPC || comm == GG_DD_LOOPBACK,
+               GG_EINVAL, "dd: unknown communicator");
+    GG_REQUIRE(comm != GG_DD_LOOPBACK || (rank >= 0 && rank < nparts), GG_EINVAL,
+               "dd: loopback needs 0 <= rank < nparts");
     GG_REQUIRE(comm != GG_DD_RCCL || (id && rank >= 0 && rank < nparts), GG_EINVAL,
                "dd: RCCL needs an id and 0 <= rank < nparts");
     GG_REQUIRE(comm != GG_DD_IPC || (rank >= 0 && rank < nparts), GG_EINVAL,

@@ -128,6 +128,17 @@ struct Levels {
 // ext_cols: columns >= n (an upper tail's references into the bordered grid,
 // solved before it) are ignored rather than rejected
 Levels level_sets(const CanonTri &T, bool ext_cols = false);
+// Reverse Cuthill-McKee order of the symmetric pattern of the two triangles
+// (order[k] = the row placed at slot k): the layout of the flow-kernel path
+// (gg_set_precond_split off the wavefront), so that the rows of a level task
+// and their terms' x sit close together in memory.  Deterministic: BFS from a
+// pseudo-peripheral node of each component (lowest degree, then index),
+// neighbours by (degree, index).
+std::vector<int> rcm_order(const CanonTri &L, const CanonTri &U);
+// T in the layout space of nat2lay (a permutation of the rows): row p = row
+// nat(p) with its columns mapped, term order kept; levels from the natural
+// triangle, each level's rows in ascending slot order
+void relabel_tri(const CanonTri &C, const std::vector<long long> &nat2lay, CanonTri &out, Levels &lv);
 
 // 2D structured-grid wavefront layout (SURVEY.md 7 hard parts)
 //   natural row r = j*nx + i, band = j/64, lane l = j%64, step t = i + l:

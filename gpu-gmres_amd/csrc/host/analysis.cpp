@@ -344,4 +344,112 @@ Wave2D select_split_layout(const CanonTri &L, const CanonTri &U, CanonTri &gl, C
     return w;
 }
 
+
+std::vector<int> rcm_order(const CanonTri &L, const CanonTri &U)
+{
+    const int n = L.off.n;
+    // symmetric adjacency of L + U (off-diagonal terms only)
+    std::vector<int> deg(n, 0);
+    auto each = [&](auto &&f) {
+        for (const CanonTri *T : {&L, &U})
+            for (int r = 0; r < n; r++)
+                for (int k = T->off.rp[r]; k < T->off.rp[r + 1]; k++) {
+                    const int c = T->off.ci[k];
+                    if (c >= 0 && c < n && c != r) f(r, c);
+                }
+    };
+    each([&](int r, int c) {
+        deg[r]++;
+        deg[c]++;
+    });
+    std::vector<long long> ap(n + 1, 0);
+    for (int r = 0; r < n; r++) ap[r + 1] = ap[r] + deg[r];
+    std::vector<int> adj(ap[n]);
+    std::vector<long long> fill(ap.begin(), ap.end() - 1);
+    each([&](int r, int c) {
+        adj[fill[r]++] = c;
+        adj[fill[c]++] = r;
+    });
+    // neighbours sorted by (degree, index), duplicates dropped
+    std::vector<int> ndeg(n);
+    for (int r = 0; r < n; r++) {
+        auto b = adj.begin() + ap[r], e = adj.begin() + ap[r + 1];
+        std::sort(b, e);
+        e = std::unique(b, e);
+        ndeg[r] = (int)(e - b);
+        std::sort(b, e, [&](int a, int c) { return deg[a] != deg[c] ? deg[a] < deg[c] : a < c; });
+    }
+    std::vector<int> order;
+    order.reserve(n);
+    std::vector<char> seen(n, 0);
+    std::vector<int> lvl(n, -1);
+    auto bfs = [&](int root, std::vector<int> &out) {     // one component from root
+        size_t h = out.size();
+        out.push_back(root);
+        seen[root] = 1;
+        while (h < out.size()) {
+            const int r = out[h++];
+            for (long long k = ap[r]; k < ap[r] + ndeg[r]; k++) {
+                const int c = adj[k];
+                if (!seen[c]) {
+                    seen[c] = 1;
+                    out.push_back(c);
+                }
+            }
+        }
+    };
+    // components in order of their lowest-(degree, index) node
+    std::vector<int> byd(n);
+    for (int r = 0; r < n; r++) byd[r] = r;
+    std::sort(byd.begin(), byd.end(), [&](int a, int c) { return ndeg[a] != ndeg[c] ? ndeg[a] < ndeg[c] : a < c; });
+    std::vector<int> comp;
+    for (int start : byd) {
+        if (seen[start]) continue;
+        // pseudo-peripheral root: two BFS sweeps, the last node of the first
+        // (lowest degree in its last level) starts the second
+        comp.clear();
+        bfs(start, comp);
+        int root = comp.back();
+        for (int c : comp) seen[c] = 0;
+        comp.clear();
+        bfs(root, comp);
+        order.insert(order.end(), comp.begin(), comp.end());
+    }
+    std::reverse(order.begin(), order.end());
+    return order;
+}
+
+void relabel_tri(const CanonTri &C, const std::vector<long long> &nat2lay, CanonTri &out, Levels &lv)
+{
+    const int n = C.off.n;
+    std::vector<int> l2n(n, -1);
+    for (int r = 0; r < n; r++) l2n[nat2lay[r]] = r;
+    out.lower = C.lower;
+    out.off.n = n;
+    out.off.rp.assign(n + 1, 0);
+    out.d.assign(n, 1.0);
+    for (int p = 0; p < n; p++) {
+        const int r = l2n[p];
+        out.off.rp[p + 1] = out.off.rp[p] + (C.off.rp[r + 1] - C.off.rp[r]);
+        out.d[p] = C.d[r];
+    }
+    out.off.ci.resize(C.off.ci.size());
+    out.off.v.resize(C.off.v.size());
+    for (int p = 0; p < n; p++) {
+        const int r = l2n[p];
+        int o = out.off.rp[p];
+        for (int k = C.off.rp[r]; k < C.off.rp[r + 1]; k++, o++) {
+            out.off.ci[o] = (int)nat2lay[C.off.ci[k]];
+            out.off.v[o] = C.off.v[k];
+        }
+    }
+    const Levels nl = level_sets(C);
+    lv.ptr = nl.ptr;
+    lv.rows.resize(n);
+    for (size_t l = 0; l + 1 < nl.ptr.size(); l++) {
+        for (int q = nl.ptr[l]; q < nl.ptr[l + 1]; q++) lv.rows[q] = (int)nat2lay[nl.rows[q]];
+        std::sort(lv.rows.begin() + nl.ptr[l], lv.rows.begin() + nl.ptr[l + 1]);
+    }
+}
+
 }  // namespace gg

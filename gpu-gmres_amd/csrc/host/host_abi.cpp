@@ -131,7 +131,16 @@ int gg_host_split_layout(int n, const int *l_rp, const int *l_ci, const double *
         CanonTri gl, gu;
         const Wave2D w = select_split_layout(cl, cu, gl, gu);
         for (int k = 0; k < 9; k++) info[k] = 0;
-        if (!w.ok) return 0;
+        if (!w.ok) {
+            // the flow path: an RCM layout (GG_FLOW_RCM=0: natural, as the solver)
+            const char *fr = std::getenv("GG_FLOW_RCM");
+            if (fr && fr[0] == '0') return 0;
+            const std::vector<int> order = rcm_order(cl, cu);
+            info[0] = 6;
+            if (slot)
+                for (int k = 0; k < n; k++) slot[order[k]] = k;
+            return 1;
+        }
         info[0] = w.bnt ? 5 : 2;
         info[1] = w.nx;
         info[2] = w.ny;

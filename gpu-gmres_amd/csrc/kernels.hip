@@ -1084,7 +1084,12 @@ constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 // 3,723 / 3,787 / 3,700 / 3,689 it/s (more waves: more LDS reads and a later
 // barrier), so 2.  Not kept: four ds_write_addtid_b32 per pair instead of the
 // b128 (one data dword, no address): 53 cycles per step -- a single wave's
-// addtid stores run at a fraction of their rate.
+// addtid stores run at a fraction of their rate.  Nor (round 5, C2 one box,
+// profiles/r05/stage_ab.txt): the compute waves storing x themselves (one
+// global_store_dwordx4 per pair) and handing only the edge lane's batch to the
+// writer through LDS: 3,408 / 3,440 it/s (NC 2 / 1) against 3,773 -- stores
+// from one active lane cost the store path what full ones do (8 b128 at the
+// batch end: 551 cycles to the barrier).
 #ifndef GG_WAVE_NC
 #define GG_WAVE_NC 2
 #endif
@@ -3074,6 +3079,10 @@ __device__ __forceinline__ unsigned long long poll_granule(const unsigned long l
 // one memory round trip for the row instead of one per granule (a poll loop
 // per granule serializes them: G = 544 put three sc1 round trips on every
 // all-gather).  The sum is taken afterwards in q order, as before: same bits.
+// Measured and not kept (round 5, profiles/r05/stage_ab.txt): two poll rounds
+// in flight (a second load of every pending granule half a round trip after
+// the first, here and in the blocks' slot poll): MGS 59.7 -> 75 us -- the
+// extra polls slow the hand-offs more than they shorten the detection.
 constexpr int kGatherPer = 4;
 template <int NP>
 __device__ __forceinline__ bool gather_row(const unsigned long long *row, int G, unsigned long long (&a)[NP],

@@ -136,6 +136,13 @@ std::vector<int> tile_order(const Wave2D &w)
 // grid layout is active, else LEVEL (one launch per dependency level).
 void build_level(DevTri &T, const CanonTri &C, const Levels &lv, hipStream_t st, bool no_long = false);
 
+bool identity_map(const std::vector<long long> &m, int n)
+{
+    for (int r = 0; r < n; r++)
+        if (m[r] != r) return false;
+    return true;
+}
+
 void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector<long long> *nat2lay,
                long long Ppad, hipStream_t st)
 {
@@ -234,6 +241,12 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         // algorithmic bytes: b, two coefficients, (divisor (, reciprocal)), x per grid point
         T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
         T.bytes_mul = (double)n * (8.0 * ((unit ? 4 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
+    } else if (nat2lay && !identity_map(*nat2lay, n)) {
+        // a relabeled (RCM) layout: the triangle in layout space
+        CanonTri Cr;
+        Levels lv;
+        relabel_tri(C, *nat2lay, Cr, lv);
+        build_level(T, Cr, lv, st);
     } else {
         build_level(T, C, level_sets(C), st);
     }
@@ -444,6 +457,7 @@ struct gg_solver {
 
     // vector space (natural or wavefront layout)
     bool wave = false;
+    bool relabeled = false;   // off the wavefront, an RCM layout (setup_space)
     Wave2D wl;
     long long P = 0, Ppad = 0;
     std::vector<long long> nat2lay_h;
@@ -558,7 +572,10 @@ void set_device(gg_solver *s) { GG_HIP(hipSetDevice(s->device)); }
 // choose the vector space and upload A in it
 // The solver's vector space.  prow / pcol (split engine): A' has row lay(j) =
 // A row prow[j] and column c -> lay(pcol[c]); null: A in layout space.
-void setup_space(gg_solver *s, const Wave2D *wl, const int *prow = nullptr, const int *pcol = nullptr)
+// order (off the wavefront): the layout places row order[k] at slot k (RCM,
+// gg_set_precond_split); natural when null
+void setup_space(gg_solver *s, const Wave2D *wl, const int *prow = nullptr, const int *pcol = nullptr,
+                 const std::vector<int> *order = nullptr)
 {
     const int n = s->A.n;
     s->wave = wl && wl->ok;
@@ -572,11 +589,16 @@ void setup_space(gg_solver *s, const Wave2D *wl, const int *prow = nullptr, cons
     s->Ppad = round_up(std::max<long long>(s->P, 1), 512);
     s->nat2lay_h.resize(n);
     std::vector<long long> l2n(s->Ppad, -1);
+    if (!s->wave && order) {
+        GG_REQUIRE((int)order->size() == n, GG_EINVAL, "layout order: wrong length");
+        for (int k = 0; k < n; k++) s->nat2lay_h[(*order)[k]] = k;
+    }
     for (int r = 0; r < n; r++) {
-        long long p = s->wave ? wl->slot(r) : r;
+        long long p = s->wave ? wl->slot(r) : order ? s->nat2lay_h[r] : r;
         s->nat2lay_h[r] = p;
         l2n[p] = r;
     }
+    s->relabeled = !s->wave && order;
     s->lay2nat.upload(l2n, s->st);
     s->nat2lay.upload(s->nat2lay_h, s->st);
     s->G = reduce_grid(s->Ppad / 2);
@@ -584,7 +606,7 @@ void setup_space(gg_solver *s, const Wave2D *wl, const int *prow = nullptr, cons
     if (wf && wf[0] == '1') s->G = kWideG;
     // A in layout space: row p = A row nat(p) (split: prow[nat(p)]), columns
     // remapped (split: through pcol), entry order kept
-    if (!s->wave && !prow) {
+    if (!s->wave && !prow && !order) {
         Csr Ap = s->A;
         Ap.n = (int)s->P;
         s->dA.upload(Ap, s->st);
@@ -1652,7 +1674,14 @@ int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const d
     // the flow kernel for everything)
     CanonTri gl, gu;
     Wave2D wl = select_split_layout(cl, cu, gl, gu);
-    setup_space(s, &wl, perm_row, perm_col);
+    // off the wavefront the flow kernel's rows and their terms' x sit where an
+    // RCM order of the factors' pattern puts them (a randomly permuted split
+    // has no locality in its own index order); GG_FLOW_RCM=0 keeps the natural
+    // layout.  The rows' terms keep their order: the same arithmetic.
+    std::vector<int> rcm;
+    const char *fr = std::getenv("GG_FLOW_RCM");
+    if (!wl.ok && !(fr && fr[0] == '0')) rcm = rcm_order(cl, cu);
+    setup_space(s, &wl, perm_row, perm_col, rcm.empty() ? nullptr : &rcm);
     if (wl.ok && wl.bnt) {
         build_tri_bordered(s->L, cl, gl, wl, s->st);
         build_tri_bordered(s->U, cu, gu, wl, s->st);
@@ -1730,6 +1759,17 @@ int gg_set_precond_user(gg_solver *s, int split, gg_precond_fn fn, void *ctx)
 
 int gg_precond_kind(gg_solver *s) { return s ? s->pkind : GG_EINVAL; }
 int gg_uses_wavefront(gg_solver *s) { return (s && s->wave) ? 1 : 0; }
+
+long long gg_layout(gg_solver *s, long long *lay2nat, long long cap)
+{
+    if (!s || s->pkind < 0) return GG_ESTATE;
+    if (lay2nat && cap > 0) {
+        std::fill(lay2nat, lay2nat + std::min(cap, s->Ppad), -1LL);
+        for (size_t r = 0; r < s->nat2lay_h.size(); r++)
+            if (s->nat2lay_h[r] < cap) lay2nat[s->nat2lay_h[r]] = (long long)r;
+    }
+    return s->Ppad;
+}
 int gg_set_division(gg_solver *s, int mode)
 {
     if (!s) return GG_EINVAL;

@@ -33,7 +33,7 @@ EXPORTS = [
     "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced",
     "gg_transient_mna", "gg_set_division", "gg_division_active",
     "gg_trsv_kernel", "gg_mgs_kernel", "gg_set_precond_user", "gg_solve_device_f32",
-    "gg_device_fingerprint", "gg_set_matrix_count", "gg_trsv_levels",
+    "gg_device_fingerprint", "gg_set_matrix_count", "gg_trsv_levels", "gg_layout",
 ]
 # gg_precond_fn: int (*)(void *ctx, int op, const float *in, float *out, int n), device arrays
 PRECOND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -129,6 +129,8 @@ def lib():
         L.gg_bytes_trsv.argtypes = [_VP, ctypes.c_int]
         L.gg_bytes_trsv.restype = ctypes.c_double
         L.gg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.gg_layout.argtypes = [_VP, ctypes.c_void_p, ctypes.c_longlong]
+        L.gg_layout.restype = ctypes.c_longlong
         L.gg_profile_enable.argtypes = [_VP, ctypes.c_int]
         L.gg_profile_reset.argtypes = [_VP]
         L.gg_profile_get.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
@@ -471,6 +473,19 @@ class Solver:
             mask = (1 << PROF_NKINDS) - 1 if kinds is None else sum(1 << int(k) for k in set(kinds))
         _check(lib().gg_profile_enable(self.h, mask))
         _check(lib().gg_profile_reset(self.h))
+
+    def layout(self):
+        """(lay2nat, G): the natural row at each slot of the solver's vector space
+        (-1 = padding) and the reduction grid of its dots -- the order the
+        order-matched oracle needs (oracle.set_dot_order)."""
+        P = int(lib().gg_layout(self.h, None, 0))
+        if P < 0:
+            _check(P)
+        out = np.empty(P, np.int64)
+        lib().gg_layout(self.h, out.ctypes.data, P)
+        units = P // 2          # kernels.hip reduce_grid (tests/helpers.py device_layout)
+        G = 512 if units > 1024 * 256 * 8 else min(1024, max(1, (units + 1023) // 1024))
+        return out, G
 
     def profile_select(self, kinds):
         """Switch the timed families to `kinds` WITHOUT clearing what was

@@ -7,6 +7,9 @@ DD(nparts, rank=r, comm="ipc", device=d) one shard per process, device-initiated
                                         exchanges through hipIpc-mapped areas; then
                                         d.connect_ipc(allgather) with any host
                                         all-gather of bytes (e.g. torch.distributed)
+DD(nparts, rank=r, comm="loopback")     timing only: shard r alone, every exchange the
+                                        in-process all-gather over its own buffer (run a
+                                        fixed iteration count: the values are not the system's)
 """
 import ctypes
 
@@ -14,7 +17,7 @@ import numpy as np
 
 from . import Options, Result, _check, _csr_arrays, lib
 
-LOCAL, RCCL, IPC = 0, 1, 2
+LOCAL, RCCL, IPC, LOOPBACK = 0, 1, 2, 3
 ID_BYTES = 128
 IPC_HANDLE_BYTES = 64
 _VP = ctypes.c_void_p
@@ -76,9 +79,9 @@ def unique_id():
 class DD:
     def __init__(self, nparts, device=0, rank=None, uid=None, comm=None):
         h = _VP()
-        kind = IPC if comm == "ipc" else LOCAL if rank is None else RCCL
-        if kind == IPC and rank is None:
-            raise ValueError("dd: comm='ipc' needs a rank")
+        kind = IPC if comm == "ipc" else LOOPBACK if comm == "loopback" else LOCAL if rank is None else RCCL
+        if kind in (IPC, LOOPBACK) and rank is None:
+            raise ValueError(f"dd: comm={comm!r} needs a rank")
         _check(_lib().gg_dd_create(int(device), int(nparts), kind, int(rank or 0),
                                    uid if uid is not None else None, ctypes.byref(h)))
         self.h, self.P, self.kind, self.rank = h, nparts, kind, rank

@@ -219,6 +219,13 @@ int gg_mgs_kernel(gg_solver *s, char *name, int cap);
 int gg_trsv_levels(gg_solver *s, int which);
 /* 1 if the structured-grid wavefront triangular solve is active, else 0 */
 int gg_uses_wavefront(gg_solver *s);
+/* The solver's vector space, fixed by gg_set_precond_*: lay2nat[p] = the
+ * natural row held at slot p (-1 = padding) for p < min(cap, Ppad); returns
+ * Ppad (negative: error).  The 2D / 3D wavefront layouts, or off the
+ * wavefront the natural order -- or, for the split engine's flow-kernel path,
+ * an RCM order of the factors (GG_FLOW_RCM=0: natural).  Every reduction runs
+ * in this order (tests: the order-matched oracle). */
+long long gg_layout(gg_solver *s, long long *lay2nat, long long cap);
 /* the SpMV kernel the solver's matrix takes: 1 sliced ELL (k_spmv_sell: short,
  * evenly filled rows), 0 CSR-stream (k_spmv_stream) */
 int gg_spmv_sliced(gg_solver *s);

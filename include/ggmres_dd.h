@@ -58,7 +58,13 @@ extern "C" {
 enum gg_dd_comm {
     GG_DD_LOCAL = 0,
     GG_DD_RCCL = 1,
-    GG_DD_IPC = 2
+    GG_DD_IPC = 2,
+    /* timing only: ONE process holds shard `rank` of nparts and every exchange
+     * is the in-process all-gather kernel over its own buffer (the other
+     * shards' slots keep stale values) -- the per-rank kernel and exchange-launch
+     * time of a one-shard-per-GPU run on this device alone.  The solve's values
+     * are NOT the system's: run it for a fixed iteration count. */
+    GG_DD_LOOPBACK = 3
 };
 
 typedef struct gg_dd gg_dd;

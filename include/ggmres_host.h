@@ -97,9 +97,11 @@ int gg_host_wave_layout(int n, const int *l_row_ptr, const int *l_col_idx, const
  * src/preconditioner.cu:1094-1137): info[0] = 2 (2D bands) or 5 (bordered
  * grid: the first info[6] rows -- an MNA system's pads and voltage-source
  * branches -- at slots [0, info[6]), the grid rows at info[7] + their 2D
- * slot), info[1..5] = nx, ny, nz, bands, T.  0 when the layout is natural.
- * The solver's environment overrides apply here too (GG_NO_WAVEFRONT=1: natural;
- * GG_NO_BORDER=1: no bordered grid). */
+ * slot), info[1..5] = nx, ny, nz, bands, T) or 6 (off the wavefront: the flow
+ * kernel's RCM layout, slot[r] = r's position in a reverse Cuthill-McKee order
+ * of the factors' pattern).  0 when the layout is natural (GG_FLOW_RCM=0).
+ * The solver's environment overrides apply here too (GG_NO_WAVEFRONT=1: no
+ * wavefront; GG_NO_BORDER=1: no bordered grid). */
 int gg_host_split_layout(int n, const int *l_row_ptr, const int *l_col_idx, const double *l_val,
                          const int *u_row_ptr, const int *u_col_idx, const double *u_val,
                          long long *slot, int *info);

@@ -331,13 +331,24 @@ def test_split_layout_bordered_netlist(ggmres_lib, tmp_path, grid, stride):
     assert np.array_equal(lay2nat[slot], np.arange(n))
 
 
-def test_split_layout_plain_and_natural(ggmres_lib):
+def test_split_layout_plain_and_rcm(ggmres_lib, monkeypatch):
     """grid-shaped split factors: the plain 2D layout; a random symmetric
-    permutation of the grid: natural order"""
+    permutation of the grid: the flow path's RCM layout -- a permutation whose
+    bandwidth is back near the grid's line length -- or, with GG_FLOW_RCM=0,
+    natural order"""
     from helpers import make_split
     A = M.laplacian_5pt(48, 40)
     P = make_split(A, seed=9, identity_perm=True)
     ok, slot, info = split_layout(ggmres_lib, P.L, P.U)
     assert ok == 1 and info[0] == 2 and info[6] == 0 and tuple(info[1:3]) == (48, 40)
     P = make_split(A, seed=9)
+    ok, slot, info = split_layout(ggmres_lib, P.L, P.U)
+    n = A.shape[0]
+    assert ok == 1 and info[0] == 6 and np.array_equal(np.sort(slot), np.arange(n))
+    # bandwidth of L + U in the relabeled order vs in the random order
+    rows = np.repeat(np.arange(n), np.diff(P.L.rp))
+    bw_rand = np.max(np.abs(rows - P.L.ci))
+    bw_rcm = np.max(np.abs(slot[rows] - slot[P.L.ci]))
+    assert bw_rcm <= 3 * 48 < bw_rand
+    monkeypatch.setenv("GG_FLOW_RCM", "0")
     assert split_layout(ggmres_lib, P.L, P.U)[0] == 0

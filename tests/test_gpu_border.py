@@ -182,6 +182,7 @@ def test_no_border_flow_kernel_same_bits(systems, monkeypatch):
     finally:
         O.set_dot_order(None)
     monkeypatch.setenv("GG_NO_BORDER", "1")
+    monkeypatch.setenv("GG_FLOW_RCM", "0")          # the natural layout (the RCM one: test_gpu_parity)
     s = split_solver(A, P)
     try:
         assert not s.uses_wavefront and s.trsv_kernel(0) == "k_trsv_flow"

@@ -23,6 +23,8 @@ import struct
 import subprocess
 
 import numpy as np
+
+import ggmres
 import pytest
 import scipy.sparse as sp
 
@@ -90,7 +92,15 @@ def test_pg_classes_solve_sequence(tmp_path, mode):
     # GMRES_dev_PG / gmresInterfacePG::GMRES_host_PG: max_it 10000 (written back);
     # gmresInterfacePGfloat::GMRES_host_PG: max_iter = 60000 (src/defs.h:11), members untouched
     max_iter = 60000 if mode == 1 else 10000
-    lay, G = device_layout(n)
+    # the engine's vector space: the split's flow path takes an RCM layout, a
+    # deterministic function of the factors -- read it from a solver of our own
+    ref = ggmres.Solver(0)
+    try:
+        ref.set_matrix(Ad)
+        ref.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+        lay, G = ref.layout()
+    finally:
+        ref.close()
     x = x0.astype(np.float64)
     for k in range(nsteps):
         rc, max_it, tol = struct.unpack_from("<iif", data, k * rec)

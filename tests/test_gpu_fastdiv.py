@@ -34,11 +34,11 @@ def solver():
     s.close()
 
 
-def oracle_mul(run, n, nx=None, ny=None, mul=(False, True)):
+def oracle_mul(run, n, nx=None, ny=None, mul=(False, True), layout=None):
     """(serial-order oracle with the reference's division, order-matched oracle
-    with the device's division)"""
+    with the device's division; layout: the solver's own, Solver.layout())"""
     o_serial = run()
-    O.set_dot_order(*device_layout(n, nx, ny))
+    O.set_dot_order(*(layout if layout is not None else device_layout(n, nx, ny)))
     O.set_div_mode(*mul)
     try:
         o_tree = run()
@@ -149,7 +149,7 @@ def test_rcp_split_parity(solver):
     solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
     mul = (solver.division_active(0) == ggmres.DIV_RCP, solver.division_active(1) == ggmres.DIV_RCP)
     o, ot = oracle_mul(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
-                       A.shape[0], mul=mul)
+                       A.shape[0], mul=mul, layout=solver.layout())
     g = solver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
     check_exact(g, ot)
     check_tol(g, o)
@@ -323,7 +323,8 @@ def test_fma_split_parity(fsolver, perm):
         assert fsolver.trsv_kernel(0) in ("k_trsv_wave2d_spmv<5>", "k_trsv_wave2d<true, 5, false, false, 1, false>")
         assert fsolver.trsv_kernel(1).startswith("k_trsv_wave2d<false, 5,")
     o, ot = oracle_mul(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
-                       A.shape[0], nx=48 if perm == "identity" else None, mul=md)
+                       A.shape[0], nx=48 if perm == "identity" else None, mul=md,
+                       layout=None if perm == "identity" else fsolver.layout())
     g = fsolver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
     check_exact(g, ot)
     check_tol(g, o)

@@ -236,10 +236,11 @@ def check_exact(g, o):
     assert np.array_equal(g["x"], o["x"]), rel_err(g["x"], o["x"])
 
 
-def oracle_both(run, n, nx=None, ny=None, skew=1):
-    """run() under serial and under order-matched dot products."""
+def oracle_both(run, n, nx=None, ny=None, skew=1, layout=None):
+    """run() under serial and under order-matched dot products (layout: the
+    solver's own (lay2nat, G), Solver.layout(), e.g. an RCM flow layout)."""
     o_serial = run()
-    lay, G = device_layout(n, nx, ny, skew)
+    lay, G = layout if layout is not None else device_layout(n, nx, ny, skew)
     O.set_dot_order(lay, G)
     try:
         o_tree = run()
@@ -418,10 +419,33 @@ def test_gmres_split_parity(solver, ell, monkeypatch):
     P = make_split(A, seed=9)
     b = M.rhs_uniform(A.shape[0])
     x0 = np.random.default_rng(3).random(A.shape[0]) * 0.1
-    o, ot = oracle_both(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
-                        A.shape[0])
     solver.set_matrix(A)
     solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    assert not solver.uses_wavefront
+    lay, G = solver.layout()                    # the flow path's RCM layout (gg_layout)
+    assert not np.array_equal(lay[:A.shape[0]], np.arange(A.shape[0]))
+    assert np.array_equal(np.sort(lay[lay >= 0]), np.arange(A.shape[0]))
+    o, ot = oracle_both(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
+                        A.shape[0], layout=(lay, G))
+    g = solver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
+    check_gmres(g, o)
+    check_exact(g, ot)
+
+
+def test_gmres_split_parity_natural_layout(solver, monkeypatch):
+    """GG_FLOW_RCM=0: the flow path in the natural layout, the same arithmetic
+    per row (only the dots' reduction order follows the layout)"""
+    monkeypatch.setenv("GG_FLOW_RCM", "0")
+    A = M.laplacian_5pt(40)
+    P = make_split(A, seed=9)
+    b = M.rhs_uniform(A.shape[0])
+    x0 = np.random.default_rng(3).random(A.shape[0]) * 0.1
+    solver.set_matrix(A)
+    solver.set_precond_split(P.L, P.U, P.middle, P.perm_row, P.perm_col, P.lscale, P.rscale)
+    lay, G = solver.layout()
+    assert np.array_equal(lay[:A.shape[0]], np.arange(A.shape[0]))
+    o, ot = oracle_both(lambda: O.gmres_split(A, P, b, x0=x0, m=32, max_iter=2000, tol=1e-11),
+                        A.shape[0])
     g = solver.solve(b, x0=x0, restart=32, max_iter=2000, tol=1e-11)
     check_gmres(g, o)
     check_exact(g, ot)

@@ -24,6 +24,7 @@ r = d.get("rooflines") or {}
 print(sys.argv[1], d["value"], {k: v["avg_us"] for k, v in r.items()})
 PY
     done
+    [ "${TRACE:-1}" = 1 ] || continue
     GGMRES_LIB=variants/libggmres_$v.so timeout -k 10 120 python -u tools/wave_trace.py > gpurun_out/${T}_trace_$v.txt 2>&1 || { tail -20 gpurun_out/${T}_trace_$v.txt; exit 1; }
     grep -E "total|phase|publish|seen" gpurun_out/${T}_trace_$v.txt
 done
