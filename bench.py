@@ -95,6 +95,7 @@ def parse():
                         "(1000^2 5-pt, the default sharded system at --gpus N > 1)")
     p.add_argument("--pg-perm", choices=["identity", "random"], default="identity",
                    help="pg: the split's row / column permutations")
+    p.add_argument("--pg-seed", type=int, default=20261015, help="pg: the split's seed (permutations, scales)")
     p.add_argument("--pad-stride", type=int, default=50,
                    help="netlist: a VDD pad (package R + voltage source) every this many nodes per direction")
     p.add_argument("--workload", choices=["c2", "c3", "c3s", "c4", "c5", "dd", "replicas", "pg", "netlist"],
@@ -583,8 +584,11 @@ def bench_dd(a, torch, dist, world, rank, local):
                    "exchange_ranks": ranks if world > 1 else None,
                    "exchange_latency": xch,
                    "division": dd_div,
-                   "orthogonalization": ("CGS2: 3 all-gathers per inner iteration (GG_SOLVE_CGS2, tolerance "
-                                         "parity 1e-10 vs MGS over the first cycle)") if a.dd_orth == "cgs2"
+                   "orthogonalization": (("CGS2 in 4 launches, its 3 exchanges inside the kernels "
+                                          "(GG_SOLVE_CGS2, Xch" if info.get("cgs2_in_kernel_exchange") else
+                                          "CGS2: 3 all-gathers per inner iteration (GG_SOLVE_CGS2") +
+                                         ", tolerance parity 1e-10 vs MGS over the first cycle)")
+                                        if a.dd_orth == "cgs2"
                                         else "MGS (the reference's): i + 2 all-gathers per inner iteration",
                    "all_gathers_per_iteration": (2 + 3) if a.dd_orth == "cgs2" else
                                                 "2 + (i + 2) at cycle index i",
@@ -709,7 +713,7 @@ def main():
     kilu = a.ilu_level if a.workload in ("c2", "c3s") else 0
     if pg or netlist:
         if pg:
-            split = pg_split(A, local, identity=a.pg_perm == "identity")
+            split = pg_split(A, local, seed=a.pg_seed, identity=a.pg_perm == "identity")
         s.set_precond_split(*split)
     elif kilu:
         s.set_precond_iluk_device(kilu)

@@ -88,8 +88,16 @@ struct gg_dd {
     // differ, so the communicator is unusable -- every later exchange is
     // refused with GG_ESTATE (create a new gg_dd to recover)
     bool ipc_broken = false;
+    // CGS2 with the exchanges inside the kernels (GG_DD_IPC / GG_DD_LOOPBACK,
+    // P > 1; GG_DD_XK=0 turns it off): the areas above (loopback: this rank's
+    // own as every peer's) and the reducers' hand-off words (uncached)
+    bool xk = false;
+    bool xk_shared = false;                 // IPC peers on this rank's own GPU (tests)
+    void *xk_local = nullptr;
+    Xch xch{};
     hipStream_t st = nullptr;
     hipStream_t st2 = nullptr;              // the SpMV's interface exchange, beside the interior rows
+    bool halo_inline = false;               // GG_DD_HALO_INLINE: exchange on st, no st2 overlap
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evx = nullptr, evh = nullptr;
     bool have = false;
     int n = 0, nsep = 0, maxI = 0;
@@ -347,6 +355,17 @@ void spmv_rows(gg_dd *d, const Get &x, const Get &b, const Get &y, bool resid,
 {
     const long long S0 = d->S0;
     const bool xch = d->maxI > 0 && d->P > 1;
+    if (xch && d->halo_inline) {
+        // the exchange in line on the solver's stream: no cross-stream event
+        // wait pair per SpMV (GG_DD_HALO_INLINE)
+        halo(d, x, d->st);
+        for (auto &sp : d->sh) {
+            Shard &s = *sp;
+            launch_spmv(gate(s), s.AI, x(s), resid ? b(s) : nullptr, y(s), resid, d->st);
+            launch_spmv(gate(s), s.AS, x(s), resid ? b(s) + S0 : nullptr, y(s) + S0, resid, d->st);
+        }
+        return;
+    }
     if (xch) {
         GG_HIP(hipEventRecord(d->evx, d->st));              // x complete
         GG_HIP(hipStreamWaitEvent(d->st2, d->evx, 0));
@@ -402,8 +421,10 @@ void ensure_workspace(gg_dd *d, int m)
         }
         s.H.alloc((size_t)(m + 1) * m);
         GG_HIP(hipMemsetAsync(s.H.p, 0, (size_t)(m + 1) * m * sizeof(double), d->st));
-        s.partC.alloc((size_t)d->P * (m + 1) * d->G);
-        GG_HIP(hipMemsetAsync(s.partC.p, 0, (size_t)d->P * (m + 1) * d->G * sizeof(double), d->st));
+        // two halves: the first and the second pass's partials (in-kernel
+        // exchanges: a launch reads one while it writes the other)
+        s.partC.alloc((size_t)2 * d->P * (m + 1) * d->G);
+        GG_HIP(hipMemsetAsync(s.partC.p, 0, (size_t)2 * d->P * (m + 1) * d->G * sizeof(double), d->st));
         s.hcgs.alloc(m + 1);
         s.s.alloc(m + 1);
         s.cs.alloc(m + 1);
@@ -413,6 +434,17 @@ void ensure_workspace(gg_dd *d, int m)
         if (!s.err.p) s.err.alloc(d->P);
     }
     d->m_alloc = m;
+}
+
+// the in-kernel CGS2 exchanges apply (one shard per process, the dots of
+// inner iteration nk - 1 within the kernels' and the area's range)
+bool use_xk(gg_dd *d, int nk)
+{
+    // several ranks on one GPU: a rank's waiting blocks must not starve a
+    // peer's producer of CUs -- only when every rank's grid fits one block per CU
+    if (d->xk_shared && (long long)d->P * d->G > 256) return false;
+    return d->xk && d->sh.size() == 1 && nk <= kCgsXMax && d->G <= kIpcXF && (long long)nk * d->G <= d->ipc_capd &&
+           (long long)d->G <= d->ipc_capd;
 }
 
 void enqueue_init(gg_dd *d)
@@ -438,6 +470,27 @@ void enqueue_cycle(gg_dd *d, int m)
         prof_end(d, mk);
         apply_minv(d, i, 0, vec(&Shard::ww), vec(&Shard::w));                   // w = M^-1 ww
         mk = prof_begin(d, GG_DD_PROF_ORTH, i);
+        if (d->cgs2 && use_xk(d, i + 1)) {
+            // CGS2 with the exchanges inside four launches (Xch): the same
+            // values as below, exchange sequence numbers shared with ipc_allgather
+            Shard &s = *d->sh[0];
+            const int nk = i + 1;
+            const long long cnt = (long long)nk * d->G;
+            const long long half = (long long)d->P * (m + 1) * d->G;
+            double *p1 = s.partC.p + (long long)s.p * cnt, *p2 = s.partC.p + half + (long long)s.p * cnt;
+            double *pn = s.partA.p + (long long)s.p * d->G;
+            const unsigned long long q1 = ++d->ipc_seq, q2 = ++d->ipc_seq, q3 = ++d->ipc_seq;
+            const Gate gt = gate_i(s, i);
+            launch_multidot_x(gt, s.w.p, s.V.p, Pl, nk, p1, d->G, dot_len(d, s), d->xch, q1, d->st);
+            launch_cgs_update_x(gt, s.w.p, s.V.p, Pl, nk, d->G, H0, dot_len(d, s), p1, q1, s.H.p, i, m, false, p2,
+                                nullptr, d->xch, q2, d->st);
+            launch_cgs_update_x(gt, s.w.p, s.V.p, Pl, nk, d->G, H0, dot_len(d, s), p2, q2, s.H.p, i, m, true,
+                                nullptr, pn, d->xch, q3, d->st);
+            launch_arnoldi_finalize_x(gt, i, m, s.ds.p, pn, q3, d->G, s.w.p, s.V.p + (long long)(i + 1) * Pl, s.H.p,
+                                      s.cs.p, s.sn.p, s.s.p, s.hist.p, H0, d->xch, d->st);
+            prof_end(d, mk);
+            continue;
+        }
         if (d->cgs2) {
             // CGS2: h = V^T w, w -= V h, h2 = V^T w, w -= V h2 (+ the norm's
             // partials), H[:, i] = h + h2 -- three all-gathers
@@ -537,6 +590,7 @@ void check_err(gg_dd *d)
         Shard &s = *d->sh[0];
         GG_NCCL(ncclAllGather(s.err.p + s.p, s.err.p, 1, ncclInt32, d->comm, d->st));
     }
+    if (d->kind == GG_DD_LOOPBACK && d->xk) ipc_check(d);
     if (d->kind == GG_DD_IPC) {
         ipc_check(d);
         if (d->P > 1) {
@@ -926,6 +980,10 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
     d->rank = comm == GG_DD_LOCAL ? 0 : rank;
     set_dev(d.get());
     GG_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
+    {
+        const char *hi = std::getenv("GG_DD_HALO_INLINE");
+        d->halo_inline = hi && hi[0] == '1';
+    }
     GG_HIP(hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking));
     GG_HIP(hipEventCreate(&d->ev0));
     GG_HIP(hipEventCreate(&d->ev1));
@@ -942,7 +1000,7 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
         // this rank's polls meet in memory
         const char *cap = std::getenv("GG_DD_IPC_CAP");
         d->ipc_capd = cap ? std::max(1LL, atoll(cap)) : (1LL << 20);
-        const size_t bytes = sizeof(double) * ((size_t)kMaxShards * kIpcXB + 2ull * nparts * d->ipc_capd);
+        const size_t bytes = xch_area_bytes(nparts, d->ipc_capd);
         GG_HIP(hipExtMallocWithFlags(&d->ipc_area, bytes, hipDeviceMallocUncached));
         GG_HIP(hipMemset(d->ipc_area, 0, bytes));
         GG_HIP(hipDeviceSynchronize());
@@ -950,6 +1008,34 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
         GG_HIP(hipMemset(d->xerr.p, 0, sizeof(int)));
         d->ipc.base[rank] = d->ipc_area;
         d->ipc_connected = nparts == 1;
+    }
+    if (comm == GG_DD_LOOPBACK && nparts > 1) {
+        // the in-kernel exchanges' area, this rank's own standing in for every peer's
+        d->ipc_capd = 1LL << 16;
+        const size_t bytes = xch_area_bytes(nparts, d->ipc_capd);
+        GG_HIP(hipExtMallocWithFlags(&d->ipc_area, bytes, hipDeviceMallocUncached));
+        GG_HIP(hipMemset(d->ipc_area, 0, bytes));
+        d->xerr.alloc(1);
+        GG_HIP(hipMemset(d->xerr.p, 0, sizeof(int)));
+        for (int q = 0; q < nparts; q++) d->ipc.base[q] = d->ipc_area;
+    }
+    if ((comm == GG_DD_IPC || comm == GG_DD_LOOPBACK) && nparts > 1) {
+        const char *xk = std::getenv("GG_DD_XK");
+        d->xk = !(xk && xk[0] == '0');
+        const size_t bytes = 2 * 64 * sizeof(double);            // hx[64] | hf[64]
+        GG_HIP(hipExtMallocWithFlags(&d->xk_local, bytes, hipDeviceMallocUncached));
+        GG_HIP(hipMemset(d->xk_local, 0, bytes));
+        GG_HIP(hipDeviceSynchronize());
+        d->xch.me = rank;
+        d->xch.P = nparts;
+        d->xch.loop = comm == GG_DD_LOOPBACK;
+        d->xch.capd = d->ipc_capd;
+        d->xch.err = d->xerr.p;
+        d->xch.hx = static_cast<double *>(d->xk_local);
+        d->xch.hf = reinterpret_cast<unsigned long long *>(static_cast<double *>(d->xk_local) + 64);
+        // (xch.pp is filled when the areas are connected: now for loopback,
+        // in gg_dd_ipc_connect for IPC)
+        d->xch.pp = d->ipc;
     }
     *out = d.release();
     return GG_OK;
@@ -967,10 +1053,12 @@ int gg_dd_destroy(gg_dd *d)
     if (d->comm) (void)ncclCommDestroy(d->comm);
     if (d->ipc_area) {
         (void)hipDeviceSynchronize();
-        for (int q = 0; q < d->P; q++)
-            if (q != d->rank && d->ipc.base[q]) (void)hipIpcCloseMemHandle(d->ipc.base[q]);
+        if (d->kind == GG_DD_IPC)
+            for (int q = 0; q < d->P; q++)
+                if (q != d->rank && d->ipc.base[q]) (void)hipIpcCloseMemHandle(d->ipc.base[q]);
         (void)hipFree(d->ipc_area);
     }
+    if (d->xk_local) (void)hipFree(d->xk_local);
     d->xerr.release();
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
@@ -1014,8 +1102,16 @@ int gg_dd_ipc_connect(gg_dd *d, const unsigned char *handles)
         d->ipc.base[q] = p;
     }
     d->ipc_connected = true;
-    // a first exchange: every rank has mapped every area before anyone moves on
-    (void)ipc_allgather_host(d, d->rank);
+    d->xch.pp = d->ipc;
+    // a first exchange: every rank has mapped every area before anyone moves
+    // on; it carries a hash of each rank's PCI bus id (ranks sharing a GPU)
+    char bus[64] = {};
+    GG_HIP(hipDeviceGetPCIBusId(bus, sizeof bus, d->device));
+    long long hb = 1469598103934665603LL;
+    for (const char *c = bus; *c; c++) hb = (hb ^ (unsigned char)*c) * 1099511628211LL;
+    int same = 0;
+    for (long long v : ipc_allgather_host(d, hb)) same += v == hb;
+    d->xk_shared = same > 1;
     return GG_OK;
     GG_API_END
 }
@@ -1081,6 +1177,7 @@ int gg_dd_info(gg_dd *d, int *info)
     info[7] = (int)d->Pl;
     info[8] = (int)d->sh.size();
     info[9] = d->P * d->maxI;
+    info[10] = use_xk(d, 1) ? 1 : 0;
     return GG_OK;
     GG_API_END
 }

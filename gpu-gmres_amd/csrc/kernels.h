@@ -23,6 +23,11 @@ struct DevState {
     int pad;
 };
 constexpr int DONE_INNER = 1, DONE_RESTART = 2, DONE_INIT = 4, DONE_ABORT = 8;
+// a cycle enqueued behind the one that ends the solve (the host's pipelined
+// cycle loop) must do nothing: DONE_FINAL = the converged cycle's update has
+// been applied (set by k_end_cycle), DONE_EXH = max_iter exhausted before the
+// cycle (set by k_init_cycle)
+constexpr int DONE_FINAL = 16, DONE_EXH = 32;
 
 // A kernel is skipped when (*done & mask) != 0, or (nit && i >= *nit).
 struct Gate {
@@ -114,6 +119,41 @@ struct IpcPeers { void *base[kMaxShards]; };
 // me already in place); err |= 4 when a peer did not arrive in time
 void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long long cnt,
                           unsigned long long seq, long long capd, int *err, hipStream_t st);
+
+// The CGS2 exchanges inside the kernels (GG_DD_IPC / GG_DD_LOOPBACK, one shard
+// per process, inner iterations with i + 1 <= kCgsXMax): a producer kernel
+// stores each block's partials into its own slot (part + me*cnt) and straight
+// into every peer's area (data[seq & 1][me], as k_ipc_allgather), then raises
+// the block's flag xflag[me][b] = seq there; the consumer kernel's reducer
+// blocks wait for the P*G flags of their dot, sum the partials in
+// k_cgs_reduce's order (the same bits) and hand the value to every block of
+// the launch through `hx` / `hf` (this rank's uncached scratch).  Area of rank
+// q: [flags kMaxShards x kIpcXB][data 2 x P x capd][xflags kMaxShards x kIpcXF].
+constexpr int kIpcXF = 1024;           // in-kernel exchange flag words per source rank (>= the dot grid)
+constexpr int kCgsXMax = 32;           // dots per inner iteration the in-kernel path takes
+struct Xch {
+    IpcPeers pp;                       // areas (loopback: this rank's own for every q)
+    int me = 0, P = 1, loop = 0;       // loop: the peers' slots are this rank's own (timing only)
+    long long capd = 0;
+    int *err = nullptr;                // |= 4: a flag did not arrive within ~30 s
+    double *hx = nullptr;              // reduced values (kCgsXMax + 1)
+    unsigned long long *hf = nullptr;  // their flags (sequence numbers)
+};
+size_t xch_area_bytes(int P, long long capd);
+// <w, v_k>, k < nk: block partials published as exchange seq (part: this rank's slot)
+void launch_multidot_x(Gate g, const double *w, const double *V, long long ldv, int nk, double *part, int G,
+                       long long Pdot, const Xch &x, unsigned long long seq, hipStream_t st);
+// h = the reduced exchange sin (H[k, i] = h[k], or += when add), w -= V h, and
+// (part_out != null) the next pass's dot partials, or (norm_out) the norm's,
+// published as exchange sout
+void launch_cgs_update_x(Gate g, double *w, const double *V, long long ldv, int nk, int G, long long Ppad,
+                         long long Pdot, const double *part_in, unsigned long long sin, double *H, int i, int m,
+                         bool add, double *part_out, double *norm_out, const Xch &x, unsigned long long sout,
+                         hipStream_t st);
+// k_arnoldi_finalize with the norm reduced from exchange sin
+void launch_arnoldi_finalize_x(Gate g, int i, int m, DevState *ds, const double *part_in, unsigned long long sin,
+                               int G, const double *w, double *vnext, double *H, double *cs, double *sn,
+                               double *s, double *hist, long long Ppad, const Xch &x, hipStream_t st);
 
 // ---- split (PG) elementwise maps -------------------------------------------
 void launch_f64_to_f32(Gate g, const double *in, float *out, int n, hipStream_t st);   // out = RN_f32(in)

@@ -1070,6 +1070,9 @@ constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 #ifndef GG_WAVE_EARLYBAR
 #define GG_WAVE_EARLYBAR 0
 #endif
+// (Measured, not kept, round 5: the 2D boundary wave retrying a batch's
+// granules with two polls in flight, s_sleep 0 / 1 / 10 between them: C2 U
+// 99.6 -> 102.6-105.6 us, L 95.7 -> 97.8-101.5 us, profiles/r05/stage_ab.txt.)
 #ifndef GG_WAVE_XCD
 #define GG_WAVE_XCD 8
 #endif
@@ -1118,8 +1121,11 @@ struct WaveCfg {
     static constexpr int B = (B16 == 16 && 3 * A * 8 * 64 + 64 + 2 * 8 * 64 > 150 * 1024 / 16) ? 8 : B16;
     static constexpr int PBN = B / 2;                                     // step pairs per batch
     static constexpr int SLOT = A * PBN * 64;                            // double2 per ring slot
-    static constexpr int LOADERS = kWaveLoaders == 1 ? 1 : A;           // loader waves
-    static constexpr int NPER = (LOADERS == 1 ? A : 1) * PBN;           // DMA instructions per batch per loader
+    // loader waves: GG_WAVE_LOADERS where it divides the arrays (2D, unskewed),
+    // each streaming A / LOADERS of them with its own vmcnt budget
+    static constexpr int LOADERS = (!D3 && S == 1 && kWaveLoaders > 1 && A % kWaveLoaders == 0) ? kWaveLoaders : 1;
+    static constexpr int NA = A / LOADERS;                              // arrays per loader wave
+    static constexpr int NPER = NA * PBN;                               // DMA instructions per batch per loader
     // ring slots: kWaveRing, at most what fits 150 KiB of LDS beside the boundary
     // values and the x staging, and at most what the 6-bit vmcnt can count
     static constexpr int RFIT = (150 * 1024 / 16 - 64 - 2 * PBN * 64) / SLOT;
@@ -1321,7 +1327,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // write go after the pair (C2 fused L 86.7 -> 84.5 us, netlist L 91.5 ->
     // 90.4; the other forms keep it: the exact unit L 88.9 -> 90.3 without)
     constexpr bool SH = kWaveShadow && DIV != WD_UFMA;
-    static_assert(!FS || (FWD && !D3 && S == 1 && !TRACE && C::LOADERS == 1), "fused SpMV: forward 2D, one loader");
+    static_assert(!FS || (FWD && !D3 && S == 1 && !TRACE), "fused SpMV: forward 2D");
     static_assert(!IL || (S == 1 && !D3), "in-line-first rows: unskewed 2D grids");
     constexpr bool FM = DIV == WD_UFMA || DIV == WD_SFMA;     // GG_DIV_FMA rows
     static_assert(!FM || (S == 1 && !D3 && !IL), "fused rows: unskewed 2D grids (one order for both IL)");
@@ -1362,7 +1368,8 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // Measured on C2: U 121.0 -> 117.9 us, while L (3 streamed arrays) slows
     // 88.9 -> 90.0 us (round 3, re-measured: 89.4 / 90.3 -> 89.9 / 90.4 us), so
     // the forward solve keeps one workgroup per band.
-    constexpr int XS = D3 ? 1 : FWD ? GG_WAVE_XCD_L : GG_WAVE_XCD;
+    // (the fused SpMV's launch holds one workgroup per band: no placement there)
+    constexpr int XS = (D3 || FS) ? 1 : FWD ? GG_WAVE_XCD_L : GG_WAVE_XCD;
     if (XS > 1 && bid % XS) return;
     const int blk = bid / XS;
     const int ntask = nz * nbands;
@@ -1382,6 +1389,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
     static_assert(NC >= 1 && NC <= 4 && (NC == 1 || !GG_WAVE_DECOUPLE), "redundant compute waves");
     if (wave >= NC + 2) {
         // ------------------------------------------------ loader wave(s)
+        const int li = wave - NC - 2;           // this loader's arrays: [li * NA, (li + 1) * NA)
         const double2 *src[7] = {reinterpret_cast<const double2 *>(b) + boff,
                                  reinterpret_cast<const double2 *>(c1) + boff,
                                  reinterpret_cast<const double2 *>(c2) + boff,
@@ -1412,10 +1420,11 @@ __device__ __forceinline__ void trsv_wave2d_body(
                 }
             }
         }
-        if constexpr (FS) {
+        if (FS && li == 0) {
             // this band's b rows all stored by the SpMV blocks (no DMA in flight
             // yet: a blocking poll is free); the counter is re-armed after the
             // stream (a store in flight would upset the loader's vmcnt count)
+            // -- by the loader of b (array 0) alone
             const int gpb = T / kFsGroup;
             const unsigned long long *fl = fs.cnt + (long long)band * gpb;
             auto all_stored = [&]() {
@@ -1435,10 +1444,12 @@ __device__ __forceinline__ void trsv_wave2d_body(
         }
         if constexpr (C::LOADERS == 1) {
             wave_loader<FWD, C::R, C::SLOT, C::A, C::PBN, D3 ? C::A2 + 1 : FS ? 0 : -1>(src, ring, np, nbatch);
+        } else if (li == 0) {
+            wave_loader<FWD, C::R, C::SLOT, C::NA, C::PBN, FS ? 0 : -1>(src, ring, np, nbatch);
         } else {
-            wave_loader<FWD, C::R, C::SLOT, 1, C::PBN>(src + (wave - NC - 2), ring + (wave - NC - 2) * PB, np, nbatch);
+            wave_loader<FWD, C::R, C::SLOT, C::NA, C::PBN>(src + li * C::NA, ring + li * C::NA * PB, np, nbatch);
         }
-        if constexpr (FS) {
+        if (FS && li == 0) {
             const int gpb = T / kFsGroup;
             for (int k = lane; k < gpb; k += 64) st_agent(fs.cnt + (long long)band * gpb + k, 0ull);   // re-arm
         }
@@ -2737,6 +2748,13 @@ __global__ __launch_bounds__(kBlock) void k_init_cycle(DevState *ds, const doubl
                                                        double *s, long long units)
 {
     if (ds->done) return;
+    if (ds->max_iter - ds->j + 1 <= 0) {   // a cycle past max_iter (pipelined): nothing runs
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            ds->nit = 0;
+            ds->done |= DONE_EXH;
+        }
+        return;
+    }
     const double beta = ds->beta;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         int nit = ds->max_iter - ds->j + 1;
@@ -3013,6 +3031,241 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
                 st2(vnext, u0 + j * stride, a[j]);
             }
         }
+    }
+}
+
+// ---- CGS2 with its exchanges inside the kernels (kernels.h, Xch) ------------
+// Four launches per inner iteration instead of nine plus three all-gathers:
+// k_multidot_x -> k_cgs_update_x<dots> -> k_cgs_update_x<norm> ->
+// k_arnoldi_finalize_x, each producer publishing its block partials into every
+// rank's area itself and each consumer reducing them in k_cgs_reduce's order
+// (so every value has the bits of the launch-per-step path).  A consumer waits
+// only for exchanges its peers' EARLIER launches produce, so the waits form no
+// cycle; inside a launch the reducer blocks (blockIdx < nk) hand their values to
+// the rest through hx / hf -- they are dispatched first and wait on nothing of
+// this launch.  Every spin is bounded (~30 s, err |= 4); after one time-out the
+// others give up at once (the broken word hf[kCgsXMax + 1]).
+__device__ __forceinline__ unsigned long long *xk_flag(void *base, int P, long long capd, int src)
+{
+    return reinterpret_cast<unsigned long long *>(base) + (long long)kMaxShards * kIpcXB + 2LL * P * capd +
+           (long long)src * kIpcXF;
+}
+__device__ __forceinline__ double *xk_slot(void *base, int P, long long capd, unsigned long long seq, int src)
+{
+    return reinterpret_cast<double *>(base) + (long long)kMaxShards * kIpcXB +
+           ((long long)(seq & 1) * P + src) * capd;
+}
+__device__ __noinline__ bool xk_wait_slow(const unsigned long long *f, unsigned long long seq, const Xch &x)
+{
+    unsigned long long *broken = x.hf + kCgsXMax + 1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned n = 1;; n++) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= seq) return true;
+        if ((n & 255) == 0) {
+            if (__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {     // ~30 s of the 100 MHz clock
+                atomicOr(x.err, 4);
+                __hip_atomic_store(broken, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+        }
+    }
+}
+__device__ __forceinline__ bool xk_wait(const unsigned long long *f, unsigned long long seq, const Xch &x)
+{
+    if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= seq) return true;
+    return xk_wait_slow(f, seq, x);
+}
+// thread t < n holds v for index idx of this rank's slot: into the own slot
+// and every peer's area, then this block's flag in every peer's area
+__device__ __forceinline__ void xk_publish(const Xch &x, unsigned long long seq, double *own, bool has,
+                                           long long idx, double v)
+{
+    if (has) {
+        own[idx] = v;
+        for (int q = 0; q < x.P; q++)
+            if (q != x.me) xk_slot(x.pp.base[q], x.P, x.capd, seq, x.me)[idx] = v;
+    }
+    __threadfence_system();
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < x.P && t != x.me)
+        __hip_atomic_store(xk_flag(x.pp.base[t], x.P, x.capd, x.me) + blockIdx.x, seq, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// dot k over every rank's G block partials, in k_cgs_reduce's order (e = q*G + b,
+// thread-strided, block_sum); own = this rank's slot
+__device__ __forceinline__ double xk_reduce(const Xch &x, unsigned long long seq, const double *own, int G, int k)
+{
+    double v = 0.0;
+    void *mine = x.pp.base[x.me];
+    for (int e = threadIdx.x; e < x.P * G; e += kBlock) {
+        const int q = e / G, b = e % G;
+        const long long idx = (long long)k * G + b;
+        if (q == x.me) {
+            v += own[idx];
+        } else {
+            const int src = x.loop ? x.me : q;
+            (void)xk_wait(xk_flag(mine, x.P, x.capd, src) + b, seq, x);
+            v += xk_slot(mine, x.P, x.capd, seq, src)[idx];
+        }
+    }
+    return block_sum(v);
+}
+// a reducer's value to every block of the launch (thread 0)
+__device__ __forceinline__ void xk_post(const Xch &x, int slot, double v, unsigned long long seq)
+{
+    x.hx[slot] = v;
+    __hip_atomic_store(x.hf + slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// block_sum_store's sums, thread k < nk receiving sum k
+template <int NK>
+__device__ __forceinline__ double block_sum_pick(const double (&acc)[NK], int nk)
+{
+    __shared__ double sh[kBlock / 64][NK];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        if (k < nk) {
+            const double v = wave_sum(acc[k]);
+            if (lane == 0) sh[w][k] = v;
+        }
+    }
+    __syncthreads();
+    const int k = threadIdx.x < nk ? threadIdx.x : 0;
+    return (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_multidot_x(Gate g, const double *__restrict__ w,
+                                                       const double *__restrict__ V, long long ldv, int nk,
+                                                       double *part, int G, long long dunits, Xch x,
+                                                       unsigned long long seq)
+{
+    if (gated(g)) return;
+    double acc[kCgsXMax];
+#pragma unroll
+    for (int k = 0; k < kCgsXMax; k++) acc[k] = 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < dunits; u += stride) {
+        const double2 a = ld2(w, u);
+#pragma unroll
+        for (int k = 0; k < kCgsXMax; k++) {
+            if (k < nk) {
+                const double2 b = ld2_nt(V + (long long)k * ldv, u);
+                acc[k] += a.x * b.x;
+                acc[k] += a.y * b.y;
+            }
+        }
+    }
+    const double v = block_sum_pick<kCgsXMax>(acc, nk);
+    xk_publish(x, seq, part, threadIdx.x < nk, (long long)threadIdx.x * G + blockIdx.x, v);
+}
+
+// h = reduced exchange sin (H[k, i] = h, or += with add); w -= V h; then
+// DOTS: the partials of <w, v_k> (k_cgs_update_dot), else the norm's
+// (k_cgs_update<true>), published as exchange sout into part_out
+template <bool DOTS>
+__global__ __launch_bounds__(kBlock) void k_cgs_update_x(Gate g, double *__restrict__ w,
+                                                         const double *__restrict__ V, long long ldv, int nk,
+                                                         long long units, long long dunits, int G,
+                                                         const double *part_in, unsigned long long sin, double *H,
+                                                         int i, int m, int add, double *part_out, Xch x,
+                                                         unsigned long long sout)
+{
+    if (gated(g)) return;
+    __shared__ double hs[kCgsXMax];
+    for (int k = blockIdx.x; k < nk; k += gridDim.x) {
+        const double v = xk_reduce(x, sin, part_in, G, k);
+        if (threadIdx.x == 0) {
+            double *hk = H + k + (long long)i * (m + 1);
+            *hk = add ? *hk + v : v;
+            xk_post(x, k, v, sin);
+        }
+    }
+    if (threadIdx.x < nk) {
+        (void)xk_wait(x.hf + threadIdx.x, sin, x);
+        hs[threadIdx.x] = x.hx[threadIdx.x];
+    }
+    __syncthreads();
+    double acc[DOTS ? kCgsXMax : 1];
+#pragma unroll
+    for (int k = 0; k < (DOTS ? kCgsXMax : 1); k++) acc[k] = 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units; u += stride) {
+        double2 a = ld2(w, u);
+        double2 b[kCgsChunk];
+        cgs_axpy_chunk(a, b, V, ldv, hs, 0, nk, u);
+        st2(w, u, a);
+        if (u < dunits) {
+            if constexpr (DOTS) {
+#pragma unroll
+                for (int k = 0; k < kCgsXMax; k++) {
+                    if (k < nk) {
+                        acc[k] += a.x * b[k].x;
+                        acc[k] += a.y * b[k].y;
+                    }
+                }
+            } else {
+                acc[0] += a.x * a.x;
+                acc[0] += a.y * a.y;
+            }
+        }
+    }
+    if constexpr (DOTS) {
+        const double v = block_sum_pick<kCgsXMax>(acc, nk);
+        xk_publish(x, sout, part_out, threadIdx.x < nk, (long long)threadIdx.x * G + blockIdx.x, v);
+    } else {
+        const double v = block_sum(acc[0]);
+        xk_publish(x, sout, part_out, threadIdx.x == 0, blockIdx.x, v);
+    }
+}
+
+// k_arnoldi_finalize, ||w||^2 reduced from exchange sin by block 0
+__global__ __launch_bounds__(kBlock) void k_arnoldi_finalize_x(Gate g, int i, int m, DevState *ds,
+                                                               const double *part_in, unsigned long long sin,
+                                                               int G, const double *w, double *vnext, double *H,
+                                                               double *cs, double *sn, double *s, double *hist,
+                                                               long long units, Xch x)
+{
+    if (gated(g)) return;
+    __shared__ double nrm2;
+    if (blockIdx.x == 0) {
+        const double v = xk_reduce(x, sin, part_in, G, 0);
+        if (threadIdx.x == 0) xk_post(x, kCgsXMax, v, sin);
+    }
+    if (threadIdx.x == 0) {
+        (void)xk_wait(x.hf + kCgsXMax, sin, x);
+        nrm2 = x.hx[kCgsXMax];
+    }
+    __syncthreads();
+    const double hn = sqrt(nrm2);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {      // as k_arnoldi_finalize
+        const int ld = m + 1;
+        double *Hc = H + i * ld;
+        Hc[i + 1] = hn;
+        for (int k = 0; k < i; k++) apply_rot(Hc[k], Hc[k + 1], cs[k], sn[k]);
+        double c, sv;
+        gen_rot(Hc[i], Hc[i + 1], c, sv);
+        cs[i] = c;
+        sn[i] = sv;
+        apply_rot(Hc[i], Hc[i + 1], c, sv);
+        apply_rot(s[i], s[i + 1], c, sv);
+        const double resid = fabs(s[i + 1]) / ds->normb;
+        hist[ds->hist_len + i] = resid;
+        ds->resid = resid;
+        if (resid < ds->tol) {
+            ds->conv_i = i;
+            ds->done = DONE_INNER;
+        }
+    }
+    const double inv = (hn != 0.0) ? 1.0 / hn : 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units; u += stride) {
+        double2 a = ld2(w, u);
+        a.x = inv * a.x;
+        a.y = inv * a.y;
+        st2(vnext, u, a);
     }
 }
 
@@ -3774,7 +4027,12 @@ __global__ __launch_bounds__(kBlock) void k_update_x(Gate g, const DevState *ds,
 // beta = ||r|| after a restart; history; j += nit
 __global__ void k_end_cycle(const double *part, int G, DevState *ds, double *hist)
 {
-    if (ds->done) return;
+    if (ds->done) {
+        // the cycle that converged inside has applied its update: a cycle
+        // enqueued behind it must not apply it again
+        if (threadIdx.x == 0 && (ds->done & DONE_INNER)) ds->done |= DONE_FINAL;
+        return;
+    }
     double s = sum_partials(part, G);
     if (threadIdx.x == 0) {
         double beta = sqrt(s);
@@ -4416,6 +4674,35 @@ void launch_arnoldi_finalize_r(Gate g, int i, int m, DevState *ds, const double 
 {
     k_arnoldi_finalize<<<G, kBlock, 0, st>>>(g, i, m, ds, part, nparts_in, w, vnext, H, cs, sn, s,
                                               hist, Ppad / 2);
+}
+size_t xch_area_bytes(int P, long long capd)
+{
+    return sizeof(double) * ((size_t)kMaxShards * kIpcXB + 2ull * P * capd + (size_t)kMaxShards * kIpcXF);
+}
+void launch_multidot_x(Gate g, const double *w, const double *V, long long ldv, int nk, double *part, int G,
+                       long long Pdot, const Xch &x, unsigned long long seq, hipStream_t st)
+{
+    // (the caller checks nk <= kCgsXMax, G <= kIpcXF, nk * G <= x.capd)
+    k_multidot_x<<<G, kBlock, 0, st>>>(g, w, V, ldv, nk, part, G, Pdot / 2, x, seq);
+}
+void launch_cgs_update_x(Gate g, double *w, const double *V, long long ldv, int nk, int G, long long Ppad,
+                         long long Pdot, const double *part_in, unsigned long long sin, double *H, int i, int m,
+                         bool add, double *part_out, double *norm_out, const Xch &x, unsigned long long sout,
+                         hipStream_t st)
+{
+    if (part_out)
+        k_cgs_update_x<true><<<G, kBlock, 0, st>>>(g, w, V, ldv, nk, Ppad / 2, Pdot / 2, G, part_in, sin, H, i, m,
+                                                    add ? 1 : 0, part_out, x, sout);
+    else
+        k_cgs_update_x<false><<<G, kBlock, 0, st>>>(g, w, V, ldv, nk, Ppad / 2, Pdot / 2, G, part_in, sin, H, i,
+                                                     m, add ? 1 : 0, norm_out, x, sout);
+}
+void launch_arnoldi_finalize_x(Gate g, int i, int m, DevState *ds, const double *part_in, unsigned long long sin,
+                               int G, const double *w, double *vnext, double *H, double *cs, double *sn,
+                               double *s, double *hist, long long Ppad, const Xch &x, hipStream_t st)
+{
+    k_arnoldi_finalize_x<<<G, kBlock, 0, st>>>(g, i, m, ds, part_in, sin, G, w, vnext, H, cs, sn, s, hist,
+                                                Ppad / 2, x);
 }
 #ifndef GG_MGS_GATHER_DEFAULT
 #define GG_MGS_GATHER_DEFAULT 2

@@ -501,6 +501,11 @@ struct gg_solver {
     // round trip per restart cycle reads both)
     DevState *h_state = nullptr;
     int *h_err = nullptr;
+    // the pipelined cycle loop: two pinned slots, each the state after one cycle
+    DevState *p_state[2] = {nullptr, nullptr};
+    int *p_err[2] = {nullptr, nullptr};
+    hipEvent_t p_ev[2] = {nullptr, nullptr};
+    std::vector<size_t> mark_ends;      // marks.size() after each enqueued cycle (pipelined)
     int resid_fallbacks = 0;            // cycles rerun after a persistent grid was not co-resident
     // transient tap-node statistics (gg_transient_set_taps / _get_taps)
     std::vector<int> taps;
@@ -830,18 +835,26 @@ void prof_end(gg_solver *s, int mark)
     s->marks[mark].e1 = prof_event(s);
 }
 // after a cycle has completed: account marks of iterations that really ran
-void prof_collect(gg_solver *s, int executed)
+// (the first `upto` marks -- the pipelined loop keeps the next cycle's, whose
+// events are still pending; the pool is reused once no mark is left)
+void prof_collect(gg_solver *s, int executed, size_t upto = (size_t)-1)
 {
-    if (!s->prof_mask) return;
-    for (const auto &mk : s->marks) {
+    if (!s->prof_mask) {
+        s->marks.clear();
+        s->prof_used = 0;
+        return;
+    }
+    upto = std::min(upto, s->marks.size());
+    for (size_t q = 0; q < upto; q++) {
+        const auto &mk = s->marks[q];
         if (mk.i >= executed || mk.e1 < 0) continue;
         float ms = 0.f;
         GG_HIP(hipEventElapsedTime(&ms, s->prof_pool[mk.e0], s->prof_pool[mk.e1]));
         s->prof_ms[mk.kind] += ms;
         s->prof_cnt[mk.kind]++;
     }
-    s->marks.clear();
-    s->prof_used = 0;
+    s->marks.erase(s->marks.begin(), s->marks.begin() + upto);
+    if (s->marks.empty()) s->prof_used = 0;
 }
 
 // ---- GMRES phases ------------------------------------------------------------
@@ -1034,7 +1047,7 @@ void enqueue_cycle(gg_solver *s, int m)
     }
     Gate gu;
     gu.done = &ds->done;
-    gu.mask = DONE_RESTART | DONE_INIT | DONE_ABORT;
+    gu.mask = DONE_RESTART | DONE_INIT | DONE_ABORT | DONE_FINAL | DONE_EXH;
     launch_update(gu, m, ds, s->H.p, s->s.p, s->ysm.p, s->V.p, P, split || usplit ? s->y.p : s->xv.p, s->G, P,
                   s->st, um);
     if (split) apply_right(s, gu, s->y.p, s->xv.p);                            // x = Mr y
@@ -1178,17 +1191,121 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
 
     GG_HIP(hipEventRecord(s->ev0, s->st));
     enqueue_init(s);
+    int ret = 1, iters = 0, inner = 0, restarts = 0;
+    long long hist_len = 1;
+    double relres = 0.0;
+    // Pipelined cycles (GG_CYCLE_PIPE, default on): cycle c+1 is enqueued before
+    // the state after cycle c is read, so the device never waits for the host's
+    // round trip between restart cycles (C2: ~59 us a cycle).  The cycle behind
+    // the last one runs gated off (DONE_* bits: its init, Arnoldi, update and
+    // residual do nothing).  Host-driven operators (user plug-ins) keep one cycle
+    // at a time.
+    const char *pe = std::getenv("GG_CYCLE_PIPE");
+    const bool pipe = !(pe && pe[0] == '0') && !user_kind(s) && opt->max_iter >= 1;
+    if (pipe) {
+        for (int k = 0; k < 2; k++)
+            if (!s->p_state[k]) {
+                GG_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->p_state[k]), sizeof(DevState), hipHostMallocDefault));
+                GG_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->p_err[k]), sizeof(int), hipHostMallocDefault));
+                GG_HIP(hipEventCreateWithFlags(&s->p_ev[k], hipEventDisableTiming));
+            }
+        s->mark_ends.clear();
+        auto enqueue = [&](int slot) {          // one cycle and the read of the state after it
+            enqueue_cycle(s, m);
+            s->mark_ends.push_back(s->marks.size());
+            GG_HIP(hipMemcpyAsync(s->p_state[slot], s->ds.p, sizeof(DevState), hipMemcpyDeviceToHost, s->st));
+            GG_HIP(hipMemcpyAsync(s->p_err[slot], s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
+            GG_HIP(hipEventRecord(s->p_ev[slot], s->st));
+        };
+        auto collect = [&](int executed) {      // the oldest enqueued cycle's marks
+            const size_t upto = s->mark_ends.empty() ? s->marks.size() : s->mark_ends.front();
+            prof_collect(s, executed, upto);
+            if (!s->mark_ends.empty()) {
+                s->mark_ends.erase(s->mark_ends.begin());
+                for (size_t &e : s->mark_ends) e -= upto;
+            }
+        };
+        auto drain = [&]() {                    // the speculative cycle behind the last (gated off)
+            GG_HIP(hipStreamSynchronize(s->st));
+            while (!s->mark_ends.empty()) collect(0);
+            prof_collect(s, 0);
+        };
+        // cycle 1 is gated on DONE_INIT (converged at the start) like the rest
+        enqueue(0);
+        enqueue(1);
+        int cur = 0;
+        DevState prev{};
+        prev.j = 1;
+        prev.hist_len = 1;
+        while (true) {
+            GG_HIP(hipEventSynchronize(s->p_ev[cur]));
+            const int err = *s->p_err[cur];
+            DevState h = *s->p_state[cur];
+            if (err & 8) {
+                drain();
+                throw Fallback{err};
+            }
+            if (err & 1) {
+                drain();
+                GG_REQUIRE(false, GG_ETIMEOUT, "wavefront triangular solve: boundary wait timed out");
+            }
+            if (err & 2) {
+                drain();
+                throw Fallback{err};
+            }
+            if (h.done & DONE_ABORT) {
+                // this cycle aborted, the one behind it ran gated off: rerun this
+                // one on the per-step kernels, then refill the pipeline
+                drain();
+                h = rerun_aborted_cycle(s, m, h);
+                prof_collect(s, (h.done & DONE_INNER) ? h.conv_i + 1 : h.nit);   // the rerun's marks
+                s->mark_ends.clear();
+                enqueue(cur ^ 1);
+            } else {
+                collect((h.done & DONE_INNER) ? h.conv_i + 1 : (h.done & DONE_INIT) ? 0 : h.nit);
+            }
+            relres = h.resid;
+            if (h.done & DONE_INIT) {
+                ret = 0;
+                iters = 0;
+                hist_len = 1;
+                break;
+            }
+            restarts++;
+            if (h.done & DONE_INNER) {
+                ret = 0;
+                iters = prev.j + h.conv_i;
+                inner += h.conv_i + 1;
+                hist_len = h.hist_len + h.conv_i + 1;
+                break;
+            }
+            inner += h.nit;
+            hist_len = h.hist_len;
+            if (h.done & DONE_RESTART) {
+                ret = 0;
+                iters = h.j;
+                break;
+            }
+            if (h.j > opt->max_iter) {          // while (j <= *max_iter) exhausted
+                ret = 1;
+                iters = opt->max_iter;          // the reference leaves *max_iter untouched
+                break;
+            }
+            prev = h;
+            enqueue(cur);                       // the cycle after the one in flight
+            cur ^= 1;
+        }
+        drain();
+    } else {
     // The first cycle goes in before the state after the initial residual is
     // read: its kernels are gated on DONE_INIT (converged at the start), so a
     // solve costs one host round trip less.  The state after init is j = 1,
     // hist_len = 1 (k_init_beta).
     bool first = opt->max_iter >= 1;
     if (first) enqueue_cycle(s, m);
-    h = read_state_checked(s);
+    DevState h = read_state_checked(s);
     if (first && (h.done & DONE_ABORT)) h = rerun_aborted_cycle(s, m, h);
-    int ret = 1, iters = 0, inner = 0, restarts = 0;
-    long long hist_len = 1;
-    double relres = h.resid;
+    relres = h.resid;
     if (h.done & DONE_INIT) {
         ret = 0;
         iters = 0;
@@ -1236,6 +1353,7 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
             hist_len = h.hist_len;
             relres = h.resid;
         }
+    }
     }
     GG_HIP(hipEventRecord(s->ev1, s->st));
     check_err(s);
@@ -1348,6 +1466,11 @@ int gg_destroy(gg_solver *s)
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->h_state) (void)hipHostFree(s->h_state);
     if (s->h_err) (void)hipHostFree(s->h_err);
+    for (int k = 0; k < 2; k++) {
+        if (s->p_state[k]) (void)hipHostFree(s->p_state[k]);
+        if (s->p_err[k]) (void)hipHostFree(s->p_err[k]);
+        if (s->p_ev[k]) (void)hipEventDestroy(s->p_ev[k]);
+    }
     hipStream_t st = s->st;
     delete s;
     if (st) (void)hipStreamDestroy(st);

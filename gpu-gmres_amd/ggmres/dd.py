@@ -127,10 +127,10 @@ class DD:
         _check(_lib().gg_dd_set_system(self.h, n, rp, ci, v, int(method)))
 
     def info(self):
-        a = np.zeros(10, np.int32)
+        a = np.zeros(11, np.int32)
         _check(_lib().gg_dd_info(self.h, a))
         keys = ["n", "nparts", "nsep", "max_iface", "n_interior", "wave_interior", "wave_separator",
-                "local_len", "shards_here", "halo_doubles"]
+                "local_len", "shards_here", "halo_doubles", "cgs2_in_kernel_exchange"]
         return dict(zip(keys, (int(x) for x in a)))
 
     def perm(self):

@@ -87,12 +87,14 @@ int gg_dd_comm_ranks(gg_dd *d, int *ranks, int *rank);
  * ggmres_host.h), arrow permutation, ILU(0) of the permuted matrix, shards */
 int gg_dd_set_system(gg_dd *d, int n, const int *row_ptr, const int *col_idx, const double *val,
                      int method);
-/* info[0..9]: n, nparts, separator rows, max interface per shard, this
+/* info[0..10]: n, nparts, separator rows, max interface per shard, this
  * process's first shard: interior rows, interior solves (0 level-scheduled,
  * 2 / 3 the 2D / 3D wavefront), separator solves (0 level-scheduled launches,
  * 1 the fused separator step, 2 / 3 wavefront), local vector length (slots),
  * shards in this process, halo doubles exchanged per all-gather (received,
- * per shard) */
+ * per shard), 1 when GG_SOLVE_CGS2 runs with its exchanges inside the
+ * orthogonalization's kernels (GG_DD_IPC / GG_DD_LOOPBACK, P > 1; GG_DD_XK=0
+ * turns it off) */
 int gg_dd_info(gg_dd *d, int *info);
 /* the arrow permutation in use: pinv[j] = new index of node j; q = its inverse */
 int gg_dd_perm(gg_dd *d, int *pinv, int *q);

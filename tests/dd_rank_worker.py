@@ -56,6 +56,10 @@ def run(d, A, n, out):
     x0 = np.random.default_rng(9).standard_normal(n)
     g2 = d.solve(M.rhs_uniform(n), x0=x0, restart=7, max_iter=40, tol=1e-14)
     out.update(x2=np.where(own, g2["x"], np.nan), hist2=g2["hist"], iters2=g2["iters"], ret2=g2["ret"])
+    # CGS2: the exchanges inside the orthogonalization's kernels (Xch)
+    import ggmres
+    g3 = d.solve(b, restart=30, max_iter=1500, tol=1e-10, flags=ggmres.SOLVE_CGS2)
+    out.update(x3=np.where(own, g3["x"], np.nan), hist3=g3["hist"], iters3=g3["iters"], ret3=g3["ret"])
 
 
 def main():

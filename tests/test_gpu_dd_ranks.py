@@ -86,9 +86,9 @@ def test_dd_ipc_ranks_match_local_and_oracle(case, tmp_path):
     # every rank holds the same plan and an identical control flow
     for r in rs[1:]:
         assert np.array_equal(r["q"], rs[0]["q"])
-        for k in ("hist", "hist2"):
+        for k in ("hist", "hist2", "hist3"):
             assert np.array_equal(r[k], rs[0][k]), k
-        for k in ("iters", "inner", "ret", "iters2", "ret2"):
+        for k in ("iters", "inner", "ret", "iters2", "ret2", "iters3", "ret3"):
             assert int(r[k]) == int(rs[0][k]), k
     inf = rs[0]["info"]
     assert inf[1] == P and inf[8] == 1            # nparts, one shard in this process
@@ -113,6 +113,12 @@ def test_dd_ipc_ranks_match_local_and_oracle(case, tmp_path):
     assert int(rs[0]["ret2"]) == g2["ret"] == 1 and int(rs[0]["iters2"]) == g2["iters"] == 40
     assert np.array_equal(rs[0]["hist2"], g2["hist"])
     assert np.array_equal(merge(rs, "x2"), g2["x"])
+    # CGS2 with the in-kernel exchanges: bit-identical to the launch-per-step path
+    import ggmres
+    g3 = loc.solve(b, restart=30, max_iter=1500, tol=1e-10, flags=ggmres.SOLVE_CGS2)
+    assert int(rs[0]["ret3"]) == g3["ret"] == 0 and int(rs[0]["iters3"]) == g3["iters"]
+    assert np.array_equal(rs[0]["hist3"], g3["hist"])
+    assert np.array_equal(merge(rs, "x3"), g3["x"])
     # the oracle on B in the sharded reduction order
     segs, G = zip(*[loc.dot_layout(p) for p in range(P)])
     loc.close()
