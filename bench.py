@@ -142,10 +142,10 @@ KERNEL_NAMES = {
 }
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 # bare dependent-chain latency of one wavefront step (cycles, tools/lat_probe.hip
-# built like the library, -ffp-contract=off, on MI355X: profiles/r03_lat_probe.txt
+# built like the library, -ffp-contract=off, on MI355X: profiles/r03/r03_lat_probe.txt
 # "step(dpp)" = unit L, "U step (WD_RCP)" = the bit-exact reciprocal-FMA
 # division, "U step (WD_MUL)" = GG_DIV_RCP's one multiply; "L step (UFMA)" /
-# "U step (SFMA)" = GG_DIV_FMA's fused rows, profiles/r03_lat_probe_fma.txt) and
+# "U step (SFMA)" = GG_DIV_FMA's fused rows, profiles/r03/r03_lat_probe_fma.txt) and
 # the shader clock
 CHAIN_CYCLES = {"trsv_L": 38.89, "trsv_U": 62.66, "trsv_U_mul": 43.72,
                 "trsv_L_fma": 29.19, "trsv_U_fma": 29.58}
@@ -670,8 +670,8 @@ def main():
     a.dd_grid = a.dd_grid or "c4"
     # rectangles / boxes (GG_PART_GRID: chains nx/px + ny/py (+ nz/pz)): C2
     # converges in 3,910 iterations vs the slabs' 6,369 at 4 shards
-    # (profiles/r04k_dd_4_*.json); C4 at 8 shards 230 vs 175 it/s
-    # (profiles/r04r_dd_c4grid_8.json vs r04q_dd_c4_8.json)
+    # (profiles/r04/r04k_dd_4_*.json); C4 at 8 shards 230 vs 175 it/s
+    # (profiles/r04/r04r_dd_c4grid_8.json vs r04q_dd_c4_8.json)
     a.dd_part = a.dd_part or "grid"
     replicas = a.workload == "replicas"
     if replicas:
@@ -916,7 +916,7 @@ def main():
                                       "cycle index i, averaged over the launches timed")
         # the triangular solves are latency-bound: their other roofline is the
         # dependency chain, nx + ny - 1 wavefront steps at the bare per-step chain
-        # latency (tools/lat_probe.hip on MI355X, profiles/r01_lat_probe.txt)
+        # latency (tools/lat_probe.hip on MI355X, profiles/r01/r01_lat_probe.txt)
         lat = None
         if name in ("trsv_L", "trsv_U") and s.uses_wavefront and not c5:
             # a non-unit L (the split engine's) divides like U
@@ -933,7 +933,7 @@ def main():
         elif name in ("trsv_L", "trsv_U") and not s.uses_wavefront:
             # the dataflow solve (k_trsv_flow): its chain is the triangle's level
             # count, each level one cross-workgroup hand-off (idle sc1 store -> sc1
-            # poll: 0.47 us same XCD, profiles/r04_xcd_handoff.txt)
+            # poll: 0.47 us same XCD, profiles/r04/r04_xcd_handoff.txt)
             lv = s.trsv_levels(0 if name == "trsv_L" else 1)
             floor_us = lv * 0.47
             lat = {"kernel": roof["kernel"], "bound": "dependency chain (levels x hand-off)", "critical_steps": lv,

@@ -97,7 +97,7 @@ struct gg_dd {
     Xch xch{};
     hipStream_t st = nullptr;
     hipStream_t st2 = nullptr;              // the SpMV's interface exchange, beside the interior rows
-    bool halo_inline = false;               // GG_DD_HALO_INLINE: exchange on st, no st2 overlap
+    bool halo_inline = true;                // GG_DD_HALO_INLINE=0: the exchange on st2 beside the interior rows
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evx = nullptr, evh = nullptr;
     bool have = false;
     int n = 0, nsep = 0, maxI = 0;
@@ -443,7 +443,8 @@ bool use_xk(gg_dd *d, int nk)
     // several ranks on one GPU: a rank's waiting blocks must not starve a
     // peer's producer of CUs -- only when every rank's grid fits one block per CU
     if (d->xk_shared && (long long)d->P * d->G > 256) return false;
-    return d->xk && d->sh.size() == 1 && nk <= kCgsXMax && d->G <= kIpcXF && (long long)nk * d->G <= d->ipc_capd &&
+    return d->xk && d->sh.size() == 1 && nk <= kCgsXMax &&
+           (long long)d->G * ((kCgsXMax + kCgsKC - 1) / kCgsKC) <= kIpcXF && (long long)nk * d->G <= d->ipc_capd &&
            (long long)d->G <= d->ipc_capd;
 }
 
@@ -529,6 +530,27 @@ void enqueue_cycle(gg_dd *d, int m)
                                           s.V.p + (long long)(i + 1) * Pl, s.H.p, s.cs.p, s.sn.p, s.s.p,
                                           s.hist.p, H0, d->st);
             }
+            prof_end(d, mk);
+            continue;
+        }
+        if (use_xk(d, 1)) {
+            // MGS on the in-kernel exchanges: i + 3 launches
+            Shard &s = *d->sh[0];
+            const Gate gt = gate_i(s, i);
+            double *pa = s.partA.p + (long long)s.p * d->G, *pb = s.partB.p + (long long)s.p * d->G;
+            unsigned long long q = ++d->ipc_seq;
+            launch_dot_x(gt, s.w.p, s.V.p, pa, d->G, dot_len(d, s), d->xch, q, d->st);
+            for (int k = 0; k <= i; k++) {
+                const double *vk = s.V.p + (long long)k * Pl;
+                const double *vn = (k < i) ? s.V.p + (long long)(k + 1) * Pl : nullptr;
+                const unsigned long long qn = ++d->ipc_seq;
+                launch_mgs_step_x(gt, i, k, m, s.w.p, vk, vn, pa, q, pb, s.H.p, d->G, H0, dot_len(d, s), d->xch, qn,
+                                  d->st);
+                std::swap(pa, pb);
+                q = qn;
+            }
+            launch_arnoldi_finalize_x(gt, i, m, s.ds.p, pa, q, d->G, s.w.p, s.V.p + (long long)(i + 1) * Pl, s.H.p,
+                                      s.cs.p, s.sn.p, s.s.p, s.hist.p, H0, d->xch, d->st);
             prof_end(d, mk);
             continue;
         }
@@ -981,8 +1003,10 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
     set_dev(d.get());
     GG_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
     {
+        // default: in line (round 5, loopback C2/8: the SpMV family 41 -> 16.5 us,
+        // C4/8 58 -> 47 us -- the event pair of the overlap cost more than it hid)
         const char *hi = std::getenv("GG_DD_HALO_INLINE");
-        d->halo_inline = hi && hi[0] == '1';
+        d->halo_inline = !(hi && hi[0] == '0');
     }
     GG_HIP(hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking));
     GG_HIP(hipEventCreate(&d->ev0));

@@ -129,8 +129,9 @@ void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long l
 // k_cgs_reduce's order (the same bits) and hand the value to every block of
 // the launch through `hx` / `hf` (this rank's uncached scratch).  Area of rank
 // q: [flags kMaxShards x kIpcXB][data 2 x P x capd][xflags kMaxShards x kIpcXF].
-constexpr int kIpcXF = 1024;           // in-kernel exchange flag words per source rank (>= the dot grid)
+constexpr int kIpcXF = 4096;           // in-kernel exchange flag words per source rank (>= 4 x the dot grid)
 constexpr int kCgsXMax = 32;           // dots per inner iteration the in-kernel path takes
+constexpr int kCgsKC = 8;              // dots per block of the multidot kernels (grid G x ceil(nk / 8))
 struct Xch {
     IpcPeers pp;                       // areas (loopback: this rank's own for every q)
     int me = 0, P = 1, loop = 0;       // loop: the peers' slots are this rank's own (timing only)
@@ -150,6 +151,14 @@ void launch_cgs_update_x(Gate g, double *w, const double *V, long long ldv, int 
                          long long Pdot, const double *part_in, unsigned long long sin, double *H, int i, int m,
                          bool add, double *part_out, double *norm_out, const Xch &x, unsigned long long sout,
                          hipStream_t st);
+// MGS on the same exchanges: <a, b> published as exchange seq; one MGS step
+// with h reduced from exchange sin, its next partials published as sout
+// (vnext null: the norm's)
+void launch_dot_x(Gate g, const double *a, const double *b, double *part, int G, long long Pdot, const Xch &x,
+                  unsigned long long seq, hipStream_t st);
+void launch_mgs_step_x(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
+                       const double *part_in, unsigned long long sin, double *part_out, double *H, int G,
+                       long long Ppad, long long Pdot, const Xch &x, unsigned long long sout, hipStream_t st);
 // k_arnoldi_finalize with the norm reduced from exchange sin
 void launch_arnoldi_finalize_x(Gate g, int i, int m, DevState *ds, const double *part_in, unsigned long long sin,
                                int G, const double *w, double *vnext, double *H, double *cs, double *sn,

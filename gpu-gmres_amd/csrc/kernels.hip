@@ -707,7 +707,7 @@ __device__ __forceinline__ void flow_long_row(int r, const int *__restrict__ rp,
 // ELL: short rows read their terms from the sliced copy (DevTri::eci / ev,
 // task {.z, .w}) instead of rp / ci / v: no rp -> ci -> poll chain of dependent
 // loads, one coalesced load per term index; the operations are the same (pgr:
-// L 84.0 -> 62.8, U 103.0 -> 68.9 us, profiles/r04y_pgr_e*.json; a software-
+// L 84.0 -> 62.8, U 103.0 -> 68.9 us, profiles/r04/r04y_pgr_e*.json; a software-
 // pipelined task loop -- the next task's loads behind this one's polls --
 // measured 67.1 / 73.1 us, r04z_pgr_e1.json, not kept).
 template <bool ELL>
@@ -1251,7 +1251,7 @@ struct FusedSpmv {
     int ns = 0;                             // SpMV blocks: blockIdx < ns, the bands after them
 };
 // slices per group: C2 fused L 92.5 / 87.0 / 85.8 us at 8 / 4 / 2 (a group's
-// chain is shorter with fewer loads per lane; profiles/r03_fs_knobs.txt)
+// chain is shorter with fewer loads per lane; profiles/r03/r03_fs_knobs.txt)
 constexpr int kFsGroup = 2;                 // (kWaveTAlign is a multiple)
 
 __device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands, int T, int nwv)
@@ -1854,7 +1854,7 @@ __global__ __launch_bounds__((WaveCfg<DIV>::THREADS)) void k_trsv_wave2d_spmv(
 #endif
 // 3 slots: 59-70 KiB of LDS, two workgroups per CU -- at the C4 wavefront's
 // peak more tiles are ready than there are CUs (C4 L 227 -> 222 us, U 234 ->
-// 233 us against 5 slots, profiles/r03_tile_ring.txt)
+// 233 us against 5 slots, profiles/r03/r03_tile_ring.txt)
 #ifndef GG_TILE_RING
 #define GG_TILE_RING 3
 #endif
@@ -1990,7 +1990,7 @@ __global__ __launch_bounds__(256) void k_trsv_tile3d(
     // while it runs and the smallest unfinished tile's owner has finished every
     // tile it claimed before it -- any grid drains, resident or not.  (The
     // queue is the fallback, not the default: C4 L / U 221.6 / 230.1 us static
-    // against 242.7 / 257.3 us claimed, profiles/r04_tile_queue_ab.txt.)
+    // against 242.7 / 257.3 us claimed, profiles/r04/r04_tile_queue_ab.txt.)
     // q[0] = next tile, q[16] = workgroups finished; the last one re-arms both.
     unsigned long long *q = gran + (long long)ntask * tgran + 128LL * kTileDummyBlocks;
     __shared__ int tq[2];                       // the current and the next claimed tile
@@ -2841,7 +2841,6 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
 // instead of MGS's i + 2.  Every dot keeps k_dot's tree (thread t of block b:
 // units b*256 + t + j*G*256 ascending, block_sum), so the oracle restates it
 // bit for bit (orc_set_orth).
-constexpr int kCgsKC = 8;                  // dots per block of k_multidot
 __global__ __launch_bounds__(kBlock) void k_multidot(Gate g, const double *__restrict__ w,
                                                      const double *__restrict__ V, long long ldv, int nk,
                                                      double *part, int G, long long dunits)
@@ -3045,6 +3044,12 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
 // the rest through hx / hf -- they are dispatched first and wait on nothing of
 // this launch.  Every spin is bounded (~30 s, err |= 4); after one time-out the
 // others give up at once (the broken word hf[kCgsXMax + 1]).
+// Memory ordering without cache maintenance: the areas and hx / hf are
+// uncached device memory, so a producer's stores are in memory once its
+// s_waitcnt has drained them, and a consumer's relaxed system-scope loads
+// issued after it saw the flag read memory.  No release / acquire here: on
+// gfx950 those write back / invalidate the whole L2 (the first version of this
+// path, with them: CGS2 64 -> 278 us per iteration at C2/8).
 __device__ __forceinline__ unsigned long long *xk_flag(void *base, int P, long long capd, int src)
 {
     return reinterpret_cast<unsigned long long *>(base) + (long long)kMaxShards * kIpcXB + 2LL * P * capd +
@@ -3061,7 +3066,7 @@ __device__ __noinline__ bool xk_wait_slow(const unsigned long long *f, unsigned 
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned n = 1;; n++) {
         __builtin_amdgcn_s_sleep(1);
-        if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= seq) return true;
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= seq) return true;
         if ((n & 255) == 0) {
             if (__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return false;
             if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {     // ~30 s of the 100 MHz clock
@@ -3074,50 +3079,94 @@ __device__ __noinline__ bool xk_wait_slow(const unsigned long long *f, unsigned 
 }
 __device__ __forceinline__ bool xk_wait(const unsigned long long *f, unsigned long long seq, const Xch &x)
 {
-    if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= seq) return true;
-    return xk_wait_slow(f, seq, x);
+    bool ok = true;
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) ok = xk_wait_slow(f, seq, x);
+    asm volatile("" ::: "memory");        // what follows reads after the flag was seen
+    return ok;
 }
 // thread t < n holds v for index idx of this rank's slot: into the own slot
 // and every peer's area, then this block's flag in every peer's area
-__device__ __forceinline__ void xk_publish(const Xch &x, unsigned long long seq, double *own, bool has,
-                                           long long idx, double v)
+__device__ __forceinline__ void st_sys(double *p, double v)
 {
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys(const double *p)
+{
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+__device__ __forceinline__ void xk_publish(const Xch &x, unsigned long long seq, double *own, bool has,
+                                           long long idx, double v, int fblock)
+{
+    // (loopback: this rank's area stands in for every peer's and receives the
+    // values in the slots and flags the peers' would use, q's for peer q)
     if (has) {
         own[idx] = v;
         for (int q = 0; q < x.P; q++)
-            if (q != x.me) xk_slot(x.pp.base[q], x.P, x.capd, seq, x.me)[idx] = v;
+            if (q != x.me) st_sys(xk_slot(x.pp.base[q], x.P, x.capd, seq, x.loop ? q : x.me) + idx, v);
     }
-    __threadfence_system();
+    __builtin_amdgcn_s_waitcnt(0);          // this thread's stores are in memory
     __syncthreads();
     const int t = threadIdx.x;
     if (t < x.P && t != x.me)
-        __hip_atomic_store(xk_flag(x.pp.base[t], x.P, x.capd, x.me) + blockIdx.x, seq, __ATOMIC_RELEASE,
+        __hip_atomic_store(xk_flag(x.pp.base[t], x.P, x.capd, x.loop ? t : x.me) + fblock, seq, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // dot k over every rank's G block partials, in k_cgs_reduce's order (e = q*G + b,
-// thread-strided, block_sum); own = this rank's slot
-__device__ __forceinline__ double xk_reduce(const Xch &x, unsigned long long seq, const double *own, int G, int k)
+// thread-strided, block_sum); own = this rank's slot.  A thread takes its
+// partials kXkChunk at a time: the chunk's flags polled together (relaxed,
+// only the pending ones re-polled), one acquire fence, the chunk's values
+// loaded together -- two memory round trips per chunk, not two per partial.
+constexpr int kXkChunk = 8;
+__device__ __forceinline__ double xk_reduce(const Xch &x, unsigned long long seq, const double *own, int G, int k,
+                                           int kfl = 0)
 {
+    // kfl: the producer's grid took kfl dots per block row (flag (k / kfl) * G + b), 0: one row
     double v = 0.0;
     void *mine = x.pp.base[x.me];
-    for (int e = threadIdx.x; e < x.P * G; e += kBlock) {
-        const int q = e / G, b = e % G;
-        const long long idx = (long long)k * G + b;
-        if (q == x.me) {
-            v += own[idx];
-        } else {
-            const int src = x.loop ? x.me : q;
-            (void)xk_wait(xk_flag(mine, x.P, x.capd, src) + b, seq, x);
-            v += xk_slot(mine, x.P, x.capd, seq, src)[idx];
+    const int PG = x.P * G;
+    const int frow = kfl ? (k / kfl) * G : 0;
+    for (int e0 = threadIdx.x; e0 < PG; e0 += kXkChunk * kBlock) {
+        unsigned long long f[kXkChunk];
+#pragma unroll
+        for (int j = 0; j < kXkChunk; j++) {
+            const int e = e0 + j * kBlock, q = e / G;
+            f[j] = ~0ull;
+            if (e < PG && q != x.me)
+                f[j] = __hip_atomic_load(xk_flag(mine, x.P, x.capd, q) + frow + e % G, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
         }
+#pragma unroll
+        for (int j = 0; j < kXkChunk; j++) {
+            if (f[j] < seq) {
+                const int e = e0 + j * kBlock, q = e / G;
+                (void)xk_wait(xk_flag(mine, x.P, x.capd, q) + frow + e % G, seq, x);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        asm volatile("" ::: "memory");
+        double val[kXkChunk];
+#pragma unroll
+        for (int j = 0; j < kXkChunk; j++) {
+            const int e = e0 + j * kBlock, q = e / G, b = e % G;
+            const long long idx = (long long)k * G + b;
+            val[j] = 0.0;
+            if (e < PG)
+                val[j] = q == x.me ? own[idx] : ld_sys(xk_slot(mine, x.P, x.capd, seq, q) + idx);
+        }
+#pragma unroll
+        for (int j = 0; j < kXkChunk; j++)
+            if (e0 + j * kBlock < PG) v += val[j];
     }
     return block_sum(v);
 }
 // a reducer's value to every block of the launch (thread 0)
 __device__ __forceinline__ void xk_post(const Xch &x, int slot, double v, unsigned long long seq)
 {
-    x.hx[slot] = v;
-    __hip_atomic_store(x.hf + slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    st_sys(x.hx + slot, v);
+    __builtin_amdgcn_s_waitcnt(0);
+    __hip_atomic_store(x.hf + slot, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // block_sum_store's sums, thread k < nk receiving sum k
 template <int NK>
@@ -3142,24 +3191,28 @@ __global__ __launch_bounds__(kBlock) void k_multidot_x(Gate g, const double *__r
                                                        double *part, int G, long long dunits, Xch x,
                                                        unsigned long long seq)
 {
+    // block (b, y): dots y*kCgsKC + kk as k_multidot; flag y*G + b
     if (gated(g)) return;
-    double acc[kCgsXMax];
+    const int k0 = blockIdx.y * kCgsKC;
+    const int kc = nk - k0 < kCgsKC ? nk - k0 : kCgsKC;
+    double acc[kCgsKC];
 #pragma unroll
-    for (int k = 0; k < kCgsXMax; k++) acc[k] = 0.0;
+    for (int kk = 0; kk < kCgsKC; kk++) acc[kk] = 0.0;
     const long long stride = (long long)gridDim.x * kBlock;
     for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < dunits; u += stride) {
         const double2 a = ld2(w, u);
 #pragma unroll
-        for (int k = 0; k < kCgsXMax; k++) {
-            if (k < nk) {
-                const double2 b = ld2_nt(V + (long long)k * ldv, u);
-                acc[k] += a.x * b.x;
-                acc[k] += a.y * b.y;
+        for (int kk = 0; kk < kCgsKC; kk++) {
+            if (kk < kc) {
+                const double2 b = ld2_nt(V + (long long)(k0 + kk) * ldv, u);
+                acc[kk] += a.x * b.x;
+                acc[kk] += a.y * b.y;
             }
         }
     }
-    const double v = block_sum_pick<kCgsXMax>(acc, nk);
-    xk_publish(x, seq, part, threadIdx.x < nk, (long long)threadIdx.x * G + blockIdx.x, v);
+    const double v = block_sum_pick<kCgsKC>(acc, kc);
+    xk_publish(x, seq, part, threadIdx.x < kc, (long long)(k0 + threadIdx.x) * G + blockIdx.x, v,
+               blockIdx.y * gridDim.x + blockIdx.x);
 }
 
 // h = reduced exchange sin (H[k, i] = h, or += with add); w -= V h; then
@@ -3171,12 +3224,12 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update_x(Gate g, double *__restr
                                                          long long units, long long dunits, int G,
                                                          const double *part_in, unsigned long long sin, double *H,
                                                          int i, int m, int add, double *part_out, Xch x,
-                                                         unsigned long long sout)
+                                                         unsigned long long sout, int kfl)
 {
     if (gated(g)) return;
     __shared__ double hs[kCgsXMax];
     for (int k = blockIdx.x; k < nk; k += gridDim.x) {
-        const double v = xk_reduce(x, sin, part_in, G, k);
+        const double v = xk_reduce(x, sin, part_in, G, k, kfl);
         if (threadIdx.x == 0) {
             double *hk = H + k + (long long)i * (m + 1);
             *hk = add ? *hk + v : v;
@@ -3185,7 +3238,7 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update_x(Gate g, double *__restr
     }
     if (threadIdx.x < nk) {
         (void)xk_wait(x.hf + threadIdx.x, sin, x);
-        hs[threadIdx.x] = x.hx[threadIdx.x];
+        hs[threadIdx.x] = ld_sys(x.hx + threadIdx.x);
     }
     __syncthreads();
     double acc[DOTS ? kCgsXMax : 1];
@@ -3214,11 +3267,101 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update_x(Gate g, double *__restr
     }
     if constexpr (DOTS) {
         const double v = block_sum_pick<kCgsXMax>(acc, nk);
-        xk_publish(x, sout, part_out, threadIdx.x < nk, (long long)threadIdx.x * G + blockIdx.x, v);
+        xk_publish(x, sout, part_out, threadIdx.x < nk, (long long)threadIdx.x * G + blockIdx.x, v, blockIdx.x);
     } else {
         const double v = block_sum(acc[0]);
-        xk_publish(x, sout, part_out, threadIdx.x == 0, blockIdx.x, v);
+        xk_publish(x, sout, part_out, threadIdx.x == 0, blockIdx.x, v, blockIdx.x);
     }
+}
+
+// MGS of the sharded solve on the same exchanges (the reference's
+// orthogonalization, i + 3 launches per inner iteration instead of 2i + 5):
+// k_dot_x = k_dot publishing its partials; k_mgs_step_x = k_mgs_step with h
+// reduced from exchange sin by block 0 (sum_partials' order over the P*G
+// partials) and its partials published as exchange sout
+__global__ __launch_bounds__(kBlock) void k_dot_x(Gate g, const double *a, const double *b, double *part,
+                                                  long long units, Xch x, unsigned long long seq)
+{
+    if (gated(g)) return;
+    double acc = 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x; u0 < units; u0 += 4 * stride) {
+        double2 p[4], q[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const long long u = u0 + j * stride;
+            if (u < units) { p[j] = ld2(a, u); q[j] = ld2(b, u); }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (u0 + j * stride < units) {
+                acc += p[j].x * q[j].x;
+                acc += p[j].y * q[j].y;
+            }
+        }
+    }
+    acc = block_sum(acc);
+    xk_publish(x, seq, part, threadIdx.x == 0, blockIdx.x, acc, blockIdx.x);
+}
+template <bool NORM>
+__global__ __launch_bounds__(kBlock) void k_mgs_step_x(Gate g, int i, int k, int m, double *__restrict__ w,
+                                                       const double *__restrict__ vk,
+                                                       const double *__restrict__ vnext, const double *part_in,
+                                                       unsigned long long sin, double *part_out, double *H, int G,
+                                                       long long units, long long dunits, Xch x,
+                                                       unsigned long long sout)
+{
+    if (gated(g)) return;
+    __shared__ double hsh;
+    double acc = 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x;
+    double2 wv[kUnroll], vv[kUnroll], nv[kUnroll];
+    auto load = [&]() {
+#pragma unroll
+        for (int j = 0; j < kUnroll; j++) {
+            const long long u = u0 + j * stride;
+            if (u < units) {
+                wv[j] = ld2(w, u);
+                vv[j] = ld2_nt(vk, u);
+                if (!NORM) nv[j] = ld2_nt(vnext, u);
+            }
+        }
+    };
+    load();                 // the first chunk is in flight while h is summed
+    if (blockIdx.x == 0) {
+        const double v = xk_reduce(x, sin, part_in, G, 0);
+        if (threadIdx.x == 0) {
+            H[k + i * (m + 1)] = v;
+            xk_post(x, 0, v, sin);
+        }
+    }
+    if (threadIdx.x == 0) {
+        (void)xk_wait(x.hf, sin, x);
+        hsh = ld_sys(x.hx);
+    }
+    __syncthreads();
+    const double a = -hsh;
+    while (u0 < units) {
+#pragma unroll
+        for (int j = 0; j < kUnroll; j++) {
+            const long long u = u0 + j * stride;
+            if (u < units) {
+                wv[j].x = a * vv[j].x + wv[j].x;
+                wv[j].y = a * vv[j].y + wv[j].y;
+                st2(w, u, wv[j]);
+                if (NORM) nv[j] = wv[j];
+                if (u < dunits) {
+                    acc += wv[j].x * nv[j].x;
+                    acc += wv[j].y * nv[j].y;
+                }
+            }
+        }
+        u0 += kUnroll * stride;
+        load();
+    }
+    acc = block_sum(acc);
+    xk_publish(x, sout, part_out, threadIdx.x == 0, blockIdx.x, acc, blockIdx.x);
 }
 
 // k_arnoldi_finalize, ||w||^2 reduced from exchange sin by block 0
@@ -3236,7 +3379,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize_x(Gate g, int i, in
     }
     if (threadIdx.x == 0) {
         (void)xk_wait(x.hf + kCgsXMax, sin, x);
-        nrm2 = x.hx[kCgsXMax];
+        nrm2 = ld_sys(x.hx + kCgsXMax);
     }
     __syncthreads();
     const double hn = sqrt(nrm2);
@@ -3281,7 +3424,7 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize_x(Gate g, int i, in
 // the per-step kernels'.  Needs all G blocks resident (checked on the host);
 // every spin is bounded (err bit 0).
 // Co-residency: the grid is sized from the occupancy API, which
-// has over-promised on this pool (profiles/r03_gather_ab.txt).  So the kernels
+// has over-promised on this pool (profiles/r03/r03_gather_ab.txt).  So the kernels
 // do not trust it: the FIRST all-gather of a launch waits at most kResidSpin
 // polls; a block that times out there sets DONE_ABORT in the control block
 // (agent-scope atomic, drained before the block exits) and leaves.  A block
@@ -3427,7 +3570,7 @@ __device__ __forceinline__ bool gather_first(const unsigned long long *row, int 
 // publishes the sum in one granule hg; the other blocks' thread 0 polls that
 // granule and hands the value over through LDS -- G line requests per poll
 // round instead of G x G/32 on the few channels that hold the row, for one
-// more hop.  Measured (C2 / C4, profiles/r03_gather_ab.txt): k_arnoldi_wide
+// more hop.  Measured (C2 / C4, profiles/r03/r03_gather_ab.txt): k_arnoldi_wide
 // (C4, streaming the basis beside the polls) 472.5 -> 456.6 us, so it leads;
 // k_arnoldi_persist (C2) 73.2 -> 77.5 us, so every block gathers there.
 template <bool LEADER, int NP = kGatherPer>
@@ -3482,7 +3625,7 @@ __device__ __forceinline__ bool gather_h_first(const unsigned long long *row, un
 // XCD's slot; the XCD's other blocks poll that slot (thread 0, sc1 loads).
 // A plain store keeps the line in the XCD's L2, where the sc1 (L1-bypassing)
 // polls of the same XCD find it: 234 / 677 ns a hop idle / streaming against
-// 470 / 740 for sc1 stores (profiles/r04_xcd_handoff.txt).  Correct by
+// 470 / 740 for sc1 stores (profiles/r04/r04_xcd_handoff.txt).  Correct by
 // construction, not by placement: a block polls only the slot of the XCD it
 // runs on (HW_REG_XCC_ID), which only a reducer ON that XCD writes.  8 pollers
 // of the G-granule row instead of G.
@@ -4453,7 +4596,7 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
             const long long wave_slots = 4LL * std::max(cus, 1);          // 4 waves per block, 1 block per CU
             // (the randomly permuted PG split, 1,100 tasks per level: 2 blocks per
             // CU 84 / 102 us for L / U against 95 / 127 at 4 and 102 / 131 at 8,
-            // profiles/r04s_pgr_bpc*.json -- so the extra factor 2 only beyond
+            // profiles/r04/r04s_pgr_bpc*.json -- so the extra factor 2 only beyond
             // two waves per slot)
             const long long wpl = (per_level + wave_slots - 1) / wave_slots;
             const int bpc = bpc_s ? std::max(1, atoi(bpc_s))
@@ -4683,7 +4826,7 @@ void launch_multidot_x(Gate g, const double *w, const double *V, long long ldv, 
                        long long Pdot, const Xch &x, unsigned long long seq, hipStream_t st)
 {
     // (the caller checks nk <= kCgsXMax, G <= kIpcXF, nk * G <= x.capd)
-    k_multidot_x<<<G, kBlock, 0, st>>>(g, w, V, ldv, nk, part, G, Pdot / 2, x, seq);
+    k_multidot_x<<<dim3(G, (nk + kCgsKC - 1) / kCgsKC), kBlock, 0, st>>>(g, w, V, ldv, nk, part, G, Pdot / 2, x, seq);
 }
 void launch_cgs_update_x(Gate g, double *w, const double *V, long long ldv, int nk, int G, long long Ppad,
                          long long Pdot, const double *part_in, unsigned long long sin, double *H, int i, int m,
@@ -4692,10 +4835,26 @@ void launch_cgs_update_x(Gate g, double *w, const double *V, long long ldv, int 
 {
     if (part_out)
         k_cgs_update_x<true><<<G, kBlock, 0, st>>>(g, w, V, ldv, nk, Ppad / 2, Pdot / 2, G, part_in, sin, H, i, m,
-                                                    add ? 1 : 0, part_out, x, sout);
+                                                    add ? 1 : 0, part_out, x, sout, add ? 0 : kCgsKC);
     else
         k_cgs_update_x<false><<<G, kBlock, 0, st>>>(g, w, V, ldv, nk, Ppad / 2, Pdot / 2, G, part_in, sin, H, i,
-                                                     m, add ? 1 : 0, norm_out, x, sout);
+                                                     m, add ? 1 : 0, norm_out, x, sout, add ? 0 : kCgsKC);
+}
+void launch_dot_x(Gate g, const double *a, const double *b, double *part, int G, long long Pdot, const Xch &x,
+                  unsigned long long seq, hipStream_t st)
+{
+    k_dot_x<<<G, kBlock, 0, st>>>(g, a, b, part, Pdot / 2, x, seq);
+}
+void launch_mgs_step_x(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
+                       const double *part_in, unsigned long long sin, double *part_out, double *H, int G,
+                       long long Ppad, long long Pdot, const Xch &x, unsigned long long sout, hipStream_t st)
+{
+    if (!vnext)
+        k_mgs_step_x<true><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, nullptr, part_in, sin, part_out, H, G, Ppad / 2,
+                                                  Pdot / 2, x, sout);
+    else
+        k_mgs_step_x<false><<<G, kBlock, 0, st>>>(g, i, k, m, w, vk, vnext, part_in, sin, part_out, H, G, Ppad / 2,
+                                                   Pdot / 2, x, sout);
 }
 void launch_arnoldi_finalize_x(Gate g, int i, int m, DevState *ds, const double *part_in, unsigned long long sin,
                                int G, const double *w, double *vnext, double *H, double *cs, double *sn,

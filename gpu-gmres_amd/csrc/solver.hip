@@ -1007,7 +1007,7 @@ void enqueue_cycle(gg_solver *s, int m)
             // gathers (the same division per term, k_spmv_sell<.., XDIV>) --
             // on grid-ordered factors, whose gathers are local (netlist 3,595
             // -> 3,635 it/s; on the randomly permuted split the second gather
-            // doubles the SpMV's misses, 49.8 -> 112.7 us: profiles/r04p_*_x*.json)
+            // doubles the SpMV's misses, 49.8 -> 112.7 us: profiles/r04/r04p_*_x*.json)
             launch_mul(gi, vi, s->mid_l.p, s->t1.p, (int)s->P, s->st);
             trsv(s, gi, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
             mk = prof_begin(s, GG_PROF_SPMV, i);

@@ -40,13 +40,17 @@ def _port():
         return sk.getsockname()[1]
 
 
-def run_ranks(mode, P, outdir, timeout=240):
-    """start P rank processes, wait for all; kill exactly those on failure"""
+def run_ranks(mode, P, outdir, timeout=240, xk=None):
+    """start P rank processes, wait for all; kill exactly those on failure
+    (xk: GG_DD_XK for the ranks -- the orthogonalization's exchanges inside its
+    kernels, 1, or as separate all-gather launches, 0)"""
     port = _port()
     procs = []
     for r in range(P):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(P), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), OMP_NUM_THREADS="2")
+        if xk is not None:
+            env["GG_DD_XK"] = str(xk)
         procs.append(subprocess.Popen([sys.executable, "-u", WORKER, mode, str(outdir)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -77,10 +81,11 @@ def merge(rs, key):
     return v
 
 
+@pytest.mark.parametrize("xk", [0, 1])
 @pytest.mark.parametrize("case", sorted(W.CASES))
-def test_dd_ipc_ranks_match_local_and_oracle(case, tmp_path):
+def test_dd_ipc_ranks_match_local_and_oracle(case, xk, tmp_path):
     P = int(case.split("_P")[1][0])
-    rs = run_ranks(f"ipc:{case}", P, tmp_path)
+    rs = run_ranks(f"ipc:{case}", P, tmp_path, xk=xk)
     A, method = W.system(case)
     n = A.shape[0]
     # every rank holds the same plan and an identical control flow
@@ -92,6 +97,7 @@ def test_dd_ipc_ranks_match_local_and_oracle(case, tmp_path):
             assert int(r[k]) == int(rs[0][k]), k
     inf = rs[0]["info"]
     assert inf[1] == P and inf[8] == 1            # nparts, one shard in this process
+    assert int(inf[10]) == xk                     # the in-kernel exchanges ran (or not)
     # the same decomposition in one process (GG_DD_LOCAL), the same inputs
     loc = DD(P, device=0)
     loc.set_system(A, method)
