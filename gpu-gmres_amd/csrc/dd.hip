@@ -88,9 +88,10 @@ struct gg_dd {
     // differ, so the communicator is unusable -- every later exchange is
     // refused with GG_ESTATE (create a new gg_dd to recover)
     bool ipc_broken = false;
-    // CGS2 with the exchanges inside the kernels (GG_DD_IPC / GG_DD_LOOPBACK,
-    // P > 1; GG_DD_XK=0 turns it off): the areas above (loopback: this rank's
-    // own as every peer's) and the reducers' hand-off words (uncached)
+    // CGS2 / MGS with the exchanges inside the kernels (GG_DD_IPC /
+    // GG_DD_LOOPBACK, P > 1, GG_DD_XK=1): the areas above (loopback: this
+    // rank's own standing in for every peer's) and the reducers' hand-off
+    // words (uncached)
     bool xk = false;
     bool xk_shared = false;                 // IPC peers on this rank's own GPU (tests)
     void *xk_local = nullptr;
@@ -1044,8 +1045,13 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
         for (int q = 0; q < nparts; q++) d->ipc.base[q] = d->ipc_area;
     }
     if ((comm == GG_DD_IPC || comm == GG_DD_LOOPBACK) && nparts > 1) {
+        // off by default: measured slower than the launch-per-exchange path
+        // (loopback C2/8, one box: CGS2 81 vs 52.5 us per iteration, C4/8 256 vs
+        // 193 us; profiles/r05/xk_ab.txt) -- the uncached-memory round trips of
+        // the reducers' hand-off inside a launch cost more than the launch
+        // boundaries they replace.  GG_DD_XK=1 turns it on.
         const char *xk = std::getenv("GG_DD_XK");
-        d->xk = !(xk && xk[0] == '0');
+        d->xk = xk && xk[0] == '1';
         const size_t bytes = 2 * 64 * sizeof(double);            // hx[64] | hf[64]
         GG_HIP(hipExtMallocWithFlags(&d->xk_local, bytes, hipDeviceMallocUncached));
         GG_HIP(hipMemset(d->xk_local, 0, bytes));
