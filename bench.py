@@ -892,7 +892,8 @@ def main():
         f["share_of_step"] = round(f["est_ms_timed_region"] / (el * 1e3), 4)
     dom = max(timed, key=lambda k: timed[k]["est_ms_timed_region"]) if timed else None
 
-    pmc_wl = "c4" if c4 else "c3s" if c3s else "pg" if pg else "netlist" if netlist else None
+    pmc_wl = ("c4" if c4 else "c3s" if c3s else ("pgr" if a.pg_perm == "random" else "pg") if pg
+              else "netlist" if netlist else None)
 
     def roof_of(name):
         """(roofline, latency_roofline) of one timed family"""

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Refresh the committed profile set on a GPU box (run through gpurun from the repo root):
-#   tools/profile_round.sh TAG [WORKLOAD]        (WORKLOAD: c2 (default), c4, pg, c5, c3s)
+#   tools/profile_round.sh TAG [WORKLOAD]        (WORKLOAD: c2 (default), c4, pg, pgr, netlist, c5, c3, c3s)
 # writes gpurun_out/prof_TAG[_WORKLOAD]/{bench.json, kernel_stats.csv, pmc_traffic.json}
 # Each GPU step has its own time limit; the steps are chained with && so the
 # script ends at the first failure.
@@ -10,6 +10,7 @@ WL=${2:-c2}
 OUT=gpurun_out/prof_${TAG}_${WL}
 ARGS=""
 [ "$WL" = c2 ] || ARGS="--workload $WL"
+[ "$WL" = pgr ] && ARGS="--workload pg --pg-perm random"      # the split on the flow kernel
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u bench.py $ARGS > $OUT/bench.json 2> $OUT/bench.err
