@@ -710,6 +710,10 @@ __device__ __forceinline__ void flow_long_row(int r, const int *__restrict__ rp,
 // L 84.0 -> 62.8, U 103.0 -> 68.9 us, profiles/r04/r04y_pgr_e*.json; a software-
 // pipelined task loop -- the next task's loads behind this one's polls --
 // measured 67.1 / 73.1 us, r04z_pgr_e1.json, not kept).
+// s_sleep between a wave's poll rounds while a lane waits on a source
+#ifndef GG_FLOW_SLEEP
+#define GG_FLOW_SLEEP 4
+#endif
 template <bool ELL>
 __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const int4 *__restrict__ tasks,
                                                       const int *__restrict__ rows,
@@ -788,7 +792,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                     }
                 }
                 if (__any(pending)) {
-                    __builtin_amdgcn_s_sleep(4);
+                    __builtin_amdgcn_s_sleep(GG_FLOW_SLEEP);
                     if (++spins > kSpinLimit) {
                         if (pending) atomicOr(err, 1);
                         pending = false;
@@ -831,7 +835,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                 }
             }
             if (__any(pending)) {
-                __builtin_amdgcn_s_sleep(4);
+                __builtin_amdgcn_s_sleep(GG_FLOW_SLEEP);
                 if (++spins > kSpinLimit) {
                     if (pending) atomicOr(err, 1);
                     pending = false;
