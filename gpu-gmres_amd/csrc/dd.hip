@@ -233,16 +233,58 @@ void exchange(gg_dd *d, const Get &buf, long long off, long long cnt, hipStream_
     }
 }
 void exchange(gg_dd *d, const Get &buf, long long off, long long cnt) { exchange(d, buf, off, cnt, d->st); }
+// every shard's interface values of vector x -> every shard's halo slots
+// (x + H0 + q*maxI), and (f0 / f1, nf > 0) nf words of two vectors of every
+// shard set to the sentinel: the gather in the exchange's launch where the
+// exchange is a kernel of ours (GG_DD_LOCAL / LOOPBACK / IPC: one launch instead
+// of a gather per shard plus the all-gather), RCCL: gathers + ncclAllGather
+void gather_exchange(gg_dd *d, const Get &x, hipStream_t st, const Get &f0 = Get{}, const Get &f1 = Get{},
+                     long long nf = 0)
+{
+    const long long H0 = d->H0, mI = d->maxI;
+    if (d->kind == GG_DD_RCCL) {
+        for (auto &sp : d->sh) {
+            Shard &s = *sp;
+            double *v = x(s);
+            launch_gather(v, s.iface_slot.p, v + H0 + (long long)s.p * mI, mI, st, f0 ? f0(s) : nullptr,
+                          f1 ? f1(s) : nullptr, nf);
+        }
+        exchange(d, x, H0, mI, st);
+        return;
+    }
+    if (d->kind == GG_DD_IPC) {
+        Shard &s = *d->sh[0];
+        launch_ipc_gather_allgather(d->ipc, d->rank, d->P, x(s), s.iface_slot.p, x(s) + H0, mI, ++d->ipc_seq,
+                                    d->ipc_capd, d->xerr.p, f0 ? f0(s) : nullptr, f1 ? f1(s) : nullptr, nf, st);
+        return;
+    }
+    ShardPtrs b{};
+    IdxPtrs gi{};
+    FillPtrs fl{};
+    if (d->kind == GG_DD_LOOPBACK) {
+        Shard &s = *d->sh[0];
+        for (int q = 0; q < d->P; q++) {
+            b.p[q] = x(s);
+            gi.p[q] = s.iface_slot.p;
+        }
+        fl.f0[0] = f0 ? f0(s) : nullptr;
+        fl.f1[0] = f1 ? f1(s) : nullptr;
+    } else {
+        for (auto &sp : d->sh) {
+            Shard &s = *sp;
+            b.p[s.p] = x(s);
+            gi.p[s.p] = s.iface_slot.p;
+            fl.f0[s.p] = f0 ? f0(s) : nullptr;
+            fl.f1[s.p] = f1 ? f1(s) : nullptr;
+        }
+    }
+    launch_gather_allgather_local(b, gi, d->P, H0, mI, fl, nf, st);
+}
 // own interface values of vector x -> halo slot p, then the all-gather
 void halo(gg_dd *d, const Get &x, hipStream_t st)
 {
     if (d->maxI == 0 || d->P == 1) return;
-    for (auto &sp : d->sh) {
-        Shard &s = *sp;
-        double *v = x(s);
-        launch_gather(v, s.iface_slot.p, v + d->H0 + (long long)s.p * d->maxI, d->maxI, st);
-    }
-    exchange(d, x, d->H0, d->maxI, st);
+    gather_exchange(d, x, st);
 }
 
 Get vec(DBuf<double> Shard::*m) { return [m](Shard &s) { return (s.*m).p; }; }
@@ -303,16 +345,18 @@ void apply_minv(gg_dd *d, int gi, int mask, const Get &in, const Get &out)
     mk = prof_begin(d, GG_DD_PROF_SEP, gi);
     // interface y (halo); the fused separator step's sentinel fills ride on the gathers
     const bool xch = d->maxI > 0 && d->P > 1;
-    for (auto &sp : d->sh) {
-        Shard &s = *sp;
-        double *f0 = s.sepflow ? s.t1.p + S0 : nullptr, *f1 = s.sepflow ? out(s) + S0 : nullptr;
-        if (xch)
-            launch_gather(s.t1.p, s.iface_slot.p, s.t1.p + d->H0 + (long long)s.p * d->maxI, d->maxI, d->st, f0, f1,
-                          s.sepflow ? s.nS : 0);
-        else if (s.sepflow)
-            launch_gather(s.t1.p, s.iface_slot.p, s.t1.p, 0, d->st, f0, f1, s.nS);
+    if (xch) {
+        // (the separator is replicated: nS is the same on every shard)
+        const Shard &s0 = *d->sh[0];
+        gather_exchange(d, vec(&Shard::t1), d->st, [S0](Shard &s) { return s.sepflow ? s.t1.p + S0 : nullptr; },
+                        [S0, &out](Shard &s) { return s.sepflow ? out(s) + S0 : nullptr; },
+                        s0.sepflow ? s0.nS : 0);
+    } else {
+        for (auto &sp : d->sh) {
+            Shard &s = *sp;
+            if (s.sepflow) launch_gather(s.t1.p, s.iface_slot.p, s.t1.p, 0, d->st, s.t1.p + S0, out(s) + S0, s.nS);
+        }
     }
-    if (xch) exchange(d, vec(&Shard::t1), d->H0, d->maxI, d->st);
     for (auto &sp : d->sh) {
         Shard &s = *sp;
         Gate g = gate(s);

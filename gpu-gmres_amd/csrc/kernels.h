@@ -110,6 +110,15 @@ void launch_sep_flow(Gate g, int ntask, const int4 *tasks, const int *rows, cons
 struct ShardPtrs { double *p[kMaxShards]; };
 // every shard's slot (b.p[s] + off + s*cnt, cnt doubles) copied to every other shard
 void launch_allgather_local(const ShardPtrs &b, int P, long long off, long long cnt, hipStream_t st);
+// The interface exchange with its gather in the same launch (the SpMV halo and
+// the separator step's interface values): shard s's slot is formed from its
+// own vector, b.p[s][gi.p[s][e]] (-1: 0), and stored into every shard's slot s
+// (own included); f0 / f1: nf words of each shard set to the sentinel (the
+// fills k_gather carried).  Loopback: every pointer is the one shard's.
+struct IdxPtrs { const long long *p[kMaxShards]; };
+struct FillPtrs { double *f0[kMaxShards], *f1[kMaxShards]; };
+void launch_gather_allgather_local(const ShardPtrs &b, const IdxPtrs &gi, int P, long long off, long long cnt,
+                                   const FillPtrs &fl, long long nf, hipStream_t st);
 void launch_scatter_idx(const double *in, const long long *src, const long long *dst, double *out,
                         long long n, hipStream_t st);   // out[dst[i]] = in[src[i]]
 // GG_DD_IPC: the exchange areas of all ranks as mapped in this process
@@ -119,6 +128,11 @@ struct IpcPeers { void *base[kMaxShards]; };
 // me already in place); err |= 4 when a peer did not arrive in time
 void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long long cnt,
                           unsigned long long seq, long long capd, int *err, hipStream_t st);
+// the same with this rank's slot gathered in the launch: buf[me*cnt + e] =
+// x[gidx[e]] (-1: 0) first, and nf words of f0 / f1 set to the sentinel
+void launch_ipc_gather_allgather(const IpcPeers &pp, int me, int P, const double *x, const long long *gidx,
+                                 double *buf, long long cnt, unsigned long long seq, long long capd, int *err,
+                                 double *f0, double *f1, long long nf, hipStream_t st);
 
 // The CGS2 exchanges inside the kernels (GG_DD_IPC / GG_DD_LOOPBACK, one shard
 // per process, inner iterations with i + 1 <= kCgsXMax): a producer kernel

@@ -307,6 +307,27 @@ __global__ void k_allgather_local(ShardPtrs b, int P, long long off, long long c
             if (q != src) b.p[q][off + e] = v;
     }
 }
+// k_allgather_local with each shard's slot gathered from its own vector in the
+// same launch (kernels.h launch_gather_allgather_local)
+__global__ void k_gather_allgather_local(ShardPtrs b, IdxPtrs gi, int P, long long off, long long cnt, FillPtrs fl,
+                                         long long nf)
+{
+    const long long tot = P * cnt;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot;
+         e += (long long)gridDim.x * blockDim.x) {
+        const int src = (int)(e / cnt);
+        const long long s = gi.p[src][e - src * cnt];
+        const double v = s < 0 ? 0.0 : b.p[src][s];
+        for (int q = 0; q < P; q++) b.p[q][off + e] = v;
+    }
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nf;
+         i += (long long)gridDim.x * blockDim.x) {
+        for (int q = 0; q < P; q++) {
+            if (fl.f0[q]) reinterpret_cast<unsigned long long *>(fl.f0[q])[i] = kSentinel;
+            if (fl.f1[q]) reinterpret_cast<unsigned long long *>(fl.f1[q])[i] = kSentinel;
+        }
+    }
+}
 // GG_DD_IPC all-gather: one process per shard, every shard's exchange area
 // mapped into every process (hipIpc; xGMI between GPUs).  Area of rank q:
 // [flags: kMaxShards x kIpcXB u64][data: 2 parities x P slots x capd doubles].
@@ -320,16 +341,30 @@ __global__ void k_allgather_local(ShardPtrs b, int P, long long off, long long c
 // finished copying out exchange k-1.  The area is uncached device memory
 // (hipDeviceMallocUncached): remote stores and local polls need no cache
 // maintenance beyond the system-scope release / acquire.
+// gidx (k_ipc_gather_allgather's form): this rank's slot is gathered first,
+// buf[me*cnt + e] = x[gidx[e]] (-1: 0), by the block that sends it
 __global__ __launch_bounds__(kBlock) void k_ipc_allgather(IpcPeers pp, int me, int P, double *buf,
                                                           long long cnt, unsigned long long seq,
-                                                          long long capd, int *err)
+                                                          long long capd, int *err, const double *x,
+                                                          const long long *gidx, unsigned long long *f0,
+                                                          unsigned long long *f1, long long nf)
 {
     const int nb = gridDim.x, b = blockIdx.x, t = threadIdx.x;
     const long long chunk = (cnt + nb - 1) / nb;
     const long long lo = (long long)b * chunk, hi = lo + chunk < cnt ? lo + chunk : cnt;
     const int par = (int)(seq & 1);
     constexpr long long kFlagWords = (long long)kMaxShards * kIpcXB;
-    const double *src = buf + (long long)me * cnt;
+    double *src = buf + (long long)me * cnt;
+    if (gidx) {
+        for (long long e = lo + t; e < hi; e += kBlock) {
+            const long long s = gidx[e];
+            src[e] = s < 0 ? 0.0 : x[s];
+        }
+    }
+    for (long long i = b * (long long)kBlock + t; i < nf; i += (long long)nb * kBlock) {
+        f0[i] = kSentinel;
+        f1[i] = kSentinel;
+    }
     for (int q = 0; q < P; q++) {
         if (q == me) continue;
         double *dst = reinterpret_cast<double *>(pp.base[q]) + kFlagWords + ((long long)par * P + me) * capd;
@@ -4348,7 +4383,26 @@ void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long l
 {
     // every rank must pick the same block count for the same cnt
     const int nb = (int)std::min<long long>(kIpcXB, std::max<long long>(1, (cnt + 2047) / 2048));
-    k_ipc_allgather<<<nb, kBlock, 0, st>>>(pp, me, P, buf, cnt, seq, capd, err);
+    k_ipc_allgather<<<nb, kBlock, 0, st>>>(pp, me, P, buf, cnt, seq, capd, err, nullptr, nullptr, nullptr, nullptr,
+                                           0);
+}
+void launch_ipc_gather_allgather(const IpcPeers &pp, int me, int P, const double *x, const long long *gidx,
+                                 double *buf, long long cnt, unsigned long long seq, long long capd, int *err,
+                                 double *f0, double *f1, long long nf, hipStream_t st)
+{
+    // the block count depends on cnt only, as launch_ipc_allgather's (every rank the same)
+    const int nb = (int)std::min<long long>(kIpcXB, std::max<long long>(1, (cnt + 2047) / 2048));
+    if (!f0 || !f1) nf = 0;
+    k_ipc_allgather<<<nb, kBlock, 0, st>>>(pp, me, P, buf, cnt, seq, capd, err, x, gidx,
+                                           reinterpret_cast<unsigned long long *>(f0),
+                                           reinterpret_cast<unsigned long long *>(f1), nf);
+}
+void launch_gather_allgather_local(const ShardPtrs &b, const IdxPtrs &gi, int P, long long off, long long cnt,
+                                   const FillPtrs &fl, long long nf, hipStream_t st)
+{
+    if (P * cnt == 0 && nf == 0) return;
+    k_gather_allgather_local<<<blocks_for(std::max(P * cnt, nf), kBlock, 8192), kBlock, 0, st>>>(b, gi, P, off, cnt,
+                                                                                             fl, nf);
 }
 void launch_scatter_idx(const double *in, const long long *src, const long long *dst, double *out,
                         long long n, hipStream_t st)
