@@ -130,7 +130,10 @@ def parse():
     p.add_argument("--c5-scenarios", type=int, default=1,
                    help="c5: independent source scenarios per GPU, solved concurrently (one solver, "
                         "stream and host thread each; GG_SOLVE_SHARED_DEVICE)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.dd_comm == "loopback" and (a.gpus > 1 or not 0 <= a.dd_rank < a.dd_parts):
+        p.error("--dd-comm loopback times one rank alone: --gpus 1 and 0 <= --dd-rank < --dd-parts")
+    return a
 
 
 # bench family -> the kernel it times (rocprofv3 kernel names in profiles/)

@@ -113,3 +113,20 @@ def test_ipc_setup_lockstep_fallback(tmp_path, fail):
     for r in res:
         assert r["ok"] == (fail == "none")
         assert r["ran"] == order[:stop]          # every rank stopped after the same step
+
+
+@pytest.mark.parametrize("argv", [["--gpus", "2"], ["--dd-rank", "8"], ["--dd-rank", "-1"]])
+def test_loopback_refuses_other_than_one_rank_alone(argv, monkeypatch, capsys):
+    """--dd-comm loopback times ONE rank of --dd-parts alone on one GPU"""
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "dd", "--dd-comm", "loopback", "--dd-parts", "8"] + argv)
+    with pytest.raises(SystemExit) as e:
+        bench.parse()
+    assert e.value.code == 2
+    assert "loopback" in capsys.readouterr().err
+
+
+def test_loopback_arguments_parse(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "dd", "--dd-comm", "loopback", "--dd-parts", "8",
+                                      "--dd-rank", "7"])
+    a = bench.parse()
+    assert (a.dd_comm, a.dd_parts, a.dd_rank, a.gpus) == ("loopback", 8, 7, 1)
