@@ -256,7 +256,8 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             double *hist, unsigned long long *gran, unsigned long long *hg, int G,
                             long long Ppad, int *err, unsigned long long *xb, unsigned long long *elect,
                             unsigned long long seq, const UnitMap &um, hipStream_t st,
-                            long long *trace = nullptr);   // diagnostics: GG_MGS_TRACE (solver.hip)
+                            long long *trace = nullptr,    // diagnostics: GG_MGS_TRACE (solver.hip)
+                            const double *msc = nullptr, double *mout = nullptr);   // + mout = v_{i+1} * msc
 // the same for long vectors (w on chip, the basis streamed): kWideG blocks
 constexpr int kWideG = 512;
 bool arnoldi_wide_ok(int G, long long Ppad);

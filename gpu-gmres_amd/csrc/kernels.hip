@@ -3782,8 +3782,11 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
                                                             unsigned long long *gran, unsigned long long *hg,
                                                             long long units, int *err, unsigned long long *xb,
                                                             unsigned long long *elect, unsigned long long seq,
-                                                            UnitMap um, long long *trace)
+                                                            UnitMap um, long long *trace, const double *msc,
+                                                            double *mout)
 {
+    // msc / mout (the split engine): also mout = v_{i+1} * msc, k_mul's product
+    // for the next iteration's Mr (one pass fewer per iteration)
     // granules per thread loaded at once in the all-gathers (persist_np; J =
     // 8 polls them one by one: the parallel form would cost it an occupancy step)
     constexpr int kNP = persist_np(J);
@@ -3963,6 +3966,14 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             a.x = inv * a.x;
             a.y = inv * a.y;
             st2(vout, u, a);
+            if (mout) {
+                const double2 c = ld2(msc, u);
+                st2(mout, u, make_double2(a.x * c.x, a.y * c.y));
+            }
+        } else if (mout && u < units) {
+            // padding: k_mul's product of the slot as it stands (never written here)
+            const double2 a = ld2(vout, u), c = ld2(msc, u);
+            st2(mout, u, make_double2(a.x * c.x, a.y * c.y));
         }
     }
 }
@@ -4938,7 +4949,8 @@ int arnoldi_persist_units(int G, long long Ppad)
 // and the launch: ADVICE r4)
 using PersistFn = void (*)(Gate, int, int, DevState *, const double *, double *, long long, double *, double *,
                            double *, double *, double *, unsigned long long *, unsigned long long *, long long, int *,
-                           unsigned long long *, unsigned long long *, unsigned long long, UnitMap, long long *);
+                           unsigned long long *, unsigned long long *, unsigned long long, UnitMap, long long *,
+                           const double *, double *);
 template <int XG, int PF>
 PersistFn persist_fn_j(int J)
 {
@@ -5023,7 +5035,7 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             long long ldv, double *H, double *cs, double *sn, double *s,
                             double *hist, unsigned long long *gran, unsigned long long *hg, int G, long long Ppad,
                             int *err, unsigned long long *xb, unsigned long long *elect, unsigned long long seq,
-                            const UnitMap &um, hipStream_t st, long long *trace)
+                            const UnitMap &um, hipStream_t st, long long *trace, const double *msc, double *mout)
 {
     const int J = arnoldi_persist_units(G, Ppad);
     GG_REQUIRE(persist_np(J) == 0 || G <= persist_np(J) * kBlock, GG_EINVAL,
@@ -5031,7 +5043,7 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
     const PersistFn f = persist_fn(J);
     const int extra = (mgs_gather_form() == 3 && mgs_prefetch()) ? kXcds : 0;   // reducer-only blocks
     f<<<G + extra, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2,
-                                                     err, xb, elect, seq, um, trace);
+                                                     err, xb, elect, seq, um, trace, msc, mout);
 }
 
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,

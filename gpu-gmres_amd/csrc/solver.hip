@@ -761,9 +761,10 @@ void apply_left(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 // column convention: with the column permutation in A' the gather is gone and
 // D_r^-1 is a contiguous pass (folding it into the 2D wavefront U solve's
 // writer wave cost more than the pass: U 99.7 -> 142 us at C2)
-void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
+void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1, bool t1_ready = false)
 {
-    launch_mul(g, in, s->mid_l.p, s->t1.p, (int)s->P, s->st);
+    // t1_ready: t1 = M v already formed by the previous iteration's persistent MGS
+    if (!t1_ready) launch_mul(g, in, s->mid_l.p, s->t1.p, (int)s->P, s->st);
     trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
     launch_div(g, s->t2.p, s->rs_l.p, out, (int)s->P, s->st);
 }
@@ -955,6 +956,13 @@ void mgs_trace_print(gg_solver *s)
     s->mgs_trace_i = -1;
 }
 
+// GG_SPLIT_MULFOLD=0: the split engine keeps k_mul as its own launch
+static bool mulfold_on()
+{
+    const char *e = std::getenv("GG_SPLIT_MULFOLD");
+    return !(e && e[0] == '0');
+}
+
 void enqueue_cycle(gg_solver *s, int m)
 {
     const UnitMap um = unit_map(s);
@@ -966,6 +974,9 @@ void enqueue_cycle(gg_solver *s, int m)
     launch_init_cycle(ds, s->r.p, s->V.p, s->s.p, s->G, P, s->st);
     const bool persist = s->persist && !s->shared;
     const bool wide = s->wide && !s->shared;
+    // the split engine: the persistent MGS of iteration i also forms Mr's first
+    // pass for iteration i + 1, t1 = M v_{i+1} (k_mul's product, one launch fewer)
+    const bool mulfold = persist && split && mulfold_on();
     if (persist || wide) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
     if (persist) launch_fill_u64(s->xgran.p, (long long)s->xgran.n, kSentinel, s->st);
     const bool fuse = fuse_spmv_active(s);
@@ -1008,7 +1019,7 @@ void enqueue_cycle(gg_solver *s, int m)
             // on grid-ordered factors, whose gathers are local (netlist 3,595
             // -> 3,635 it/s; on the randomly permuted split the second gather
             // doubles the SpMV's misses, 49.8 -> 112.7 us: profiles/r04/r04p_*_x*.json)
-            launch_mul(gi, vi, s->mid_l.p, s->t1.p, (int)s->P, s->st);
+            if (!(mulfold && i > 0)) launch_mul(gi, vi, s->mid_l.p, s->t1.p, (int)s->P, s->st);
             trsv(s, gi, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
             mk = prof_begin(s, GG_PROF_SPMV, i);
             launch_spmv_xdiv(gi, s->dA, s->t2.p, s->rs_l.p, s->t1.p, s->st, s->ls_l.p);
@@ -1017,7 +1028,7 @@ void enqueue_cycle(gg_solver *s, int m)
             trsv(s, gi, s->L, GG_PROF_TRSV_L, i, s->t1.p, s->w.p);              // w = Ml A z
             prof_end(s, mk);
         } else {
-            apply_right(s, gi, vi, s->z.p, i);                                 // z = Mr v_i
+            apply_right(s, gi, vi, s->z.p, i, mulfold && i > 0);              // z = Mr v_i
             spmv_left(s, gi, s->z.p, nullptr, s->w.p, i, fuse);                // w = Ml A z
         }
         mk = prof_begin(s, GG_PROF_MGS, i);
@@ -1025,7 +1036,8 @@ void enqueue_cycle(gg_solver *s, int m)
             launch_arnoldi_persist(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                    s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
                                    P, s->err.p, s->xgran.p + (size_t)i * (m + 2) * kMgsXcdWords, s->elect.p,
-                                   ++s->mgs_seq, um, s->st, mgs_trace_for(s, i, m));
+                                   ++s->mgs_seq, um, s->st, mgs_trace_for(s, i, m), mulfold ? s->mid_l.p : nullptr,
+                                   mulfold ? s->t1.p : nullptr);
         } else if (wide) {
             launch_arnoldi_wide(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                 s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
