@@ -202,7 +202,8 @@ void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStr
 // (GG_FUSE_SPMV): fused_spmv_ok says whether triangle T and A admit it
 bool fused_spmv_ok(const DevTri &T, const DevCsr &A);
 void launch_trsv_spmv(Gate g, DevTri &T, const DevCsr &A, const double *v, double *w, double *x, int *err,
-                      hipStream_t st, const double *ydiv = nullptr);
+                      hipStream_t st, const double *ydiv = nullptr,
+                      const double *xdiv = nullptr);   // v[c] / xdiv[c] per gathered term
 int wave_batch_steps(int div, bool d3 = false, int skew = 1);   // steps per batch of the wavefront kernel
 int tile_batch_steps();                                          // steps per batch of the 3D tile kernel
 

@@ -1286,6 +1286,7 @@ struct FusedSpmv {
     double *w = nullptr;                    // = the solve's b
     unsigned long long *cnt = nullptr;      // per slice group: 1 = stored (0 between launches)
     const double *ydiv = nullptr;           // split engine: row divisors (k_spmv_sell's YDIV)
+    const double *xdiv = nullptr;           // split engine: v[c] / xdiv[c] per gathered term (k_spmv_sell's XDIV)
     int n = 0;                              // rows of A (layout space)
     int ns = 0;                             // SpMV blocks: blockIdx < ns, the bands after them
 };
@@ -1293,7 +1294,8 @@ struct FusedSpmv {
 // chain is shorter with fewer loads per lane; profiles/r03/r03_fs_knobs.txt)
 constexpr int kFsGroup = 2;                 // (kWaveTAlign is a multiple)
 
-__device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands, int T, int nwv)
+template <bool XD>
+__device__ __forceinline__ void fused_spmv_groups(const FusedSpmv &fs, int nbands, int T, int nwv)
 {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1329,6 +1331,19 @@ __device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands,
 #pragma unroll
                 for (int k = 0; k < 8; k++)
                     if (k0 + k < wd[j] && c[j][k] >= 0) xv[j][k] = fs.v[c[j][k]];
+            if constexpr (XD) {
+                double dv[kFsGroup][8];
+#pragma unroll
+                for (int j = 0; j < kFsGroup; j++)
+#pragma unroll
+                    for (int k = 0; k < 8; k++)
+                        if (k0 + k < wd[j] && c[j][k] >= 0) dv[j][k] = fs.xdiv[c[j][k]];
+#pragma unroll
+                for (int j = 0; j < kFsGroup; j++)
+#pragma unroll
+                    for (int k = 0; k < 8; k++)
+                        if (k0 + k < wd[j] && c[j][k] >= 0) xv[j][k] = xv[j][k] / dv[j][k];
+            }
 #pragma unroll
             for (int j = 0; j < kFsGroup; j++)
 #pragma unroll
@@ -1346,6 +1361,13 @@ __device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the group's rows stored
         if (lane == 0) st_agent(fs.cnt + q, 1ull);          // one word per group: no contention
     }
+}
+// xdiv (the split engine's D_r^-1 pass folded into the gathers, as
+// k_spmv_sell<.., XDIV>): one uniform branch, the loops unchanged otherwise
+__device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands, int T, int nwv)
+{
+    if (fs.xdiv) fused_spmv_groups<true>(fs, nbands, T, nwv);
+    else fused_spmv_groups<false>(fs, nbands, T, nwv);
 }
 
 // IL: the in-line term (|offset| = 1) comes first in the row's canonical order,
@@ -4560,7 +4582,7 @@ bool fused_spmv_ok(const DevTri &T, const DevCsr &A)
 }
 
 void launch_trsv_spmv(Gate g, DevTri &T, const DevCsr &A, const double *v, double *w, double *x, int *err,
-                      hipStream_t st, const double *ydiv)
+                      hipStream_t st, const double *ydiv, const double *xdiv)
 {
     const Wave2D &wl = T.wl;
     const size_t nflag = (size_t)wl.nbands * (wl.T / kFsGroup);
@@ -4584,6 +4606,7 @@ void launch_trsv_spmv(Gate g, DevTri &T, const DevCsr &A, const double *v, doubl
     fs.w = w;
     fs.cnt = T.fcnt.p;
     fs.ydiv = ydiv;
+    fs.xdiv = xdiv;
     fs.n = A.n;
     fs.ns = ns;
     if (T.eff_div() == WD_UFMA)

@@ -761,12 +761,14 @@ void apply_left(gg_solver *s, Gate g, const double *in, double *out, int i = -1)
 // column convention: with the column permutation in A' the gather is gone and
 // D_r^-1 is a contiguous pass (folding it into the 2D wavefront U solve's
 // writer wave cost more than the pass: U 99.7 -> 142 us at C2)
-void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1, bool t1_ready = false)
+void apply_right(gg_solver *s, Gate g, const double *in, double *out, int i = -1, bool t1_ready = false,
+                 bool no_div = false)
 {
-    // t1_ready: t1 = M v already formed by the previous iteration's persistent MGS
+    // t1_ready: t1 = M v already formed by the previous iteration's persistent MGS;
+    // no_div: leave U^-1 M v in t2, the consumer divides by D_r per gathered term
     if (!t1_ready) launch_mul(g, in, s->mid_l.p, s->t1.p, (int)s->P, s->st);
     trsv(s, g, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
-    launch_div(g, s->t2.p, s->rs_l.p, out, (int)s->P, s->st);
+    if (!no_div) launch_div(g, s->t2.p, s->rs_l.p, out, (int)s->P, s->st);
 }
 // the split engine's inner iteration folds Mr's D_r^-1 into the SpMV when A'
 // has its sliced copy (GG_SPMV_XDIV=0: the separate pass, apply_right)
@@ -780,13 +782,14 @@ static bool xdiv_fold()
 }
 // Ml(A' z) with Ml's row gather and D_l^-1 in the SpMV (resid: Ml(b - A x))
 void spmv_left(gg_solver *s, Gate g, const double *z, const double *b, double *out, int i = -1,
-               bool fuse = false)
+               bool fuse = false, const double *xdiv = nullptr)
 {
     if (fuse && !b) {
-        // A' z and its row scaling computed inside the forward solve's launch (GG_FUSE_SPMV)
+        // A' z and its row scaling computed inside the forward solve's launch
+        // (GG_FUSE_SPMV); xdiv: z[c] / xdiv[c] per gathered term (D_r^-1 folded)
         const int mk = prof_begin(s, GG_PROF_PRECOND, i);
         const int ml = prof_begin(s, GG_PROF_TRSV_L, i);
-        launch_trsv_spmv(g, s->L, s->dA, z, s->t1.p, out, s->err.p, s->st, s->ls_l.p);
+        launch_trsv_spmv(g, s->L, s->dA, z, s->t1.p, out, s->err.p, s->st, s->ls_l.p, xdiv);
         prof_end(s, ml);
         prof_end(s, mk);
         return;
@@ -956,6 +959,13 @@ void mgs_trace_print(gg_solver *s)
     s->mgs_trace_i = -1;
 }
 
+// GG_SPLIT_DIVFOLD=0: the split engine keeps k_div (Mr's D_r^-1) as its own
+// launch on the fused-SpMV path
+static bool divfold_on()
+{
+    const char *e = std::getenv("GG_SPLIT_DIVFOLD");
+    return !(e && e[0] == '0');
+}
 // GG_SPLIT_MULFOLD=0: the split engine keeps k_mul as its own launch
 static bool mulfold_on()
 {
@@ -1028,8 +1038,14 @@ void enqueue_cycle(gg_solver *s, int m)
             trsv(s, gi, s->L, GG_PROF_TRSV_L, i, s->t1.p, s->w.p);              // w = Ml A z
             prof_end(s, mk);
         } else {
-            apply_right(s, gi, vi, s->z.p, i, mulfold && i > 0);              // z = Mr v_i
-            spmv_left(s, gi, s->z.p, nullptr, s->w.p, i, fuse);                // w = Ml A z
+            if (fuse && divfold_on()) {
+                // D_r^-1 (Mr's last pass) in the fused SpMV's gathers: z stays U^-1 M v
+                apply_right(s, gi, vi, nullptr, i, mulfold && i > 0, true);   // t2 = U^-1 M v_i
+                spmv_left(s, gi, s->t2.p, nullptr, s->w.p, i, fuse, s->rs_l.p); // w = Ml A D_r^-1 t2
+            } else {
+                apply_right(s, gi, vi, s->z.p, i, mulfold && i > 0);          // z = Mr v_i
+                spmv_left(s, gi, s->z.p, nullptr, s->w.p, i, fuse);            // w = Ml A z
+            }
         }
         mk = prof_begin(s, GG_PROF_MGS, i);
         if (persist) {
