@@ -494,6 +494,7 @@ struct gg_solver {
     DBuf<double> partA, partB, H, s, cs, sn, ysm;
     // persistent Arnoldi orthogonalization (kernels.hip k_arnoldi_persist)
     bool persist = false;
+    bool split_local = false;   // the split engine's vectors in a local layout (grid / RCM): its gathers are near
     bool wide = false;                  // k_arnoldi_wide (vectors beyond persist's registers)
     bool shared = false;                // GG_SOLVE_SHARED_DEVICE for the solve in progress
     int div_mode = GG_DIV_EXACT;        // gg_set_division: the wavefront solves' division
@@ -1023,12 +1024,13 @@ void enqueue_cycle(gg_solver *s, int m)
             mk = prof_begin(s, GG_PROF_PRECOND, i);
             apply_minv(s, gi, s->ww.p, s->w.p, i);                             // w = M^-1 ww
             prof_end(s, mk);
-        } else if (!fuse && s->dA.sell && s->U.kind == DevTri::WAVE2D && xdiv_fold()) {
+        } else if (!fuse && s->dA.sell && (s->U.kind == DevTri::WAVE2D || s->split_local) && xdiv_fold()) {
             // z = Mr v_i without its last pass: D_r^-1 goes into the SpMV's
             // gathers (the same division per term, k_spmv_sell<.., XDIV>) --
-            // on grid-ordered factors, whose gathers are local (netlist 3,595
-            // -> 3,635 it/s; on the randomly permuted split the second gather
-            // doubles the SpMV's misses, 49.8 -> 112.7 us: profiles/r04/r04p_*_x*.json)
+            // on grid-ordered or RCM-placed factors, whose gathers are local
+            // (netlist 3,595 -> 3,635 it/s; on the randomly permuted split in
+            // its natural order the second gather doubled the SpMV's misses,
+            // 49.8 -> 112.7 us: profiles/r04/r04p_*_x*.json)
             if (!(mulfold && i > 0)) launch_mul(gi, vi, s->mid_l.p, s->t1.p, (int)s->P, s->st);
             trsv(s, gi, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
             mk = prof_begin(s, GG_PROF_SPMV, i);
@@ -1833,6 +1835,7 @@ int gg_set_precond_split(gg_solver *s, const int *l_rp, const int *l_ci, const d
     const char *fr = std::getenv("GG_FLOW_RCM");
     if (!wl.ok && !(fr && fr[0] == '0')) rcm = rcm_order(cl, cu);
     setup_space(s, &wl, perm_row, perm_col, rcm.empty() ? nullptr : &rcm);
+    s->split_local = wl.ok || !rcm.empty();
     if (wl.ok && wl.bnt) {
         build_tri_bordered(s->L, cl, gl, wl, s->st);
         build_tri_bordered(s->U, cu, gu, wl, s->st);
