@@ -194,7 +194,8 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
 // y[r] = (sum_k a_k RN(x[c_k] / xdiv[c_k])) / ydiv[r] on the sliced copy (false, nothing
 // launched, when A has none): the split engine's D_r^-1 in the SpMV's gathers
 bool launch_spmv_xdiv(Gate g, const DevCsr &A, const double *x, const double *xdiv, double *y, hipStream_t st,
-                      const double *ydiv);
+                      const double *ydiv, double *fill = nullptr,
+                      int nfill = 0);   // + fill[< nfill] = sentinel (the next flow solve's x)
 
 // ---- triangular solves ---------------------------------------------------------
 void launch_trsv(Gate g, DevTri &T, const double *b, double *x, int *err, hipStream_t st);
@@ -258,7 +259,8 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             long long Ppad, int *err, unsigned long long *xb, unsigned long long *elect,
                             unsigned long long seq, const UnitMap &um, hipStream_t st,
                             long long *trace = nullptr,    // diagnostics: GG_MGS_TRACE (solver.hip)
-                            const double *msc = nullptr, double *mout = nullptr);   // + mout = v_{i+1} * msc
+                            const double *msc = nullptr, double *mout = nullptr,    // + mout = v_{i+1} * msc
+                            double *fill = nullptr, long long nfill = 0);            // + fill[< nfill] = sentinel
 // the same for long vectors (w on chip, the basis streamed): kWideG blocks
 constexpr int kWideG = 512;
 bool arnoldi_wide_ok(int G, long long Ppad);

@@ -562,11 +562,18 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
                                                       const double *__restrict__ b,
                                                       double *__restrict__ y,
                                                       const double *__restrict__ ydiv,
-                                                      const double *__restrict__ xdiv)
+                                                      const double *__restrict__ xdiv,
+                                                      unsigned long long *fill = nullptr, int nfill = 0)
 {
+    // (XDIV, fill: the next flow solve's x set to the sentinel, rows < nfill --
+    // the k_fill_gated launch that solve would make)
     if (gated(g)) return;
     const int s = xcd_block() * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (s >= nslice) return;
+    if constexpr (XDIV) {
+        const int r = s * 64 + (int)(threadIdx.x & 63);
+        if (fill && r < nfill) fill[r] = kSentinel;
+    }
     const int lane = threadIdx.x & 63;
     const int off = sptr[s], w = (sptr[s + 1] - off) >> 6;
     const int *cp = ci + off + lane;
@@ -3805,10 +3812,11 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
                                                             long long units, int *err, unsigned long long *xb,
                                                             unsigned long long *elect, unsigned long long seq,
                                                             UnitMap um, long long *trace, const double *msc,
-                                                            double *mout)
+                                                            double *mout, unsigned long long *fill, long long nfill)
 {
     // msc / mout (the split engine): also mout = v_{i+1} * msc, k_mul's product
-    // for the next iteration's Mr (one pass fewer per iteration)
+    // for the next iteration's Mr (one pass fewer per iteration); fill: slots
+    // < nfill set to the sentinel (the next flow U solve's x, its fill launch)
     // granules per thread loaded at once in the all-gathers (persist_np; J =
     // 8 polls them one by one: the parallel form would cost it an occupancy step)
     constexpr int kNP = persist_np(J);
@@ -3996,6 +4004,10 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
             // padding: k_mul's product of the slot as it stands (never written here)
             const double2 a = ld2(vout, u), c = ld2(msc, u);
             st2(mout, u, make_double2(a.x * c.x, a.y * c.y));
+        }
+        if (fill && u < units) {
+            if (2 * u < nfill) fill[2 * u] = kSentinel;
+            if (2 * u + 1 < nfill) fill[2 * u + 1] = kSentinel;
         }
     }
 }
@@ -4490,12 +4502,14 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
 }
 
 bool launch_spmv_xdiv(Gate g, const DevCsr &A, const double *x, const double *xdiv, double *y, hipStream_t st,
-                      const double *ydiv)
+                      const double *ydiv, double *fill, int nfill)
 {
     if (!A.sell || !ydiv) return false;
     if (A.nblk == 0) return true;
+    if (!fill || nfill > A.nslice * 64) fill = nullptr;
     k_spmv_sell<false, true, true><<<(A.nslice + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st>>>(
-        g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, nullptr, y, ydiv, xdiv);
+        g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, nullptr, y, ydiv, xdiv,
+        reinterpret_cast<unsigned long long *>(fill), fill ? nfill : 0);
     return true;
 }
 
@@ -4973,7 +4987,7 @@ int arnoldi_persist_units(int G, long long Ppad)
 using PersistFn = void (*)(Gate, int, int, DevState *, const double *, double *, long long, double *, double *,
                            double *, double *, double *, unsigned long long *, unsigned long long *, long long, int *,
                            unsigned long long *, unsigned long long *, unsigned long long, UnitMap, long long *,
-                           const double *, double *);
+                           const double *, double *, unsigned long long *, long long);
 template <int XG, int PF>
 PersistFn persist_fn_j(int J)
 {
@@ -5058,7 +5072,8 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             long long ldv, double *H, double *cs, double *sn, double *s,
                             double *hist, unsigned long long *gran, unsigned long long *hg, int G, long long Ppad,
                             int *err, unsigned long long *xb, unsigned long long *elect, unsigned long long seq,
-                            const UnitMap &um, hipStream_t st, long long *trace, const double *msc, double *mout)
+                            const UnitMap &um, hipStream_t st, long long *trace, const double *msc, double *mout,
+                            double *fill, long long nfill)
 {
     const int J = arnoldi_persist_units(G, Ppad);
     GG_REQUIRE(persist_np(J) == 0 || G <= persist_np(J) * kBlock, GG_EINVAL,
@@ -5066,7 +5081,8 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
     const PersistFn f = persist_fn(J);
     const int extra = (mgs_gather_form() == 3 && mgs_prefetch()) ? kXcds : 0;   // reducer-only blocks
     f<<<G + extra, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2,
-                                                     err, xb, elect, seq, um, trace, msc, mout);
+                                                     err, xb, elect, seq, um, trace, msc, mout,
+                                                     reinterpret_cast<unsigned long long *>(fill), fill ? nfill : 0);
 }
 
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,

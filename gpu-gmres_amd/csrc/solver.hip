@@ -967,6 +967,12 @@ static bool divfold_on()
     const char *e = std::getenv("GG_SPLIT_DIVFOLD");
     return !(e && e[0] == '0');
 }
+// GG_FLOW_FILLFOLD=0: the flow solves fill their x themselves (own launch)
+static bool fill_fold_on()
+{
+    const char *e = std::getenv("GG_FLOW_FILLFOLD");
+    return !(e && e[0] == '0');
+}
 // GG_SPLIT_MULFOLD=0: the split engine keeps k_mul as its own launch
 static bool mulfold_on()
 {
@@ -988,6 +994,14 @@ void enqueue_cycle(gg_solver *s, int m)
     // the split engine: the persistent MGS of iteration i also forms Mr's first
     // pass for iteration i + 1, t1 = M v_{i+1} (k_mul's product, one launch fewer)
     const bool mulfold = persist && split && mulfold_on();
+    // the permuted split on the flow kernels (the x-division fold path): the
+    // fills of the U / L solves' outputs move into the MGS / SpMV launches
+    const bool xpath = split && !fuse_spmv_active(s) && s->dA.sell && xdiv_fold() &&
+                       (s->U.kind == DevTri::WAVE2D || s->split_local);
+    const bool lfill = xpath && fill_fold_on() && s->L.kind == DevTri::LEVEL && !s->L.tail && s->L.bofs == 0 &&
+                       !s->L.lev_ptr.empty();
+    const bool ufill = xpath && mulfold && fill_fold_on() && s->U.kind == DevTri::LEVEL && !s->U.tail &&
+                       s->U.bofs == 0 && !s->U.lev_ptr.empty();
     if (persist || wide) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
     if (persist) launch_fill_u64(s->xgran.p, (long long)s->xgran.n, kSentinel, s->st);
     const bool fuse = fuse_spmv_active(s);
@@ -1032,12 +1046,19 @@ void enqueue_cycle(gg_solver *s, int m)
             // its natural order the second gather doubled the SpMV's misses,
             // 49.8 -> 112.7 us: profiles/r04/r04p_*_x*.json)
             if (!(mulfold && i > 0)) launch_mul(gi, vi, s->mid_l.p, s->t1.p, (int)s->P, s->st);
+            // flow solves' sentinel fills ride on the launch before each: the
+            // previous iteration's MGS filled t2, the SpMV fills w
+            s->U.prefilled = ufill && i > 0;
             trsv(s, gi, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
+            s->U.prefilled = false;
             mk = prof_begin(s, GG_PROF_SPMV, i);
-            launch_spmv_xdiv(gi, s->dA, s->t2.p, s->rs_l.p, s->t1.p, s->st, s->ls_l.p);
+            launch_spmv_xdiv(gi, s->dA, s->t2.p, s->rs_l.p, s->t1.p, s->st, s->ls_l.p, lfill ? s->w.p : nullptr,
+                             lfill ? s->L.lev_ptr.back() : 0);
             prof_end(s, mk);
             mk = prof_begin(s, GG_PROF_PRECOND, i);
+            s->L.prefilled = lfill;
             trsv(s, gi, s->L, GG_PROF_TRSV_L, i, s->t1.p, s->w.p);              // w = Ml A z
+            s->L.prefilled = false;
             prof_end(s, mk);
         } else {
             if (fuse && divfold_on()) {
@@ -1055,7 +1076,8 @@ void enqueue_cycle(gg_solver *s, int m)
                                    s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
                                    P, s->err.p, s->xgran.p + (size_t)i * (m + 2) * kMgsXcdWords, s->elect.p,
                                    ++s->mgs_seq, um, s->st, mgs_trace_for(s, i, m), mulfold ? s->mid_l.p : nullptr,
-                                   mulfold ? s->t1.p : nullptr);
+                                   mulfold ? s->t1.p : nullptr, ufill ? s->t2.p : nullptr,
+                                   ufill ? s->U.lev_ptr.back() : 0);
         } else if (wide) {
             launch_arnoldi_wide(gi, i, m, ds, s->w.p, s->V.p, P, s->H.p, s->cs.p, s->sn.p, s->s.p,
                                 s->hist.p, s->gran.p + (size_t)i * (m + 2) * s->G, hgran(s, m, i), s->G,
