@@ -803,10 +803,11 @@ def main():
             if cnt == 0:
                 continue
             avg_us = ms * 1e3 / cnt
-            byt = per() if per is not None else (mgs_f / mgs_it if mgs_it else float("nan"))
+            # (c5: the per-step cycle lengths are not collected, so MGS has no byte count -> null)
+            byt = per() if per is not None else (mgs_f / mgs_it if mgs_it else None)
             fam[name] = {"launches": cnt, "avg_us": round(avg_us, 3),
                          "alg_bytes_per_launch": byt,
-                         "achieved_gbs": round(byt / (avg_us * 1e-6) / 1e9, 1),
+                         "achieved_gbs": round(byt / (avg_us * 1e-6) / 1e9, 1) if byt is not None else None,
                          "share_of_step": round(ms / (el * 1e3), 4)}
             if per is None and mgs_it:
                 # SURVEY.md 8(d)'s unfused count over the same time: what the reference's
@@ -849,7 +850,8 @@ def main():
         if not c5 and s.mgs_kernel():
             KERNEL_NAMES["mgs_givens"] = s.mgs_kernel()
         fused_l = s.trsv_kernel(0).startswith("k_trsv_wave2d_spmv")
-        single = {k: v for k, v in fam.items() if k in KERNEL_NAMES and not (k == "spmv" and fused_l)}
+        single = {k: v for k, v in fam.items()
+                  if k in KERNEL_NAMES and not (k == "spmv" and fused_l) and v.get("achieved_gbs") is not None}
         if single:
             top = max(v["share_of_step"] for v in single.values())
             cands = [k for k in ("spmv", "trsv_L", "trsv_U", "mgs_givens")
