@@ -1086,6 +1086,12 @@ __global__ __launch_bounds__(kBlock) void k_sep_flow(Gate g, int ntask, const in
 #define GG_WAVE_LOOK 3
 #endif
 constexpr int kWaveLook = GG_WAVE_LOOK;
+// the unit forward solve (3 streams) looks further ahead (round 5, C2 on one
+// box: L 96.2 -> 93.8 us at 4 pairs, while U lost 1.5 us at 4: the U keeps 3)
+#ifndef GG_WAVE_LOOK_L
+#define GG_WAVE_LOOK_L 4
+#endif
+constexpr int kWaveLookL = GG_WAVE_LOOK_L;
 // the compute wave's LDS traffic is issued in the shadow of each step's DPP shift
 #ifndef GG_WAVE_SHADOW
 #define GG_WAVE_SHADOW 1
@@ -1119,8 +1125,12 @@ constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 // (Measured, not kept, round 5: the 2D boundary wave retrying a batch's
 // granules with two polls in flight, s_sleep 0 / 1 / 10 between them: C2 U
 // 99.6 -> 102.6-105.6 us, L 95.7 -> 97.8-101.5 us, profiles/r05/stage_ab.txt.)
+// GG_WAVE_XCD = X workgroups dealt per band of the backward solve, one running:
+// the bands land on 8 / X of the XCDs (8: all on one XCD, 4: alternating over
+// two, 2: over four).  Round 5, two compute waves per band, C2 on one box:
+// U 99.3 us at 8 -> 97.9 at 4, 98.7 at 2 (profiles/r05/stage_ab.txt r05ab / r05ad)
 #ifndef GG_WAVE_XCD
-#define GG_WAVE_XCD 8
+#define GG_WAVE_XCD 4
 #endif
 // Redundant compute waves: GG_WAVE_NC waves (on distinct SIMDs) run the same
 // recurrence on the same operands -- bit-identical values -- and wave c stages
@@ -1185,7 +1195,7 @@ struct WaveCfg {
     static_assert(kWaveTAlign % (B * GG_WAVE_POLL) == 0, "batches per band must be a multiple of the poll depth");
     static_assert(!D3 || LOADERS == 1, "3D grids stream every array from one loader wave");
     static_assert(S >= 1 && S <= 3 && (S == 1 || (!D3 && LOADERS == 1)), "skew: 2D, one loader");
-    static_assert(kWaveLook >= 1 && kWaveLook <= PBN, "lookahead");
+    static_assert(kWaveLook >= 1 && kWaveLook <= PBN && kWaveLookL >= 1 && kWaveLookL <= PBN, "lookahead");
     static_assert(LDS2 * 16 <= 160 * 1024, "LDS budget");
 };
 
@@ -1700,6 +1710,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // ahead of their use; the boundary values are read first (LDS returns in
     // order and they are needed at the batch's first step).
     double2 rg[C::PBN][C::A];
+    constexpr int LK = (FWD && !D3 && (DIV == WD_UNIT || DIV == WD_UFMA)) ? kWaveLookL : kWaveLook;
     // one step pair's x into staging half h, pair kk (.x = the value at the
     // lower memory address)
     auto stage = [&](int h, int kk, double vx, double vy) {
@@ -1735,7 +1746,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
         for (int a = 0; a < C::A; a++) rg[0][a] = sc[a * PB];
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kk = 1; kk < kWaveLook; kk++)
+        for (int kk = 1; kk < LK; kk++)
 #pragma unroll
             for (int a = 0; a < C::A; a++) rg[kk][a] = sc[a * PB + kk * 64];
 #pragma unroll
@@ -1777,9 +1788,9 @@ __device__ __forceinline__ void trsv_wave2d_body(
                     // the look-ahead reads at the first step, the previous
                     // pair's x staging at the second
                     __builtin_amdgcn_sched_barrier(0);
-                    if (h == 0 && kk + kWaveLook < C::PBN) {
+                    if (h == 0 && kk + LK < C::PBN) {
 #pragma unroll
-                        for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
+                        for (int a = 0; a < C::A; a++) rg[kk + LK][a] = sc[a * PB + (kk + LK) * 64];
                     }
                     if (h == 1 && kk > 0) {
                         if (FWD) stage(bi & 1, kk - 1, xv[2 * kk - 2], xv[2 * kk - 1]);
@@ -1843,9 +1854,9 @@ __device__ __forceinline__ void trsv_wave2d_body(
                 else stage(bi & 1, kk, xv[2 * kk + 1], xv[2 * kk]);
             }
 
-            if (!SH && kk + kWaveLook < C::PBN) {
+            if (!SH && kk + LK < C::PBN) {
 #pragma unroll
-                for (int a = 0; a < C::A; a++) rg[kk + kWaveLook][a] = sc[a * PB + (kk + kWaveLook) * 64];
+                for (int a = 0; a < C::A; a++) rg[kk + LK][a] = sc[a * PB + (kk + LK) * 64];
             }
             __builtin_amdgcn_sched_barrier(0);
         }
