@@ -7,7 +7,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-T=${1:-r05t}
+T=${1:-r05h}
 for g in c2 c4; do
     for P in 2 4 8; do
         f=gpurun_out/${T}_loop_${g}_$P
