@@ -1086,8 +1086,9 @@ __global__ __launch_bounds__(kBlock) void k_sep_flow(Gate g, int ntask, const in
 #define GG_WAVE_LOOK 3
 #endif
 constexpr int kWaveLook = GG_WAVE_LOOK;
-// the unit forward solve (3 streams) looks further ahead (round 5, C2 on one
-// box: L 96.2 -> 93.8 us at 4 pairs, while U lost 1.5 us at 4: the U keeps 3)
+// the unit forward solve with the SpMV in its launch looks further ahead
+// (round 5, one box each: C2's fused L 96.2 -> 93.8 us at 4 pairs; the U solve
+// lost 1.5 us at 4 and the netlist's unfused unit L 2.2 us, so they keep 3)
 #ifndef GG_WAVE_LOOK_L
 #define GG_WAVE_LOOK_L 4
 #endif
@@ -1710,7 +1711,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // ahead of their use; the boundary values are read first (LDS returns in
     // order and they are needed at the batch's first step).
     double2 rg[C::PBN][C::A];
-    constexpr int LK = (FWD && !D3 && (DIV == WD_UNIT || DIV == WD_UFMA)) ? kWaveLookL : kWaveLook;
+    constexpr int LK = (FS && (DIV == WD_UNIT || DIV == WD_UFMA)) ? kWaveLookL : kWaveLook;
     // one step pair's x into staging half h, pair kk (.x = the value at the
     // lower memory address)
     auto stage = [&](int h, int kk, double vx, double vy) {
