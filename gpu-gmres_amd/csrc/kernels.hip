@@ -9,6 +9,7 @@
 // Wave = 64 lanes; vector kernels use 256-thread blocks and 16-B (double2)
 // loads; every reduction is a fixed tree (deterministic, no atomics).
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -1700,7 +1701,13 @@ __device__ __forceinline__ void trsv_wave2d_body(
     }
 
     // ---------------------------------------------------- compute wave(s)
-    const int cw = wave;                        // this compute wave's share of the staging
+    // One copy of the loop per compute wave, its share of the staging (pairs
+    // kk with kk % NC == cw) a compile-time choice: a run-time test of the
+    // wave index put a scalar branch around every staging store, splitting
+    // the scheduled pair into basic blocks (C2 L / U 85 -> 93 / 97 us on one
+    // box, profiles/r05/r05_vs_r04/)
+    auto compute_wave = [&](auto cw_tag) {
+    constexpr int cw = decltype(cw_tag)::value;
     constexpr int ctrl = FWD ? 0x138 : 0x130;   // wave_shr:1 / wave_shl:1
     long long *tr = TRACE && cw == 0 ? trace + (long long)band * (3 * nbatch + 8) : nullptr;
     long long ph[4] = {0, 0, 0, 0};     // TRACE: barrier wait, top->step0, step0->last, last->end
@@ -1874,6 +1881,11 @@ __device__ __forceinline__ void trsv_wave2d_body(
 #pragma unroll
         for (int k = 0; k < 4; k++) tr[nbatch + 1 + k] = ph[k];
     }
+    };
+    if (NC == 1 || wave == 0) compute_wave(std::integral_constant<int, 0>{});
+    else if (NC == 2 || wave == 1) compute_wave(std::integral_constant<int, NC >= 2 ? 1 : 0>{});
+    else if (NC == 3 || wave == 2) compute_wave(std::integral_constant<int, NC >= 3 ? 2 : 0>{});
+    else compute_wave(std::integral_constant<int, NC >= 4 ? 3 : 0>{});
     }   // task loop
 }
 
