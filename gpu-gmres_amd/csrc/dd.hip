@@ -1181,8 +1181,11 @@ int gg_dd_ipc_connect(gg_dd *d, const unsigned char *handles)
     // on; it carries a hash of each rank's PCI bus id (ranks sharing a GPU)
     char bus[64] = {};
     GG_HIP(hipDeviceGetPCIBusId(bus, sizeof bus, d->device));
-    long long hb = 1469598103934665603LL;
-    for (const char *c = bus; *c; c++) hb = (hb ^ (unsigned char)*c) * 1099511628211LL;
+    // FNV-1a in unsigned arithmetic (wraps by definition), sent as its bits
+    unsigned long long hu = 1469598103934665603ULL;
+    for (const char *c = bus; *c; c++) hu = (hu ^ (unsigned char)*c) * 1099511628211ULL;
+    long long hb;
+    std::memcpy(&hb, &hu, sizeof hb);
     int same = 0;
     for (long long v : ipc_allgather_host(d, hb)) same += v == hb;
     d->xk_shared = same > 1;
@@ -1251,7 +1254,16 @@ int gg_dd_info(gg_dd *d, int *info)
     info[7] = (int)d->Pl;
     info[8] = (int)d->sh.size();
     info[9] = d->P * d->maxI;
-    info[10] = use_xk(d, 1) ? 1 : 0;
+    return GG_OK;
+    GG_API_END
+}
+
+int gg_dd_xk_active(gg_dd *d, int *on)
+{
+    GG_API_BEGIN
+    GG_REQUIRE(d && on, GG_EINVAL, "null argument");
+    GG_REQUIRE(d->have, GG_ESTATE, "dd: no system");
+    *on = use_xk(d, 1) ? 1 : 0;
     return GG_OK;
     GG_API_END
 }

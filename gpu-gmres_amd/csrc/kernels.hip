@@ -1159,10 +1159,6 @@ constexpr int kWaveNC = GG_WAVE_NC;
 #ifndef GG_WAVE_NOSTAGE
 #define GG_WAVE_NOSTAGE 0
 #endif
-// the same placement for the forward solve (1: one workgroup per band)
-#ifndef GG_WAVE_XCD_L
-#define GG_WAVE_XCD_L 1
-#endif
 
 template <int DIV, bool D3 = false, int S = 1>
 struct WaveCfg {
@@ -1449,7 +1445,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // 88.9 -> 90.0 us (round 3, re-measured: 89.4 / 90.3 -> 89.9 / 90.4 us), so
     // the forward solve keeps one workgroup per band.
     // (the fused SpMV's launch holds one workgroup per band: no placement there)
-    constexpr int XS = (D3 || FS) ? 1 : FWD ? GG_WAVE_XCD_L : GG_WAVE_XCD;
+    constexpr int XS = (D3 || FS || FWD) ? 1 : GG_WAVE_XCD;
     if (XS > 1 && bid % XS) return;
     const int blk = bid / XS;
     const int ntask = nz * nbands;
@@ -4529,8 +4525,15 @@ bool launch_spmv_xdiv(Gate g, const DevCsr &A, const double *x, const double *xd
                       const double *ydiv, double *fill, int nfill)
 {
     if (!A.sell || !ydiv) return false;
+    // the caller relies on the fill having happened (DevTri::prefilled): when
+    // it cannot ride on the SpMV's lanes it gets a launch of its own
+    if (fill && (A.nblk == 0 || nfill > A.nslice * 64)) {
+        k_fill_gated<<<blocks_for(nfill, kBlock, 8192), kBlock, 0, st>>>(
+            g, reinterpret_cast<unsigned long long *>(fill), nfill, kSentinel);
+        fill = nullptr;
+    }
     if (A.nblk == 0) return true;
-    if (!fill || nfill > A.nslice * 64) fill = nullptr;
+    if (!fill) nfill = 0;
     k_spmv_sell<false, true, true><<<(A.nslice + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st>>>(
         g, A.n, A.nslice, A.sptr.p, A.sci.p, A.sv.p, x, nullptr, y, ydiv, xdiv,
         reinterpret_cast<unsigned long long *>(fill), fill ? nfill : 0);
@@ -4765,7 +4768,7 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
         const double *rv = div == WD_RCP ? T.rw.p : nullptr;
         if ((div == WD_UFMA || div == WD_SFMA) && !w.tile) {
             // GG_DIV_FMA on a 2D grid (build_tri admits unskewed ones in canonical order)
-            dim3 grid(w.nbands * (T.lower ? GG_WAVE_XCD_L : GG_WAVE_XCD));
+            dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
             const double *k1 = div == WD_SFMA ? T.c1s.p : T.c1.p, *k2 = div == WD_SFMA ? T.c2s.p : T.c2.p;
 #define GG_FMA_LAUNCH(FWD, DIV, TR)                                                                \
     k_trsv_wave2d<FWD, DIV, TR><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                           \
@@ -4820,7 +4823,7 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
             }
 #undef GG_TILE_LAUNCH
         } else if (w.nz == 1) {
-            dim3 grid(w.nbands * (T.lower ? GG_WAVE_XCD_L : GG_WAVE_XCD));
+            dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
 #define GG_WAVE_LAUNCH_S(FWD, DIV, S, IL)                                                          \
     k_trsv_wave2d<FWD, DIV, false, false, S, IL><<<grid, WaveCfg<DIV, false, S>::THREADS, 0, st>>>( \
         g, w.T, w.nbands, b, T.c1.p, T.c2.p, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr,   \

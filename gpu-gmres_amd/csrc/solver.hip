@@ -529,6 +529,7 @@ struct gg_solver {
     int prof_mask = 0;                  // (1 << GG_PROF_*) bits being timed
     std::vector<hipEvent_t> prof_pool;
     size_t prof_used = 0;
+    std::vector<int> prof_free;         // pool slots of collected marks, reusable
     struct Mark { int kind, i, e0, e1; };
     std::vector<Mark> marks;
     double prof_ms[GG_PROF_NKINDS] = {};
@@ -820,13 +821,22 @@ void apply_rhs(gg_solver *s, Gate g, const double *in, double *out)
 // ---- in-solve profiling ---------------------------------------------------------
 int prof_event(gg_solver *s)
 {
-    if (s->prof_used == s->prof_pool.size()) {
-        hipEvent_t e;
-        GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));   // timing only
-        s->prof_pool.push_back(e);
+    // slots of collected marks first (the pipelined cycle loop always has a
+    // cycle's marks pending, so the pool would otherwise grow with the solve)
+    int idx;
+    if (!s->prof_free.empty()) {
+        idx = s->prof_free.back();
+        s->prof_free.pop_back();
+    } else {
+        if (s->prof_used == s->prof_pool.size()) {
+            hipEvent_t e;
+            GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));   // timing only
+            s->prof_pool.push_back(e);
+        }
+        idx = (int)s->prof_used++;
     }
-    GG_HIP(hipEventRecord(s->prof_pool[s->prof_used], s->st));
-    return (int)s->prof_used++;
+    GG_HIP(hipEventRecord(s->prof_pool[idx], s->st));
+    return idx;
 }
 int prof_begin(gg_solver *s, int kind, int i)
 {
@@ -847,19 +857,27 @@ void prof_collect(gg_solver *s, int executed, size_t upto = (size_t)-1)
     if (!s->prof_mask) {
         s->marks.clear();
         s->prof_used = 0;
+        s->prof_free.clear();
         return;
     }
     upto = std::min(upto, s->marks.size());
     for (size_t q = 0; q < upto; q++) {
         const auto &mk = s->marks[q];
-        if (mk.i >= executed || mk.e1 < 0) continue;
-        float ms = 0.f;
-        GG_HIP(hipEventElapsedTime(&ms, s->prof_pool[mk.e0], s->prof_pool[mk.e1]));
-        s->prof_ms[mk.kind] += ms;
-        s->prof_cnt[mk.kind]++;
+        if (mk.i < executed && mk.e1 >= 0) {
+            float ms = 0.f;
+            GG_HIP(hipEventElapsedTime(&ms, s->prof_pool[mk.e0], s->prof_pool[mk.e1]));
+            s->prof_ms[mk.kind] += ms;
+            s->prof_cnt[mk.kind]++;
+        }
+        // the cycle these marks belong to has completed: their events are free
+        s->prof_free.push_back(mk.e0);
+        if (mk.e1 >= 0) s->prof_free.push_back(mk.e1);
     }
     s->marks.erase(s->marks.begin(), s->marks.begin() + upto);
-    if (s->marks.empty()) s->prof_used = 0;
+    if (s->marks.empty()) {
+        s->prof_used = 0;
+        s->prof_free.clear();
+    }
 }
 
 // ---- GMRES phases ------------------------------------------------------------
@@ -1052,11 +1070,12 @@ void enqueue_cycle(gg_solver *s, int m)
             trsv(s, gi, s->U, GG_PROF_TRSV_U, i, s->t1.p, s->t2.p);
             s->U.prefilled = false;
             mk = prof_begin(s, GG_PROF_SPMV, i);
-            launch_spmv_xdiv(gi, s->dA, s->t2.p, s->rs_l.p, s->t1.p, s->st, s->ls_l.p, lfill ? s->w.p : nullptr,
-                             lfill ? s->L.lev_ptr.back() : 0);
+            const bool sx = launch_spmv_xdiv(gi, s->dA, s->t2.p, s->rs_l.p, s->t1.p, s->st, s->ls_l.p,
+                                             lfill ? s->w.p : nullptr, lfill ? s->L.lev_ptr.back() : 0);
+            GG_REQUIRE(sx, GG_EINVAL, "split engine: the x-division SpMV needs A's sliced copy");
             prof_end(s, mk);
             mk = prof_begin(s, GG_PROF_PRECOND, i);
-            s->L.prefilled = lfill;
+            s->L.prefilled = lfill;     // launch_spmv_xdiv performed the fill (riding or its own launch)
             trsv(s, gi, s->L, GG_PROF_TRSV_L, i, s->t1.p, s->w.p);              // w = Ml A z
             s->L.prefilled = false;
             prof_end(s, mk);
@@ -1945,6 +1964,13 @@ long long gg_layout(gg_solver *s, long long *lay2nat, long long cap)
             if (s->nat2lay_h[r] < cap) lay2nat[s->nat2lay_h[r]] = (long long)r;
     }
     return s->Ppad;
+}
+int gg_reduce_blocks(gg_solver *s, int *G)
+{
+    if (!s || !G) return GG_EINVAL;
+    if (s->pkind < 0) return GG_ESTATE;
+    *G = s->G;
+    return GG_OK;
 }
 int gg_set_division(gg_solver *s, int mode)
 {

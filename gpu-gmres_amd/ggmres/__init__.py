@@ -33,7 +33,7 @@ EXPORTS = [
     "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced",
     "gg_transient_mna", "gg_set_division", "gg_division_active",
     "gg_trsv_kernel", "gg_mgs_kernel", "gg_set_precond_user", "gg_solve_device_f32",
-    "gg_device_fingerprint", "gg_set_matrix_count", "gg_trsv_levels", "gg_layout",
+    "gg_device_fingerprint", "gg_set_matrix_count", "gg_trsv_levels", "gg_layout", "gg_reduce_blocks",
 ]
 # gg_precond_fn: int (*)(void *ctx, int op, const float *in, float *out, int n), device arrays
 PRECOND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -131,6 +131,7 @@ def lib():
         L.gg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.gg_layout.argtypes = [_VP, ctypes.c_void_p, ctypes.c_longlong]
         L.gg_layout.restype = ctypes.c_longlong
+        L.gg_reduce_blocks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int)]
         L.gg_profile_enable.argtypes = [_VP, ctypes.c_int]
         L.gg_profile_reset.argtypes = [_VP]
         L.gg_profile_get.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
@@ -483,9 +484,9 @@ class Solver:
             _check(P)
         out = np.empty(P, np.int64)
         lib().gg_layout(self.h, out.ctypes.data, P)
-        units = P // 2          # kernels.hip reduce_grid (tests/helpers.py device_layout)
-        G = 512 if units > 1024 * 256 * 8 else min(1024, max(1, (units + 1023) // 1024))
-        return out, G
+        G = ctypes.c_int()
+        _check(lib().gg_reduce_blocks(self.h, ctypes.byref(G)))     # the solver's own s->G
+        return out, G.value
 
     def profile_select(self, kinds):
         """Switch the timed families to `kinds` WITHOUT clearing what was

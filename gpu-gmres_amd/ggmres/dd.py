@@ -27,7 +27,7 @@ _done = False
 
 EXPORTS = ["gg_dd_unique_id", "gg_dd_create", "gg_dd_destroy", "gg_dd_comm_ranks",
            "gg_dd_ipc_handle", "gg_dd_ipc_connect",
-           "gg_dd_set_system", "gg_dd_info",
+           "gg_dd_set_system", "gg_dd_info", "gg_dd_xk_active",
            "gg_dd_perm", "gg_dd_dot_layout", "gg_dd_solve", "gg_dd_solve_device",
            "gg_dd_get_history", "gg_dd_spmv", "gg_dd_precond_apply", "gg_dd_set_division",
            "gg_dd_time_exchange", "gg_dd_profile_enable", "gg_dd_profile_reset", "gg_dd_profile_get",
@@ -50,6 +50,7 @@ def _lib():
         L.gg_dd_comm_ranks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.gg_dd_set_system.argtypes = [_VP, ctypes.c_int, _I, _I, _D, ctypes.c_int]
         L.gg_dd_info.argtypes = [_VP, _I]
+        L.gg_dd_xk_active.argtypes = [_VP, ctypes.POINTER(ctypes.c_int)]
         L.gg_dd_perm.argtypes = [_VP, _I, _I]
         L.gg_dd_dot_layout.argtypes = [_VP, ctypes.c_int, _VP, ctypes.c_longlong,
                                        ctypes.POINTER(ctypes.c_int)]
@@ -127,11 +128,15 @@ class DD:
         _check(_lib().gg_dd_set_system(self.h, n, rp, ci, v, int(method)))
 
     def info(self):
-        a = np.zeros(11, np.int32)
+        a = np.zeros(10, np.int32)
         _check(_lib().gg_dd_info(self.h, a))
         keys = ["n", "nparts", "nsep", "max_iface", "n_interior", "wave_interior", "wave_separator",
-                "local_len", "shards_here", "halo_doubles", "cgs2_in_kernel_exchange"]
-        return dict(zip(keys, (int(x) for x in a)))
+                "local_len", "shards_here", "halo_doubles"]
+        out = dict(zip(keys, (int(x) for x in a)))
+        on = ctypes.c_int()
+        _check(_lib().gg_dd_xk_active(self.h, ctypes.byref(on)))
+        out["cgs2_in_kernel_exchange"] = on.value
+        return out
 
     def perm(self):
         pinv = np.zeros(self.n, np.int32)

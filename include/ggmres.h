@@ -226,6 +226,9 @@ int gg_uses_wavefront(gg_solver *s);
  * an RCM order of the factors (GG_FLOW_RCM=0: natural).  Every reduction runs
  * in this order (tests: the order-matched oracle). */
 long long gg_layout(gg_solver *s, long long *lay2nat, long long cap);
+/* the block partials G of every dot in that space (the reduction grid the
+ * solver actually uses, GG_WIDE_FORCE included) */
+int gg_reduce_blocks(gg_solver *s, int *G);
 /* the SpMV kernel the solver's matrix takes: 1 sliced ELL (k_spmv_sell: short,
  * evenly filled rows), 0 CSR-stream (k_spmv_stream) */
 int gg_spmv_sliced(gg_solver *s);

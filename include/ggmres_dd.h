@@ -87,15 +87,17 @@ int gg_dd_comm_ranks(gg_dd *d, int *ranks, int *rank);
  * ggmres_host.h), arrow permutation, ILU(0) of the permuted matrix, shards */
 int gg_dd_set_system(gg_dd *d, int n, const int *row_ptr, const int *col_idx, const double *val,
                      int method);
-/* info[0..10]: n, nparts, separator rows, max interface per shard, this
- * process's first shard: interior rows, interior solves (0 level-scheduled,
- * 2 / 3 the 2D / 3D wavefront), separator solves (0 level-scheduled launches,
- * 1 the fused separator step, 2 / 3 wavefront), local vector length (slots),
- * shards in this process, halo doubles exchanged per all-gather (received,
- * per shard), 1 when the orthogonalization runs with its exchanges inside
- * its kernels (GG_DD_IPC / GG_DD_LOOPBACK, P > 1, environment GG_DD_XK=1 at
- * gg_dd_create; measured slower than the default) */
+/* info[0..9] (exactly 10 ints): n, nparts, separator rows, max interface per
+ * shard, this process's first shard: interior rows, interior solves (0
+ * level-scheduled, 2 / 3 the 2D / 3D wavefront), separator solves (0
+ * level-scheduled launches, 1 the fused separator step, 2 / 3 wavefront),
+ * local vector length (slots), shards in this process, halo doubles exchanged
+ * per all-gather (received, per shard) */
 int gg_dd_info(gg_dd *d, int *info);
+/* *on = 1 when the orthogonalization runs with its exchanges inside its
+ * kernels (GG_DD_IPC / GG_DD_LOOPBACK, P > 1, environment GG_DD_XK=1 at
+ * gg_dd_create; measured slower than the default), else 0 */
+int gg_dd_xk_active(gg_dd *d, int *on);
 /* the arrow permutation in use: pinv[j] = new index of node j; q = its inverse */
 int gg_dd_perm(gg_dd *d, int *pinv, int *q);
 
