@@ -128,8 +128,12 @@ def parse():
                         "parity; default), mgs = the reference's modified Gram-Schmidt (i + 2 all-gathers)")
     p.add_argument("--c5-steps", type=int, default=1000)
     p.add_argument("--c5-scenarios", type=int, default=1,
-                   help="c5: independent source scenarios per GPU, solved concurrently (one solver, "
-                        "stream and host thread each; GG_SOLVE_SHARED_DEVICE)")
+                   help="c5: independent source scenarios per GPU (many-RHS), solved as one batch "
+                        "(--c5-mode batch) or concurrently")
+    p.add_argument("--c5-mode", choices=["batch", "streams"], default="batch",
+                   help="c5 with several scenarios: batch = gg_transient_batch, every launch serving all "
+                        "scenarios (batch.hip); streams = one solver, stream and host thread per scenario "
+                        "(GG_SOLVE_SHARED_DEVICE)")
     a = p.parse_args()
     if a.dd_comm == "loopback" and (a.gpus > 1 or not 0 <= a.dd_rank < a.dd_parts):
         p.error("--dd-comm loopback times one rank alone: --gpus 1 and 0 <= --dd-rank < --dd-parts")
@@ -745,15 +749,25 @@ def main():
         cdiag = np.full(n, 1e-3 / h5)
         ports = np.array([0, n // 2, n - 1], np.int32)
         solvers = [s]
-        for _ in range(S - 1):
-            s2 = ggmres.Solver(local)
-            s2.set_matrix(A)
-            s2.set_precond_ilu0()
-            s2.set_division(DIV_MODES[a.division])
-            solvers.append(s2)
+        c5_batch = S > 1 and a.c5_mode == "batch"
+        if c5_batch:
+            assert s.batch_engine, "c5 batch: the solver's configuration takes no batched launches"
+        else:
+            for _ in range(S - 1):
+                s2 = ggmres.Solver(local)
+                s2.set_matrix(A)
+                s2.set_precond_ilu0()
+                s2.set_division(DIV_MODES[a.division])
+                solvers.append(s2)
         flags = ggmres.SOLVE_SHARED_DEVICE if S > 1 else 0
+        X0 = np.zeros((S, n))
 
     def step():
+        if c5 and c5_batch:
+            r = s.transient_batch(a.c5_steps, h5, cdiag, scen, ports, X0, restart=a.restart,
+                                  max_iter=a.max_iter, tol=a.tol)
+            tot = sum(r["iters_total"])
+            return dict(inner=tot, iters=tot, relres=None, ret=r["ret"])
         if c5:
             out = [None] * len(solvers)
 
@@ -1017,8 +1031,10 @@ def main():
                                (f"C5: {a.grid}x{a.grid} 5-pt grid, A = G + C/h (c 1e-3, h 1e-2), "
                                 f"1% PULSE sources (own seeded scenarios), ILU(0) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, {a.c5_steps} backward-Euler "
-                                f"steps per step, warm start, {a.c5_scenarios} concurrent scenario(s) "
-                                f"per GPU") if c5 else
+                                f"steps per step, warm start, {a.c5_scenarios} scenario(s) per GPU"
+                                + (f" solved as one batch (gg_transient_batch)" if a.c5_scenarios > 1 and
+                                   a.c5_mode == "batch" else " on concurrent streams" if a.c5_scenarios > 1
+                                   else "")) if c5 else
                                (f"C3 stand-in: seeded power-law CSR with circuit5M's n and nnz "
                                 f"(no parity claim at this size), ILU({kilu}) left (device-factored; "
                                 f"C3 names ILU(1)), GMRES({a.restart}), tol {a.tol:g}, "

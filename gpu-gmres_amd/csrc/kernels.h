@@ -273,4 +273,51 @@ void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s
                    const UnitMap &um = UnitMap{});
 void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st);
 
+// ---- batched (many-RHS) launches, kernels.hip: nsc scenarios per launch,
+// scenario q's per-scenario buffers (vectors, partials, H, Givens, history,
+// control block, hand-off granules) q * zs bytes after scenario 0's; the gate's
+// done / nit likewise.  Same kernels and per-scenario arithmetic as above.
+constexpr int kBatchSpmv = 8;     // scenarios per batched SpMV launch (A read once for them)
+void launch_fill_u64_b(unsigned long long *p, long long n, unsigned long long v, int nsc, long long zs,
+                       hipStream_t st);
+// out_q[i] = idx[i] < 0 ? 0 : in_q[idx[i]]  (in / out strides zin / zout bytes)
+void launch_gather_b(const double *in, long long zin, const long long *idx, double *out, long long zout,
+                     long long n, int nsc, hipStream_t st);
+void launch_init_state_b(DevState *ds, long long zs, int nsc, double tol, int max_iter, int m, hipStream_t st);
+// out[q] = scenario q's control block, q < nsc; out[nsc].err = *err
+void launch_pack_states_b(const DevState *ds, long long zs, int nsc, DevState *out, const int *err, hipStream_t st);
+// u = each scenario's sources at time index it (soff: nsc + 1 offsets into the
+// concatenated kind / dptr tables, maxsrc the largest count); w_q = B_q u + (C/h) x_q
+// with scenario q's B^T rows at sptr + q * (n + 1) (sidx: global source indices)
+void launch_transient_step_b(int n, int nsc, int maxsrc, const int *soff, const int *kind, const int *dptr,
+                             const double *data, int it, double h, double *u, const int *sptr, const int *sidx,
+                             const double *cdiag, const double *x, double *w, long long ldx, hipStream_t st);
+void launch_gather_ports_b(int nport, const int *port, const double *x, long long ldx, double *out, long long ldo,
+                           int nsc, hipStream_t st);
+void launch_spmv_b(Gate g, const DevCsr &A, const double *x, const double *b, double *y, bool resid, int nsc,
+                   long long zs, hipStream_t st);
+// the 2D wavefront solve batched over scenarios (bnd: scenario 0's granules,
+// trsv_b_granules(T) words per scenario, armed); trsv_batchable: T admits it
+bool trsv_batchable(const DevTri &T);
+long long trsv_b_granules(const DevTri &T);
+int batch_zmap();   // GG_BATCH_ZMAP: workgroup -> (scenario, band) placement (kernels.hip trsv_wave2d_body)
+void launch_trsv_b(Gate g, DevTri &T, const double *b, double *x, unsigned long long *bnd, int *err, int nsc,
+                   long long zs, hipStream_t st);
+void launch_dot_b(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, int nsc,
+                  long long zs, hipStream_t st);
+void launch_set_normb_b(const double *part, int G, DevState *ds, int nsc, long long zs, hipStream_t st);
+void launch_init_beta_b(const double *part, int G, DevState *ds, double *hist, int nsc, long long zs, hipStream_t st);
+void launch_init_cycle_b(DevState *ds, const double *r, double *v0, double *s, int G, long long Ppad, int nsc,
+                         long long zs, hipStream_t st);
+void launch_mgs_step_b(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
+                       const double *part_in, double *part_out, double *H, int G, long long Ppad, int nsc,
+                       long long zs, hipStream_t st);
+void launch_arnoldi_finalize_b(Gate g, int i, int m, DevState *ds, const double *part, int G, const double *w,
+                               double *vnext, double *H, double *cs, double *sn, double *s, double *hist,
+                               long long Ppad, int nsc, long long zs, hipStream_t st);
+void launch_update_b(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall, const double *V,
+                     long long ldv, double *acc, int G, long long Ppad, const UnitMap &um, int nsc, long long zs,
+                     hipStream_t st);
+void launch_end_cycle_b(const double *part, int G, DevState *ds, double *hist, int nsc, long long zs, hipStream_t st);
+
 }  // namespace gg

@@ -24,6 +24,23 @@ __device__ __forceinline__ bool gated(const Gate &g)
     return false;
 }
 
+// Batched launches (kernels.h, the many-RHS solve): scenario sc's copy of a
+// per-scenario buffer (vectors, partials, H, the control block, hand-off
+// granules -- one arena per scenario) lies sc * zs bytes after scenario 0's.
+// zs = 0: the single-scenario launch, every pointer as given.
+template <class T>
+__device__ __forceinline__ T *zp(T *p, long long zs, int sc)
+{
+    return p ? reinterpret_cast<T *>(reinterpret_cast<unsigned long long>(p) + (unsigned long long)(sc * zs)) : p;
+}
+__device__ __forceinline__ bool gated_z(const Gate &g, long long zs, int sc)
+{
+    Gate h = g;
+    h.done = zp(g.done, zs, sc);
+    h.nit = zp(g.nit, zs, sc);
+    return gated(h);
+}
+
 // ---- reductions -------------------------------------------------------------
 // The xor butterfly v += v[lane ^ o], o = 32, 16, .., 1 (every lane ends with
 // the same sum).  After the steps above o, v depends only on the lane bits
@@ -218,8 +235,9 @@ __device__ __forceinline__ void st_sc1_16(double2 *p, double2 v)
 }
 
 // ============================================================== vector ops
-__global__ void k_fill_u64(unsigned long long *p, long long n, unsigned long long v)
+__global__ void k_fill_u64(unsigned long long *p, long long n, unsigned long long v, long long zs = 0)
 {
+    p = zp(p, zs, blockIdx.y);
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x)
         p[i] = v;
@@ -249,11 +267,15 @@ __global__ void k_copy(const double *in, double *out, long long units)
 }
 
 __global__ __launch_bounds__(kBlock) void k_dot(Gate g, const double *a, const double *b,
-                                                double *part, long long units)
+                                                double *part, long long units, long long zs = 0)
 {
     // units: the dot range (a prefix of the vector space; the sharded solve
-    // counts its separator replica on one shard only)
-    if (gated(g)) return;
+    // counts its separator replica on one shard only); zs: batched (blockIdx.y
+    // = scenario, every operand per scenario)
+    if (gated_z(g, zs, blockIdx.y)) return;
+    a = zp(a, zs, blockIdx.y);
+    b = zp(b, zs, blockIdx.y);
+    part = zp(part, zs, blockIdx.y);
     double acc = 0.0;
     const long long stride = (long long)gridDim.x * kBlock;
     for (long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x; u0 < units; u0 += 4 * stride) {
@@ -609,6 +631,67 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
     if (r < n) {
         const double o = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
         y[r] = YDIV ? o / ydiv[r] : o;
+    }
+}
+
+// Batched SpMV (the many-RHS solve): y_sc = A x_sc (RESID: b_sc - A x_sc) for
+// up to NS scenarios per launch (scenario sc's vectors sc * zs bytes after
+// scenario 0's), A's sliced-ELL entries read ONCE per wave for all of them.
+// Every row of every scenario is summed exactly as k_spmv_sell sums it (entry
+// order from 0.0, no contraction): the same bits.  A scenario whose gate is
+// closed (converged) is skipped.
+template <bool RESID, int NS>
+__global__ __launch_bounds__(kBlock) void k_spmv_sell_b(Gate g, long long zs, int nsc, int n, int nslice,
+                                                        const int *sptr, const int *__restrict__ ci,
+                                                        const double *__restrict__ v, const double *x,
+                                                        const double *b, double *y)
+{
+    const int s = xcd_block() * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (s >= nslice) return;
+    bool act[NS];
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
+        act[q] = q < nsc && !gated_z(g, zs, q);
+        any |= act[q];
+    }
+    if (!any) return;
+    const int lane = threadIdx.x & 63;
+    const int off = sptr[s], w = (sptr[s + 1] - off) >> 6;
+    const int *cp = ci + off + lane;
+    const double *vp = v + off + lane;
+    double acc[NS];
+#pragma unroll
+    for (int q = 0; q < NS; q++) acc[q] = 0.0;
+    for (int k0 = 0; k0 < w; k0 += 8) {
+        int c[8];
+        double a[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k0 + k < w) {
+                c[k] = __builtin_nontemporal_load(cp + (k0 + k) * 64);
+                a[k] = __builtin_nontemporal_load(vp + (k0 + k) * 64);
+            }
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            if (!act[q]) continue;
+            const double *xq = zp(x, zs, q);
+            double xv[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (k0 + k < w && c[k] >= 0) xv[k] = xq[c[k]];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (k0 + k < w && c[k] >= 0) acc[q] += a[k] * xv[k];
+        }
+    }
+    const int r = s * 64 + lane;
+    if (r < n) {
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            if (!act[q]) continue;
+            zp(y, zs, q)[r] = RESID ? (-1.0 * acc[q] + 1.0 * zp(b, zs, q)[r]) : acc[q];
+        }
     }
 }
 
@@ -1389,13 +1472,21 @@ __device__ __forceinline__ void fused_spmv_role(const FusedSpmv &fs, int nbands,
 // then the line term -- the split (ILU++) U factor's ascending-column rows
 // (MyILUPP::HostPrecond_right, src/preconditioner.cu:1117-1137).
 // FS: the SpMV fused into the launch (see FusedSpmv; forward unskewed 2D only).
-template <bool FWD, int DIV, bool TRACE, bool D3, int S, bool IL, bool FS>
+// BT: a batched launch (the many-RHS solve) -- zS scenarios of nbands
+// workgroups each; scenario sc's b, x and hand-off granules (with its dummies)
+// lie sc * zs bytes after scenario 0's, its control block likewise (the gate).
+// zmap 0: workgroup = band * zS + sc (workgroups being dealt round-robin over
+// the XCDs, a scenario's bands share an XCD when zS is a multiple of 8, so its
+// hand-offs stay in one L2); zmap 1: workgroup = sc * nbands + band (band b of
+// every scenario on one XCD: the coefficient streams shared in its L2).
+template <bool FWD, int DIV, bool TRACE, bool D3, int S, bool IL, bool FS, bool BT = false>
 __device__ __forceinline__ void trsv_wave2d_body(
     Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
     const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
     double *__restrict__ x, unsigned long long *bnd, int *err, long long *trace,
     int nz, long long P2, const double *__restrict__ c0, unsigned long long *prog,
-    const double *__restrict__ ce1, const double *__restrict__ ce2, const FusedSpmv &fs)
+    const double *__restrict__ ce1, const double *__restrict__ ce2, const FusedSpmv &fs,
+    int zS = 1, long long zs = 0, int zmap = 0)
 {
     using C = WaveCfg<DIV, D3, S>;
     // LDS work in the lane shift's shadow -- not for the unit L's fused rows,
@@ -1410,8 +1501,17 @@ __device__ __forceinline__ void trsv_wave2d_body(
     static_assert(!(TRACE && S > 1), "no trace for skewed grids");
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
     static_assert(!(D3 && TRACE), "no trace for 3D grids");
-    if (gated(g)) return;
+    static_assert(!BT || (!FS && !D3 && !TRACE), "batched: 2D, separate SpMV, no trace");
+    if (!BT && gated(g)) return;
     int bid = (int)blockIdx.x;                  // this workgroup among the bands
+    if constexpr (BT) {
+        const int sc = zmap == 0 ? bid % zS : bid / nbands;
+        bid = zmap == 0 ? bid / zS : bid % nbands;
+        if (gated_z(g, zs, sc)) return;
+        b = zp(b, zs, sc);
+        x = zp(x, zs, sc);
+        bnd = zp(bnd, zs, sc);
+    }
     if constexpr (FS) {
         if (bid < fs.ns) {
             fused_spmv_role(fs, nbands, T, C::THREADS / 64);
@@ -1445,11 +1545,11 @@ __device__ __forceinline__ void trsv_wave2d_body(
     // 88.9 -> 90.0 us (round 3, re-measured: 89.4 / 90.3 -> 89.9 / 90.4 us), so
     // the forward solve keeps one workgroup per band.
     // (the fused SpMV's launch holds one workgroup per band: no placement there)
-    constexpr int XS = (D3 || FS || FWD) ? 1 : GG_WAVE_XCD;
+    constexpr int XS = (D3 || FS || FWD || BT) ? 1 : GG_WAVE_XCD;
     if (XS > 1 && bid % XS) return;
     const int blk = bid / XS;
     const int ntask = nz * nbands;
-    for (int task = blk; task < ntask; task += (FS ? nbands : (int)gridDim.x / XS)) {
+    for (int task = blk; task < ntask; task += ((FS || BT) ? nbands : (int)gridDim.x / XS)) {
     const int kq = task / nbands, bq = task % nbands;
     const int band = FWD ? bq : (nbands - 1 - bq);
     const int kp = FWD ? kq : (nz - 1 - kq);    // plane
@@ -1907,6 +2007,18 @@ __global__ __launch_bounds__((WaveCfg<DIV>::THREADS)) void k_trsv_wave2d_spmv(
     trsv_wave2d_body<true, DIV, false, false, 1, false, true>(g, T, nbands, fs.w, c1, c2, dv, rv, x, bnd, err,
                                                               nullptr, 1, P2, nullptr, nullptr, nullptr, nullptr,
                                                               fs);
+}
+
+// batched 2D solve (the many-RHS solve): zS scenarios, nbands workgroups each
+template <bool FWD, int DIV>
+__global__ __launch_bounds__((WaveCfg<DIV>::THREADS)) void k_trsv_wave2d_batch(
+    Gate g, int T, int nbands, const double *__restrict__ b, const double *__restrict__ c1,
+    const double *__restrict__ c2, const double *__restrict__ dv, const double *__restrict__ rv,
+    double *__restrict__ x, unsigned long long *bnd, int *err, long long P2, int zS, long long zs, int zmap)
+{
+    trsv_wave2d_body<FWD, DIV, false, false, 1, false, false, true>(g, T, nbands, b, c1, c2, dv, rv, x, bnd, err,
+                                                                    nullptr, 1, P2, nullptr, nullptr, nullptr,
+                                                                    nullptr, FusedSpmv{}, zS, zs, zmap);
 }
 
 // ================================================ 3D 7-point grids: tile wavefront
@@ -2806,9 +2918,83 @@ __global__ void k_gather_ports(int nport, const int *port, const double *x, doub
     if (j < nport) out[j] = x[port[j]];
 }
 
-// ============================================================ GMRES kernels
-__global__ void k_set_normb(const double *part, int G, DevState *ds)
+// ---- batched (many-RHS) helpers: blockIdx.y = scenario ----------------------
+// out_sc[i] = idx[i] < 0 ? 0 : in_sc[idx[i]], in / out strides zin / zout bytes
+__global__ void k_gather_b(const double *in, long long zin, const long long *idx, double *out, long long zout,
+                           long long n)
 {
+    in = zp(in, zin, blockIdx.y);
+    out = zp(out, zout, blockIdx.y);
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long s = idx[i];
+        out[i] = s < 0 ? 0.0 : in[s];
+    }
+}
+// every scenario's control block at the start of a solve (as the host writes
+// the single solver's)
+__global__ void k_init_state_b(DevState *ds, long long zs, int nsc, double tol, int max_iter, int m)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nsc) return;
+    DevState h{};
+    h.tol = tol;
+    h.max_iter = max_iter;
+    h.m = m;
+    h.j = 1;
+    *zp(ds, zs, q) = h;
+}
+// the scenarios' control blocks side by side (one copy to the host per cycle)
+__global__ void k_pack_states_b(const DevState *ds, long long zs, int nsc, DevState *out, const int *err)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nsc) out[q] = *zp(ds, zs, q);
+    if (q == nsc) out[nsc].err = *err;          // the error word after every launch before this one
+}
+// transient step of every scenario: u_sc = its sources at time index it; w_sc
+// = B_sc u_sc + (C/h) x_sc (k_sources + k_transient_rhs per scenario; tables
+// concatenated, scenario sc's sources [soff[sc], soff[sc+1]) and its B^T rows
+// at sptr + sc * (n + 1); x and w natural order, stride ldx doubles)
+__global__ void k_sources_b(const int *soff, const int *kind, const int *dptr, const double *data, int it,
+                            double h, double *u)
+{
+    const int q = blockIdx.y;
+    const int k = soff[q] + blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= soff[q + 1]) return;
+    const double *d = data + dptr[k];
+    const double t = it * h;
+    double value = 0.0;
+    if (kind[k] == GG_SRC_DC) value = d[0];
+    else if (kind[k] == GG_SRC_PULSE) value = pulse_value(d, t);
+    else value = pwl_value(d, (dptr[k + 1] - dptr[k]) / 2, t);
+    u[k] = value;
+}
+__global__ void k_transient_rhs_b(int n, const int *sptr, const int *sidx, const double *u, const double *cdiag,
+                                  const double *x, double *w, long long ldx)
+{
+    const int q = blockIdx.y;
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int *sp = sptr + (long long)q * (n + 1);
+    double bu = 0.0;
+    for (int k = sp[r]; k < sp[r + 1]; k++) bu = bu + 1.0 * u[sidx[k]];
+    double xnr = 0.0;
+    xnr = xnr + cdiag[r] * x[(long long)q * ldx + r];
+    w[(long long)q * ldx + r] = bu + xnr;
+}
+__global__ void k_gather_ports_b(int nport, const int *port, const double *x, long long ldx, double *out,
+                                 long long ldo)
+{
+    const int q = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < nport) out[(long long)q * ldo + j] = x[(long long)q * ldx + port[j]];
+}
+
+// ============================================================ GMRES kernels
+__global__ void k_set_normb(const double *part, int G, DevState *ds, long long zs = 0)
+{
+    part = zp(part, zs, blockIdx.y);
+    ds = zp(ds, zs, blockIdx.y);
     double s = sum_partials(part, G);
     if (threadIdx.x == 0) {
         double nb = sqrt(s);
@@ -2816,8 +3002,11 @@ __global__ void k_set_normb(const double *part, int G, DevState *ds)
     }
 }
 
-__global__ void k_init_beta(const double *part, int G, DevState *ds, double *hist)
+__global__ void k_init_beta(const double *part, int G, DevState *ds, double *hist, long long zs = 0)
 {
+    part = zp(part, zs, blockIdx.y);
+    ds = zp(ds, zs, blockIdx.y);
+    hist = zp(hist, zs, blockIdx.y);
     double s = sum_partials(part, G);
     if (threadIdx.x == 0) {
         double beta = sqrt(s);
@@ -2833,8 +3022,12 @@ __global__ void k_init_beta(const double *part, int G, DevState *ds, double *his
 
 // v0 = r * (1/beta); s = 0; s[0] = beta; nit = min(m, max_iter - j + 1)
 __global__ __launch_bounds__(kBlock) void k_init_cycle(DevState *ds, const double *r, double *v0,
-                                                       double *s, long long units)
+                                                       double *s, long long units, long long zs = 0)
 {
+    ds = zp(ds, zs, blockIdx.y);
+    r = zp(r, zs, blockIdx.y);
+    v0 = zp(v0, zs, blockIdx.y);
+    s = zp(s, zs, blockIdx.y);
     if (ds->done) return;
     if (ds->max_iter - ds->j + 1 <= 0) {   // a cycle past max_iter (pipelined): nothing runs
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2876,12 +3069,21 @@ __global__ __launch_bounds__(kBlock) void k_mgs_step(Gate g, int i, int k, int m
                                                      const double *__restrict__ vnext,
                                                      const double *part_in, double *part_out,
                                                      double *H, int G, long long units,
-                                                     long long dunits)
+                                                     long long dunits, long long zs = 0)
 {
     // the AXPY runs over [0, units); the next dot accumulates over [0, dunits)
     // (dunits < units on the shards of a sharded solve that do not own the
     // separator replica); part_in holds G partials (all shards' in that case)
-    if (gated(g)) return;
+    if (gated_z(g, zs, blockIdx.y)) return;
+    if (zs) {
+        const int sc = blockIdx.y;
+        w = zp(w, zs, sc);
+        vk = zp(vk, zs, sc);
+        vnext = zp(vnext, zs, sc);
+        part_in = zp(part_in, zs, sc);
+        part_out = zp(part_out, zs, sc);
+        H = zp(H, zs, sc);
+    }
     double acc = 0.0;
     const long long stride = (long long)gridDim.x * kBlock;
     long long u0 = blockIdx.x * (long long)kBlock + threadIdx.x;
@@ -3079,9 +3281,21 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_finalize(Gate g, int i, int 
                                                              const double *w, double *vnext,
                                                              double *H, double *cs, double *sn,
                                                              double *s, double *hist,
-                                                             long long units)
+                                                             long long units, long long zs = 0)
 {
-    if (gated(g)) return;
+    if (gated_z(g, zs, blockIdx.y)) return;
+    if (zs) {
+        const int sc = blockIdx.y;
+        ds = zp(ds, zs, sc);
+        part = zp(part, zs, sc);
+        w = zp(w, zs, sc);
+        vnext = zp(vnext, zs, sc);
+        H = zp(H, zs, sc);
+        cs = zp(cs, zs, sc);
+        sn = zp(sn, zs, sc);
+        s = zp(s, zs, sc);
+        hist = zp(hist, zs, sc);
+    }
     const double hn = sqrt(sum_partials(part, G));
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const int ld = m + 1;
@@ -4205,9 +4419,13 @@ __global__ __launch_bounds__(kBlock, 2) void k_arnoldi_wide(Gate g, int i, int m
 // operations in the same order as the serial back-substitution.
 constexpr int kMaxRestart = 64;
 __global__ __launch_bounds__(64) void k_update_y(Gate g, int m, DevState *ds, const double *H,
-                                                 const double *s, double *y)
+                                                 const double *s, double *y, long long zs = 0)
 {
-    if (gated(g)) return;
+    if (gated_z(g, zs, blockIdx.y)) return;
+    ds = zp(ds, zs, blockIdx.y);
+    H = zp(H, zs, blockIdx.y);
+    s = zp(s, zs, blockIdx.y);
+    y = zp(y, zs, blockIdx.y);
     const int lane = threadIdx.x;
     const int k = (ds->done & DONE_INNER) ? ds->conv_i : ds->nit - 1;
     if (lane == 0) ds->upd_k = k;
@@ -4228,9 +4446,13 @@ __global__ __launch_bounds__(64) void k_update_y(Gate g, int m, DevState *ds, co
 
 // the same for restarts above kMaxRestart: one thread, serial
 __global__ void k_update_y_serial(Gate g, int m, DevState *ds, const double *H, const double *s,
-                                  double *y)
+                                  double *y, long long zs = 0)
 {
-    if (gated(g)) return;
+    if (gated_z(g, zs, blockIdx.y)) return;
+    ds = zp(ds, zs, blockIdx.y);
+    H = zp(H, zs, blockIdx.y);
+    s = zp(s, zs, blockIdx.y);
+    y = zp(y, zs, blockIdx.y);
     if (threadIdx.x != 0) return;
     const int k = (ds->done & DONE_INNER) ? ds->conv_i : ds->nit - 1;
     ds->upd_k = k;
@@ -4245,9 +4467,13 @@ __global__ void k_update_y_serial(Gate g, int m, DevState *ds, const double *H, 
 // acc += sum_{j<=k} V_j y_j   (ascending j, as the reference's x[i] += v*y loop)
 __global__ __launch_bounds__(kBlock) void k_update_x(Gate g, const DevState *ds, const double *y,
                                                      const double *V, long long ldv, double *acc,
-                                                     long long units, UnitMap um)
+                                                     long long units, UnitMap um, long long zs = 0)
 {
-    if (gated(g)) return;
+    if (gated_z(g, zs, blockIdx.y)) return;
+    ds = zp(ds, zs, blockIdx.y);
+    y = zp(y, zs, blockIdx.y);
+    V = zp(V, zs, blockIdx.y);
+    acc = zp(acc, zs, blockIdx.y);
     const int k = ds->upd_k;
     for (long long u = blockIdx.x * (long long)kBlock + threadIdx.x; u < units;
          u += (long long)gridDim.x * kBlock) {
@@ -4272,8 +4498,11 @@ __global__ __launch_bounds__(kBlock) void k_update_x(Gate g, const DevState *ds,
 }
 
 // beta = ||r|| after a restart; history; j += nit
-__global__ void k_end_cycle(const double *part, int G, DevState *ds, double *hist)
+__global__ void k_end_cycle(const double *part, int G, DevState *ds, double *hist, long long zs = 0)
 {
+    part = zp(part, zs, blockIdx.y);
+    ds = zp(ds, zs, blockIdx.y);
+    hist = zp(hist, zs, blockIdx.y);
     if (ds->done) {
         // the cycle that converged inside has applied its update: a cycle
         // enqueued behind it must not apply it again
@@ -5123,6 +5352,174 @@ void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s
 void launch_end_cycle(const double *part, int G, DevState *ds, double *hist, hipStream_t st)
 {
     k_end_cycle<<<1, kBlock, 0, st>>>(part, G, ds, hist);
+}
+
+}  // namespace gg
+
+// ================================================= batched (many-RHS) launchers
+// nsc scenarios per launch; scenario q's per-scenario buffers q * zs bytes after
+// scenario 0's (solver.hip / batch.hip: one arena per scenario).  The same
+// kernels as the single-scenario launchers with blockIdx.y = scenario: the
+// same per-scenario arithmetic, bit for bit.
+namespace gg {
+
+void launch_fill_u64_b(unsigned long long *p, long long n, unsigned long long v, int nsc, long long zs,
+                       hipStream_t st)
+{
+    k_fill_u64<<<dim3(blocks_for(n, kBlock, 4096), nsc), kBlock, 0, st>>>(p, n, v, zs);
+}
+void launch_gather_b(const double *in, long long zin, const long long *idx, double *out, long long zout,
+                     long long n, int nsc, hipStream_t st)
+{
+    k_gather_b<<<dim3(blocks_for(n, kBlock, 4096), nsc), kBlock, 0, st>>>(in, zin, idx, out, zout, n);
+}
+void launch_init_state_b(DevState *ds, long long zs, int nsc, double tol, int max_iter, int m, hipStream_t st)
+{
+    k_init_state_b<<<(nsc + 63) / 64, 64, 0, st>>>(ds, zs, nsc, tol, max_iter, m);
+}
+void launch_pack_states_b(const DevState *ds, long long zs, int nsc, DevState *out, const int *err, hipStream_t st)
+{
+    k_pack_states_b<<<(nsc + 64) / 64, 64, 0, st>>>(ds, zs, nsc, out, err);
+}
+void launch_transient_step_b(int n, int nsc, int maxsrc, const int *soff, const int *kind, const int *dptr,
+                             const double *data, int it, double h, double *u, const int *sptr, const int *sidx,
+                             const double *cdiag, const double *x, double *w, long long ldx, hipStream_t st)
+{
+    if (maxsrc > 0) k_sources_b<<<dim3((maxsrc + kBlock - 1) / kBlock, nsc), kBlock, 0, st>>>(soff, kind, dptr, data, it, h, u);
+    if (n > 0) k_transient_rhs_b<<<dim3((n + kBlock - 1) / kBlock, nsc), kBlock, 0, st>>>(n, sptr, sidx, u, cdiag, x, w, ldx);
+}
+void launch_gather_ports_b(int nport, const int *port, const double *x, long long ldx, double *out, long long ldo,
+                           int nsc, hipStream_t st)
+{
+    if (nport > 0)
+        k_gather_ports_b<<<dim3((nport + kBlock - 1) / kBlock, nsc), kBlock, 0, st>>>(nport, port, x, ldx, out, ldo);
+}
+void launch_spmv_b(Gate g, const DevCsr &A, const double *x, const double *b, double *y, bool resid, int nsc,
+                   long long zs, hipStream_t st)
+{
+    if (A.nblk == 0) return;
+    if (!A.sell) {
+        // CSR-stream (no sliced copy): one launch per scenario, the same kernel
+        for (int q = 0; q < nsc; q++) {
+            const long long o = (long long)q * zs;
+            auto at = [o](auto *p) { return p ? reinterpret_cast<decltype(p)>(reinterpret_cast<char *>(const_cast<void *>(static_cast<const void *>(p))) + o) : p; };
+            Gate gq = g;
+            gq.done = at(g.done);
+            gq.nit = at(g.nit);
+            launch_spmv(gq, A, at(x), resid ? at(b) : nullptr, at(y), resid, st);
+        }
+        return;
+    }
+    const int blocks = (A.nslice + kBlock / 64 - 1) / (kBlock / 64);
+    // up to 8 scenarios per launch (A's entries read once for all of them)
+    for (int q0 = 0; q0 < nsc; q0 += kBatchSpmv) {
+        const int c = std::min(kBatchSpmv, nsc - q0);
+        const long long o = (long long)q0 * zs;
+        auto at = [o](auto *p) { return p ? reinterpret_cast<decltype(p)>(reinterpret_cast<char *>(const_cast<void *>(static_cast<const void *>(p))) + o) : p; };
+        Gate gq = g;
+        gq.done = at(g.done);
+        gq.nit = at(g.nit);
+        if (resid)
+            k_spmv_sell_b<true, kBatchSpmv><<<blocks, kBlock, 0, st>>>(gq, zs, c, A.n, A.nslice, A.sptr.p, A.sci.p,
+                                                                       A.sv.p, at(x), at(b), at(y));
+        else
+            k_spmv_sell_b<false, kBatchSpmv><<<blocks, kBlock, 0, st>>>(gq, zs, c, A.n, A.nslice, A.sptr.p, A.sci.p,
+                                                                        A.sv.p, at(x), nullptr, at(y));
+    }
+}
+bool trsv_batchable(const DevTri &T)
+{
+    const Wave2D &w = T.wl;
+    if (T.kind != DevTri::WAVE2D || T.tail || !w.ok || w.tile || w.nz != 1 || w.skew != 1 || T.il || T.trace)
+        return false;
+    const int e = T.eff_div();
+    return T.lower ? (e == WD_UNIT || e == WD_UFMA) : (e == WD_HW || e == WD_RCP || e == WD_MUL || e == WD_SFMA);
+}
+int batch_zmap()
+{
+    static const int z = [] {
+        const char *e = std::getenv("GG_BATCH_ZMAP");
+        return e ? std::atoi(e) : 0;
+    }();
+    return z;
+}
+void launch_trsv_b(Gate g, DevTri &T, const double *b, double *x, unsigned long long *bnd, int *err, int nsc,
+                   long long zs, hipStream_t st)
+{
+    GG_REQUIRE(trsv_batchable(T), GG_EINVAL, "batched triangular solve: 2D wavefront, canonical order only");
+    const Wave2D &w = T.wl;
+    const int e = T.eff_div();
+    const int zmap = batch_zmap();
+    const dim3 grid(w.nbands * nsc);
+    const double *k1 = e == WD_SFMA ? T.c1s.p : T.c1.p, *k2 = e == WD_SFMA ? T.c2s.p : T.c2.p;
+    const double *dv = (e == WD_UNIT || e == WD_UFMA) ? nullptr : (e == WD_MUL || e == WD_SFMA) ? T.rw.p : T.dw.p;
+    const double *rv = e == WD_RCP ? T.rw.p : nullptr;
+#define GG_BT(FWD, DIV)                                                                                     \
+    k_trsv_wave2d_batch<FWD, DIV><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(g, w.T, w.nbands, b, k1, k2, dv, rv, \
+                                                                          x, bnd, err, w.P2, nsc, zs, zmap)
+    if (T.lower) {
+        if (e == WD_UFMA) GG_BT(true, WD_UFMA);
+        else GG_BT(true, WD_UNIT);
+    } else {
+        if (e == WD_SFMA) GG_BT(false, WD_SFMA);
+        else if (e == WD_MUL) GG_BT(false, WD_MUL);
+        else if (e == WD_RCP) GG_BT(false, WD_RCP);
+        else GG_BT(false, WD_HW);
+    }
+#undef GG_BT
+}
+long long trsv_b_granules(const DevTri &T)
+{
+    // hand-off granules, then per band workgroup 64 zero + 64 write-only dummies, + 64
+    return T.wl.ngran() + 128LL * T.wl.nbands + 64;
+}
+void launch_dot_b(Gate g, const double *a, const double *b, double *part, int G, long long Ppad, int nsc,
+                  long long zs, hipStream_t st)
+{
+    k_dot<<<dim3(G, nsc), kBlock, 0, st>>>(g, a, b, part, Ppad / 2, zs);
+}
+void launch_set_normb_b(const double *part, int G, DevState *ds, int nsc, long long zs, hipStream_t st)
+{
+    k_set_normb<<<dim3(1, nsc), kBlock, 0, st>>>(part, G, ds, zs);
+}
+void launch_init_beta_b(const double *part, int G, DevState *ds, double *hist, int nsc, long long zs, hipStream_t st)
+{
+    k_init_beta<<<dim3(1, nsc), kBlock, 0, st>>>(part, G, ds, hist, zs);
+}
+void launch_init_cycle_b(DevState *ds, const double *r, double *v0, double *s, int G, long long Ppad, int nsc,
+                         long long zs, hipStream_t st)
+{
+    k_init_cycle<<<dim3(G, nsc), kBlock, 0, st>>>(ds, r, v0, s, Ppad / 2, zs);
+}
+void launch_mgs_step_b(Gate g, int i, int k, int m, double *w, const double *vk, const double *vnext,
+                       const double *part_in, double *part_out, double *H, int G, long long Ppad, int nsc,
+                       long long zs, hipStream_t st)
+{
+    if (vnext == w)
+        k_mgs_step<true><<<dim3(G, nsc), kBlock, 0, st>>>(g, i, k, m, w, vk, nullptr, part_in, part_out, H, G,
+                                                          Ppad / 2, Ppad / 2, zs);
+    else
+        k_mgs_step<false><<<dim3(G, nsc), kBlock, 0, st>>>(g, i, k, m, w, vk, vnext, part_in, part_out, H, G,
+                                                           Ppad / 2, Ppad / 2, zs);
+}
+void launch_arnoldi_finalize_b(Gate g, int i, int m, DevState *ds, const double *part, int G, const double *w,
+                               double *vnext, double *H, double *cs, double *sn, double *s, double *hist,
+                               long long Ppad, int nsc, long long zs, hipStream_t st)
+{
+    k_arnoldi_finalize<<<dim3(G, nsc), kBlock, 0, st>>>(g, i, m, ds, part, G, w, vnext, H, cs, sn, s, hist,
+                                                        Ppad / 2, zs);
+}
+void launch_update_b(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall, const double *V,
+                     long long ldv, double *acc, int G, long long Ppad, const UnitMap &um, int nsc, long long zs,
+                     hipStream_t st)
+{
+    if (m <= kMaxRestart) k_update_y<<<dim3(1, nsc), 64, 0, st>>>(g, m, ds, H, s, ysmall, zs);
+    else k_update_y_serial<<<dim3(1, nsc), 64, 0, st>>>(g, m, ds, H, s, ysmall, zs);
+    k_update_x<<<dim3(G, nsc), kBlock, 0, st>>>(g, ds, ysmall, V, ldv, acc, Ppad / 2, um, zs);
+}
+void launch_end_cycle_b(const double *part, int G, DevState *ds, double *hist, int nsc, long long zs, hipStream_t st)
+{
+    k_end_cycle<<<dim3(1, nsc), kBlock, 0, st>>>(part, G, ds, hist, zs);
 }
 
 }  // namespace gg

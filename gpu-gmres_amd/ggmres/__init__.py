@@ -34,6 +34,7 @@ EXPORTS = [
     "gg_transient_mna", "gg_set_division", "gg_division_active",
     "gg_trsv_kernel", "gg_mgs_kernel", "gg_set_precond_user", "gg_solve_device_f32",
     "gg_device_fingerprint", "gg_set_matrix_count", "gg_trsv_levels", "gg_layout", "gg_reduce_blocks",
+    "gg_solve_batch_device", "gg_solve_batch", "gg_batch_engine", "gg_batch_history", "gg_transient_batch",
 ]
 # gg_precond_fn: int (*)(void *ctx, int op, const float *in, float *out, int n), device arrays
 PRECOND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -132,6 +133,15 @@ def lib():
         L.gg_layout.argtypes = [_VP, ctypes.c_void_p, ctypes.c_longlong]
         L.gg_layout.restype = ctypes.c_longlong
         L.gg_reduce_blocks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int)]
+        L.gg_solve_batch_device.argtypes = [_VP, ctypes.c_int, _VP, ctypes.c_longlong, _VP, ctypes.c_longlong,
+                                            ctypes.POINTER(Options), ctypes.POINTER(Result)]
+        L.gg_solve_batch.argtypes = [_VP, ctypes.c_int, _D, ctypes.c_longlong, _D, ctypes.c_longlong,
+                                     ctypes.POINTER(Options), ctypes.POINTER(Result)]
+        L.gg_batch_engine.argtypes = [_VP]
+        L.gg_batch_history.argtypes = [_VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong]
+        L.gg_batch_history.restype = ctypes.c_longlong
+        L.gg_transient_batch.argtypes = [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_double, _D, _I, _I, _I, _I, _D,
+                                         ctypes.c_int, _I, _D, ctypes.POINTER(Options), _D, _I]
         L.gg_profile_enable.argtypes = [_VP, ctypes.c_int]
         L.gg_profile_reset.argtypes = [_VP]
         L.gg_profile_get.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
@@ -316,6 +326,87 @@ class Solver:
                                           ctypes.byref(r)), allow_nc=True)
         return dict(ret=rc, iters=r.iters, inner=r.inner_iters, restarts=r.restarts,
                     relres=r.relres, solve_ms=r.solve_ms)
+
+    # ---- many right-hand sides (gg_solve_batch*, batch.hip) -----------------
+    @property
+    def batch_engine(self):
+        """True when gg_solve_batch* runs batched launches (else scenario by scenario)"""
+        return bool(_check(lib().gg_batch_engine(self.h), allow_nc=True))
+
+    @staticmethod
+    def _batch_out(rc, res):
+        return dict(ret=rc, iters=[r.iters for r in res], inner=[r.inner_iters for r in res],
+                    restarts=[r.restarts for r in res], relres=[r.relres for r in res],
+                    status=[r.status for r in res], solve_ms=res[0].solve_ms if len(res) else 0.0)
+
+    def solve_batch(self, B, X0=None, restart=30, max_iter=3000, tol=1e-10):
+        """nrhs independent solves A x_q = b_q (rows of B), batched; returns
+        dict(x [nrhs, n], iters / inner / restarts / relres / status per
+        scenario, hist = per-scenario histories)."""
+        B = np.ascontiguousarray(np.atleast_2d(B), np.float64)
+        S, n = B.shape
+        X = np.zeros((S, n)) if X0 is None else np.array(np.atleast_2d(X0), np.float64, copy=True, order="C")
+        o = Options(int(restart), int(max_iter), float(tol), 0)
+        res = (Result * S)()
+        rc = _check(lib().gg_solve_batch(self.h, S, B.reshape(-1), n, X.reshape(-1), n, ctypes.byref(o), res),
+                    allow_nc=True)
+        out = self._batch_out(rc, res)
+        out["x"] = X
+        out["hist"] = [self.batch_history(q) for q in range(S)]
+        return out
+
+    def solve_batch_device(self, b_ptr, x_ptr, nrhs, ld=None, restart=30, max_iter=3000, tol=1e-10):
+        """device addresses of nrhs right-hand sides / solutions, leading dimension ld (default n)"""
+        ld = self.n if ld is None else int(ld)
+        o = Options(int(restart), int(max_iter), float(tol), 0)
+        res = (Result * int(nrhs))()
+        rc = _check(lib().gg_solve_batch_device(self.h, int(nrhs), _VP(b_ptr), ld, _VP(x_ptr), ld,
+                                                ctypes.byref(o), res), allow_nc=True)
+        return self._batch_out(rc, res)
+
+    def batch_history(self, q):
+        """scenario q's residual history of the last batched solve (empty when
+        the scenarios ran one by one: see history() after each)"""
+        n = int(lib().gg_batch_history(self.h, int(q), None, 0))
+        if n < 0:
+            return np.zeros(0)
+        out = np.zeros(n)
+        lib().gg_batch_history(self.h, int(q), out.ctypes.data, n)
+        return out
+
+    def transient_batch(self, nsteps, h, cdiag, scenarios, ports, X0, restart=32, max_iter=10000, tol=1e-7):
+        """gg_transient_batch: scenarios = [(src_node, sources), ...] with sources
+        = [(kind, params), ...] (as transient_src) or a PULSE parameter array
+        (n_src x 7); X0 [nrhs, n].  Returns dict(x [nrhs, n], ports [nrhs, nport,
+        nsteps+1], iters_total [nrhs], ret)."""
+        S = len(scenarios)
+        X = np.array(np.atleast_2d(X0), np.float64, copy=True, order="C")
+        assert X.shape == (S, self.n)
+        nodes, kinds, lens, datas, off = [], [], [], [], [0]
+        for src_node, sources in scenarios:
+            if not isinstance(sources, (list, tuple)):
+                sources = [(SRC_PULSE, q) for q in np.asarray(sources, np.float64).reshape(-1, 7)]
+            nodes.append(np.asarray(src_node, np.int32))
+            kinds += [k for k, _ in sources]
+            lens += [len(q) for _, q in sources]
+            datas += [np.asarray(q, np.float64) for _, q in sources]
+            off.append(off[-1] + len(sources))
+        node = np.concatenate(nodes).astype(np.int32) if off[-1] else np.zeros(1, np.int32)
+        kind = np.array(kinds or [0], np.int32)
+        ptr = np.zeros(off[-1] + 1, np.int32)
+        ptr[1:] = np.cumsum(lens) if lens else []
+        data = np.concatenate(datas) if datas else np.zeros(1)
+        ports = np.ascontiguousarray(ports, np.int32)
+        pv = np.zeros(max(S * len(ports) * (nsteps + 1), 1))
+        tot = np.zeros(S, np.int32)
+        o = Options(int(restart), int(max_iter), float(tol), 0)
+        one = np.zeros(1, np.int32)
+        rc = _check(lib().gg_transient_batch(self.h, S, int(nsteps), float(h), np.ascontiguousarray(cdiag, np.float64),
+                                             np.array(off, np.int32), node, kind, ptr, data, len(ports),
+                                             ports if len(ports) else one, X.reshape(-1), ctypes.byref(o), pv, tot),
+                    allow_nc=True)
+        return dict(x=X, ports=pv[: S * len(ports) * (nsteps + 1)].reshape(S, len(ports), nsteps + 1),
+                    iters_total=[int(t) for t in tot], ret=rc)
 
     def transient(self, nsteps, h, cdiag, src_node, pulse, ports, x0, restart=32,
                   max_iter=10000, tol=1e-7, flags=0):

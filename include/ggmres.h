@@ -348,6 +348,41 @@ int gg_transient_mna(gg_solver *s, int it0, int nsteps, double h, const int *r_r
 int gg_transient_set_taps(gg_solver *s, int ntap, const int *tap_node);
 int gg_transient_get_taps(gg_solver *s, double *max_v, double *min_v, double *avg_v, double *ir);
 
+/* ---- many right-hand sides (batch.hip; SURVEY.md 8(d) C5 "many-RHS") ----
+ * nrhs independent systems A x_q = b_q on the solver's matrix and
+ * preconditioner (the reference runs its step driver, src/mna_solve_gpu_gmres.
+ * cpp:564-647, once per source scenario).  Scenario q's b / x at b + q * ldb /
+ * x + q * ldx (natural order; x in = warm start, out = solution), res[q] its
+ * result.  Each scenario runs exactly the single-RHS GMRES -- same iteration
+ * count, history and solution bits as gg_solve_device on it alone -- while
+ * every launch serves all of them: the SpMV reads A once for up to 8
+ * scenarios, the wavefront triangular solves run every scenario's bands in one
+ * launch (one dependency chain for all), each MGS launch reduces nrhs dots.
+ * Batched when gg_batch_engine() = 1 (left ILU(0)/ILU(k)/LU factors of a 2D
+ * grid on the unskewed wavefront); otherwise the scenarios are solved one
+ * after the other with the same results.  Returns GG_OK when every scenario
+ * converged, 1 when some did not, < 0 on error. */
+int gg_solve_batch_device(gg_solver *s, int nrhs, const double *d_b, long long ldb, double *d_x, long long ldx,
+                          const gg_options *opt, gg_result *res);
+int gg_solve_batch(gg_solver *s, int nrhs, const double *b, long long ldb, double *x, long long ldx,
+                   const gg_options *opt, gg_result *res);   /* host arrays */
+/* 1 if batched launches serve gg_solve_batch*, 0 if scenario by scenario */
+int gg_batch_engine(gg_solver *s);
+/* scenario rhs's residual history of the last batched solve (as
+ * gg_get_history): copies min(len, cap) entries, returns len */
+long long gg_batch_history(gg_solver *s, int rhs, double *out, long long cap);
+/* gg_transient_src for nrhs source scenarios at once, each its own source set,
+ * all on the solver's A = G + C/h and cdiag: scenario q's sources are
+ * k = src_off[q] .. src_off[q+1]-1 (node src_node[k], kind src_kind[k],
+ * parameters src_data[src_ptr[k] .. src_ptr[k+1]), as gg_transient_src); x
+ * holds nrhs states of n (in / out); port_out[(q * nport + j) * (nsteps + 1)
+ * + it]; iters_total[q] per scenario.  Per step: every scenario's right-hand
+ * side in one launch, then gg_solve_batch_device (warm start). */
+int gg_transient_batch(gg_solver *s, int nrhs, int nsteps, double h, const double *cdiag, const int *src_off,
+                       const int *src_node, const int *src_kind, const int *src_ptr, const double *src_data,
+                       int nport, const int *port, double *x, const gg_options *opt, double *port_out,
+                       int *iters_total);
+
 /* Diagnostics: run one wavefront triangular solve (which: 0 = L / Ml, 1 = U / Mr)
  * on the current right-hand side and return, per band, the device real-time
  * clock (100 MHz) at the start of each batch (8 or 16 steps) plus one end stamp, then
