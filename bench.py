@@ -130,10 +130,10 @@ def parse():
     p.add_argument("--c5-scenarios", type=int, default=1,
                    help="c5: independent source scenarios per GPU (many-RHS), solved as one batch "
                         "(--c5-mode batch) or concurrently")
-    p.add_argument("--c5-mode", choices=["batch", "streams"], default="batch",
-                   help="c5 with several scenarios: batch = gg_transient_batch, every launch serving all "
-                        "scenarios (batch.hip); streams = one solver, stream and host thread per scenario "
-                        "(GG_SOLVE_SHARED_DEVICE)")
+    p.add_argument("--c5-mode", choices=["auto", "batch", "streams"], default="auto",
+                   help="c5: batch = gg_transient_batch, every launch serving all scenarios (batch.hip); "
+                        "streams = one solver, stream and host thread per scenario (GG_SOLVE_SHARED_DEVICE); "
+                        "auto = batch for several scenarios, gg_transient for one")
     a = p.parse_args()
     if a.dd_comm == "loopback" and (a.gpus > 1 or not 0 <= a.dd_rank < a.dd_parts):
         p.error("--dd-comm loopback times one rank alone: --gpus 1 and 0 <= --dd-rank < --dd-parts")
@@ -749,7 +749,7 @@ def main():
         cdiag = np.full(n, 1e-3 / h5)
         ports = np.array([0, n // 2, n - 1], np.int32)
         solvers = [s]
-        c5_batch = S > 1 and a.c5_mode == "batch"
+        c5_batch = a.c5_mode == "batch" or (S > 1 and a.c5_mode == "auto")
         if c5_batch:
             assert s.batch_engine, "c5 batch: the solver's configuration takes no batched launches"
         else:
@@ -1032,9 +1032,8 @@ def main():
                                 f"1% PULSE sources (own seeded scenarios), ILU(0) left, "
                                 f"GMRES({a.restart}), tol {a.tol:g}, {a.c5_steps} backward-Euler "
                                 f"steps per step, warm start, {a.c5_scenarios} scenario(s) per GPU"
-                                + (f" solved as one batch (gg_transient_batch)" if a.c5_scenarios > 1 and
-                                   a.c5_mode == "batch" else " on concurrent streams" if a.c5_scenarios > 1
-                                   else "")) if c5 else
+                                + (" solved as one batch (gg_transient_batch)" if c5_batch else
+                                   " on concurrent streams" if a.c5_scenarios > 1 else "")) if c5 else
                                (f"C3 stand-in: seeded power-law CSR with circuit5M's n and nnz "
                                 f"(no parity claim at this size), ILU({kilu}) left (device-factored; "
                                 f"C3 names ILU(1)), GMRES({a.restart}), tol {a.tol:g}, "

@@ -9,6 +9,10 @@
 // needed by the fp64 engine and are left null (no caller reads them).
 // Errors: the reference exits or asserts; here an error is printed, Precond
 // stays null and the solve methods return 1 ("Failed to converge.").
+// Engines as in the reference: GMRES_dev_PG runs the device engine (gg_solve,
+// the split preconditioner on the GPU); GMRES_host_PG runs the HOST engine
+// (csrc/host/gmres_host.cpp: GMRESilu with HostPrecond_*, fp64 on the CPU) --
+// Precond holds both (PGEngines).
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -18,6 +22,7 @@
 
 #include "gmres_interface_pg.h"
 #include "ggmres.h"
+#include "host/gmres_host.h"
 
 // ---- the layout is the ABI (x86-64, LP64) --------------------------------------
 static_assert(sizeof(MySpMatrix) == 64 && offsetof(MySpMatrix, val) == 40 &&
@@ -56,6 +61,13 @@ std::vector<double> promote(const T *p, int n)
     return d;
 }
 
+// what Precond points at: the device solver and the host engine's operands
+struct PGEngines {
+    gg_solver *dev = nullptr;
+    gg::HostSplitEngine host;
+    ~PGEngines() { gg_destroy(dev); }
+};
+
 template <class ScaleT>
 gg_solver *build_solver(MySpMatrix *A, MySpMatrixDouble *L, MySpMatrixDouble *U, MySpMatrix *middle,
                         MySpMatrix *prow, MySpMatrix *pcol, const ScaleT *lscale, const ScaleT *rscale)
@@ -85,11 +97,60 @@ gg_solver *build_solver(MySpMatrix *A, MySpMatrixDouble *L, MySpMatrixDouble *U,
     return s;
 }
 
+// both engines for one interface object
+template <class ScaleT>
+void *build_engines(MySpMatrix *A, MySpMatrixDouble *L, MySpMatrixDouble *U, MySpMatrix *middle,
+                    MySpMatrix *prow, MySpMatrix *pcol, const ScaleT *lscale, const ScaleT *rscale)
+{
+    // (the host engine needs no device: a CPU-only caller of GMRES_host_PG keeps
+    // working when the device set-up failed -- only GMRES_dev_PG then fails)
+    PGEngines *e = new PGEngines;
+    e->dev = build_solver(A, L, U, middle, prow, pcol, lscale, rscale);
+    gg::HostSplitEngine &h = e->host;
+    const int n = A->numRows;
+    h.n = n;
+    h.arp.assign(A->rowIndices, A->rowIndices + n + 1);
+    h.aci.assign(A->indices, A->indices + h.arp[n]);
+    h.av = promote(A->val, h.arp[n]);
+    h.lrp.assign(L->rowIndices, L->rowIndices + n + 1);
+    h.lci.assign(L->indices, L->indices + h.lrp[n]);
+    h.lv.assign(L->val, L->val + h.lrp[n]);
+    h.urp.assign(U->rowIndices, U->rowIndices + n + 1);
+    h.uci.assign(U->indices, U->indices + h.urp[n]);
+    h.uv.assign(U->val, U->val + h.urp[n]);
+    h.mid = promote(middle->val, n);
+    h.prow.assign(prow->indices, prow->indices + n);
+    h.pcol.assign(pcol->indices, pcol->indices + n);
+    h.ls = promote(lscale, n);
+    h.rs = promote(rscale, n);
+    return e;
+}
+
+// the host engine with fp32 I/O at the boundary; returns the reference's 0/1
+int solve_host_f32(void *handle, int n, const float *rhs, float *x, int max_iter, double tol, int *it_out,
+                   float *tol_out)
+{
+    PGEngines *e = (PGEngines *)handle;
+    if (!e) {
+        std::printf("Failed to converge.\n");
+        return 1;
+    }
+    std::vector<double> b = promote(rhs, n), xd = promote(x, n);
+    int it = max_iter;
+    double t = tol;
+    const int rc = gg::gmres_split_host(e->host, b.data(), xd.data(), kRestart, &it, &t, nullptr);
+    for (int i = 0; i < n; i++) x[i] = (float)xd[i];
+    if (it_out) *it_out = it;
+    if (tol_out) *tol_out = (float)t;
+    if (rc != 0) std::printf("Failed to converge.\n");
+    return rc;
+}
+
 // solve with fp32 I/O at the boundary; returns the reference's 0/1
 int solve_f32(void *handle, int n, const float *rhs, float *x, int max_iter, double tol,
               int *it_out, float *tol_out)
 {
-    gg_solver *s = (gg_solver *)handle;
+    gg_solver *s = handle ? ((PGEngines *)handle)->dev : nullptr;
     if (!s) {
         std::printf("Failed to converge.\n");
         return 1;
@@ -126,22 +187,22 @@ void gmresInterfacePG::setPrecondPG(MySpMatrix *A, MySpMatrixDouble *PrLeft, MyS
     rhs_h = (float *)std::malloc(matrixSize * sizeof(float));
     max_it = kMaxIterPG;
     tol = (float)kTolPG;
-    Precond = build_solver(A, PrLeft, PrRight, PrMiddle, PrPermRow, PrPermCol, PrLscale->val,
-                           PrRscale->val);
+    Precond = build_engines(A, PrLeft, PrRight, PrMiddle, PrPermRow, PrPermCol, PrLscale->val,
+                            PrRscale->val);
 }
 
 int gmresInterfacePG::GMRES_host_PG()
 {
     max_it = kMaxIterPG;
     tol = (float)kTolPG;
-    return solve_f32(Precond, matrixSize, rhs_h, xgmres_h, max_it, kTolPG, &max_it, &tol);
+    return solve_host_f32(Precond, matrixSize, rhs_h, xgmres_h, max_it, kTolPG, &max_it, &tol);
 }
 
 gmresInterfacePG::~gmresInterfacePG()
 {
     std::free(xgmres_h);
     std::free(rhs_h);
-    gg_destroy((gg_solver *)Precond);
+    delete (PGEngines *)Precond;
 }
 
 // ------------------------------------------------------ gmresInterfacePGfloat
@@ -163,8 +224,8 @@ void gmresInterfacePGfloat::setPrecondPG(MySpMatrix *A, MySpMatrixDouble *PrLeft
     rhs_h = (float *)std::malloc(matrixSize * sizeof(float));
     max_it = kMaxIterPG;
     tol = (float)kTolPG;
-    Precond = build_solver(A, PrLeft, PrRight, PrMiddle, PrPermRow, PrPermCol, PrLscale->val,
-                           PrRscale->val);
+    Precond = build_engines(A, PrLeft, PrRight, PrMiddle, PrPermRow, PrPermCol, PrLscale->val,
+                            PrRscale->val);
 }
 
 int gmresInterfacePGfloat::GMRES_host_PG()
@@ -173,7 +234,7 @@ int gmresInterfacePGfloat::GMRES_host_PG()
     // the members are not updated
     int it = 0;
     float t = 0.f;
-    return solve_f32(Precond, matrixSize, rhs_h, xgmres_h, kMaxIterDefs, kTolPG, &it, &t);
+    return solve_host_f32(Precond, matrixSize, rhs_h, xgmres_h, kMaxIterDefs, kTolPG, &it, &t);
 }
 
 int gmresInterfacePGfloat::GMRES_dev_PG()
@@ -187,5 +248,5 @@ gmresInterfacePGfloat::~gmresInterfacePGfloat()
 {
     std::free(xgmres_h);
     std::free(rhs_h);
-    gg_destroy((gg_solver *)Precond);
+    delete (PGEngines *)Precond;
 }

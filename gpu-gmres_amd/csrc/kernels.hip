@@ -28,16 +28,20 @@ __device__ __forceinline__ bool gated(const Gate &g)
 // per-scenario buffer (vectors, partials, H, the control block, hand-off
 // granules -- one arena per scenario) lies sc * zs bytes after scenario 0's.
 // zs = 0: the single-scenario launch, every pointer as given.
+// (char-pointer arithmetic, not an integer round trip: the compiler keeps the
+// global address space -- global_* instead of flat_* accesses, which the
+// wavefront kernel's writer could not afford)
 template <class T>
 __device__ __forceinline__ T *zp(T *p, long long zs, int sc)
 {
-    return p ? reinterpret_cast<T *>(reinterpret_cast<unsigned long long>(p) + (unsigned long long)(sc * zs)) : p;
+    using C = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+    return reinterpret_cast<T *>(reinterpret_cast<C *>(p) + (long long)sc * zs);
 }
 __device__ __forceinline__ bool gated_z(const Gate &g, long long zs, int sc)
 {
     Gate h = g;
-    h.done = zp(g.done, zs, sc);
-    h.nit = zp(g.nit, zs, sc);
+    if (g.done) h.done = zp(g.done, zs, sc);
+    if (g.nit) h.nit = zp(g.nit, zs, sc);
     return gated(h);
 }
 
@@ -5454,6 +5458,18 @@ void launch_trsv_b(Gate g, DevTri &T, const double *b, double *x, unsigned long 
     const double *k1 = e == WD_SFMA ? T.c1s.p : T.c1.p, *k2 = e == WD_SFMA ? T.c2s.p : T.c2.p;
     const double *dv = (e == WD_UNIT || e == WD_UFMA) ? nullptr : (e == WD_MUL || e == WD_SFMA) ? T.rw.p : T.dw.p;
     const double *rv = e == WD_RCP ? T.rw.p : nullptr;
+    static const bool s1single = [] {
+        const char *e = std::getenv("GG_BATCH_S1_SINGLE");     // diagnostics: one scenario on the single kernel
+        return e && e[0] == '1';
+    }();
+    if (nsc == 1 && s1single) {
+        DevTri &T2 = T;
+        unsigned long long *keep = T2.bnd.p;
+        T2.bnd.p = bnd;
+        launch_trsv(g, T2, b, x, err, st);
+        T2.bnd.p = keep;
+        return;
+    }
 #define GG_BT(FWD, DIV)                                                                                     \
     k_trsv_wave2d_batch<FWD, DIV><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(g, w.T, w.nbands, b, k1, k2, dv, rv, \
                                                                           x, bnd, err, w.P2, nsc, zs, zmap)

@@ -8,7 +8,8 @@
  *
  *   setPrecondPG   src/gmres_interface_pg.cu:9-60    -> gg_set_matrix + gg_set_precond_split
  *   GMRES_dev_PG   src/gmres_interface_pg.cu:110-139 -> gg_solve (restart 32, max_it 10000, tol 1e-7)
- *   GMRES_host_PG  src/gmres_interface_pg.cu:62-108  -> gg_solve (same engine; no CPU twin is shipped)
+ *   GMRES_host_PG  src/gmres_interface_pg.cu:62-108  -> the host GMRESilu engine (CPU, fp64,
+ *                                                       csrc/host/gmres_host.cpp)
  */
 #ifndef _GMRES_INTERFACE_PG_H_
 #define _GMRES_INTERFACE_PG_H_
@@ -30,7 +31,7 @@ class gmresInterfacePG {
   float *xgmres_h;
   float *rhs_h;
 
-  void *Precond;   /* opaque: the gg_solver handle */
+  void *Precond;   /* opaque: the device solver and the host engine */
 
   int max_it; /* both input and output */
   float tol;
@@ -66,7 +67,7 @@ class gmresInterfacePGfloat {
   float *xgmres_d;
   float *rhs_d;
 
-  void *Precond;   /* opaque: the gg_solver handle */
+  void *Precond;   /* opaque: the device solver and the host engine */
 
   int max_it; /* both input and output */
   float tol;

@@ -113,12 +113,19 @@ def test_pg_classes_solve_sequence(tmp_path, mode):
         finally:
             O.set_dot_order(None)
         assert rc == ot["ret"] == o["ret"] == 0
-        assert np.array_equal(xg, ot["x"].astype(np.float32))
-        assert np.linalg.norm(xg - o["x"]) <= 1e-6 * np.linalg.norm(o["x"])     # fp32 output
-        if mode == 1:
-            assert max_it == 10000 and tol == np.float32(1e-7)      # local copies in the reference
-        else:
+        if mode == 0:
+            # the device engine: bit-identical with the device's reduction order
+            assert np.array_equal(xg, ot["x"].astype(np.float32))
             assert max_it == ot["iters"] and tol == np.float32(ot["relres"])
+        else:
+            # GMRES_host_PG: the host engine (csrc/host/gmres_host.cpp), the
+            # reference's serial order -- bit-identical to the serial oracle
+            assert np.array_equal(xg, o["x"].astype(np.float32))
+            if mode == 1:
+                assert max_it == 10000 and tol == np.float32(1e-7)  # local copies in the reference
+            else:
+                assert max_it == o["iters"] and tol == np.float32(o["relres"])
+        assert np.linalg.norm(xg - o["x"]) <= 1e-6 * np.linalg.norm(o["x"])     # fp32 output
         x = xg.astype(np.float64)          # the next solve warm-starts from xgmres_h (fp32)
     assert "Failed to converge" not in stdout
 
