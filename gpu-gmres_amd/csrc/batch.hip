@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <climits>
 #include <cstdint>
 #include <cstdlib>
@@ -48,6 +49,20 @@ namespace {
 
 constexpr long long kAlign = 256;
 long long align_up(long long a) { return (a + kAlign - 1) / kAlign * kAlign; }
+
+// GG_BATCH_MGS: the orthogonalization of a batched inner iteration -- 0 the
+// per-step kernels with every scenario in each launch (k_dot, k_mgs_step,
+// k_arnoldi_finalize: i + 3 launches), 1 the single-scenario persistent kernel
+// once per scenario (k_arnoldi_persist: w and the basis step in registers, the
+// same reduction tree, so the same bits)
+int batch_mgs()
+{
+    static const int k = [] {
+        const char *e = std::getenv("GG_BATCH_MGS");
+        return e ? std::atoi(e) : 1;
+    }();
+    return k;
+}
 
 int batch_chunk()
 {
@@ -69,7 +84,15 @@ struct BatchWs {
     long long zs = 0;                    // bytes per scenario
     DBuf<char> arena;
     long long oV = 0, ow = 0, oww = 0, or_ = 0, orr = 0, obb = 0, ot1 = 0, oxv = 0, obv = 0, opA = 0, opB = 0,
-              oH = 0, os = 0, ocs = 0, osn = 0, oy = 0, ohist = 0, ods = 0, oLg = 0, oUg = 0;
+              oH = 0, os = 0, ocs = 0, osn = 0, oy = 0, ohist = 0, ods = 0, oLg = 0, oUg = 0, ogran = 0, oxgran = 0;
+    // the persistent orthogonalization (GG_BATCH_MGS 1): its all-gather granules
+    // per scenario (m (m+2) G, then m (m+2) sums) and XCD slots, and the
+    // solver-wide election words; persist = admitted (co-residency), cleared
+    // for the solver's life when a launch was not co-resident
+    bool persist = false;
+    long long ngran = 0, nxgran = 0;
+    DBuf<unsigned long long> elect;
+    unsigned long long seq = 0;
     // read-back slots: the scenarios' control blocks + the error word, written
     // by k_pack_states_b straight into mapped pinned memory
     static constexpr int kSlots = 4;
@@ -159,6 +182,19 @@ void ensure_batch(gg_solver *s, int S, int m, long long hist_need)
     B->ods = take((long long)sizeof(DevState));
     B->oLg = take(B->ngL * 8);
     B->oUg = take(B->ngU * 8);
+    {
+        const int pj = arnoldi_persist_units(s->G, s->Ppad);
+        const int xr = (mgs_gather_form() == 3 && mgs_prefetch()) ? kMgsXcds : 0;
+        B->persist = batch_mgs() == 1 && pj != 0 && s->G + xr <= arnoldi_persist_max_blocks(pj);
+        if (B->persist) {
+            B->ngran = (long long)m * (m + 2) * (s->G + 1);
+            B->nxgran = (long long)m * (m + 2) * kMgsXcdWords;
+            B->ogran = take(B->ngran * 8);
+            B->oxgran = take(B->nxgran * 8);
+            B->elect.alloc(kMgsElectWords);
+            GG_HIP(hipMemsetAsync(B->elect.p, 0, kMgsElectWords * sizeof(unsigned long long), s->st));
+        }
+    }
     B->zs = align_up(o);
     B->arena.alloc((size_t)B->zs * S);
     // every vector +0 in its padding slots, every dummy granule 0 (read as ready)
@@ -183,6 +219,7 @@ void readback(gg_solver *s, BatchWs *B, int k)
 struct BatchErr {
     int bits;
 };
+struct BatchAbort {};     // a persistent orthogonalization grid was not co-resident
 // wait for slot k; the error word: bit 0 time-out (fatal), bit 1 a WD_RCP range
 // miss (the caller repeats the solve with IEEE division)
 const DevState *wait_slot(BatchWs *B, int k)
@@ -202,8 +239,15 @@ struct Ctx {
     UnitMap um;
     DevState *ds;
     double *V, *w, *ww, *r, *rr, *bb, *t1, *xv, *bv, *pA, *pB, *H, *sv, *cs, *sn, *y, *hist;
-    unsigned long long *Lg, *Ug;
+    unsigned long long *Lg, *Ug, *gran, *xgran;
 };
+// scenario q's copy of a per-scenario pointer
+template <class T>
+T *zq(T *p, long long zs, int q)
+{
+    return reinterpret_cast<T *>(reinterpret_cast<char *>(const_cast<typename std::remove_const<T>::type *>(p)) +
+                                 (long long)q * zs);
+}
 
 void trsv_pair(const Ctx &c, Gate g, const double *in, double *out)
 {
@@ -239,6 +283,22 @@ void enqueue_iters_b(const Ctx &c, int i0, int i1)
         const double *vi = c.V + (long long)i * c.P;
         launch_spmv_b(gi, s->dA, vi, nullptr, c.ww, false, c.S, c.zs, s->st);   // ww = A v_i
         trsv_pair(c, gi, c.ww, c.w);                                            // w = M^-1 ww
+        if (c.B->persist) {
+            // the single-scenario persistent kernel, once per scenario
+            for (int q = 0; q < c.S; q++) {
+                Gate gq = gi;
+                gq.done = zq(gi.done, c.zs, q);
+                gq.nit = zq(gi.nit, c.zs, q);
+                unsigned long long *gr = zq(c.gran, c.zs, q);
+                launch_arnoldi_persist(gq, i, c.m, zq(c.ds, c.zs, q), zq(c.w, c.zs, q), zq(c.V, c.zs, q), c.P,
+                                       zq(c.H, c.zs, q), zq(c.cs, c.zs, q), zq(c.sn, c.zs, q), zq(c.sv, c.zs, q),
+                                       zq(c.hist, c.zs, q), gr + (size_t)i * (c.m + 2) * c.G,
+                                       gr + (size_t)c.m * (c.m + 2) * c.G + (size_t)i * (c.m + 2), c.G, c.P,
+                                       s->err.p, zq(c.xgran, c.zs, q) + (size_t)i * (c.m + 2) * kMgsXcdWords,
+                                       c.B->elect.p, ++c.B->seq, c.um, s->st);
+            }
+            continue;
+        }
         double *pin = c.pA, *pout = c.pB;
         launch_dot_b(gi, c.w, c.V, pin, c.G, c.P, c.S, c.zs, s->st);            // <w, v_0>
         for (int k = 0; k <= i; k++) {
@@ -306,6 +366,8 @@ int solve_batch_once(gg_solver *s, int S, const double *d_b, long long ldb, doub
     c.hist = B->dp(B->ohist);
     c.Lg = reinterpret_cast<unsigned long long *>(B->arena.p + B->oLg);
     c.Ug = reinterpret_cast<unsigned long long *>(B->arena.p + B->oUg);
+    c.gran = B->persist ? reinterpret_cast<unsigned long long *>(B->arena.p + B->ogran) : nullptr;
+    c.xgran = B->persist ? reinterpret_cast<unsigned long long *>(B->arena.p + B->oxgran) : nullptr;
     hipStream_t st = s->st;
 
     // inputs into the solver's vector space; hand-off granules armed; control blocks
@@ -343,6 +405,10 @@ int solve_batch_once(gg_solver *s, int S, const double *d_b, long long ldb, doub
     while (left > 0) {
         // ---- one restart cycle, in chunks of K inner iterations
         launch_init_cycle_b(c.ds, c.r, c.V, c.sv, c.G, c.P, S, c.zs, st);
+        if (B->persist) {
+            launch_fill_u64_b(c.gran, B->ngran, kSentinel, S, c.zs, st);
+            launch_fill_u64_b(c.xgran, B->nxgran, kSentinel, S, c.zs, st);
+        }
         for (Track &t : tr) t.cyc_over = t.fin;
         std::deque<std::pair<int, int>> pend;              // (read-back slot, iterations enqueued)
         int issued = 0;
@@ -361,6 +427,8 @@ int solve_batch_once(gg_solver *s, int S, const double *d_b, long long ldb, doub
             const auto [k, iend] = pend.front();
             pend.pop_front();
             h = wait_slot(B, k);
+            for (int q = 0; q < S; q++)
+                if (h[q].done & DONE_ABORT) throw BatchAbort{};
             bool over = true;
             for (int q = 0; q < S; q++) {
                 Track &t = tr[q];
@@ -489,11 +557,16 @@ int solve_batch(gg_solver *s, int S, const double *d_b, long long ldb, double *d
     for (int attempt = 0;; attempt++) {
         try {
             return solve_batch_once(s, S, d_b, ldb, d_x, ldx, opt, res);
+        } catch (BatchAbort &) {
+            // not co-resident: the per-step kernels for the solver's life, repeat
+            GG_HIP(hipStreamSynchronize(s->st));
+            if (attempt >= 2) throw Error{GG_EHIP, "gg_solve_batch: fallbacks exhausted"};
+            s->batch->persist = false;
         } catch (BatchErr &e) {
             // a WD_RCP range miss: IEEE division for the solver's life, repeat
             // (d_x is written only at the end)
             GG_HIP(hipStreamSynchronize(s->st));
-            if (attempt >= 1) throw Error{GG_EHIP, "gg_solve_batch: fallbacks exhausted"};
+            if (attempt >= 2) throw Error{GG_EHIP, "gg_solve_batch: fallbacks exhausted"};
             for (DevTri *T : {&s->L, &s->U})
                 if (T->kind == DevTri::WAVE2D && T->div == WD_RCP) T->div = WD_HW;
         }
