@@ -157,6 +157,7 @@ PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 CHAIN_CYCLES = {"trsv_L": 38.89, "trsv_U": 62.66, "trsv_U_mul": 43.72,
                 "trsv_L_fma": 29.19, "trsv_U_fma": 29.58}
 SHADER_GHZ = 2.399
+TIE_FRAC = 0.05          # roofline kernel: candidates within 5 % of the top time are tied
 
 
 def chain_key(kernel, dom, fma, mul):
@@ -171,12 +172,22 @@ def chain_key(kernel, dom, fma, mul):
     return (dom + "_fma") if fma else "trsv_U_mul" if mul else dom
 
 
+def kernel_key(name):
+    """a kernel's template name with trailing default arguments dropped, so the
+    bench's short names ('k_spmv_stream<false>') and rocprof's
+    ('k_spmv_stream<false, false>') meet: ', false' / ', 0' suffixes removed"""
+    name = name.replace(" ", "")
+    while name.endswith((",false>", ",0>")):
+        name = name[: name.rindex(",")] + ">"
+    return name
+
+
 def pmc_traffic(kernel, workload=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, or profiles/pmc_traffic_<workload>.json; written
     by profiles/pmc_traffic.py: FETCH_SIZE doubled for 16-B/lane streaming
     reads, + WRITE_SIZE; MI355X_MICROARCH.md HBM section), or None when that
-    file has no entry for it."""
+    file has no entry for it (names compared by kernel_key)."""
     path = PMC_FILE if workload is None else PMC_FILE.replace(".json", f"_{workload}.json")
     try:
         with open(path) as f:
@@ -185,7 +196,12 @@ def pmc_traffic(kernel, workload=None):
         from pmc_traffic import src_sha
         if d.get("src_sha") != src_sha():      # counters taken on other kernel sources: stale
             return None
-        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+        ks = d["kernels"]
+        if kernel in ks:
+            return ks[kernel]["hbm_bytes_per_launch"]
+        want = kernel_key(kernel)
+        hit = [v for k, v in ks.items() if kernel_key(k) == want]
+        return hit[0]["hbm_bytes_per_launch"] if len(hit) == 1 else None
     except (OSError, KeyError, ValueError):
         return None
 
@@ -909,10 +925,22 @@ def main():
         f["solves_bracketed"] = bracketed[k]
         f["est_ms_timed_region"] = round(f["avg_us"] * 1e-3 * f["launches"] / bracketed[k] * a.steps, 3)
         f["share_of_step"] = round(f["est_ms_timed_region"] / (el * 1e3), 4)
-    dom = max(timed, key=lambda k: timed[k]["est_ms_timed_region"]) if timed else None
+    # the roofline kernel: the most time over the timed region; candidates within
+    # TIE_FRAC of it count as tied (L and U 1.4 % apart made the
+    # choice a coin flip) and the tie goes to the lowest HBM fraction -- the
+    # conservative figure, and a stable name from run to run
+    dom = None
+    if timed:
+        order = sorted(timed, key=lambda k: -timed[k]["est_ms_timed_region"])
+        top = timed[order[0]]["est_ms_timed_region"]
+        tied = [k for k in order if timed[k]["est_ms_timed_region"] >= (1 - TIE_FRAC) * top
+                and timed[k].get("achieved_gbs") is not None]
+        dom = min(tied, key=lambda k: timed[k]["achieved_gbs"]) if tied else order[0]
 
     pmc_wl = ("c4" if c4 else "c3s" if c3s else ("pgr" if a.pg_perm == "random" else "pg") if pg
               else "netlist" if netlist else None)
+    if kilu:                            # ILU(k): its own PMC pass (tools/profile_round.sh c2_ilu1 / c3s_ilu1)
+        pmc_wl = f"{pmc_wl or 'c2'}_ilu{kilu}"
 
     def roof_of(name):
         """(roofline, latency_roofline) of one timed family"""
@@ -927,7 +955,7 @@ def main():
         roof = {"kernel": kname, "bound": "hbm", "achieved": f["achieved_gbs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(f["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(kname, pmc_wl) if not kilu else None,
+                "traffic": pmc_traffic(kname, pmc_wl),
                 "alg_bytes_per_launch": f["alg_bytes_per_launch"], "avg_us": f["avg_us"],
                 "launches_timed": f["launches"], "solves_bracketed": f["solves_bracketed"],
                 "share_of_timed_region": f["share_of_step"]}
@@ -963,6 +991,33 @@ def main():
 
     roofs = {k: roof_of(k) for k in timed}
     roof, lat = roofs[dom] if dom else (None, None)
+    if roof:
+        roof["chosen_by"] = (f"most time over the timed region; candidates within {TIE_FRAC:.0%} of it tied, "
+                             f"the lowest HBM fraction among them")
+    # the whole Arnoldi iteration against HBM: the reference's
+    # operations' algorithmic bytes per inner iteration at cycle index i --
+    # SpMV + ILU apply + MGS 40 n (i+1) + norm/scale 24 n -- plus each cycle's
+    # update (8 n m + 16 n) and residual (B_spmv + 8n + B_ilu + 8n + 16n), summed
+    # over the timed solves' iterations, times it/s, over 8 TB/s
+    iter_roof = None
+    if not c5 and not kilu and not netlist:
+        nnz_a = int(A.nnz)
+        b_spmv = 12.0 * nnz_a + 4.0 * (n + 1) + 16.0 * n
+        b_ilu = 12.0 * nnz_a + 8.0 * (n + 1) + 32.0 * n            # ILU(0): pattern of A
+        tot_b = tot_it = 0.0
+        for r in res:
+            full, rem = divmod(int(r["inner"]), a.restart)
+            for i in list(range(a.restart)) * full + list(range(rem)):
+                tot_b += b_spmv + b_ilu + 40.0 * n * (i + 1) + 24.0 * n
+                tot_it += 1
+            cycles = full + (1 if rem else 0)
+            tot_b += cycles * (8.0 * n * a.restart + 16.0 * n + b_spmv + 8.0 * n + b_ilu + 8.0 * n + 16.0 * n)
+        if tot_it:
+            per = tot_b / tot_it
+            iter_roof = {"bytes_per_iteration": round(per), "achieved_gbs": round(per * value / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(per * value / 1e9 / HBM_PEAK_GBS, 4),
+                         "basis": "SURVEY.md 8(d): the reference's unfused operations, ILU(0) (nnz_LU = nnz(A)); "
+                                  "fused kernels move fewer bytes than this count"}
     rooflines = {k: dict(r, **({"latency_frac": l["frac"], "latency_floor_us": l["floor_us"]} if l else {}))
                  for k, (r, l) in roofs.items()}
     spmv_bytes = s.bytes_spmv()
@@ -1065,7 +1120,7 @@ def main():
                                 "x = RN(acc / d) (the reference's division, bit-exact)"),
                    "parallelism": "single" if world == 1 else f"replicas{world}",
                    "setup_s": round(t_setup, 3)},
-        "roofline": roof, "latency_roofline": lat,
+        "roofline": roof, "latency_roofline": lat, "iteration_roofline": iter_roof,
         "rooflines": rooflines,
         "rooflines_from": ("one candidate family bracketed with hipEvents per timed solve, rotating; "
                            "roofline = the candidate with the most time over the timed region"),

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Refresh the committed profile set on a GPU box (run through gpurun from the repo root):
-#   tools/profile_round.sh TAG [WORKLOAD]        (WORKLOAD: c2 (default), c4, pg, pgr, netlist, c5, c3, c3s)
+#   tools/profile_round.sh TAG [WORKLOAD]        (WORKLOAD: c2 (default), c4, pg, pgr, netlist, c5, c3, c3s,
+#                                                 c2_ilu1, c3s_ilu1)
 # writes gpurun_out/prof_TAG[_WORKLOAD]/{bench.json, kernel_stats.csv, pmc_traffic.json}
 # Each GPU step has its own time limit; the steps are chained with && so the
 # script ends at the first failure.
@@ -11,6 +12,8 @@ OUT=gpurun_out/prof_${TAG}_${WL}
 ARGS=""
 [ "$WL" = c2 ] || ARGS="--workload $WL"
 [ "$WL" = pgr ] && ARGS="--workload pg --pg-perm random"      # the split on the flow kernel
+[ "$WL" = c2_ilu1 ] && ARGS="--ilu-level 1"                     # ILU(1) grid factors (skewed wavefront)
+[ "$WL" = c3s_ilu1 ] && ARGS="--workload c3s --ilu-level 1"     # C3's own preconditioner on the stand-in
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u bench.py $ARGS > $OUT/bench.json 2> $OUT/bench.err
