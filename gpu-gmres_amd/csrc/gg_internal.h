@@ -281,7 +281,25 @@ struct DevCsr {
     int nslice = 0;
     DBuf<int> sptr, sci;
     DBuf<double> sv;
+    // column panels (k_spmv_panel; large matrices with scattered columns and
+    // rows in ascending column order, GG_SPMV_PANEL): x cut into npanel panels
+    // of pw entries, small enough for an XCD's L2; per panel its row segments
+    // (seg_row: the row, ~row for a row's first segment; seg_ptr: the
+    // segment's entries in the panel-major copy pci / pv), pan_seg[p] the
+    // panel's first segment.  Panel by panel, a row's terms are added into its
+    // running sum kept in y -- the CSR order, so the same bits
+    bool panel = false;
+    int npanel = 0, pw = 0;
+    long long nseg = 0;
+    DBuf<int> pan_seg, seg_row, seg_ptr, pci, zero_rows;
+    // k_spmv_panel's blocks: per panel runs of <= 256 segments / <= kSpmvCap
+    // entries, pblk = their first segments (panel p's blocks at pan_blk_h[p])
+    DBuf<int> pblk;
+    std::vector<int> pan_blk_h;
+    DBuf<double> pv;
+    int nzero = 0;
     void upload(const Csr &A, hipStream_t st);
+    void build_panels(const Csr &A, hipStream_t st);   // (upload: the column panels when they apply)
     void copy_from(const DevCsr &o, hipStream_t st);   // device-side duplicate
 };
 

@@ -638,6 +638,76 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
     }
 }
 
+// Column-panel SpMV, one launch per panel p (DevCsr::panel): a block owns a
+// run of <= 256 of the panel's row segments (a row's terms whose columns fall
+// in the panel, in CSR order) holding <= kSpmvCap entries (pblk, host-made),
+// and works like k_spmv_stream on it -- entries loaded coalesced, x gathered
+// (from the panel's slice, which the XCD's L2 keeps), products into LDS, then
+// each segment's products summed by its thread in order, continuing the row's
+// running sum kept in y (0.0 at the row's first segment, seg_row = ~row).
+// Every row is thus summed exactly as computeSpMV sums it.  Empty rows get 0
+// in pass 0.
+__global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__restrict__ pblk,
+                                                       const int *__restrict__ seg_row,
+                                                       const int *__restrict__ seg_ptr,
+                                                       const int *__restrict__ pci, const double *__restrict__ pv,
+                                                       const double *__restrict__ x, double *__restrict__ y,
+                                                       const int *__restrict__ zero_rows, int nzero)
+{
+    if (gated(g)) return;
+    constexpr int U = kSpmvCap / kBlock;        // entries per thread
+    __shared__ double prod[kSpmvCap];
+    __shared__ int sp[kBlock + 1];
+    const int tid = threadIdx.x;
+    if (nzero)
+        for (long long i = blockIdx.x * (long long)kBlock + tid; i < nzero; i += (long long)gridDim.x * kBlock)
+            y[zero_rows[i]] = 0.0;
+    const int s0 = pblk[blockIdx.x], s1 = pblk[blockIdx.x + 1];
+    const int ns = s1 - s0;                     // <= kBlock segments
+    if (tid < ns) sp[tid] = seg_ptr[s0 + tid];
+    if (tid == 0) sp[ns] = seg_ptr[s1];
+    int rr = 0;
+    double acc = 0.0;
+    if (tid < ns) {
+        rr = seg_row[s0 + tid];
+        if (rr >= 0) acc = y[rr];               // the row's running sum so far
+    }
+    __syncthreads();
+    const int e0 = sp[0], cnt = sp[ns] - e0;
+    int c[U];
+    double a[U], xv[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int q = tid + u * kBlock;
+        if (q < cnt) {
+            c[u] = pci[e0 + q];
+            a[u] = pv[e0 + q];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        if (tid + u * kBlock < cnt) xv[u] = x[c[u]];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int q = tid + u * kBlock;
+        if (q < cnt) prod[q] = a[u] * xv[u];
+    }
+    __syncthreads();
+    if (tid < ns) {
+        const int lo = sp[tid] - e0, hi = sp[tid + 1] - e0;
+        int e = lo;
+        for (; e + 8 <= hi; e += 8) {
+            double t[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) t[q] = prod[e + q];
+#pragma unroll
+            for (int q = 0; q < 8; q++) acc += t[q];
+        }
+        for (; e < hi; e++) acc += prod[e];
+        y[rr < 0 ? ~rr : rr] = acc;
+    }
+}
+
 // Batched SpMV (the many-RHS solve): y_sc = A x_sc (RESID: b_sc - A x_sc) for
 // up to NS scenarios per launch (scenario sc's vectors sc * zs bytes after
 // scenario 0's), A's sliced-ELL entries read ONCE per wave for all of them.
@@ -4735,6 +4805,16 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
                  hipStream_t st, const double *ydiv)
 {
     if (A.nblk == 0) return;
+    if (A.panel && !resid && !ydiv && x != y) {
+        // column panels: one launch per panel over its segment blocks
+        for (int p = 0; p < A.npanel; p++) {
+            const int nb = A.pan_blk_h[p + 1] - A.pan_blk_h[p];
+            if (nb > 0)
+                k_spmv_panel<<<nb, kBlock, 0, st>>>(g, A.pblk.p + A.pan_blk_h[p], A.seg_row.p, A.seg_ptr.p, A.pci.p,
+                                                     A.pv.p, x, y, A.zero_rows.p, p == 0 ? A.nzero : 0);
+        }
+        return;
+    }
 #define GG_SPMV(R, D)                                                                                  \
     do {                                                                                               \
         if (A.sell)                                                                                    \

@@ -86,6 +86,87 @@ void DevCsr::upload(const Csr &A, hipStream_t st)
             GG_HIP(hipStreamSynchronize(st));   // the host staging vectors go out of scope
         }
     }
+    build_panels(A, st);
+}
+
+// Column panels for the CSR-stream matrices whose gathers scatter over an x
+// far larger than an XCD's L2 (the C3 stand-in: 44 MB of x, uniform columns,
+// one 64-B line fetched per 8-B term, profiles/pmc_traffic_c3.json).  Panel
+// width GG_SPMV_PANEL doubles (default 524,288 = 4 MiB, the XCD's L2; the C3
+// stand-in's SpMV 971 us unpanelled, 702 / 648 / 652 / 716 / 921 us at 3 / 4
+// / 6 / 8 / 22 MiB panels, profiles/r06/c3_panel_ab.txt); used when the matrix
+// has at least GG_SPMV_PANEL_MIN rows (default 2^21), more than one panel, and
+// every row's columns strictly ascending (the panel order is then the CSR
+// order).  GG_SPMV_PANEL=0 turns it off.
+void DevCsr::build_panels(const Csr &A, hipStream_t st)
+{
+    panel = false;
+    const char *pe = std::getenv("GG_SPMV_PANEL");
+    const long long w = pe ? atoll(pe) : 524288;
+    const char *me = std::getenv("GG_SPMV_PANEL_MIN");
+    const long long nmin = me ? atoll(me) : (1LL << 21);
+    if (sell || w <= 0 || n < nmin || n <= w || nnz == 0) return;
+    for (int r = 0; r < n; r++)
+        for (int k = A.rp[r] + 1; k < A.rp[r + 1]; k++)
+            if (A.ci[k] <= A.ci[k - 1]) return;            // not ascending: the panel order would differ
+    pw = (int)w;
+    npanel = (int)((n + w - 1) / w);
+    std::vector<int> cur(A.rp.begin(), A.rp.end() - 1);  // per row: its next entry
+    std::vector<int> ps(npanel + 1, 0), srow, sptr_h, pc(nnz);
+    std::vector<double> pvv(nnz);
+    std::vector<char> seen(n, 0);
+    srow.reserve((size_t)n * 4);
+    sptr_h.reserve((size_t)n * 4 + 1);
+    long long e = 0;
+    for (int p = 0; p < npanel; p++) {
+        ps[p] = (int)srow.size();
+        const long long hi = std::min<long long>((long long)(p + 1) * w, n);
+        for (int r = 0; r < n; r++) {
+            int k = cur[r];
+            const int k1 = A.rp[r + 1];
+            if (k >= k1 || A.ci[k] >= hi) continue;
+            srow.push_back(seen[r] ? r : ~r);
+            seen[r] = 1;
+            sptr_h.push_back((int)e);
+            for (; k < k1 && A.ci[k] < hi; k++, e++) {
+                pc[e] = A.ci[k];
+                pvv[e] = A.v[k];
+            }
+            cur[r] = k;
+        }
+    }
+    ps[npanel] = (int)srow.size();
+    sptr_h.push_back((int)e);
+    // per panel, blocks of <= 256 segments holding <= kSpmvCap entries (a
+    // longer segment: no panels)
+    std::vector<int> pb;
+    pan_blk_h.assign(npanel + 1, 0);
+    for (int p = 0; p < npanel; p++) {
+        pan_blk_h[p] = (int)pb.size();
+        int sg = ps[p];
+        while (sg < ps[p + 1]) {
+            pb.push_back(sg);
+            const int start = sg;
+            while (sg < ps[p + 1] && sg - start < 256 && sptr_h[sg + 1] - sptr_h[start] <= kSpmvCap) sg++;
+            if (sg == start) return;                       // one segment beyond a block's capacity
+        }
+    }
+    pan_blk_h[npanel] = (int)pb.size();
+    pb.push_back(ps[npanel]);
+    std::vector<int> zr;
+    for (int r = 0; r < n; r++)
+        if (!seen[r]) zr.push_back(r);                    // empty rows: y = 0
+    nseg = (long long)srow.size();
+    nzero = (int)zr.size();
+    pan_seg.upload(ps, st);
+    seg_row.upload(srow, st);
+    seg_ptr.upload(sptr_h, st);
+    pci.upload(pc, st);
+    pv.upload(pvv, st);
+    zero_rows.upload(zr.empty() ? std::vector<int>{0} : zr, st);
+    pblk.upload(pb, st);
+    panel = true;
+    GG_HIP(hipStreamSynchronize(st));
 }
 
 void DevCsr::copy_from(const DevCsr &o, hipStream_t st)
@@ -110,6 +191,21 @@ void DevCsr::copy_from(const DevCsr &o, hipStream_t st)
         dup(sci, o.sci);
         dup(sv, o.sv);
     }
+    panel = o.panel;
+    npanel = o.npanel;
+    pw = o.pw;
+    nseg = o.nseg;
+    nzero = o.nzero;
+    if (panel) {
+        dup(pan_seg, o.pan_seg);
+        dup(seg_row, o.seg_row);
+        dup(seg_ptr, o.seg_ptr);
+        dup(pci, o.pci);
+        dup(pv, o.pv);
+        dup(zero_rows, o.zero_rows);
+        dup(pblk, o.pblk);
+    }
+    pan_blk_h = o.pan_blk_h;
 }
 
 long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
@@ -1966,6 +2062,7 @@ int gg_division_active(gg_solver *s, int which)
     return e == WD_MUL ? GG_DIV_RCP : (e == WD_UFMA || e == WD_SFMA) ? GG_DIV_FMA : GG_DIV_EXACT;
 }
 int gg_spmv_sliced(gg_solver *s) { return (s && s->dA.sell) ? 1 : 0; }
+int gg_spmv_panels(gg_solver *s) { return (s && s->dA.panel) ? s->dA.npanel : 0; }
 
 int gg_solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
                     gg_result *res)

@@ -230,8 +230,14 @@ long long gg_layout(gg_solver *s, long long *lay2nat, long long cap);
  * solver actually uses, GG_WIDE_FORCE included) */
 int gg_reduce_blocks(gg_solver *s, int *G);
 /* the SpMV kernel the solver's matrix takes: 1 sliced ELL (k_spmv_sell: short,
- * evenly filled rows), 0 CSR-stream (k_spmv_stream) */
+ * evenly filled rows), 0 CSR-stream (k_spmv_stream); for y = A x a large
+ * CSR-stream matrix with ascending rows may also run on column panels
+ * (k_spmv_panel, gg_spmv_panels) */
 int gg_spmv_sliced(gg_solver *s);
+/* the number of column panels y = A x runs over (k_spmv_panel: x cut into
+ * L2-sized panels, each row's terms added panel by panel into its running sum,
+ * the CSR order), 0 when the matrix does not take them (GG_SPMV_PANEL) */
+int gg_spmv_panels(gg_solver *s);
 
 int gg_solve(gg_solver *s, const double *b, double *x, const gg_options *opt,
              gg_result *res);

@@ -40,10 +40,11 @@ def _port():
         return sk.getsockname()[1]
 
 
-def run_ranks(mode, P, outdir, timeout=240, xk=None):
+def run_ranks(mode, P, outdir, timeout=240, xk=None, env_extra=None):
     """start P rank processes, wait for all; kill exactly those on failure
     (xk: GG_DD_XK for the ranks -- the orthogonalization's exchanges inside its
-    kernels, 1, or as separate all-gather launches, 0)"""
+    kernels, 1, or as separate all-gather launches, 0; env_extra: more
+    environment for the ranks)"""
     port = _port()
     procs = []
     for r in range(P):
@@ -51,6 +52,7 @@ def run_ranks(mode, P, outdir, timeout=240, xk=None):
                    MASTER_PORT=str(port), OMP_NUM_THREADS="2")
         if xk is not None:
             env["GG_DD_XK"] = str(xk)
+        env.update(env_extra or {})
         procs.append(subprocess.Popen([sys.executable, "-u", WORKER, mode, str(outdir)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -143,6 +145,24 @@ def test_dd_ipc_ranks_match_local_and_oracle(case, xk, tmp_path):
         O.set_dot_order(None)
     assert np.array_equal(rs[0]["hist"], ref["hist"])
     assert np.array_equal(merge(rs, "x")[q], ref["x"])
+
+
+def test_dd_ipc_ranks_halo_on_second_stream(tmp_path):
+    """GG_DD_HALO_INLINE=0: the SpMV's interface exchange on the second stream
+    beside the interior rows (north_star's overlap) instead of in line -- the
+    same bits, every rank, against the one-process GG_DD_LOCAL run"""
+    case = "5pt_200x160_P4"
+    rs = run_ranks(f"ipc:{case}", 4, tmp_path, xk=0, env_extra={"GG_DD_HALO_INLINE": "0"})
+    A, method = W.system(case)
+    n = A.shape[0]
+    loc = DD(4, device=0)
+    loc.set_system(A, method)
+    x = np.random.default_rng(11).standard_normal(n)
+    assert np.array_equal(merge(rs, "spmv"), loc.spmv(x))
+    g = loc.solve(M.rhs_ones(A), restart=30, max_iter=1500, tol=1e-10)
+    assert int(rs[0]["iters"]) == g["iters"] and np.array_equal(rs[0]["hist"], g["hist"])
+    assert np.array_equal(merge(rs, "x"), g["x"])
+    loc.close()
 
 
 def test_torch_nccl_then_rccl(tmp_path):

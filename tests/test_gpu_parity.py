@@ -114,18 +114,66 @@ def test_spmv_long_rows(solver):
 @pytest.mark.slow
 def test_spmv_c3_standin_full_size(solver):
     """The C3 stand-in at circuit5M's size (5.56M rows, 59.5M nnz): its
-    sliced-ELL padding would overflow int32 offsets, so the CSR-stream kernel
-    takes it (a regression: the layout check must fall back, not fail)."""
+    sliced-ELL padding would overflow int32 offsets, so it is not sliced (a
+    regression: the layout check must fall back, not fail); y = A x runs on
+    column panels (k_spmv_panel), every row -- long ones too -- bit-exact."""
     A = M.power_law()
     x = np.random.default_rng(12).standard_normal(A.shape[0])
     solver.set_matrix(A)
     solver.set_precond_none()
-    assert not solver.spmv_sliced
+    assert not solver.spmv_sliced and solver.spmv_panels >= 2
     y, ref = solver.spmv(x), O.spmv(A, x)
-    rl = np.diff(A.indptr)
-    short = rl <= 2048
-    assert np.array_equal(y[short], ref[short])
-    assert np.all(np.abs(y - ref) <= 1e-13 * (abs(A) @ abs(x)))
+    assert np.array_equal(y, ref)
+
+
+@pytest.mark.parametrize("case", ["powerlaw", "long_rows", "empty_rows"])
+def test_spmv_panels_bitexact(solver, case, monkeypatch):
+    """Column panels at test size (GG_SPMV_PANEL / GG_SPMV_PANEL_MIN lowered):
+    every row bit-exact vs the serial CSR-order sum, rows above 2,048 entries
+    included (the panels sum every row serially), empty rows 0."""
+    monkeypatch.setenv("GG_SPMV_PANEL_MIN", "1000")
+    if case == "powerlaw":
+        A = M.power_law(200_000, 2_200_000, seed=5)
+        monkeypatch.setenv("GG_SPMV_PANEL", "30000")
+    elif case == "long_rows":
+        A = M.power_law(6000, 600000, seed=3)
+        monkeypatch.setenv("GG_SPMV_PANEL", "700")
+    else:
+        B = M.power_law(50_000, 400_000, seed=8).tolil()
+        for r in range(0, 50_000, 97):
+            B.rows[r] = []
+            B.data[r] = []
+        A = B.tocsr()
+        monkeypatch.setenv("GG_SPMV_PANEL", "4096")
+    x = np.random.default_rng(4).standard_normal(A.shape[0])
+    solver.set_matrix(A)
+    solver.set_precond_none()
+    assert solver.spmv_panels >= 2
+    assert np.array_equal(solver.spmv(x), O.spmv(A, x))
+
+
+def test_gmres_panels_bitexact(monkeypatch):
+    """GMRES(30) + ILU(0) on a power-law matrix whose inner SpMV runs on column
+    panels: bit-identical to the order-matched oracle (the panel sums are the
+    CSR order, so the solver's arithmetic is unchanged)"""
+    monkeypatch.setenv("GG_SPMV_PANEL_MIN", "1000")
+    monkeypatch.setenv("GG_SPMV_PANEL", "6000")
+    A = M.power_law(40_000, 400_000, seed=11)
+    b = M.rhs_ones(A)
+    s = ggmres.Solver(0)
+    s.set_matrix(A)
+    s.set_precond_ilu0()
+    assert s.spmv_panels >= 2
+    g = s.solve(b, restart=30, max_iter=300, tol=1e-10)
+    L, U = O.ilu0(A)
+    lay, G = s.layout()
+    O.set_dot_order(lay, G)
+    try:
+        ot = O.gmres_left(A, L, U, b, m=30, max_iter=300, tol=1e-10)
+    finally:
+        O.set_dot_order(None)
+    assert g["iters"] == ot["iters"] and np.array_equal(g["hist"], ot["hist"]) and np.array_equal(g["x"], ot["x"])
+    s.close()
 
 
 @pytest.mark.parametrize("name", sorted(MATS))
