@@ -64,6 +64,16 @@ int batch_mgs()
     return k;
 }
 
+// GG_BATCH_MGS2=0: one persistent launch per scenario instead of per pair
+bool batch_mgs2()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("GG_BATCH_MGS2");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int batch_chunk()
 {
     static const int k = [] {
@@ -90,6 +100,7 @@ struct BatchWs {
     // solver-wide election words; persist = admitted (co-residency), cleared
     // for the solver's life when a launch was not co-resident
     bool persist = false;
+    bool persist2 = false;               // two scenarios per persistent launch (k_arnoldi_persist2)
     long long ngran = 0, nxgran = 0;
     DBuf<unsigned long long> elect;
     unsigned long long seq = 0;
@@ -186,6 +197,8 @@ void ensure_batch(gg_solver *s, int S, int m, long long hist_need)
         const int pj = arnoldi_persist_units(s->G, s->Ppad);
         const int xr = (mgs_gather_form() == 3 && mgs_prefetch()) ? kMgsXcds : 0;
         B->persist = batch_mgs() == 1 && pj != 0 && s->G + xr <= arnoldi_persist_max_blocks(pj);
+        B->persist2 = B->persist && S > 1 && xr == 0 && mgs_gather_form() == 2 && mgs_prefetch() == 1 &&
+                      arnoldi_persist2_units(s->G, s->Ppad) != 0 && batch_mgs2();
         if (B->persist) {
             B->ngran = (long long)m * (m + 2) * (s->G + 1);
             B->nxgran = (long long)m * (m + 2) * kMgsXcdWords;
@@ -284,12 +297,23 @@ void enqueue_iters_b(const Ctx &c, int i0, int i1)
         launch_spmv_b(gi, s->dA, vi, nullptr, c.ww, false, c.S, c.zs, s->st);   // ww = A v_i
         trsv_pair(c, gi, c.ww, c.w);                                            // w = M^-1 ww
         if (c.B->persist) {
-            // the single-scenario persistent kernel, once per scenario
+            // the persistent kernel: two scenarios per launch (k_arnoldi_persist2),
+            // or one (k_arnoldi_persist) -- the same tree, the same bits
             for (int q = 0; q < c.S; q++) {
                 Gate gq = gi;
                 gq.done = zq(gi.done, c.zs, q);
                 gq.nit = zq(gi.nit, c.zs, q);
                 unsigned long long *gr = zq(c.gran, c.zs, q);
+                if (c.B->persist2 && q + 1 < c.S) {
+                    launch_arnoldi_persist2(gq, c.zs, i, c.m, zq(c.ds, c.zs, q), zq(c.w, c.zs, q), zq(c.V, c.zs, q), c.P,
+                                            zq(c.H, c.zs, q), zq(c.cs, c.zs, q), zq(c.sn, c.zs, q),
+                                            zq(c.sv, c.zs, q), zq(c.hist, c.zs, q),
+                                            gr + (size_t)i * (c.m + 2) * c.G, c.G, c.P, s->err.p,
+                                            zq(c.xgran, c.zs, q) + (size_t)i * (c.m + 2) * kMgsXcdWords,
+                                            c.B->elect.p, ++c.B->seq, c.um, s->st);
+                    q++;
+                    continue;
+                }
                 launch_arnoldi_persist(gq, i, c.m, zq(c.ds, c.zs, q), zq(c.w, c.zs, q), zq(c.V, c.zs, q), c.P,
                                        zq(c.H, c.zs, q), zq(c.cs, c.zs, q), zq(c.sn, c.zs, q), zq(c.sv, c.zs, q),
                                        zq(c.hist, c.zs, q), gr + (size_t)i * (c.m + 2) * c.G,
@@ -562,6 +586,7 @@ int solve_batch(gg_solver *s, int S, const double *d_b, long long ldb, double *d
             GG_HIP(hipStreamSynchronize(s->st));
             if (attempt >= 2) throw Error{GG_EHIP, "gg_solve_batch: fallbacks exhausted"};
             s->batch->persist = false;
+            s->batch->persist2 = false;
         } catch (BatchErr &e) {
             // a WD_RCP range miss: IEEE division for the solver's life, repeat
             // (d_x is written only at the end)

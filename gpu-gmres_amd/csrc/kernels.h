@@ -261,6 +261,14 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
                             long long *trace = nullptr,    // diagnostics: GG_MGS_TRACE (solver.hip)
                             const double *msc = nullptr, double *mout = nullptr,    // + mout = v_{i+1} * msc
                             double *fill = nullptr, long long nfill = 0);            // + fill[< nfill] = sentinel
+// two scenarios of the many-RHS batch per launch (scenario 1's buffers zs bytes
+// after scenario 0's, gran / xb per scenario as above): units per thread when
+// the grid can be co-resident, else 0
+int arnoldi_persist2_units(int G, long long Ppad);
+void launch_arnoldi_persist2(Gate g, long long zs, int i, int m, DevState *ds, const double *w, double *V,
+                             long long ldv, double *H, double *cs, double *sn, double *s, double *hist,
+                             unsigned long long *gran, int G, long long Ppad, int *err, unsigned long long *xb,
+                             unsigned long long *elect, unsigned long long seq, const UnitMap &um, hipStream_t st);
 // the same for long vectors (w on chip, the basis streamed): kWideG blocks
 constexpr int kWideG = 512;
 bool arnoldi_wide_ok(int G, long long Ppad);

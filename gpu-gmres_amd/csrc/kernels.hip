@@ -4320,6 +4320,251 @@ __global__ __launch_bounds__(kBlock) void k_arnoldi_persist(Gate g, int i, int m
     }
 }
 
+// ---- two scenarios per launch (the many-RHS batch, batch.hip) ----------------
+// k_arnoldi_persist's default form (XCD-local reducers, v_{k+1} streamed during
+// the gather) for two scenarios at once: scenario q's buffers q * zs bytes after
+// scenario 0's; per step the two rows are gathered together -- every granule of
+// both loaded at once, the pending ones re-polled, then each row summed in the
+// same q order (gather_row_sum + block_sum_pp: the same bits) -- so the two
+// scenarios share the step's hand-off latency instead of paying it in two
+// launches.  A gated scenario (converged) is skipped inside the launch.
+template <int J>
+__device__ __forceinline__ void gather2_xcd(const unsigned long long *row0, const unsigned long long *row1,
+                                            unsigned long long *slot0, unsigned long long *slot1, int G, bool red,
+                                            const bool (&act)[2], int *err, int &par, int limit,
+                                            const int *abort0, const int *abort1, double (&h)[2], int &miss)
+{
+    constexpr int NP = kGatherPer;
+    __shared__ double hb2[2][2];
+    if (red) {
+        unsigned long long a[2][NP];
+        const unsigned long long *rows[2] = {row0, row1};
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+            for (int r = 0; r < NP; r++) {
+                const int k = threadIdx.x + r * kBlock;
+                a[q][r] = (act[q] && k < G) ? ld_agent(rows[q] + k) : 0ull;
+            }
+        int spins = 0;
+        while (true) {
+            bool pend = false;
+#pragma unroll
+            for (int q = 0; q < 2; q++)
+#pragma unroll
+                for (int r = 0; r < NP; r++) pend |= a[q][r] == kSentinel;
+            if (!pend) break;
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int q = 0; q < 2; q++)
+#pragma unroll
+                for (int r = 0; r < NP; r++)
+                    if (a[q][r] == kSentinel) a[q][r] = ld_agent(rows[q] + threadIdx.x + r * kBlock);
+            if ((spins & 255) == 255 && ((act[0] && (ld_agent_int(abort0) & DONE_ABORT)) ||
+                                         (act[1] && (ld_agent_int(abort1) & DONE_ABORT)))) {
+                miss = 1;
+                break;
+            }
+            if (++spins > limit) {
+                miss = 1;
+                break;
+            }
+        }
+        unsigned long long *slots[2] = {slot0, slot1};
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            if (!act[q]) continue;                                    // (block-uniform)
+            h[q] = block_sum_pp(gather_row_sum<NP>(a[q], G), par);
+            if (threadIdx.x == 0) st_plain(slots[q], (unsigned long long)__double_as_longlong(h[q]));
+        }
+        return;
+    }
+    // the XCD's other blocks: thread q polls scenario q's slot
+    if (threadIdx.x < 2 && act[threadIdx.x]) {
+        const unsigned long long *sl = threadIdx.x ? slot1 : slot0;
+        unsigned long long v = ld_agent(sl);
+        int spins = 0;
+        while (v == kSentinel) {
+            __builtin_amdgcn_s_sleep(1);
+            v = ld_agent(sl);
+            const int *ab = threadIdx.x ? abort1 : abort0;
+            if ((spins & 255) == 255 && (ld_agent_int(ab) & DONE_ABORT)) {
+                miss = 1;
+                break;
+            }
+            if (++spins > limit) {
+                miss = 1;
+                break;
+            }
+        }
+        hb2[par & 1][threadIdx.x] = __longlong_as_double((long long)v);
+    }
+    __syncthreads();
+    h[0] = hb2[par & 1][0];
+    h[1] = hb2[par & 1][1];
+    par ^= 1;
+}
+
+template <int J>
+__global__ __launch_bounds__(kBlock) void k_arnoldi_persist2(Gate g, long long zs, int i, int m, DevState *ds,
+                                                             const double *__restrict__ w_in,
+                                                             double *__restrict__ V, long long ldv, double *H,
+                                                             double *cs, double *sn, double *s, double *hist,
+                                                             unsigned long long *gran, long long units, int *err,
+                                                             unsigned long long *xb, unsigned long long *elect,
+                                                             unsigned long long seq, UnitMap um)
+{
+    bool act[2];
+    DevState *dsq[2] = {ds, zp(ds, zs, 1)};
+    __shared__ int sab[2];
+    if (threadIdx.x < 2) sab[threadIdx.x] = ld_agent_int(&dsq[threadIdx.x]->done) & DONE_ABORT;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; q++) act[q] = !gated_z(g, zs, q) && !sab[q];
+    if (!act[0] && !act[1]) return;
+    const int G = gridDim.x;
+    const int ub = (int)blockIdx.x;
+    bool red = true;
+    unsigned xcc = 0;
+    xcd_elect(elect, seq, red, xcc);
+    const long long stride = (long long)G * kBlock;
+    const long long u0 = ub * (long long)kBlock + threadIdx.x;
+    const double *wq[2] = {w_in, zp(w_in, zs, 1)};
+    double *Vq[2] = {V, zp(V, zs, 1)};
+    unsigned long long *gq[2] = {gran, zp(gran, zs, 1)};
+    unsigned long long *xq[2] = {xb, zp(xb, zs, 1)};
+    const int *abw[2] = {&dsq[0]->done, &dsq[1]->done};
+    auto xslot = [&](int q, int k) { return xq[q] + ((long long)k * kXcds + xcc) * kXcdSlot; };
+    double2 w[2][J], vk[2][J], vn[2][J];
+    bool val[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const long long u = u0 + j * stride;
+        val[j] = u < units && unit_real(um, u);
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            if (val[j] && act[q]) {
+                w[q][j] = ld2(wq[q], u);
+                vk[q][j] = ld2(Vq[q], u);
+            }
+    }
+    int par = 0;
+    // both scenarios' partials of one step, each with block_sum_pp's tree
+    auto publish = [&](int k, double (&acc)[2]) {
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            if (!act[q]) continue;
+            const double a = block_sum_pp(acc[q], par);
+            if (threadIdx.x == 0) st_agent(gq[q] + (long long)k * G + ub, (unsigned long long)__double_as_longlong(a));
+        }
+    };
+    {
+        double acc[2] = {0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+            for (int j = 0; j < J; j++)
+                if (val[j] && act[q]) {
+                    acc[q] += w[q][j].x * vk[q][j].x;
+                    acc[q] += w[q][j].y * vk[q][j].y;
+                }
+        publish(0, acc);                                          // <w, v_0>
+    }
+    auto step = [&](int k, double2 (&cur)[2][J], double2 (&nxt)[2][J]) -> bool {
+        if (k < i) {                                              // v_{k+1}, in flight during the gather
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                if (!act[q]) continue;
+                const double *vp = Vq[q] + (long long)(k + 1) * ldv;
+#pragma unroll
+                for (int j = 0; j < J; j++)
+                    if (val[j]) nxt[q][j] = ld2_nt(vp, u0 + j * stride);
+            }
+        }
+        double h[2] = {0.0, 0.0};
+        int miss = 0;
+        gather2_xcd<J>(gq[0] + (long long)k * G, gq[1] + (long long)k * G, xslot(0, k), xslot(1, k), G, red, act,
+                       err, par, k == 0 ? kResidSpin : kSpinLimit, abw[0], abw[1], h, miss);
+        if (k == 0) {
+            // the launch's first all-gather bounds the co-residency wait
+            if (__syncthreads_or(miss)) {
+                if (threadIdx.x < 2 && act[threadIdx.x]) set_abort(dsq[threadIdx.x]);
+                return false;
+            }
+        } else if (miss && !(ld_agent_int(abw[0]) & DONE_ABORT) && !(ld_agent_int(abw[1]) & DONE_ABORT)) {
+            atomicOr(err, 1);                                     // a wait timed out
+        }
+        double acc[2] = {0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            if (!act[q]) continue;
+            if (ub == 0 && threadIdx.x == 0) zp(H, zs, q)[k + i * (m + 1)] = h[q];
+            const double a = -h[q];
+#pragma unroll
+            for (int j = 0; j < J; j++) {
+                if (val[j]) {
+                    w[q][j].x = a * cur[q][j].x + w[q][j].x;
+                    w[q][j].y = a * cur[q][j].y + w[q][j].y;
+                    const double2 o = (k < i) ? nxt[q][j] : w[q][j];
+                    acc[q] += w[q][j].x * o.x;
+                    acc[q] += w[q][j].y * o.y;
+                }
+            }
+        }
+        publish(k + 1, acc);
+        return true;
+    };
+    for (int k = 0; k <= i; k += 2) {
+        if (!step(k, vk, vn)) return;
+        if (k + 1 > i) break;
+        step(k + 1, vn, vk);
+    }
+    double hn[2] = {0.0, 0.0};
+    {
+        int miss = 0;
+        gather2_xcd<J>(gq[0] + (long long)(i + 1) * G, gq[1] + (long long)(i + 1) * G, xslot(0, i + 1),
+                       xslot(1, i + 1), G, red, act, err, par, kSpinLimit, abw[0], abw[1], hn, miss);
+        if (miss && !(ld_agent_int(abw[0]) & DONE_ABORT) && !(ld_agent_int(abw[1]) & DONE_ABORT)) atomicOr(err, 1);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        if (!act[q]) continue;
+        const double hq = sqrt(hn[q]);
+        if (ub == 0 && threadIdx.x == 0) {                        // as k_arnoldi_finalize
+            DevState *d = dsq[q];
+            const int ld = m + 1;
+            double *Hc = zp(H, zs, q) + i * ld;
+            double *csq = zp(cs, zs, q), *snq = zp(sn, zs, q), *sq = zp(s, zs, q);
+            Hc[i + 1] = hq;
+            for (int k = 0; k < i; k++) apply_rot(Hc[k], Hc[k + 1], csq[k], snq[k]);
+            double c, sv;
+            gen_rot(Hc[i], Hc[i + 1], c, sv);
+            csq[i] = c;
+            snq[i] = sv;
+            apply_rot(Hc[i], Hc[i + 1], c, sv);
+            apply_rot(sq[i], sq[i + 1], c, sv);
+            const double resid = fabs(sq[i + 1]) / d->normb;
+            zp(hist, zs, q)[d->hist_len + i] = resid;
+            d->resid = resid;
+            if (resid < d->tol) {
+                d->conv_i = i;
+                d->done = DONE_INNER;
+            }
+        }
+        const double inv = (hq != 0.0) ? 1.0 / hq : 0.0;
+        double *vout = Vq[q] + (long long)(i + 1) * ldv;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (val[j]) {
+                double2 a = w[q][j];
+                a.x = inv * a.x;
+                a.y = inv * a.y;
+                st2(vout, u0 + j * stride, a);
+            }
+        }
+    }
+}
+
 // k_arnoldi_wide -- the same inner iteration for vectors too long for
 // k_arnoldi_persist's registers (C4: 11.6M slots): only w stays on chip (kWideJR
 // units per thread in registers, kWideJL in LDS), v_k and v_{k+1} are streamed
@@ -5423,6 +5668,43 @@ void launch_arnoldi_persist(Gate g, int i, int m, DevState *ds, const double *w,
     f<<<G + extra, kBlock, persist_test_lds(), st>>>(g, i, m, ds, w, V, ldv, H, cs, sn, s, hist, gran, hg, Ppad / 2,
                                                      err, xb, elect, seq, um, trace, msc, mout,
                                                      reinterpret_cast<unsigned long long *>(fill), fill ? nfill : 0);
+}
+
+// the two-scenario persistent orthogonalization (k_arnoldi_persist2): 0 when
+// the vectors take no J or the grid cannot be co-resident
+int arnoldi_persist2_units(int G, long long Ppad)
+{
+    const int J = arnoldi_persist_units(G, Ppad);
+    if (J != 1 && J != 2 && J != 4) return 0;
+    static int cached[5] = {-1, -1, -1, -1, -1};
+    if (cached[J] < 0) {
+        int dev = 0, cus = 0, per = 0;
+        const void *f = J == 1 ? reinterpret_cast<const void *>(k_arnoldi_persist2<1>)
+                        : J == 2 ? reinterpret_cast<const void *>(k_arnoldi_persist2<2>)
+                                 : reinterpret_cast<const void *>(k_arnoldi_persist2<4>);
+        cached[J] = (hipGetDevice(&dev) == hipSuccess &&
+                     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) == hipSuccess)
+                        ? cus * per
+                        : 0;
+    }
+    return G <= cached[J] ? J : 0;
+}
+void launch_arnoldi_persist2(Gate g, long long zs, int i, int m, DevState *ds, const double *w, double *V,
+                             long long ldv, double *H, double *cs, double *sn, double *s, double *hist,
+                             unsigned long long *gran, int G, long long Ppad, int *err, unsigned long long *xb,
+                             unsigned long long *elect, unsigned long long seq, const UnitMap &um, hipStream_t st)
+{
+    const int J = arnoldi_persist_units(G, Ppad);
+    GG_REQUIRE(J == 1 || J == 2 || J == 4, GG_EINVAL, "k_arnoldi_persist2: vectors too long");
+    GG_REQUIRE(G <= kGatherPer * kBlock, GG_EINVAL, "k_arnoldi_persist2: grid beyond the all-gather's reach");
+#define GG_P2(JJ)                                                                                             \
+    k_arnoldi_persist2<JJ><<<G, kBlock, persist_test_lds(), st>>>(g, zs, i, m, ds, w, V, ldv, H, cs, sn, s, hist, \
+                                                                  gran, Ppad / 2, err, xb, elect, seq, um)
+    if (J == 1) GG_P2(1);
+    else if (J == 2) GG_P2(2);
+    else GG_P2(4);
+#undef GG_P2
 }
 
 void launch_update(Gate g, int m, DevState *ds, const double *H, const double *s, double *ysmall,
