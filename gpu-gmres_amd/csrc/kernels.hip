@@ -646,7 +646,19 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
 // each segment's products summed by its thread in order, continuing the row's
 // running sum kept in y (0.0 at the row's first segment, seg_row = ~row).
 // Every row is thus summed exactly as computeSpMV sums it.  Empty rows get 0
-// in pass 0.
+// in pass 0.  GG_PANEL_NT=1: the panel's entries and segment tables streamed
+// non-temporally, so that they do not push the x slice out of the L2.
+// (C3 stand-in, one box, profiles/r06/c3_panel_ab.txt: 648 -> 640 us at 4 MiB
+// panels, 651 -> 626 us at 6 MiB)
+#ifndef GG_PANEL_NT
+#define GG_PANEL_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T pan_ld(const T *p)
+{
+    if constexpr (GG_PANEL_NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
 __global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__restrict__ pblk,
                                                        const int *__restrict__ seg_row,
                                                        const int *__restrict__ seg_ptr,
@@ -664,12 +676,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__rest
             y[zero_rows[i]] = 0.0;
     const int s0 = pblk[blockIdx.x], s1 = pblk[blockIdx.x + 1];
     const int ns = s1 - s0;                     // <= kBlock segments
-    if (tid < ns) sp[tid] = seg_ptr[s0 + tid];
-    if (tid == 0) sp[ns] = seg_ptr[s1];
+    if (tid < ns) sp[tid] = pan_ld(seg_ptr + s0 + tid);
+    if (tid == 0) sp[ns] = pan_ld(seg_ptr + s1);
     int rr = 0;
     double acc = 0.0;
     if (tid < ns) {
-        rr = seg_row[s0 + tid];
+        rr = pan_ld(seg_row + s0 + tid);
         if (rr >= 0) acc = y[rr];               // the row's running sum so far
     }
     __syncthreads();
@@ -680,8 +692,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__rest
     for (int u = 0; u < U; u++) {
         const int q = tid + u * kBlock;
         if (q < cnt) {
-            c[u] = pci[e0 + q];
-            a[u] = pv[e0 + q];
+            c[u] = pan_ld(pci + e0 + q);
+            a[u] = pan_ld(pv + e0 + q);
         }
     }
 #pragma unroll
@@ -914,6 +926,20 @@ __device__ __forceinline__ void flow_long_row(int r, const int *__restrict__ rp,
 #ifndef GG_FLOW_SLEEP
 #define GG_FLOW_SLEEP 4
 #endif
+// how a short row's lane polls its sources (x pre-filled with the sentinel,
+// each slot written once per launch: a value other than the sentinel is final)
+//   0: every round re-loads the chunk's sources from the first unconsumed one
+//   1: a source seen ready is kept in a register; only sentinel ones re-polled
+//   2: as 1, and each source's first probe is a PLAIN load (L1/L2-served: a
+//      stale copy can only show the sentinel, which falls back to the agent poll)
+#ifndef GG_FLOW_POLL
+#define GG_FLOW_POLL 1
+#endif
+__device__ __forceinline__ unsigned long long ld_flow_first(const unsigned long long *p)
+{
+    if constexpr (GG_FLOW_POLL == 2) return *reinterpret_cast<const volatile unsigned long long *>(p);
+    else return ld_agent(p);
+}
 template <bool ELL>
 __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const int4 *__restrict__ tasks,
                                                       const int *__restrict__ rows,
@@ -960,14 +986,25 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
             const double dr = pending ? (y ? y[r] : d[r]) : 1.0;
             int kb = 0, k = 0;                  // chunk base, terms consumed
             int spins = 0;
+            unsigned long long u[4];            // GG_FLOW_POLL >= 1: the chunk's sources as last seen
+            bool fresh = true;                  // the chunk not probed yet
             while (__any(pending)) {
                 if (pending) {
                     // consume the sources in canonical order as far as they
                     // are ready (a source once seen stays final)
                     while (true) {
-                        unsigned long long u[4];
+                        if constexpr (GG_FLOW_POLL == 0) {
 #pragma unroll
-                        for (int j = 0; j < 4; j++) u[j] = (kb + j >= k && cc[j] >= 0) ? ld_agent(xu + cc[j]) : 0ull;
+                            for (int j = 0; j < 4; j++) u[j] = (kb + j >= k && cc[j] >= 0) ? ld_agent(xu + cc[j]) : 0ull;
+                        } else if (fresh) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) u[j] = (kb + j >= k && cc[j] >= 0) ? ld_flow_first(xu + cc[j]) : 0ull;
+                            fresh = false;
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; j++)
+                                if (kb + j >= k && cc[j] >= 0 && u[j] == kSentinel) u[j] = ld_agent(xu + cc[j]);
+                        }
                         bool stop = false;
 #pragma unroll
                         for (int j = 0; j < 4; j++) {
@@ -989,6 +1026,7 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                         }
                         kb += 4;
                         chunk(kb);
+                        fresh = true;
                     }
                 }
                 if (__any(pending)) {
@@ -1010,6 +1048,8 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
         double acc = pending ? ((fm && y) ? b[r] * y[r] : b[r]) : 0.0;
         const double dr = pending ? (y ? y[r] : d[r]) : 1.0;
         int spins = 0;
+        unsigned long long u[4];                // GG_FLOW_POLL >= 1: sources k .. k+3 as last seen
+        int ub = -1;                            // the k they were loaded for (-1: none)
         while (__any(pending)) {
             if (pending) {
                 // consume the sources in canonical order as far as they are
@@ -1017,9 +1057,20 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                 // once seen stays final, so acc is built incrementally
                 bool stop = false;
                 while (!stop && k < k1) {
-                    unsigned long long u[4];            // up to 4 polls in flight
+                    // up to 4 polls in flight
+                    if (GG_FLOW_POLL == 0) {
 #pragma unroll
-                    for (int j = 0; j < 4; j++) u[j] = k + j < k1 ? ld_agent(xu + ci[k + j]) : 0ull;
+                        for (int j = 0; j < 4; j++) u[j] = k + j < k1 ? ld_agent(xu + ci[k + j]) : 0ull;
+                    } else if (ub != k) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++) u[j] = k + j < k1 ? ld_flow_first(xu + ci[k + j]) : 0ull;
+                        ub = k;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (k + j < k1 && u[j] == kSentinel) u[j] = ld_agent(xu + ci[k + j]);
+                    }
+                    const int k0 = k;
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         if (stop || k >= k1) break;
@@ -1027,6 +1078,16 @@ __global__ __launch_bounds__(kBlock) void k_trsv_flow(Gate g, int ntask, const i
                         const double xj = __longlong_as_double((long long)u[j]);
                         acc = fm ? __builtin_fma(-v[k], xj, acc) : acc - v[k] * xj;
                         k++;
+                    }
+                    if (stop && k != k0) {
+                        // sources k0 .. k-1 consumed: shift the window to start at k
+                        const int sh = k - k0;          // 1..3 (selects: no indexed registers)
+                        const unsigned long long t1 = u[1], t2 = u[2], t3 = u[3];
+                        u[0] = sh == 1 ? t1 : sh == 2 ? t2 : t3;
+                        u[1] = sh == 1 ? t2 : sh == 2 ? t3 : kSentinel;
+                        u[2] = sh == 1 ? t3 : kSentinel;
+                        u[3] = kSentinel;
+                        ub = k;
                     }
                 }
                 if (k == k1) {

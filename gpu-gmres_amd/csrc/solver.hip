@@ -92,9 +92,11 @@ void DevCsr::upload(const Csr &A, hipStream_t st)
 // Column panels for the CSR-stream matrices whose gathers scatter over an x
 // far larger than an XCD's L2 (the C3 stand-in: 44 MB of x, uniform columns,
 // one 64-B line fetched per 8-B term, profiles/pmc_traffic_c3.json).  Panel
-// width GG_SPMV_PANEL doubles (default 524,288 = 4 MiB, the XCD's L2; the C3
-// stand-in's SpMV 971 us unpanelled, 702 / 648 / 652 / 716 / 921 us at 3 / 4
-// / 6 / 8 / 22 MiB panels, profiles/r06/c3_panel_ab.txt); used when the matrix
+// width GG_SPMV_PANEL doubles (default 786,432 = 6 MiB; the XCD's L2 is 4 MiB:
+// the C3 stand-in's SpMV 971 us unpanelled, 702 / 648 / 652 / 716 / 921 us at
+// 3 / 4 / 6 / 8 / 22 MiB panels with cached entry loads, 640 / 626 / 692 us at
+// 4 / 6 / 8 MiB with the entries streamed non-temporally (GG_PANEL_NT),
+// profiles/r06/c3_panel_ab.txt); used when the matrix
 // has at least GG_SPMV_PANEL_MIN rows (default 2^21), more than one panel, and
 // every row's columns strictly ascending (the panel order is then the CSR
 // order).  GG_SPMV_PANEL=0 turns it off.
@@ -102,7 +104,7 @@ void DevCsr::build_panels(const Csr &A, hipStream_t st)
 {
     panel = false;
     const char *pe = std::getenv("GG_SPMV_PANEL");
-    const long long w = pe ? atoll(pe) : 524288;
+    const long long w = pe ? atoll(pe) : 786432;
     const char *me = std::getenv("GG_SPMV_PANEL_MIN");
     const long long nmin = me ? atoll(me) : (1LL << 21);
     if (sell || w <= 0 || n < nmin || n <= w || nnz == 0) return;
