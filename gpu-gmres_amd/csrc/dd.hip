@@ -99,6 +99,11 @@ struct gg_dd {
     hipStream_t st = nullptr;
     hipStream_t st2 = nullptr;              // the SpMV's interface exchange, beside the interior rows
     bool halo_inline = true;                // GG_DD_HALO_INLINE=0: the exchange on st2 beside the interior rows
+    // GG_DD_IPC / LOOPBACK: the exchange and both row sets in one launch
+    // (k_dd_spmv_x; GG_DD_HALO_FUSED=0: the exchange, then the rows, in line)
+    bool halo_fused = true;
+    DBuf<unsigned long long> arrived;       // k_dd_spmv_x's exchange blocks, counted over its launches
+    unsigned long long fused_epoch = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evx = nullptr, evh = nullptr;
     bool have = false;
     int n = 0, nsep = 0, maxI = 0;
@@ -400,6 +405,48 @@ void spmv_rows(gg_dd *d, const Get &x, const Get &b, const Get &y, bool resid,
 {
     const long long S0 = d->S0;
     const bool xch = d->maxI > 0 && d->P > 1;
+    if (xch && d->halo_inline && d->halo_fused && d->sh.size() == 1 &&
+        (d->kind == GG_DD_IPC || d->kind == GG_DD_LOOPBACK)) {
+        // exchange, interior rows and separator rows in one launch (k_dd_spmv_x)
+        Shard &s = *d->sh[0];
+        if (!d->arrived.p) {
+            d->arrived.alloc(1);
+            GG_HIP(hipMemsetAsync(d->arrived.p, 0, sizeof(unsigned long long), d->st));
+        }
+        DdSpmvCall c;
+        c.me = d->rank;
+        c.P = d->P;
+        c.loop = d->kind == GG_DD_LOOPBACK;
+        c.resid = resid;
+        c.halo = x(s) + d->H0;
+        c.cnt = d->maxI;
+        c.gidx = s.iface_slot.p;
+        c.arrived = d->arrived.p;
+        c.AI = &s.AI;
+        c.AS = &s.AS;
+        c.x = x(s);
+        c.b = resid ? b(s) : nullptr;
+        c.y = y(s);
+        c.S0 = S0;
+        if (!c.loop) {
+            GG_REQUIRE(d->ipc_connected, GG_ESTATE, "dd: IPC exchange used before gg_dd_ipc_connect");
+            GG_REQUIRE(!d->ipc_broken, GG_ESTATE,
+                       "dd: IPC communicator unusable after a peer timeout (create a new gg_dd)");
+            GG_REQUIRE(c.cnt <= d->ipc_capd, GG_EINVAL, "dd: IPC halo exceeds the exchange area (GG_DD_IPC_CAP)");
+            c.pp = d->ipc;
+            c.capd = d->ipc_capd;
+            c.err = d->xerr.p;
+            c.seq = d->ipc_seq + 1;
+        } else {
+            c.err = d->xerr.p;
+        }
+        c.epoch = d->fused_epoch + 1;
+        if (launch_dd_spmv_x(gate(s), c, d->st)) {
+            if (!c.loop) d->ipc_seq++;
+            d->fused_epoch++;
+            return;
+        }
+    }
     if (xch && d->halo_inline) {
         // the exchange in line on the solver's stream: no cross-stream event
         // wait pair per SpMV (GG_DD_HALO_INLINE)
@@ -1052,6 +1099,8 @@ int gg_dd_create(int device, int nparts, int comm, int rank, const unsigned char
         // C4/8 58 -> 47 us -- the event pair of the overlap cost more than it hid)
         const char *hi = std::getenv("GG_DD_HALO_INLINE");
         d->halo_inline = !(hi && hi[0] == '0');
+        const char *hf = std::getenv("GG_DD_HALO_FUSED");
+        d->halo_fused = !(hf && hf[0] == '0');
     }
     GG_HIP(hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking));
     GG_HIP(hipEventCreate(&d->ev0));

@@ -130,6 +130,47 @@ void launch_ipc_allgather(const IpcPeers &pp, int me, int P, double *buf, long l
                           unsigned long long seq, long long capd, int *err, hipStream_t st);
 // the same with this rank's slot gathered in the launch: buf[me*cnt + e] =
 // x[gidx[e]] (-1: 0) first, and nf words of f0 / f1 set to the sentinel
+// the sharded SpMV and its halo exchange in one launch (kernels.hip
+// k_dd_spmv_x): y = A x (resid: b - A x) over the interior rows (AI, rows
+// [0, S0)) and the separator rows (AS, rows S0..), the halo at x + H0 (slot q at
+// halo + q * cnt) exchanged in the launch -- GG_DD_IPC (peers pp, sequence seq)
+// or loopback (loop); arrived: a device word of this shard's, target epoch *
+// (the launch's exchange blocks), epoch counting these launches from 1.  false:
+// not applicable (panelled matrices), nothing launched
+struct DdSpmvX {
+    IpcPeers pp;
+    int me, P, loop;
+    double *halo;
+    long long cnt, capd;
+    unsigned long long seq;
+    int *err;
+    const long long *gidx;
+    unsigned long long *arrived;
+    unsigned long long target;
+    int nbx, nbi, nbs;
+    int i_sell, i_n, i_nb, s_sell, s_n, s_nb;
+    const int *i_ptr, *i_rp, *i_ci, *s_ptr, *s_rp, *s_ci;
+    const double *i_v, *s_v;
+    const double *x, *b;
+    double *y;
+    long long S0;
+};
+struct DdSpmvCall {
+    IpcPeers pp;
+    int me = 0, P = 1;
+    bool loop = false, resid = false;
+    double *halo = nullptr;
+    long long cnt = 0, capd = 0;
+    unsigned long long seq = 0, epoch = 0;
+    int *err = nullptr;
+    const long long *gidx = nullptr;
+    unsigned long long *arrived = nullptr;
+    const DevCsr *AI = nullptr, *AS = nullptr;
+    const double *x = nullptr, *b = nullptr;
+    double *y = nullptr;
+    long long S0 = 0;
+};
+bool launch_dd_spmv_x(Gate g, const DdSpmvCall &c, hipStream_t st);
 void launch_ipc_gather_allgather(const IpcPeers &pp, int me, int P, const double *x, const long long *gidx,
                                  double *buf, long long cnt, unsigned long long seq, long long capd, int *err,
                                  double *f0, double *f1, long long nf, hipStream_t st);

@@ -477,18 +477,24 @@ __global__ void k_div(Gate g, const double *in, const double *s, double *out, in
 // YDIV: y[r] = (the row's result) / ydiv[r] -- the split engine's row gather
 // and D_l scaling (gather_divsrc, src/preconditioner.cu:1592-1626) folded into
 // the SpMV of the row-permuted matrix: the same division of the same value.
-template <bool RESID, bool YDIV = false>
-__global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, const int *rp,
-                                                        const int *ci, const double *v,
-                                                        const double *x, const double *b,
-                                                        double *y, const double *ydiv)
+// XA: x read with agent-scope (sc1) loads -- values handed over inside the
+// launch (k_dd_spmv_x's separator rows)
+template <bool XA>
+__device__ __forceinline__ double ld_x(const double *p)
 {
-    if (gated(g)) return;
+    if constexpr (XA) return __longlong_as_double((long long)ld_agent(reinterpret_cast<const unsigned long long *>(p)));
+    else return *p;
+}
+template <bool RESID, bool YDIV, bool XA = false>
+__device__ __forceinline__ void spmv_stream_block(int bid, const int *blk, const int *rp, const int *ci,
+                                                  const double *v, const double *x, const double *b, double *y,
+                                                  const double *ydiv)
+{
     constexpr int U = kSpmvCap / kBlock;        // products per thread
     __shared__ double prod[kSpmvCap];
     __shared__ int srp[kBlock + 1];
     const int tid = threadIdx.x;
-    const int r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int r0 = blk[bid], r1 = blk[bid + 1];
     const int nr = r1 - r0;                     // <= kBlock rows
     // the block's nr + 1 row pointers (nr <= kBlock: the last one by thread 0)
     if (tid < nr) srp[tid] = rp[r0 + tid];
@@ -498,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
     const int cnt = e1 - e0;
     if (cnt > kSpmvCap) {   // one long row: strided partial sums + tree
         double acc = 0.0;
-        for (int e = e0 + tid; e < e1; e += kBlock) acc += v[e] * x[ci[e]];
+        for (int e = e0 + tid; e < e1; e += kBlock) acc += v[e] * ld_x<XA>(x + ci[e]);
         acc = block_sum(acc);
         if (tid == 0) {
             const double o = RESID ? (-1.0 * acc + 1.0 * b[r0]) : acc;
@@ -526,8 +532,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
         const int p = tid + u * kBlock;
         const int e = ea + 2 * p;
         if (p < npair) {
-            if (e >= e0) xv[u].x = x[c[u].x];
-            if (e + 1 < e1) xv[u].y = x[c[u].y];
+            if (e >= e0) xv[u].x = ld_x<XA>(x + c[u].x);
+            if (e + 1 < e1) xv[u].y = ld_x<XA>(x + c[u].y);
         }
     }
 #pragma unroll
@@ -559,6 +565,15 @@ __global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, 
         y[r] = YDIV ? o / ydiv[r] : o;
     }
 }
+template <bool RESID, bool YDIV = false>
+__global__ __launch_bounds__(kBlock) void k_spmv_stream(Gate g, const int *blk, const int *rp,
+                                                        const int *ci, const double *v,
+                                                        const double *x, const double *b,
+                                                        double *y, const double *ydiv)
+{
+    if (gated(g)) return;
+    spmv_stream_block<RESID, YDIV>(blockIdx.x, blk, rp, ci, v, x, b, y, ydiv);
+}
 
 // Sliced ELL: one wave per 64-row slice, lane = row; the slice's entries are
 // read k-major (each load instruction is one coalesced 256-B / 512-B line per
@@ -581,6 +596,48 @@ __device__ __forceinline__ int xcd_block()
 
 // XDIV: x[c] = RN(x[c] / xdiv[c]) formed per gathered term -- the split
 // engine's D_r^-1 pass (k_div) folded into the gathers, the same division
+template <bool RESID, bool YDIV, bool XDIV, bool XA = false>
+__device__ __forceinline__ void spmv_sell_slice(int s, int n, const int *sptr, const int *__restrict__ ci,
+                                                const double *__restrict__ v, const double *x,
+                                                const double *__restrict__ b, double *__restrict__ y,
+                                                const double *__restrict__ ydiv, const double *__restrict__ xdiv)
+{
+    const int lane = threadIdx.x & 63;
+    const int off = sptr[s], w = (sptr[s + 1] - off) >> 6;
+    const int *cp = ci + off + lane;
+    const double *vp = v + off + lane;
+    double acc = 0.0;
+    for (int k0 = 0; k0 < w; k0 += 8) {
+        int c[8];
+        double a[8], xv[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k0 + k < w) {
+                c[k] = __builtin_nontemporal_load(cp + (k0 + k) * 64);
+                a[k] = __builtin_nontemporal_load(vp + (k0 + k) * 64);
+            }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k0 + k < w && c[k] >= 0) xv[k] = ld_x<XA>(x + c[k]);
+        if constexpr (XDIV) {
+            double dv[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (k0 + k < w && c[k] >= 0) dv[k] = xdiv[c[k]];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (k0 + k < w && c[k] >= 0) xv[k] = xv[k] / dv[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k0 + k < w && c[k] >= 0) acc += a[k] * xv[k];
+    }
+    const int r = s * 64 + lane;
+    if (r < n) {
+        const double o = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
+        y[r] = YDIV ? o / ydiv[r] : o;
+    }
+}
 template <bool RESID, bool YDIV = false, bool XDIV = false>
 __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice, const int *sptr,
                                                       const int *__restrict__ ci,
@@ -601,41 +658,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(Gate g, int n, int nslice,
         const int r = s * 64 + (int)(threadIdx.x & 63);
         if (fill && r < nfill) fill[r] = kSentinel;
     }
-    const int lane = threadIdx.x & 63;
-    const int off = sptr[s], w = (sptr[s + 1] - off) >> 6;
-    const int *cp = ci + off + lane;
-    const double *vp = v + off + lane;
-    double acc = 0.0;
-    for (int k0 = 0; k0 < w; k0 += 8) {
-        int c[8];
-        double a[8], xv[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (k0 + k < w) {
-                c[k] = __builtin_nontemporal_load(cp + (k0 + k) * 64);
-                a[k] = __builtin_nontemporal_load(vp + (k0 + k) * 64);
-            }
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (k0 + k < w && c[k] >= 0) xv[k] = x[c[k]];
-        if constexpr (XDIV) {
-            double dv[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                if (k0 + k < w && c[k] >= 0) dv[k] = xdiv[c[k]];
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                if (k0 + k < w && c[k] >= 0) xv[k] = xv[k] / dv[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (k0 + k < w && c[k] >= 0) acc += a[k] * xv[k];
-    }
-    const int r = s * 64 + lane;
-    if (r < n) {
-        const double o = RESID ? (-1.0 * acc + 1.0 * b[r]) : acc;
-        y[r] = YDIV ? o / ydiv[r] : o;
-    }
+    spmv_sell_slice<RESID, YDIV, XDIV>(s, n, sptr, ci, v, x, b, y, ydiv, xdiv);
 }
 
 // Column-panel SpMV, one launch per panel p (DevCsr::panel): a block owns a
@@ -717,6 +740,120 @@ __global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__rest
         }
         for (; e < hi; e++) acc += prod[e];
         y[rr < 0 ? ~rr : rr] = acc;
+    }
+}
+
+// The sharded SpMV with its interface exchange in ONE launch (dd.hip
+// spmv_rows; GG_DD_IPC / GG_DD_LOOPBACK, one shard per process): north_star's
+// overlap of the halo exchange with the interior rows, without a second
+// stream and its cross-stream event pair.
+//   blocks [0, nbx): the exchange -- k_ipc_allgather's protocol with this
+//     rank's slot gathered in the launch (IPC), or the loopback all-gather over
+//     this shard's own buffer (LOOPBACK, timing only: k_gather_allgather_local's
+//     stores); every halo value is stored write-through (sc1), each storing wave
+//     drains its stores, and after a barrier one lane adds 1 to *arrived
+//   blocks [nbx, nbx + nbi): the interior rows (they read no halo value)
+//   blocks after: the separator rows; one lane waits for *arrived >= target,
+//     the block passes a barrier, then reads x with agent-scope loads only
+//     (MI355X_MICROARCH.md's hand-off table, row 1)
+// A block waits only on blocks of lower index (dispatched first).  Each row's
+// operations are k_spmv_sell's / k_spmv_stream's: the same bits as the
+// unfused launches.
+template <bool RESID>
+__global__ __launch_bounds__(kBlock) void k_dd_spmv_x(Gate g, DdSpmvX a)
+{
+    const int bid = blockIdx.x, t = threadIdx.x;
+    if (bid < a.nbx) {
+        const int nb = a.nbx;
+        if (a.loop) {
+            // loopback: slot q of the halo = this shard's own interface values
+            const long long tot = (long long)a.P * a.cnt;
+            for (long long e = bid * (long long)kBlock + t; e < tot; e += (long long)nb * kBlock) {
+                const long long sq = a.gidx[e % a.cnt];
+                const double v = sq < 0 ? 0.0 : a.x[sq];
+                st_agent(reinterpret_cast<unsigned long long *>(a.halo + e), (unsigned long long)__double_as_longlong(v));
+            }
+        } else {
+            const long long chunk = (a.cnt + nb - 1) / nb;
+            const long long lo = (long long)bid * chunk, hi = lo + chunk < a.cnt ? lo + chunk : a.cnt;
+            const int par = (int)(a.seq & 1);
+            constexpr long long kFlagWords = (long long)kMaxShards * kIpcXB;
+            double *src = a.halo + (long long)a.me * a.cnt;
+            for (long long e = lo + t; e < hi; e += kBlock) {
+                const long long sq = a.gidx[e];
+                const double v = sq < 0 ? 0.0 : a.x[sq];
+                st_agent(reinterpret_cast<unsigned long long *>(src + e), (unsigned long long)__double_as_longlong(v));
+                for (int q = 0; q < a.P; q++) {
+                    if (q == a.me) continue;
+                    double *dst = reinterpret_cast<double *>(a.pp.base[q]) + kFlagWords + ((long long)par * a.P + a.me) * a.capd;
+                    dst[e] = v;
+                }
+            }
+            __threadfence_system();
+            __syncthreads();
+            if (t < a.P && t != a.me) {
+                unsigned long long *f = reinterpret_cast<unsigned long long *>(a.pp.base[t]) + (long long)a.me * kIpcXB + bid;
+                __hip_atomic_store(f, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                const unsigned long long *w = reinterpret_cast<const unsigned long long *>(a.pp.base[a.me]) +
+                                              (long long)t * kIpcXB + bid;
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+                        atomicOr(a.err, 4);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            for (int q = 0; q < a.P; q++) {
+                if (q == a.me) continue;
+                const double *rcv =
+                    reinterpret_cast<const double *>(a.pp.base[a.me]) + kFlagWords + ((long long)par * a.P + q) * a.capd;
+                double *dst = a.halo + (long long)q * a.cnt;
+                for (long long e = lo + t; e < hi; e += kBlock)
+                    st_agent(reinterpret_cast<unsigned long long *>(dst + e),
+                             (unsigned long long)__double_as_longlong(rcv[e]));
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave's halo stores drained
+        __syncthreads();
+        if (t == 0) __hip_atomic_fetch_add(a.arrived, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (gated(g)) return;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    if (bid < a.nbx + a.nbi) {
+        const int q = bid - a.nbx;
+        if (a.i_sell) {
+            const int sl = q * (kBlock / 64) + wv;
+            if (sl < a.i_nb) spmv_sell_slice<RESID, false, false>(sl, a.i_n, a.i_ptr, a.i_ci, a.i_v, a.x, a.b, a.y,
+                                                                  nullptr, nullptr);
+        } else {
+            spmv_stream_block<RESID, false>(q, a.i_ptr, a.i_rp, a.i_ci, a.i_v, a.x, a.b, a.y, nullptr);
+        }
+        return;
+    }
+    if (t == 0) {
+        int spins = 0;
+        while (ld_agent(a.arrived) < a.target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinLimit * 16) {
+                atomicOr(a.err, 4);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    const int q = bid - a.nbx - a.nbi;
+    const double *bs = RESID ? a.b + a.S0 : nullptr;
+    double *ys = a.y + a.S0;
+    if (a.s_sell) {
+        const int sl = q * (kBlock / 64) + wv;
+        if (sl < a.s_nb) spmv_sell_slice<RESID, false, false, true>(sl, a.s_n, a.s_ptr, a.s_ci, a.s_v, a.x, bs, ys,
+                                                                    nullptr, nullptr);
+    } else {
+        spmv_stream_block<RESID, false, true>(q, a.s_ptr, a.s_rp, a.s_ci, a.s_v, a.x, bs, ys, nullptr);
     }
 }
 
@@ -5070,6 +5207,57 @@ void launch_ipc_gather_allgather(const IpcPeers &pp, int me, int P, const double
     k_ipc_allgather<<<nb, kBlock, 0, st>>>(pp, me, P, buf, cnt, seq, capd, err, x, gidx,
                                            reinterpret_cast<unsigned long long *>(f0),
                                            reinterpret_cast<unsigned long long *>(f1), nf);
+}
+bool launch_dd_spmv_x(Gate g, const DdSpmvCall &c, hipStream_t st)
+{
+    const DevCsr &AI = *c.AI, &AS = *c.AS;
+    if (AI.panel || AS.panel || c.P < 2 || c.P > kMaxShards) return false;
+    DdSpmvX a{};
+    a.pp = c.pp;
+    a.me = c.me;
+    a.P = c.P;
+    a.loop = c.loop ? 1 : 0;
+    a.halo = c.halo;
+    a.cnt = c.cnt;
+    a.capd = c.capd;
+    a.seq = c.seq;
+    a.err = c.err;
+    a.gidx = c.gidx;
+    a.arrived = c.arrived;
+    // the exchange's block count depends on cnt only (every rank the same, as
+    // launch_ipc_gather_allgather's); loopback: k_gather_allgather_local's span
+    a.nbx = c.loop ? (int)std::min<long long>(kIpcXB, std::max<long long>(1, ((long long)c.P * c.cnt + 2047) / 2048))
+                   : (int)std::min<long long>(kIpcXB, std::max<long long>(1, (c.cnt + 2047) / 2048));
+    a.target = c.epoch * (unsigned long long)a.nbx;
+    auto rows = [](const DevCsr &A, int &sell, int &n, int &nb, const int *&ptr, const int *&rp, const int *&ci,
+                   const double *&v) {
+        sell = A.sell ? 1 : 0;
+        n = A.n;
+        if (A.sell) {
+            nb = A.nslice;
+            ptr = A.sptr.p;
+            rp = nullptr;
+            ci = A.sci.p;
+            v = A.sv.p;
+            return (A.nslice + kBlock / 64 - 1) / (kBlock / 64);
+        }
+        nb = A.nblk;
+        ptr = A.blk.p;
+        rp = A.rp.p;
+        ci = A.ci.p;
+        v = A.v.p;
+        return A.nblk;
+    };
+    a.nbi = AI.nblk == 0 ? 0 : rows(AI, a.i_sell, a.i_n, a.i_nb, a.i_ptr, a.i_rp, a.i_ci, a.i_v);
+    a.nbs = AS.nblk == 0 ? 0 : rows(AS, a.s_sell, a.s_n, a.s_nb, a.s_ptr, a.s_rp, a.s_ci, a.s_v);
+    a.x = c.x;
+    a.b = c.b;
+    a.y = c.y;
+    a.S0 = c.S0;
+    const int grid = a.nbx + a.nbi + a.nbs;
+    if (c.resid) k_dd_spmv_x<true><<<grid, kBlock, 0, st>>>(g, a);
+    else k_dd_spmv_x<false><<<grid, kBlock, 0, st>>>(g, a);
+    return true;
 }
 void launch_gather_allgather_local(const ShardPtrs &b, const IdxPtrs &gi, int P, long long off, long long cnt,
                                    const FillPtrs &fl, long long nf, hipStream_t st)

@@ -1,8 +1,9 @@
 """The sharded solve's exchange modes (csrc/dd.hip), each against the default.
 
-* GG_DD_HALO_INLINE: the SpMV's interface exchange in line on the solver's
-  stream (default) or on the second stream beside the interior rows, the
-  separator rows after an event wait (north_star's overlap) -- the same bits:
+* GG_DD_HALO_INLINE / GG_DD_HALO_FUSED: the SpMV's interface exchange in the
+  same launch as the rows (IPC / loopback default, k_dd_spmv_x), as its own
+  launch on the solver's stream, or on the second stream beside the interior
+  rows, the separator rows after an event wait -- the same bits:
   SpMV, preconditioner apply and GMRES (history, iterations, solution), for a
   2D rectangle and a 3D box partition (GG_DD_LOCAL, every shard in this
   process).
@@ -28,10 +29,19 @@ CASES = {
 }
 
 
-def _make(monkeypatch, inline, P, **kw):
-    monkeypatch.setenv("GG_DD_HALO_INLINE", "1" if inline else "0")    # read at gg_dd_create
+# halo forms: "fused" (default; IPC / loopback: exchange and rows in one
+# launch, k_dd_spmv_x -- GG_DD_LOCAL has no fused form and runs "inline"),
+# "inline" (the exchange as its own launch, then the rows), "stream2" (the
+# exchange on the second stream beside the interior rows)
+FORMS = {"fused": {}, "inline": {"GG_DD_HALO_FUSED": "0"}, "stream2": {"GG_DD_HALO_INLINE": "0"}}
+
+
+def _make(monkeypatch, form, P, **kw):
+    for k, v in FORMS[form].items():
+        monkeypatch.setenv(k, v)                                       # read at gg_dd_create
     d = DD(P, device=0, **kw)
-    monkeypatch.delenv("GG_DD_HALO_INLINE")
+    for k in FORMS[form]:
+        monkeypatch.delenv(k)
     return d
 
 
@@ -41,8 +51,8 @@ def test_halo_modes_bitexact(name, monkeypatch):
     A = make()
     n = A.shape[0]
     out = []
-    for inline in (True, False):
-        d = _make(monkeypatch, inline, P)
+    for form in ("inline", "stream2"):
+        d = _make(monkeypatch, form, P)
         d.set_system(A, method)
         rng = np.random.default_rng(5)
         x = rng.standard_normal(n)
@@ -81,8 +91,8 @@ def test_loopback_rank_interior_rows_and_run(rank, monkeypatch):
     x = np.random.default_rng(3).standard_normal(n)
     ref = loc.spmv(x)
     res = []
-    for inline in (True, False):
-        lb = _make(monkeypatch, inline, P, rank=rank, comm="loopback")
+    for form in FORMS:
+        lb = _make(monkeypatch, form, P, rank=rank, comm="loopback")
         lb.set_system(A, method)
         y = lb.spmv(x, np.full(n, np.nan))
         own = ~np.isnan(y)
@@ -94,7 +104,8 @@ def test_loopback_rank_interior_rows_and_run(rank, monkeypatch):
         assert g["iters"] == 60 and np.all(np.isfinite(g["hist"])) and g["hist"][0] == pytest.approx(1.0)
         res.append((y, g))
         lb.close()
-    (y0, g0), (y1, g1) = res
+    (y0, g0) = res[0]
     own = ~np.isnan(y0)
-    assert np.array_equal(y0[own], y1[own]) and np.array_equal(g0["hist"], g1["hist"])
+    for y1, g1 in res[1:]:
+        assert np.array_equal(y0[own], y1[own]) and np.array_equal(g0["hist"], g1["hist"])
     loc.close()

@@ -147,12 +147,16 @@ def test_dd_ipc_ranks_match_local_and_oracle(case, xk, tmp_path):
     assert np.array_equal(merge(rs, "x")[q], ref["x"])
 
 
-def test_dd_ipc_ranks_halo_on_second_stream(tmp_path):
-    """GG_DD_HALO_INLINE=0: the SpMV's interface exchange on the second stream
-    beside the interior rows (north_star's overlap) instead of in line -- the
-    same bits, every rank, against the one-process GG_DD_LOCAL run"""
+@pytest.mark.parametrize("form", ["second_stream", "separate_launches"])
+def test_dd_ipc_ranks_halo_forms(form, tmp_path):
+    """The SpMV's interface exchange in the other two forms than the default
+    (exchange and rows in one launch, k_dd_spmv_x): GG_DD_HALO_INLINE=0 on the
+    second stream beside the interior rows, GG_DD_HALO_FUSED=0 as its own
+    launch before the rows -- the same bits, every rank, against the
+    one-process GG_DD_LOCAL run"""
     case = "5pt_200x160_P4"
-    rs = run_ranks(f"ipc:{case}", 4, tmp_path, xk=0, env_extra={"GG_DD_HALO_INLINE": "0"})
+    env = {"GG_DD_HALO_INLINE": "0"} if form == "second_stream" else {"GG_DD_HALO_FUSED": "0"}
+    rs = run_ranks(f"ipc:{case}", 4, tmp_path, xk=0, env_extra=env)
     A, method = W.system(case)
     n = A.shape[0]
     loc = DD(4, device=0)
