@@ -6050,11 +6050,16 @@ bool trsv_batchable(const DevTri &T)
     const int e = T.eff_div();
     return T.lower ? (e == WD_UNIT || e == WD_UFMA) : (e == WD_HW || e == WD_RCP || e == WD_MUL || e == WD_SFMA);
 }
+// the batched wavefront's workgroup map (trsv_wave2d_body's zmap), default 1:
+// band b of every scenario on one XCD, so the scenarios share its coefficient
+// streams in the L2 -- C5 with 8 scenarios (one box, rocprofv3 FETCH_SIZE,
+// profiles/r06/c5_batch_pmc.txt): U 236 -> 83 MB, L 177 -> 75 MB per launch,
+// 10,500 -> 10,751 it/s; 0: a scenario's bands on one XCD
 int batch_zmap()
 {
     static const int z = [] {
         const char *e = std::getenv("GG_BATCH_ZMAP");
-        return e ? std::atoi(e) : 0;
+        return e ? std::atoi(e) : 1;
     }();
     return z;
 }
