@@ -4603,8 +4603,12 @@ __device__ __forceinline__ void gather2_xcd(const unsigned long long *row0, cons
     par ^= 1;
 }
 
+// three blocks per CU (168 VGPRs at J = 4, 22 spilled): C5's grid of 532
+// blocks co-resident (2 per CU at 192 VGPRs would hold 512) -- C5 with 8
+// scenarios 10,606 -> 11,255 it/s, MGS 54.3 -> 45.5 us per pair of scenarios
+// (profiles/r06/r06x_c5_pair.txt)
 template <int J>
-__global__ __launch_bounds__(kBlock) void k_arnoldi_persist2(Gate g, long long zs, int i, int m, DevState *ds,
+__global__ __launch_bounds__(kBlock, 3) void k_arnoldi_persist2(Gate g, long long zs, int i, int m, DevState *ds,
                                                              const double *__restrict__ w_in,
                                                              double *__restrict__ V, long long ldv, double *H,
                                                              double *cs, double *sn, double *s, double *hist,
