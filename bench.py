@@ -962,6 +962,16 @@ def main():
         if name == "mgs_givens":
             roof["alg_bytes_note"] = ("v_0..v_i and w read once, v_{i+1} written: 8 n (i+3) bytes at "
                                       "cycle index i, averaged over the launches timed")
+        if name in ("trsv_L", "trsv_U"):
+            # algorithmic = SURVEY.md 8(d)'s CSR share of B_ilu (12 nnz_T + 4 (n+1) + 16 n,
+            # + B_spmv when the SpMV rides in the forward solve's launch); the
+            # wavefront kernels stream no index arrays, so they move less than that
+            which = 0 if name == "trsv_L" else 1
+            sb = s.bytes_trsv_stream(which)
+            if which == 0 and s.trsv_kernel(0).startswith("k_trsv_wave2d_spmv"):
+                sb += s.bytes_spmv()
+            roof["alg_bytes_note"] = "SURVEY.md 8(d): 12 nnz_T + 4 (n+1) + 16 n per triangle (+ B_spmv if fused)"
+            roof["kernel_stream_bytes_per_launch"] = sb
         # the triangular solves are latency-bound: their other roofline is the
         # dependency chain, nx + ny - 1 wavefront steps at the bare per-step chain
         # latency (tools/lat_probe.hip on MI355X, profiles/r01/r01_lat_probe.txt)

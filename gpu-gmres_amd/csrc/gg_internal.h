@@ -363,10 +363,20 @@ struct DevTri {
     long long *trace = nullptr;  // diagnostics: per band, nbatch+1 timestamps (gg_trace_precond)
     double bytes = 0;            // algorithmic bytes per solve
     double bytes_mul = 0;        // the same with WD_MUL (y streamed in place of d (, y))
+    // WAVE2D: what the kernel streams (no index arrays; bytes above = SURVEY.md
+    // 8(d)'s CSR formulation), 0 = the same as bytes
+    double stream_bytes = 0, stream_bytes_mul = 0;
     double alg_bytes() const
     {
         const int e = eff_div();
         return ((e == WD_MUL || e == WD_SFMA) ? bytes_mul : bytes) + (tail ? tail->bytes + cbytes : 0.0);
+    }
+    double stream_alg_bytes() const
+    {
+        const int e = eff_div();
+        const double own = (e == WD_MUL || e == WD_SFMA) ? (stream_bytes_mul > 0 ? stream_bytes_mul : bytes_mul)
+                                                         : (stream_bytes > 0 ? stream_bytes : bytes);
+        return own + (tail ? tail->bytes + cbytes : 0.0);
     }
     // Bordered grid (Wave2D::bnt; this triangle = the grid block's wavefront,
     // its arrays and pointers relative to slot bofs): the tail rows as a LEVEL

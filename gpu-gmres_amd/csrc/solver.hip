@@ -337,9 +337,14 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         T.bnd.alloc((size_t)(ngran + ndummy + 64));
         launch_fill_u64(T.bnd.p, ngran, kSentinel, st);
         launch_fill_u64(T.bnd.p + ngran, ndummy + 64, 0ull, st);
-        // algorithmic bytes: b, two coefficients, (divisor (, reciprocal)), x per grid point
-        T.bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
-        T.bytes_mul = (double)n * (8.0 * ((unit ? 4 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
+        // algorithmic bytes: this triangle's share of B_ilu --
+        // its CSR entries (a stored diagonal included), one row-pointer array, b
+        // read and x written -- the reference's formulation of the same solve
+        T.bytes = T.bytes_mul = 12.0 * ((double)C.off.nnz() + (unit ? 0.0 : (double)n)) + 4.0 * (n + 1) + 16.0 * n;
+        // what the wavefront kernel itself streams (no indices): b, two
+        // coefficients, (divisor (, reciprocal)), x per grid point
+        T.stream_bytes = (double)n * (8.0 * ((unit ? 4 : T.rcp_ok ? 6 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
+        T.stream_bytes_mul = (double)n * (8.0 * ((unit ? 4 : 5) + (d3 ? (wl->tile ? 1 : 2) : 0) + K));
     } else if (nat2lay && !identity_map(*nat2lay, n)) {
         // a relabeled (RCM) layout: the triangle in layout space
         CanonTri Cr;
@@ -2588,6 +2593,13 @@ double gg_bytes_trsv(gg_solver *s, int which)
     if (!s || s->pkind < 0 || (which != 0 && which != 1)) return 0.0;
     s->L.fast = s->U.fast = s->div_mode;
     return which == 0 ? s->L.alg_bytes() : s->U.alg_bytes();
+}
+
+double gg_bytes_trsv_stream(gg_solver *s, int which)
+{
+    if (!s || s->pkind < 0 || (which != 0 && which != 1)) return 0.0;
+    s->L.fast = s->U.fast = s->div_mode;
+    return which == 0 ? s->L.stream_alg_bytes() : s->U.stream_alg_bytes();
 }
 
 }  // extern "C"

@@ -28,7 +28,7 @@ EXPORTS = [
     "gg_uses_wavefront", "gg_solve", "gg_solve_device", "gg_get_history", "gg_spmv",
     "gg_precond_apply", "gg_time_spmv", "gg_time_precond", "gg_bytes_spmv",
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
-    "gg_trace_precond", "gg_bytes_trsv", "gg_transient", "gg_set_precond_ilu0_device",
+    "gg_trace_precond", "gg_bytes_trsv", "gg_bytes_trsv_stream", "gg_transient", "gg_set_precond_ilu0_device",
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
     "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced", "gg_spmv_panels",
     "gg_transient_mna", "gg_set_division", "gg_division_active",
@@ -129,6 +129,8 @@ def lib():
         L.gg_bytes_precond.restype = ctypes.c_double
         L.gg_bytes_trsv.argtypes = [_VP, ctypes.c_int]
         L.gg_bytes_trsv.restype = ctypes.c_double
+        L.gg_bytes_trsv_stream.argtypes = [_VP, ctypes.c_int]
+        L.gg_bytes_trsv_stream.restype = ctypes.c_double
         L.gg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.gg_layout.argtypes = [_VP, ctypes.c_void_p, ctypes.c_longlong]
         L.gg_layout.restype = ctypes.c_longlong
@@ -603,8 +605,14 @@ class Solver:
         return lib().gg_bytes_precond(self.h)
 
     def bytes_trsv(self, which):
-        """algorithmic bytes of one triangular solve (0 = L / Ml, 1 = U / Mr)"""
+        """algorithmic bytes of one triangular solve (0 = L / Ml, 1 = U / Mr;
+        SURVEY.md 8(d)'s CSR formulation)"""
         return lib().gg_bytes_trsv(self.h, int(which))
+
+    def bytes_trsv_stream(self, which):
+        """bytes the triangular solve's kernel itself streams (no index arrays on
+        the wavefront)"""
+        return lib().gg_bytes_trsv_stream(self.h, int(which))
 
 
 def device_count():

@@ -296,6 +296,9 @@ int gg_profile_get(gg_solver *s, int kind, int *launches, double *total_ms);
 double gg_bytes_spmv(gg_solver *s);
 double gg_bytes_precond(gg_solver *s);
 double gg_bytes_trsv(gg_solver *s, int which);   /* 0 = L / Ml, 1 = U / Mr */
+/* what the triangular solve's kernel itself streams (the wavefront kernels read
+ * no index arrays: less than gg_bytes_trsv's CSR formulation; otherwise equal) */
+double gg_bytes_trsv_stream(gg_solver *s, int which);
 
 /* Backward-Euler transient loop on one factorization: the step driver of
  * mna_solve_gpu_gmres (src/mna_solve_gpu_gmres.cpp:564-647) with PULSE sources
