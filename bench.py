@@ -366,6 +366,15 @@ def bench_c3(a, torch, dist, world, rank, local):
     avg_us = sum(ev_ms) / len(ev_ms) * 1e3                 # events around each launch
     ach = byt / (avg_us * 1e-6) / 1e9
     rl = np.diff(A.indptr)
+    # column panels (k_spmv_panel): one launch per panel, an SpMV = all of them
+    npan = s.spmv_panels
+    if npan:
+        c3_kernel = f"k_spmv_panel ({npan} panel launches per SpMV)"
+        per = pmc_traffic("k_spmv_panel", "c3")
+        c3_traffic = per * npan if per is not None else None
+    else:
+        c3_kernel = "k_spmv_stream<false>"
+        c3_traffic = pmc_traffic("k_spmv_stream<false>", "c3")
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "GB/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el * 1e3 / a.steps, 3),
@@ -377,9 +386,9 @@ def bench_c3(a, torch, dist, world, rank, local):
                    "mean_row": round(float(rl.mean()), 2),
                    "parallelism": "single" if world == 1 else f"replicas{world}",
                    "setup_s": round(t_setup, 3)},
-        "roofline": {"kernel": "k_spmv_stream<false>", "bound": "hbm", "achieved": round(ach, 1),
+        "roofline": {"kernel": c3_kernel, "bound": "hbm", "achieved": round(ach, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic("k_spmv_stream<false>", "c3"),
+                     "traffic": c3_traffic,
                      "alg_bytes_per_launch": byt, "avg_us": round(avg_us, 3)},
         "cpu_baseline": None,
     }
@@ -557,7 +566,10 @@ def bench_dd(a, torch, dist, world, rank, local):
     inner = sum(r["inner"] for r in res)          # one system: every rank counts the same
     roof = None
     wi = d.info()["wave_interior"]
-    kname = {"spmv": "k_spmv_sell<false> / k_spmv_stream<false> (interior + separator rows)",
+    fused_halo = (((world > 1 and comm == "ipc") or (world == 1 and comm == "loopback"))
+                  and os.environ.get("GG_DD_HALO_FUSED", "1") != "0" and os.environ.get("GG_DD_HALO_INLINE", "1") != "0")
+    kname = {"spmv": ("k_dd_spmv_x (halo exchange + interior + separator rows in one launch)" if fused_halo
+                      else "k_spmv_sell<false> / k_spmv_stream<false> (interior + separator rows)"),
              "trsv_L": {2: "k_trsv_wave2d (interior L, 2D band wavefront)",
                         3: "k_trsv_tile3d (interior L, 3D tile wavefront)"}.get(wi, "k_trsv_flow (interior L)"),
              "trsv_U": {2: "k_trsv_wave2d (interior U, 2D band wavefront)",
@@ -938,7 +950,7 @@ def main():
         dom = min(tied, key=lambda k: timed[k]["achieved_gbs"]) if tied else order[0]
 
     pmc_wl = ("c4" if c4 else "c3s" if c3s else ("pgr" if a.pg_perm == "random" else "pg") if pg
-              else "netlist" if netlist else None)
+              else "netlist" if netlist else "c5" if c5 else None)
     if kilu:                            # ILU(k): its own PMC pass (tools/profile_round.sh c2_ilu1 / c3s_ilu1)
         pmc_wl = f"{pmc_wl or 'c2'}_ilu{kilu}"
 
@@ -946,7 +958,8 @@ def main():
         """(roofline, latency_roofline) of one timed family"""
         f = timed[name]
         if name == "spmv":
-            KERNEL_NAMES["spmv"] = "k_spmv_sell<false>" if s.spmv_sliced else "k_spmv_stream<false>"
+            KERNEL_NAMES["spmv"] = ("k_spmv_panel" if s.spmv_panels else
+                                    "k_spmv_sell<false>" if s.spmv_sliced else "k_spmv_stream<false>")
         if name in ("trsv_L", "trsv_U") and not s.uses_wavefront:
             kname = ("k_trsv_level (one launch per dependency level; one 'launch' here = one triangle)"
                      if os.environ.get("GG_TRSV_LEVELS") == "1" else "k_trsv_flow")
