@@ -2029,7 +2029,7 @@ int gg_mgs_kernel(gg_solver *s, char *name, int cap)
     if (s->m_alloc > 0 && !s->shared) {
         if (s->persist)
             k = "k_arnoldi_persist<" + std::to_string(arnoldi_persist_units(s->G, s->Ppad)) + ", " +
-                std::to_string(mgs_gather_form()) + ">";
+                std::to_string(mgs_gather_form()) + ", " + std::to_string(mgs_prefetch()) + ">";
         else if (s->wide) k = "k_arnoldi_wide";
     }
     std::snprintf(name, (size_t)cap, "%s", k.c_str());

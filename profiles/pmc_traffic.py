@@ -57,7 +57,17 @@ def per_kernel(d, counter):
                 key = row.get("Dispatch_Id") or row.get("Correlation_Id")
                 e = acc.setdefault(k, {})
                 e[key] = e.get(key, 0.0) + v          # sum over XCD / shader-engine instances
-    return {k: (sum(e.values()) / len(e), len(e)) for k, e in acc.items()}
+    # a launch whose gate was closed (the solve converged while later launches
+    # of its chunk were already enqueued) reads its control block and returns:
+    # its dispatches are dropped from the average (below 1 % of the kernel's
+    # largest dispatch), counted in "gated"
+    out = {}
+    for k, e in acc.items():
+        vals = list(e.values())
+        hi = max(vals)
+        keep = [v for v in vals if v >= 0.01 * hi] if hi > 64.0 else vals
+        out[k] = (sum(keep) / len(keep), len(keep), len(vals) - len(keep))
+    return out
 
 
 def main():
@@ -67,13 +77,13 @@ def main():
     write = per_kernel(wdir, "WRITE_SIZE")
     res = {}
     for k in sorted(set(fetch) | set(write)):
-        fk, fn = fetch.get(k, (0.0, 0))
-        wk, wn = write.get(k, (0.0, 0))
+        fk, fn, fg = fetch.get(k, (0.0, 0, 0))
+        wk, wn, wg = write.get(k, (0.0, 0, 0))
         rd = 2.0 * fk * 1024.0
         wr = wk * 1024.0
         res[k] = {"fetch_kib_raw": round(fk, 3), "write_kib_raw": round(wk, 3),
                   "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-                  "hbm_bytes_per_launch": rd + wr, "dispatches": [fn, wn]}
+                  "hbm_bytes_per_launch": rd + wr, "dispatches": [fn, wn], "gated": [fg, wg]}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace (separate passes)",
            "correction": "read = 2 x FETCH_SIZE KiB (gfx950 16-B/lane streaming reads); write = WRITE_SIZE KiB",
            # the kernel sources these counters were taken on: bench.py drops the
