@@ -201,6 +201,9 @@ def pmc_traffic(kernel, workload=None):
             return ks[kernel]["hbm_bytes_per_launch"]
         want = kernel_key(kernel)
         hit = [v for k, v in ks.items() if kernel_key(k) == want]
+        if not hit and "<" not in kernel:
+            # a bare name ('k_trsv_flow') and ONE instantiation of it in the file
+            hit = [v for k, v in ks.items() if k.startswith(kernel + "<")]
         return hit[0]["hbm_bytes_per_launch"] if len(hit) == 1 else None
     except (OSError, KeyError, ValueError):
         return None
