@@ -89,6 +89,7 @@ struct gg_solver {
     hipEvent_t p_ev[2] = {nullptr, nullptr};
     std::vector<size_t> mark_ends;      // marks.size() after each enqueued cycle (pipelined)
     int resid_fallbacks = 0;            // cycles rerun after a persistent grid was not co-resident
+    int iter_hint = 0;                  // transient loop: the previous step's inner iterations (0: none)
     // transient tap-node statistics (gg_transient_set_taps / _get_taps)
     std::vector<int> taps;
     std::vector<double> tap_max, tap_min, tap_avg;

@@ -1014,15 +1014,20 @@ static bool mulfold_on()
     return !(e && e[0] == '0');
 }
 
-void enqueue_cycle(gg_solver *s, int m)
+// One restart cycle: its start (i0 = 0), inner iterations [i0, i1) and, with
+// tail, its end (update, residual).  The default is the whole cycle; the
+// transient loop enqueues a cycle's first iterations alone when the previous
+// step says the solve will converge within them (solve_device_once).
+void enqueue_cycle(gg_solver *s, int m, int i0 = 0, int i1 = -1, bool tail = true)
 {
+    if (i1 < 0) i1 = m;
     const UnitMap um = unit_map(s);
     DevState *ds = s->ds.p;
     const long long P = s->Ppad;
     const bool split = s->pkind == GG_PRECOND_SPLIT;
     const bool usplit = s->pkind == GG_PRECOND_USER_SPLIT;
     const bool user = user_kind(s);
-    launch_init_cycle(ds, s->r.p, s->V.p, s->s.p, s->G, P, s->st);
+    if (i0 == 0) launch_init_cycle(ds, s->r.p, s->V.p, s->s.p, s->G, P, s->st);
     const bool persist = s->persist && !s->shared;
     const bool wide = s->wide && !s->shared;
     // the split engine: the persistent MGS of iteration i also forms Mr's first
@@ -1036,10 +1041,10 @@ void enqueue_cycle(gg_solver *s, int m)
                        !s->L.lev_ptr.empty();
     const bool ufill = xpath && mulfold && fill_fold_on() && s->U.kind == DevTri::LEVEL && !s->U.tail &&
                        s->U.bofs == 0 && !s->U.lev_ptr.empty();
-    if (persist || wide) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
-    if (persist) launch_fill_u64(s->xgran.p, (long long)s->xgran.n, kSentinel, s->st);
+    if (i0 == 0 && (persist || wide)) launch_fill_u64(s->gran.p, (long long)s->gran.n, kSentinel, s->st);
+    if (i0 == 0 && persist) launch_fill_u64(s->xgran.p, (long long)s->xgran.n, kSentinel, s->st);
     const bool fuse = fuse_spmv_active(s);
-    for (int i = 0; i < m; i++) {
+    for (int i = i0; i < i1; i++) {
         Gate gi;
         gi.done = &ds->done;
         gi.mask = ~0;
@@ -1132,6 +1137,7 @@ void enqueue_cycle(gg_solver *s, int m)
         }
         prof_end(s, mk);
     }
+    if (!tail) return;
     Gate gu;
     gu.done = &ds->done;
     gu.mask = DONE_RESTART | DONE_INIT | DONE_ABORT | DONE_FINAL | DONE_EXH;
@@ -1317,9 +1323,35 @@ int solve_device_once(gg_solver *s, const double *d_b, double *d_x, const gg_opt
             while (!s->mark_ends.empty()) collect(0);
             prof_collect(s, 0);
         };
-        // cycle 1 is gated on DONE_INIT (converged at the start) like the rest
-        enqueue(0);
-        enqueue(1);
+        // cycle 1 is gated on DONE_INIT (converged at the start) like the rest.
+        // The transient loop's hint (the previous step's inner iterations, h):
+        // cycle 1's first h + 2 iterations go in alone and their state is read;
+        // when the solve converged in them only the cycle's end follows, else
+        // the rest of the cycle and cycle 2 -- the launches a converged step
+        // would have run gated off (up to 2m - h iterations' worth, each a
+        // launch that reads its gate and returns) are never enqueued.  The
+        // kernels that do run are the same, in the same order: the same bits.
+        const int hint = s->iter_hint;
+        if (hint > 0 && hint + 2 < m) {
+            const int K = hint + 2;
+            enqueue_cycle(s, m, 0, K, false);
+            GG_HIP(hipMemcpyAsync(s->p_state[0], s->ds.p, sizeof(DevState), hipMemcpyDeviceToHost, s->st));
+            GG_HIP(hipMemcpyAsync(s->p_err[0], s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
+            GG_HIP(hipEventRecord(s->p_ev[0], s->st));
+            GG_HIP(hipEventSynchronize(s->p_ev[0]));
+            const DevState hp = *s->p_state[0];
+            const bool conv = *s->p_err[0] == 0 && (hp.done & (DONE_INIT | DONE_INNER)) != 0 &&
+                              (hp.done & DONE_ABORT) == 0;
+            enqueue_cycle(s, m, conv ? m : K, m, true);
+            s->mark_ends.push_back(s->marks.size());
+            GG_HIP(hipMemcpyAsync(s->p_state[0], s->ds.p, sizeof(DevState), hipMemcpyDeviceToHost, s->st));
+            GG_HIP(hipMemcpyAsync(s->p_err[0], s->err.p, sizeof(int), hipMemcpyDeviceToHost, s->st));
+            GG_HIP(hipEventRecord(s->p_ev[0], s->st));
+            if (!conv) enqueue(1);
+        } else {
+            enqueue(0);
+            enqueue(1);
+        }
         int cur = 0;
         DevState prev{};
         prev.j = 1;
@@ -2141,6 +2173,15 @@ static int transient_loop(gg_solver *s, int it0, int nsteps, double h, const dou
         launch_taps(ntap, d_tap.p, d_x, d_tmax.p, d_tmin.p, d_tsum.p, 0, 0.0, s->st);
     }
     int total = 0, status = GG_OK;
+    // each step's solve is told how many inner iterations the previous one took
+    // (solve_device_once: a short first chunk instead of two speculative cycles)
+    struct HintReset {
+        gg_solver *s;
+        ~HintReset() { s->iter_hint = 0; }
+    } hint_reset{s};
+    const char *he = std::getenv("GG_TRANSIENT_HINT");
+    const bool use_hint = !(he && he[0] == '0');
+    s->iter_hint = 0;
     for (int it = 1; it <= nsteps; it++) {
         const int tidx = it0 + it - 1;              // time index of the sources
         if (general)
@@ -2153,6 +2194,7 @@ static int transient_loop(gg_solver *s, int it0, int nsteps, double h, const dou
         const int rc = solve_device(s, d_w.p, d_x, opt, &r);
         if (rc != GG_OK) status = rc;
         total += r.iters;
+        s->iter_hint = use_hint && rc >= 0 ? r.inner_iters : 0;
         launch_gather_ports(nport, d_port.p, d_x, d_pv.p + (size_t)it * nport, s->st);
         launch_taps(ntap, d_tap.p, d_x, d_tmax.p, d_tmin.p, d_tsum.p, 1, 0.0, s->st);
     }
