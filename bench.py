@@ -370,8 +370,11 @@ def bench_c3(a, torch, dist, world, rank, local):
     ach = byt / (avg_us * 1e-6) / 1e9
     rl = np.diff(A.indptr)
     # column panels (k_spmv_panel): one launch per panel, an SpMV = all of them
-    npan = s.spmv_panels
-    if npan:
+    npan, nrt = s.spmv_panels, s.spmv_rtile
+    if npan and nrt:
+        c3_kernel = f"k_spmv_rtile (one launch: {nrt} row blocks over {npan} column panels)"
+        c3_traffic = pmc_traffic("k_spmv_rtile", "c3")
+    elif npan:
         c3_kernel = f"k_spmv_panel ({npan} panel launches per SpMV)"
         per = pmc_traffic("k_spmv_panel", "c3")
         c3_traffic = per * npan if per is not None else None
@@ -961,7 +964,7 @@ def main():
         """(roofline, latency_roofline) of one timed family"""
         f = timed[name]
         if name == "spmv":
-            KERNEL_NAMES["spmv"] = ("k_spmv_panel" if s.spmv_panels else
+            KERNEL_NAMES["spmv"] = ("k_spmv_rtile" if s.spmv_rtile else "k_spmv_panel" if s.spmv_panels else
                                     "k_spmv_sell<false>" if s.spmv_sliced else "k_spmv_stream<false>")
         if name in ("trsv_L", "trsv_U") and not s.uses_wavefront:
             kname = ("k_trsv_level (one launch per dependency level; one 'launch' here = one triangle)"

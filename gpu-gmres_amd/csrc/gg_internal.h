@@ -298,6 +298,13 @@ struct DevCsr {
     std::vector<int> pan_blk_h;
     DBuf<double> pv;
     int nzero = 0;
+    // row tiles (k_spmv_rtile, GG_SPMV_RTILE): ONE launch of rtile blocks, block
+    // b owning a contiguous row range and walking its sub-blocks rt_sub[b] ..
+    // rt_sub[b+1]-1 (pblk indices) panel by panel; a segment longer than a
+    // sub-block's capacity is cut into consecutive pieces (seg_row >= 0 after
+    // the first).  0: the panel-major launches above
+    int rtile = 0;
+    DBuf<int> rt_sub;
     void upload(const Csr &A, hipStream_t st);
     void build_panels(const Csr &A, hipStream_t st);   // (upload: the column panels when they apply)
     void copy_from(const DevCsr &o, hipStream_t st);   // device-side duplicate

@@ -682,22 +682,19 @@ __device__ __forceinline__ T pan_ld(const T *p)
     if constexpr (GG_PANEL_NT) return __builtin_nontemporal_load(p);
     else return *p;
 }
-__global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__restrict__ pblk,
-                                                       const int *__restrict__ seg_row,
-                                                       const int *__restrict__ seg_ptr,
-                                                       const int *__restrict__ pci, const double *__restrict__ pv,
-                                                       const double *__restrict__ x, double *__restrict__ y,
-                                                       const int *__restrict__ zero_rows, int nzero)
+// one sub-block (<= 256 segments, <= kSpmvCap entries) of the panel layout;
+// YA: the running sums read with agent-scope loads (k_spmv_rtile: the row's
+// previous segment was stored by this block, by another of its threads)
+template <bool YA>
+__device__ __forceinline__ void panel_subblock(int sb, const int *__restrict__ pblk, const int *__restrict__ seg_row,
+                                               const int *__restrict__ seg_ptr, const int *__restrict__ pci,
+                                               const double *__restrict__ pv, const double *__restrict__ x, double *y)
 {
-    if (gated(g)) return;
     constexpr int U = kSpmvCap / kBlock;        // entries per thread
     __shared__ double prod[kSpmvCap];
     __shared__ int sp[kBlock + 1];
     const int tid = threadIdx.x;
-    if (nzero)
-        for (long long i = blockIdx.x * (long long)kBlock + tid; i < nzero; i += (long long)gridDim.x * kBlock)
-            y[zero_rows[i]] = 0.0;
-    const int s0 = pblk[blockIdx.x], s1 = pblk[blockIdx.x + 1];
+    const int s0 = pblk[sb], s1 = pblk[sb + 1];
     const int ns = s1 - s0;                     // <= kBlock segments
     if (tid < ns) sp[tid] = pan_ld(seg_ptr + s0 + tid);
     if (tid == 0) sp[ns] = pan_ld(seg_ptr + s1);
@@ -705,7 +702,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__rest
     double acc = 0.0;
     if (tid < ns) {
         rr = pan_ld(seg_row + s0 + tid);
-        if (rr >= 0) acc = y[rr];               // the row's running sum so far
+        if (rr >= 0) acc = ld_x<YA>(y + rr);    // the row's running sum so far
     }
     __syncthreads();
     const int e0 = sp[0], cnt = sp[ns] - e0;
@@ -740,6 +737,43 @@ __global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__rest
         }
         for (; e < hi; e++) acc += prod[e];
         y[rr < 0 ? ~rr : rr] = acc;
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_spmv_panel(Gate g, const int *__restrict__ pblk,
+                                                       const int *__restrict__ seg_row,
+                                                       const int *__restrict__ seg_ptr,
+                                                       const int *__restrict__ pci, const double *__restrict__ pv,
+                                                       const double *__restrict__ x, double *__restrict__ y,
+                                                       const int *__restrict__ zero_rows, int nzero)
+{
+    if (gated(g)) return;
+    if (nzero)
+        for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < nzero; i += (long long)gridDim.x * kBlock)
+            y[zero_rows[i]] = 0.0;
+    panel_subblock<false>(blockIdx.x, pblk, seg_row, seg_ptr, pci, pv, x, y);
+}
+// Row tiles (DevCsr::rtile): ONE launch, block b walking its sub-blocks
+// rt_sub[b] .. rt_sub[b+1]-1 in order -- its rows' segments panel by panel, so
+// a row's terms are added in column order (the CSR order: the same bits), its
+// running sum in y only ever touched by this block.  Between sub-blocks the
+// y stores are drained and the block synchronises; the next sub-block reads y
+// with agent-scope loads (past this CU's L1).
+__global__ __launch_bounds__(kBlock) void k_spmv_rtile(Gate g, const int *__restrict__ rt_sub,
+                                                       const int *__restrict__ pblk,
+                                                       const int *__restrict__ seg_row,
+                                                       const int *__restrict__ seg_ptr,
+                                                       const int *__restrict__ pci, const double *__restrict__ pv,
+                                                       const double *__restrict__ x, double *y,
+                                                       const int *__restrict__ zero_rows, int nzero)
+{
+    if (gated(g)) return;
+    for (long long i = blockIdx.x * (long long)kBlock + threadIdx.x; i < nzero; i += (long long)gridDim.x * kBlock)
+        y[zero_rows[i]] = 0.0;
+    const int b0 = rt_sub[blockIdx.x], b1 = rt_sub[blockIdx.x + 1];
+    for (int sb = b0; sb < b1; sb++) {
+        panel_subblock<true>(sb, pblk, seg_row, seg_ptr, pci, pv, x, y);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this sub-block's y stores done
+        __syncthreads();
     }
 }
 
@@ -5303,6 +5337,12 @@ void launch_spmv(Gate g, const DevCsr &A, const double *x, const double *b, doub
                  hipStream_t st, const double *ydiv)
 {
     if (A.nblk == 0) return;
+    if (A.panel && A.rtile && !resid && !ydiv && x != y) {
+        // row tiles: one launch, each block its rows' segments panel by panel
+        k_spmv_rtile<<<A.rtile, kBlock, 0, st>>>(g, A.rt_sub.p, A.pblk.p, A.seg_row.p, A.seg_ptr.p, A.pci.p, A.pv.p, x,
+                                                  y, A.zero_rows.p, A.nzero);
+        return;
+    }
     if (A.panel && !resid && !ydiv && x != y) {
         // column panels: one launch per panel over its segment blocks
         for (int p = 0; p < A.npanel; p++) {

@@ -113,6 +113,92 @@ void DevCsr::build_panels(const Csr &A, hipStream_t st)
             if (A.ci[k] <= A.ci[k - 1]) return;            // not ascending: the panel order would differ
     pw = (int)w;
     npanel = (int)((n + w - 1) / w);
+    rtile = 0;
+    const char *rte = std::getenv("GG_SPMV_RTILE");
+    const int rtb = rte ? atoi(rte) : 0;
+    if (rtb > 0) {
+        // Row tiles: rtb contiguous row ranges of about equal cost (entries +
+        // a y access per row), each one block of ONE launch that walks its
+        // rows' segments panel by panel -- a row's segments in column order,
+        // its running sum in y touched only by its own block, and every block
+        // in about the same panel at the same time (x's slice shared in L2).
+        // Measured slower than the panel-major launches, so off by default
+        // (C3 stand-in, one box, profiles/r06/c3_rtile_ab.txt: 670-865 us at
+        // 512-2048 row blocks and 2-6 MiB panels against 623 us): a block's
+        // sub-blocks run one after another, each a dependent load -> gather ->
+        // sum -> store chain, where the panel-major launch keeps 8 of them in
+        // flight per CU
+        long long cost = 0;
+        for (int r = 0; r < n; r++) cost += (A.rp[r + 1] - A.rp[r]) + 4;
+        const long long target = std::max<long long>(1, (cost + rtb - 1) / rtb);
+        std::vector<int> rb{0};
+        long long acc = 0;
+        for (int r = 0; r < n; r++) {
+            acc += (A.rp[r + 1] - A.rp[r]) + 4;
+            if (acc >= target && r + 1 < n) {
+                rb.push_back(r + 1);
+                acc = 0;
+            }
+        }
+        rb.push_back(n);
+        const int nb = (int)rb.size() - 1;
+        std::vector<int> srow, sptr_h, pc(nnz), pb, rts, zr;
+        std::vector<double> pvv(nnz);
+        srow.reserve((size_t)n * 2);
+        sptr_h.reserve((size_t)n * 2 + 1);
+        std::vector<int> cur(A.rp.begin(), A.rp.end() - 1);
+        long long e = 0;
+        for (int b = 0; b < nb; b++) {
+            rts.push_back((int)pb.size());
+            for (int p = 0; p < npanel; p++) {
+                const long long hi = std::min<long long>((long long)(p + 1) * w, n);
+                int nseg_sb = 0, nent_sb = 0;
+                for (int r = rb[b]; r < rb[b + 1]; r++) {
+                    int k = cur[r];
+                    const int k1 = A.rp[r + 1];
+                    while (k < k1 && A.ci[k] < hi) {
+                        // one segment (or a piece of it) of at most kSpmvCap entries
+                        int kend = k;
+                        while (kend < k1 && A.ci[kend] < hi && kend - k < kSpmvCap) kend++;
+                        const int len = kend - k;
+                        if (nseg_sb == 0 || nseg_sb == 256 || nent_sb + len > kSpmvCap) {
+                            pb.push_back((int)srow.size());       // a new sub-block
+                            nseg_sb = 0;
+                            nent_sb = 0;
+                        }
+                        srow.push_back(k == A.rp[r] ? ~r : r);
+                        sptr_h.push_back((int)e);
+                        for (; k < kend; k++, e++) {
+                            pc[e] = A.ci[k];
+                            pvv[e] = A.v[k];
+                        }
+                        nseg_sb++;
+                        nent_sb += len;
+                    }
+                    cur[r] = k;
+                }
+            }
+        }
+        rts.push_back((int)pb.size());
+        pb.push_back((int)srow.size());
+        sptr_h.push_back((int)e);
+        for (int r = 0; r < n; r++)
+            if (A.rp[r + 1] == A.rp[r]) zr.push_back(r);    // empty rows: y = 0
+        nseg = (long long)srow.size();
+        nzero = (int)zr.size();
+        seg_row.upload(srow, st);
+        seg_ptr.upload(sptr_h, st);
+        pci.upload(pc, st);
+        pv.upload(pvv, st);
+        zero_rows.upload(zr.empty() ? std::vector<int>{0} : zr, st);
+        pblk.upload(pb, st);
+        rt_sub.upload(rts, st);
+        pan_blk_h.assign(npanel + 1, 0);
+        rtile = nb;
+        panel = true;
+        GG_HIP(hipStreamSynchronize(st));
+        return;
+    }
     std::vector<int> cur(A.rp.begin(), A.rp.end() - 1);  // per row: its next entry
     std::vector<int> ps(npanel + 1, 0), srow, sptr_h, pc(nnz);
     std::vector<double> pvv(nnz);
@@ -198,8 +284,10 @@ void DevCsr::copy_from(const DevCsr &o, hipStream_t st)
     pw = o.pw;
     nseg = o.nseg;
     nzero = o.nzero;
+    rtile = o.rtile;
+    if (rtile) dup(rt_sub, o.rt_sub);
+    if (panel && !rtile) dup(pan_seg, o.pan_seg);
     if (panel) {
-        dup(pan_seg, o.pan_seg);
         dup(seg_row, o.seg_row);
         dup(seg_ptr, o.seg_ptr);
         dup(pci, o.pci);
@@ -2102,6 +2190,7 @@ int gg_division_active(gg_solver *s, int which)
 }
 int gg_spmv_sliced(gg_solver *s) { return (s && s->dA.sell) ? 1 : 0; }
 int gg_spmv_panels(gg_solver *s) { return (s && s->dA.panel) ? s->dA.npanel : 0; }
+int gg_spmv_rtile(gg_solver *s) { return (s && s->dA.panel) ? s->dA.rtile : 0; }
 
 int gg_solve_device(gg_solver *s, const double *d_b, double *d_x, const gg_options *opt,
                     gg_result *res)

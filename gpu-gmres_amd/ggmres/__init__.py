@@ -30,7 +30,7 @@ EXPORTS = [
     "gg_bytes_precond", "gg_profile_enable", "gg_profile_reset", "gg_profile_get",
     "gg_trace_precond", "gg_bytes_trsv", "gg_bytes_trsv_stream", "gg_transient", "gg_set_precond_ilu0_device",
     "gg_ilu0_device_values", "gg_set_precond_iluk_device", "gg_iluk_device_factors",
-    "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced", "gg_spmv_panels",
+    "gg_transient_src", "gg_transient_set_taps", "gg_transient_get_taps", "gg_spmv_sliced", "gg_spmv_panels", "gg_spmv_rtile",
     "gg_transient_mna", "gg_set_division", "gg_division_active",
     "gg_trsv_kernel", "gg_mgs_kernel", "gg_set_precond_user", "gg_solve_device_f32",
     "gg_device_fingerprint", "gg_set_matrix_count", "gg_trsv_levels", "gg_layout", "gg_reduce_blocks",
@@ -82,7 +82,8 @@ def lib():
         L.gg_destroy.argtypes = [_VP]
         L.gg_set_matrix.argtypes = [_VP, ctypes.c_int, _I, _I, _D]
         for f in ("gg_set_precond_none", "gg_set_precond_ilu0", "gg_precond_kind",
-                  "gg_uses_wavefront", "gg_spmv_sliced", "gg_set_precond_ilu0_device", "gg_spmv_panels"):
+                  "gg_uses_wavefront", "gg_spmv_sliced", "gg_set_precond_ilu0_device", "gg_spmv_panels",
+                  "gg_spmv_rtile"):
             getattr(L, f).argtypes = [_VP]
         L.gg_set_precond_iluk.argtypes = [_VP, ctypes.c_int]
         L.gg_set_division.argtypes = [_VP, ctypes.c_int]
@@ -314,6 +315,11 @@ class Solver:
     def spmv_panels(self):
         """column panels y = A x runs over (k_spmv_panel), 0 = none"""
         return int(lib().gg_spmv_panels(self.h))
+
+    @property
+    def spmv_rtile(self):
+        """row blocks of the one-launch panel SpMV (k_spmv_rtile), 0 = panel-major launches / none"""
+        return int(lib().gg_spmv_rtile(self.h))
 
     # ---- solve -------------------------------------------------------------
     def solve(self, b, x0=None, restart=30, max_iter=3000, tol=1e-10, flags=0):

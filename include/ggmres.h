@@ -238,6 +238,10 @@ int gg_spmv_sliced(gg_solver *s);
  * L2-sized panels, each row's terms added panel by panel into its running sum,
  * the CSR order), 0 when the matrix does not take them (GG_SPMV_PANEL) */
 int gg_spmv_panels(gg_solver *s);
+/* the column panels' launch form: > 0 = ONE launch of that many row blocks,
+ * each walking its rows' segments panel by panel (k_spmv_rtile); 0 = one
+ * launch per panel (k_spmv_panel, GG_SPMV_RTILE=0) or no panels */
+int gg_spmv_rtile(gg_solver *s);
 
 int gg_solve(gg_solver *s, const double *b, double *x, const gg_options *opt,
              gg_result *res);

@@ -180,6 +180,58 @@ def test_solve_batch_sequential_fallback(monkeypatch):
     s.close()
 
 
+@pytest.mark.parametrize("case", ["ilu1_skewed", "grid3d", "nrhs1", "max_iter0"])
+def test_solve_batch_edges_match_single(case):
+    """configurations at the batch's edges, each scenario against its own
+    single solve: ILU(1) grid factors (the skewed wavefront: not batched, the
+    scenario-by-scenario path), a 3D grid (tile wavefront: not batched), one
+    right-hand side through the batched path, max_iter = 0 (no cycle: a zero
+    right-hand side converged at the start, the others not converged)"""
+    if case == "grid3d":
+        A = M.grid_7pt(20)
+    else:
+        A = M.laplacian_5pt(60, 52)
+    n = A.shape[0]
+    S = 1 if case == "nrhs1" else 3
+    B = _rhs_set(A, S, seed=21)                 # (scenario 2 is the zero vector)
+    max_iter = 0 if case == "max_iter0" else 2000
+    s = ggmres.Solver(0)
+    s.set_matrix(A)
+    if case == "ilu1_skewed":
+        s.set_precond_iluk(1)
+    else:
+        s.set_precond_ilu0()
+    s.set_division(ggmres.DIV_FMA)
+    assert s.batch_engine == (case in ("nrhs1", "max_iter0"))
+    g = s.solve_batch(B, restart=30, max_iter=max_iter, tol=1e-10)
+    for q in range(S):
+        r = s.solve(B[q], restart=30, max_iter=max_iter, tol=1e-10)
+        assert (g["status"][q], g["iters"][q]) == (r["ret"], r["iters"]), q
+        assert g["relres"][q] == r["relres"] and np.array_equal(g["x"][q], r["x"]), q
+    if case == "max_iter0":
+        assert g["status"] == [1, 1, 0] and g["iters"] == [0, 0, 0]
+    s.close()
+
+
+def test_solve_batch_bad_arguments():
+    """nrhs < 1, a leading dimension below n and unknown flags are refused"""
+    import ctypes
+    A = M.laplacian_5pt(32)
+    n = A.shape[0]
+    s = ggmres.Solver(0)
+    s.set_matrix(A)
+    s.set_precond_ilu0()
+    L = ggmres.lib()
+    b = np.ones(2 * n)
+    x = np.zeros(2 * n)
+    res = (ggmres.Result * 2)()
+    for nrhs, ld, flags in ((0, n, 0), (2, n - 1, 0), (2, n, ggmres.SOLVE_SHARED_DEVICE)):
+        o = ggmres.Options(30, 100, 1e-8, flags)
+        rc = L.gg_solve_batch(s.h, nrhs, b, ld, x, ld, ctypes.byref(o), res)
+        assert rc == -1, (nrhs, ld, flags, rc)        # GG_EINVAL
+    s.close()
+
+
 def _scenarios(n, S, h, seed0):
     return [M.pulse_sources(n, frac=0.01, h=h, seed=seed0 + q) for q in range(S)]
 

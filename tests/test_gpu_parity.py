@@ -126,12 +126,16 @@ def test_spmv_c3_standin_full_size(solver):
     assert np.array_equal(y, ref)
 
 
+@pytest.mark.parametrize("layout", ["rtile", "rtile7", "panel_major"])
 @pytest.mark.parametrize("case", ["powerlaw", "long_rows", "empty_rows"])
-def test_spmv_panels_bitexact(solver, case, monkeypatch):
+def test_spmv_panels_bitexact(solver, case, layout, monkeypatch):
     """Column panels at test size (GG_SPMV_PANEL / GG_SPMV_PANEL_MIN lowered):
     every row bit-exact vs the serial CSR-order sum, rows above 2,048 entries
-    included (the panels sum every row serially), empty rows 0."""
+    included (the panels sum every row serially), empty rows 0 -- in the
+    row-tile launch (default 1,024 row blocks; 7 blocks: long walks, segments
+    cut into pieces) and the panel-major launches (GG_SPMV_RTILE=0)."""
     monkeypatch.setenv("GG_SPMV_PANEL_MIN", "1000")
+    monkeypatch.setenv("GG_SPMV_RTILE", {"rtile": "1024", "rtile7": "7", "panel_major": "0"}[layout])
     if case == "powerlaw":
         A = M.power_law(200_000, 2_200_000, seed=5)
         monkeypatch.setenv("GG_SPMV_PANEL", "30000")
