@@ -346,6 +346,7 @@ struct DevTri {
     Wave2D wl;
     DBuf<double> c1, c2, dw, rw; // c1: |offset|=nx coef, c2: |offset|=1 coef, dw: divisor, rw: RN(1/dw)
     DBuf<double> c1s, c2s, c0s;  // WD_SFMA: RN(c1 * rw), RN(c2 * rw) (3D tiles: RN(c0 * rw))
+    DBuf<double> ce1s, ce2s;     // WD_SFMA on a skewed grid: the fill coefficients pre-scaled too
     DBuf<double> c0;             // 3D: |offset| = nx*ny coefficient
     DBuf<double> ce1, ce2;       // skew 2/3 (ILU(1)/(2) fill): |offset| = nx-1, nx-2 coefficients
     DBuf<unsigned long long> prog;   // 3D: per (plane, band) batches stored (0 between launches)

@@ -1803,7 +1803,7 @@ __device__ __forceinline__ void trsv_wave2d_body(
     static_assert(!FS || (FWD && !D3 && S == 1 && !TRACE), "fused SpMV: forward 2D");
     static_assert(!IL || (S == 1 && !D3), "in-line-first rows: unskewed 2D grids");
     constexpr bool FM = DIV == WD_UFMA || DIV == WD_SFMA;     // GG_DIV_FMA rows
-    static_assert(!FM || (S == 1 && !D3 && !IL), "fused rows: unskewed 2D grids (one order for both IL)");
+    static_assert(!FM || (!D3 && !IL), "fused rows: 2D grids (one order for both IL)");
     static_assert(!(TRACE && S > 1), "no trace for skewed grids");
     constexpr int PB = C::PBN * 64;            // double2 per array per slot
     static_assert(!(D3 && TRACE), "no trace for 3D grids");
@@ -2211,8 +2211,20 @@ __device__ __forceinline__ void trsv_wave2d_body(
                 // the neighbour line's terms oldest first (|offset| = nx, nx-1, ..),
                 // then the in-line neighbour (|offset| = 1)
                 double acc;
-                if constexpr (FM) {
+                if constexpr (FM && S == 1) {
                     acc = __builtin_fma(-e1, xs, tf);
+                } else if constexpr (FM && S == 2) {
+                    // nearest first: in-line (tf), fill nx-1 (xs), line nx (xh1)
+                    const double f1 = sx ? rg[kk][C::AE].x : rg[kk][C::AE].y;
+                    acc = __builtin_fma(-f1, xs, tf);
+                    acc = __builtin_fma(-e1, xh1, acc);
+                } else if constexpr (FM) {
+                    // in-line, fill nx-2 (xs), fill nx-1 (xh1), line nx (xh2)
+                    const double f1 = sx ? rg[kk][C::AE].x : rg[kk][C::AE].y;
+                    const double f2 = sx ? rg[kk][C::AE + 1].x : rg[kk][C::AE + 1].y;
+                    acc = __builtin_fma(-f2, xs, tf);
+                    acc = __builtin_fma(-f1, xh1, acc);
+                    acc = __builtin_fma(-e1, xh2, acc);
                 } else if constexpr (IL) {
                     acc = bz - p2;
                     acc = acc - e1 * xs;
@@ -5621,6 +5633,27 @@ static void launch_trsv_one(Gate g, DevTri &T, const double *b, double *x, int *
             // GG_DIV_FMA on a 2D grid (build_tri admits unskewed ones in canonical order)
             dim3 grid(w.nbands * (T.lower ? 1 : GG_WAVE_XCD));
             const double *k1 = div == WD_SFMA ? T.c1s.p : T.c1.p, *k2 = div == WD_SFMA ? T.c2s.p : T.c2.p;
+            if (w.skew > 1) {
+                // ILU(k) grids (skewed lanes): the fills pre-scaled with U's coefficients
+                const double *f1 = div == WD_SFMA ? T.ce1s.p : T.ce1.p, *f2 = div == WD_SFMA ? T.ce2s.p : T.ce2.p;
+#define GG_FMA_SKEW_LAUNCH(FWD, DIV, S)                                                            \
+    k_trsv_wave2d<FWD, DIV, false, false, S, false><<<grid, WaveCfg<DIV, false, S>::THREADS, 0, st>>>( \
+        g, w.T, w.nbands, b, k1, k2, dv, rv, x, T.bnd.p, err, nullptr, 1, w.P2, nullptr, nullptr, f1, f2)
+                if (T.lower && div == WD_UFMA) {
+                    if (w.skew == 2) GG_FMA_SKEW_LAUNCH(true, WD_UFMA, 2);
+                    else GG_FMA_SKEW_LAUNCH(true, WD_UFMA, 3);
+                } else if (!T.lower && div == WD_SFMA) {
+                    if (w.skew == 2) GG_FMA_SKEW_LAUNCH(false, WD_SFMA, 2);
+                    else GG_FMA_SKEW_LAUNCH(false, WD_SFMA, 3);
+                } else if (T.lower && div == WD_SFMA) {
+                    if (w.skew == 2) GG_FMA_SKEW_LAUNCH(true, WD_SFMA, 2);
+                    else GG_FMA_SKEW_LAUNCH(true, WD_SFMA, 3);
+                } else {
+                    std::abort();   // build_tri: no unit upper triangle
+                }
+#undef GG_FMA_SKEW_LAUNCH
+                return;
+            }
 #define GG_FMA_LAUNCH(FWD, DIV, TR)                                                                \
     k_trsv_wave2d<FWD, DIV, TR><<<grid, WaveCfg<DIV>::THREADS, 0, st>>>(                           \
         g, w.T, w.nbands, b, k1, k2, dv, rv, x, T.bnd.p, err, T.trace, 1, w.P2, nullptr, nullptr,   \

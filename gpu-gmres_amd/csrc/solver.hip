@@ -403,17 +403,27 @@ void build_tri(DevTri &T, const CanonTri &C, const Wave2D *wl, const std::vector
         // (the fused rows take the in-line term first whatever the canonical
         // order, so the split engine's in-line-first U is admitted too, and
         // its non-unit L as a pre-scaled lower triangle)
-        T.fma_ok = (!d3 || tile_ok) && K == 0 && (unit ? C.lower : mul_ok);
+        // Round 6: skewed 2D grids (ILU(1) / ILU(2) factors, GG_FMA_SKEW default
+        // 1) too -- nearest term first: the in-line term, then the fills
+        // (nx-2, nx-1), then the line term (nx); the fills pre-scaled for U
+        const char *fs = std::getenv("GG_FMA_SKEW");
+        const bool skew_ok = !d3 && !(fs && fs[0] == '0');
+        T.fma_ok = (!d3 || tile_ok) && (K == 0 || skew_ok) && (unit ? C.lower : mul_ok);
         if (T.fma_ok && !unit) {
             std::vector<double> s1(Ppad, 0.0), s2(Ppad, 0.0), s0(d3 ? Ppad : 0, 0.0);
+            std::vector<double> se1(K >= 1 ? Ppad : 0, 0.0), se2(K >= 2 ? Ppad : 0, 0.0);
             for (long long p = 0; p < Ppad; p++) {
                 s1[p] = c1[p] * rv[p];
                 s2[p] = c2[p] * rv[p];
                 if (d3) s0[p] = c0[p] * rv[p];
+                if (K >= 1) se1[p] = ce1[p] * rv[p];
+                if (K >= 2) se2[p] = ce2[p] * rv[p];
             }
             T.c1s.upload(s1, st);
             T.c2s.upload(s2, st);
             if (d3) T.c0s.upload(s0, st);
+            if (K >= 1) T.ce1s.upload(se1, st);
+            if (K >= 2) T.ce2s.upload(se2, st);
         }
         // one hand-off granule per band (tile) and step, then per workgroup 64
         // zero granules (dummy reads) and 64 write-only ones (dummy re-arms),
@@ -532,7 +542,7 @@ void build_tri_bordered(DevTri &T, const CanonTri &C, const CanonTri &Cg, const 
     std::vector<long long> gslot(Cg.off.n);
     for (int r = 0; r < Cg.off.n; r++) gslot[r] = wg.slot(r);
     build_tri(T, Cg, &wg, &gslot, round_up(wg.P2, 512), st);
-    const bool grid_fma = T.fma_ok, grid_unit = T.div == WD_UNIT;
+    const bool grid_fma = T.fma_ok && T.wl.skew == 1, grid_unit = T.div == WD_UNIT;
     T.bofs = wl.bofs;
     // the tail over the whole layout (its columns are slots); level sets over
     // the tail's own rows only (an upper tail's grid columns are final before it runs)

@@ -204,11 +204,10 @@ def test_rcp_c4_first_iterations(solver):
 
 
 # ---------------------------------------------------------------- GG_DIV_FMA
-# The unskewed 2D-grid and 3D-tile wavefront solves as fused multiply-adds per
-# row (nearest term first; U's b and coefficients pre-scaled by RN(1/d),
-# kernels.hip WD_UFMA / WD_SFMA), restated by oracle.set_div_mode(2, 2).  The
-# other wavefront solves (skewed ILU(k) grids, the split engine's in-line-first
-# U and non-unit L) fall back to GG_DIV_RCP's multiply.  Bars as above:
+# The 2D-grid (unskewed and, round 6, the skewed ILU(k) ones) and 3D-tile
+# wavefront solves as fused multiply-adds per row (nearest term first; U's b
+# and coefficients pre-scaled by RN(1/d), kernels.hip WD_UFMA / WD_SFMA),
+# restated by oracle.set_div_mode(2, 2).  Bars as above:
 # bit-exact vs the order-matched restatement, within 1e-10 of the serial oracle
 # with the reference's arithmetic.
 @pytest.fixture(scope="module")
@@ -262,12 +261,58 @@ def test_fma_apply(fsolver, name, scale):
     assert rel_err(z / scale, ze / scale) <= 1e-12
 
 
-def test_fma_fallbacks(fsolver):
-    """skewed ILU(1) grids and other sparsity: GG_DIV_RCP / the division"""
+@pytest.mark.parametrize("k", [1, 2])
+@pytest.mark.parametrize("scale", [1.0, 1e-250, 1e250])
+def test_fma_skewed_apply(fsolver, k, scale):
+    """ILU(1) / ILU(2) grid factors on the skewed wavefront as fused rows (round
+    6): nearest term first -- in-line, the fills nx-2 (k = 2) and nx-1, the line
+    term -- bit-exact vs oracle.set_div_mode(2, 2), within 1e-12 of the serial
+    oracle"""
+    A = M.laplacian_5pt(100, 70)
+    L, U = O.iluk(A, k)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_iluk(k)
+    assert fsolver.uses_wavefront and modes(fsolver) == (2, 2)
+    assert fsolver.trsv_kernel(0).startswith("k_trsv_wave2d<true, 4,") and f", {k + 1}, false>" in fsolver.trsv_kernel(0)
+    y = np.random.default_rng(7).standard_normal(A.shape[0]) * scale
+    z = fsolver.precond_apply(ggmres.APPLY_MINV, y)
+    O.set_div_mode(2, 2)
+    try:
+        zm = O.lusolve(L, U, y)
+    finally:
+        O.set_div_mode()
+    assert np.array_equal(z, zm)
+    assert rel_err(z / scale, O.lusolve(L, U, y) / scale) <= 1e-12
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_fma_skewed_gmres_parity(fsolver, k):
+    """GMRES(30) with ILU(k) grid factors under GG_DIV_FMA: bit-exact vs the
+    order-matched oracle, within the tolerance of the serial one"""
+    A = M.laplacian_5pt(90, 77)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    L, U = O.iluk(A, k)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_iluk(k)
+    md = modes(fsolver)
+    assert md == (2, 2)
+    o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=3000, tol=1e-10), n, mul=md,
+                       layout=fsolver.layout())
+    g = fsolver.solve(b, restart=30, max_iter=3000, tol=1e-10)
+    check_exact(g, ot)
+    check_tol(g, o)
+
+
+def test_fma_fallbacks(fsolver, monkeypatch):
+    """GG_FMA_SKEW=0 keeps skewed ILU(1) grids on GG_DIV_RCP's multiply; other
+    sparsity: the division"""
+    monkeypatch.setenv("GG_FMA_SKEW", "0")
     A = M.laplacian_5pt(100, 70)
     L, U = O.iluk(A, 1)
     fsolver.set_matrix(A)
     fsolver.set_precond_iluk(1)
+    monkeypatch.delenv("GG_FMA_SKEW")
     assert fsolver.uses_wavefront and modes(fsolver) == (0, 1)
     y = np.random.default_rng(7).standard_normal(A.shape[0])
     O.set_div_mode(0, 1)
