@@ -1510,8 +1510,12 @@ constexpr int kWaveLoaders = GG_WAVE_LOADERS;
 #ifndef GG_WAVE_DECOUPLE
 #define GG_WAVE_DECOUPLE 0
 #endif
+// Round 6, re-measured on the per-wave compute loop (C2, one box, alternating,
+// profiles/r06/earlybar_ab.txt): the early barrier helps the forward solve (L
+// 83.2 -> 81.0 us) and not the backward one (U 81.2 -> 81.7): 2 = forward only
+// (0 none, 1 both); C2 4,299 -> 4,339 it/s
 #ifndef GG_WAVE_EARLYBAR
-#define GG_WAVE_EARLYBAR 0
+#define GG_WAVE_EARLYBAR 2
 #endif
 // (Measured, not kept, round 5: the 2D boundary wave retrying a batch's
 // granules with two polls in flight, s_sleep 0 / 1 / 10 between them: C2 U
@@ -2015,6 +2019,8 @@ __device__ __forceinline__ void trsv_wave2d_body(
         // the dummy granules after the bands: 64 zeros to read, 64 to write),
         // which keeps the vmcnt arithmetic exact.
         constexpr int kPoll = GG_WAVE_POLL;
+        // the barrier before (EB) or after the re-arm store and look-ahead poll
+        constexpr bool EB = GG_WAVE_EARLYBAR == 1 || (GG_WAVE_EARLYBAR == 2 && FWD);
         // 3D: lane 32 polls the previous plane's progress instead: before
         // barrier bi it must have stored the batches the loader streams after
         // it (up to bi + R - 1); its word is never re-armed here, but reset to
@@ -2076,14 +2082,14 @@ __device__ __forceinline__ void trsv_wave2d_body(
                             (long long)__builtin_amdgcn_s_memrealtime();
                 }
                 bring[(bi & 1) * 64 + lane] = __longlong_as_double((long long)v[u]);
-                if constexpr (GG_WAVE_EARLYBAR) {
+                if constexpr (EB) {
                     // hand the values over first, then re-arm and poll ahead
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     raw_barrier();
                 }
                 st_agent(ga ? ga : dummy_st, kSentinel);       // re-arm for the next launch
                 v[u] = ld_agent(poll_addr(bi + kPoll));
-                if constexpr (!GG_WAVE_EARLYBAR) {
+                if constexpr (!EB) {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     raw_barrier();
                 }
