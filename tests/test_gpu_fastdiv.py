@@ -394,6 +394,25 @@ def test_fma_c2_first_cycle(fsolver):
 
 
 @pytest.mark.slow
+def test_fma_skewed_c2_first_cycle(fsolver):
+    """C2 with ILU(1) grid factors (the skewed wavefront's fused rows, round 6):
+    the first restart cycle at full size, bit-exact vs the order-matched oracle"""
+    A = M.laplacian_5pt(1000)
+    n = A.shape[0]
+    b = M.rhs_ones(A)
+    L, U = O.iluk(A, 1)
+    fsolver.set_matrix(A)
+    fsolver.set_precond_iluk(1)
+    assert modes(fsolver) == (2, 2) and ", 2, false>" in fsolver.trsv_kernel(1)
+    o, ot = oracle_mul(lambda: O.gmres_left(A, L, U, b, m=30, max_iter=30, tol=1e-300), n, mul=(2, 2),
+                       layout=fsolver.layout())
+    g = fsolver.solve(b, restart=30, max_iter=30, tol=1e-300)
+    assert g["iters"] == 30 and g["ret"] == 1
+    check_exact(g, ot)
+    check_tol(g, o)
+
+
+@pytest.mark.slow
 def test_fma_c2_full_solve_tolerance(fsolver):
     """C2 solved to 1e-8 (the bench's tolerance): same return code, iteration
     counts within 1 % of the serial oracle's divide-mode solve is not asserted
